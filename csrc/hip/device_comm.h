@@ -1,0 +1,33 @@
+// Device data plane for tensor parallelism: RCCL over xGMI, one process per GPU.
+//
+// Replaces the reference's TCP all-gather + local merge-add (nn-network.cpp:537-569,
+// llm.cpp:212-217, 308-314) with a single in-place f32 all-reduce per residual update and an
+// all-gather of the vocab-sharded logits (nn-network.cpp SYNC_NODE_SLICES_EXCEPT_ROOT).
+// Collectives are enqueued on the engine's stream so they are captured in the forward hipGraph.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace dl {
+
+class DeviceComm {
+  public:
+    virtual ~DeviceComm() = default;
+    virtual int rank() const = 0;
+    virtual int size() const = 0;
+    virtual void allReduceSum(float *buf, size_t n, hipStream_t s) = 0;
+    virtual void allGather(const float *send, float *recv, size_t nPerRank, hipStream_t s) = 0;
+    virtual void broadcastInts(int *buf, size_t n, int root, hipStream_t s) = 0;
+    virtual std::string name() const = 0;
+};
+
+// 128-byte RCCL unique id (generated on rank 0, distributed over the control plane).
+std::vector<unsigned char> rcclGetUniqueId();
+// Must be called with the HIP device of this rank already selected.
+std::unique_ptr<DeviceComm> makeRcclComm(const std::vector<unsigned char> &uid, int rank, int size);
+
+}  // namespace dl

@@ -1,0 +1,639 @@
+// HipEngine implementation (host side).
+//
+// Weight residency: every rank repacks ITS shard of the mmapped `.m` file on the host into the
+// GPU layout and uploads it once (reference: root streams shards to workers over TCP,
+// nn-network.cpp:766-901; llm.cpp:447-483 defines the slices). Q40 matrices become SoA
+// (16-byte nibble rows + f16 scale plane) so a lane's 16-byte load is one whole block.
+// Fusions baked into the layout:
+//   Wq|Wk|Wv row slices concatenated -> one QKV GEMV (+RoPE +KV append epilogue)
+//   W1/W3 row slices interleaved      -> one GEMV whose epilogue computes act(w1 x) * (w3 x)
+#include "engine.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <vector>
+
+#include "../core/quant.h"
+#include "kernels.h"
+
+namespace dl {
+
+#define DL_HIP(x)                                                                                        \
+    do {                                                                                                 \
+        hipError_t e_ = (x);                                                                             \
+        if (e_ != hipSuccess) throw Error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x); \
+    } while (0)
+
+int hipDeviceCount() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+namespace {
+
+struct DevMat {
+    uint8_t *qs = nullptr;
+    uint16_t *d = nullptr;
+    float *f = nullptr;
+    int rows = 0, n = 0;
+};
+
+struct DevLayer {
+    DevMat qkv, wo, w13, w2;
+    float *rmsAtt = nullptr, *rmsFfn = nullptr;
+    void *k = nullptr, *v = nullptr;
+};
+
+class HipEngineImpl : public HipEngine {
+  public:
+    HipEngineImpl(const EngineConfig &cfg, DeviceComm *comm) : cfg_(cfg), comm_(comm) {
+        const int nDev = hipDeviceCount();
+        if (nDev <= 0) throw Error("No HIP device available");
+        dev_ = cfg.gpuIndex >= 0 ? cfg.gpuIndex : 0;
+        DL_CHECK(dev_ < nDev, "gpu index out of range");
+        DL_HIP(hipSetDevice(dev_));
+        DL_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+        const u32 nRanks = comm_ ? comm_->size() : 1, rank = comm_ ? comm_->rank() : 0;
+        if (cfg.synthetic) {
+            h_ = cfg.syntheticHeader;
+            h_.origSeqLen = h_.seqLen;
+            if (cfg.maxSeqLen > 0 && h_.seqLen > cfg.maxSeqLen) h_.seqLen = cfg.maxSeqLen;
+        } else {
+            file_.reset(new ModelFile(cfg.modelPath, cfg.maxSeqLen));
+            h_ = file_->header();
+        }
+        plan_ = ShardPlan::make(h_, nRanks, rank);
+        q40_ = h_.weightType == FloatType::Q40;
+        if (q40_ && cfg.bufferType != FloatType::Q80)
+            throw Error("This version supports only Q40 weights with Q80 sync type");
+        if (!q40_ && h_.weightType != FloatType::F32) throw Error("unsupported weight type");
+        DL_CHECK(h_.headSize() == 64 || h_.headSize() == 128, "GPU kernels support head size 64 or 128");
+        DL_CHECK(cfg.maxBatch >= 1 && cfg.nSlots >= 1, "maxBatch/nSlots");
+        kvBf16_ = cfg.kvBf16;
+        allocBuffers();
+        if (cfg.synthetic)
+            loadSynthetic();
+        else
+            loadFromFile();
+        uploadRope();
+        DL_HIP(hipStreamSynchronize(stream_));
+    }
+
+    ~HipEngineImpl() override {
+        (void)hipSetDevice(dev_);
+        for (auto &kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+        for (void *p : allocs_) (void)hipFree(p);
+        for (void *p : hostAllocs_) (void)hipHostFree(p);
+        if (stream_) (void)hipStreamDestroy(stream_);
+    }
+
+    const ModelHeader &header() const override { return h_; }
+    const ShardPlan &plan() const override { return plan_; }
+    std::string name() const override { return "hip"; }
+    size_t deviceBytes() const override { return deviceBytes_; }
+    void synchronize() override { DL_HIP(hipStreamSynchronize(stream_)); }
+
+    void forward(int n, const int *tokens, const int *positions, const int *slots, float *logits) override {
+        Timer t;
+        setInputs(n, tokens, positions, slots);
+        runGraph(n, GraphKind::LOGITS);
+        const bool root = rank() == 0;
+        if (root && logits) {
+            const float *src = plan_.nRanks > 1 ? dLogitsFull_ : dLogits_;
+            DL_HIP(hipMemcpyAsync(hLogits_, src, (size_t)n * h_.vocabSize * sizeof(float), hipMemcpyDeviceToHost,
+                                  stream_));
+        }
+        DL_HIP(hipStreamSynchronize(stream_));
+        if (root && logits) std::memcpy(logits, hLogits_, (size_t)n * h_.vocabSize * sizeof(float));
+        stats_.computeMs = t.elapsedMs();
+        stats_.syncMs = 0;
+    }
+
+    void forwardArgmax(int n, const int *tokens, const int *positions, const int *slots, int *out) override {
+        Timer t;
+        setInputs(n, tokens, positions, slots);
+        runGraph(n, GraphKind::ARGMAX);
+        DL_HIP(hipMemcpyAsync(hIds_, dIds_, n * sizeof(int), hipMemcpyDeviceToHost, stream_));
+        DL_HIP(hipStreamSynchronize(stream_));
+        std::memcpy(out, hIds_, n * sizeof(int));
+        stats_.computeMs = t.elapsedMs();
+    }
+
+    double decodeGreedy(int steps, int token, int pos, int slot, int *outTokens) override {
+        return decodeGreedyBatch(steps, 1, &token, &pos, &slot, outTokens);
+    }
+
+    double decodeGreedyBatch(int steps, int nSeq, const int *tokens, const int *pos, const int *slots,
+                             int *outTokens) override {
+        DL_CHECK(nSeq >= 1 && (u32)nSeq <= cfg_.maxBatch, "nSeq");
+        for (int b = 0; b < nSeq; b++) DL_CHECK((u32)(pos[b] + steps) <= h_.seqLen, "decode exceeds seqLen");
+        setInputs(nSeq, tokens, pos, slots);
+        DL_HIP(hipMemsetAsync(dHist_, 0xff, sizeof(int) * (size_t)cfg_.maxBatch * h_.seqLen, stream_));
+        hipEvent_t e0, e1;
+        DL_HIP(hipEventCreate(&e0));
+        DL_HIP(hipEventCreate(&e1));
+        // the chained graph: forward -> argmax -> (tokens := ids, pos += 1)
+        DL_HIP(hipEventRecord(e0, stream_));
+        for (int s = 0; s < steps; s++) runGraph(nSeq, GraphKind::CHAIN);
+        DL_HIP(hipEventRecord(e1, stream_));
+        DL_HIP(hipEventSynchronize(e1));
+        float ms = 0;
+        DL_HIP(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        if (outTokens) {
+            std::vector<int> hist((size_t)cfg_.maxBatch * h_.seqLen);
+            DL_HIP(hipMemcpy(hist.data(), dHist_, hist.size() * sizeof(int), hipMemcpyDeviceToHost));
+            for (int b = 0; b < nSeq; b++)
+                for (int s = 0; s < steps; s++) outTokens[b * steps + s] = hist[(size_t)b * h_.seqLen + pos[b] + s];
+        }
+        return ms;
+    }
+
+    void profileForward(int n, const int *tokens, const int *positions, const int *slots) override {
+        setInputs(n, tokens, positions, slots);
+        profile_ = true;
+        profTimes_.clear();
+        enqueueForward(n, GraphKind::LOGITS);
+        DL_HIP(hipStreamSynchronize(stream_));
+        profile_ = false;
+        std::map<std::string, double> agg;
+        for (auto &p : profTimes_) {
+            float ms = 0;
+            DL_HIP(hipEventElapsedTime(&ms, p.second.first, p.second.second));
+            agg[p.first] += ms;
+            (void)hipEventDestroy(p.second.first);
+            (void)hipEventDestroy(p.second.second);
+        }
+        double total = 0;
+        for (auto &kv : agg) total += kv.second;
+        std::printf("⏱️  per-kernel-class device time (eager, batch %d):\n", n);
+        for (auto &kv : agg) std::printf("   %-14s %8.3f ms (%5.1f%%)\n", kv.first.c_str(), kv.second, 100.0 * kv.second / total);
+        std::printf("   %-14s %8.3f ms\n", "total", total);
+        profTimes_.clear();
+    }
+
+  private:
+    enum class GraphKind { LOGITS = 0, ARGMAX = 1, CHAIN = 2 };
+
+    int rank() const { return comm_ ? comm_->rank() : 0; }
+
+    template <typename T>
+    T *dalloc(size_t count) {
+        void *p = nullptr;
+        const size_t bytes = count * sizeof(T);
+        DL_HIP(hipMalloc(&p, bytes < 16 ? 16 : bytes));
+        allocs_.push_back(p);
+        deviceBytes_ += bytes;
+        return (T *)p;
+    }
+    template <typename T>
+    T *halloc(size_t count) {
+        void *p = nullptr;
+        DL_HIP(hipHostMalloc(&p, count * sizeof(T) < 16 ? 16 : count * sizeof(T), hipHostMallocDefault));
+        hostAllocs_.push_back(p);
+        return (T *)p;
+    }
+
+    void allocBuffers() {
+        const u32 MB = cfg_.maxBatch;
+        const ShardPlan &p = plan_;
+        dTok_ = dalloc<int>(MB);
+        dPos_ = dalloc<int>(MB);
+        dSlot_ = dalloc<int>(MB);
+        dIds_ = dalloc<int>(MB);
+        dHist_ = dalloc<int>((size_t)MB * h_.seqLen);
+        hIn_ = halloc<int>(3 * MB);
+        hIds_ = halloc<int>(MB);
+        hLogits_ = halloc<float>((size_t)MB * h_.vocabSize);
+        dX_[0] = dalloc<float>((size_t)MB * h_.dim);
+        dX_[1] = dalloc<float>((size_t)MB * h_.dim);
+        dY_ = dalloc<float>((size_t)MB * h_.dim);
+        dQ_ = dalloc<float>((size_t)MB * p.q0);
+        dAtt_ = dalloc<float>((size_t)MB * p.q0);
+        dH_ = dalloc<float>((size_t)MB * p.hidden0);
+        dLogits_ = dalloc<float>((size_t)MB * p.vocab0);
+        if (p.nRanks > 1) {
+            dLogitsAll_ = dalloc<float>((size_t)MB * h_.vocabSize);
+            dLogitsFull_ = dalloc<float>((size_t)MB * h_.vocabSize);
+        }
+        splitGrid_ = hipk::attnSplitGrid(h_.seqLen);
+        chunkMax_ = hipk::attnChunkMax(h_.seqLen, splitGrid_);
+        dPartO_ = dalloc<float>((size_t)MB * p.nHeads0 * splitGrid_ * p.headSize);
+        dPartML_ = dalloc<float>((size_t)MB * p.nHeads0 * splitGrid_ * 2);
+        dRope_ = dalloc<float2>((size_t)h_.seqLen * (p.headSize / 2));
+        layers_.resize(h_.nLayers);
+        const size_t kvElems = (size_t)cfg_.nSlots * h_.seqLen * p.kv0;
+        for (auto &L : layers_) {
+            if (kvBf16_) {
+                L.k = dalloc<uint16_t>(kvElems);
+                L.v = dalloc<uint16_t>(kvElems);
+            } else {
+                L.k = dalloc<float>(kvElems);
+                L.v = dalloc<float>(kvElems);
+            }
+            DL_HIP(hipMemsetAsync(L.k, 0, kvElems * (kvBf16_ ? 2 : 4), stream_));
+            DL_HIP(hipMemsetAsync(L.v, 0, kvElems * (kvBf16_ ? 2 : 4), stream_));
+        }
+    }
+
+    void uploadRope() {
+        std::vector<float> t = buildRopeTable(h_);
+        DL_HIP(hipMemcpy(dRope_, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
+
+    // ---------------------------------------------------------------- weight upload
+    // Append rows of a Q40 (AoS on disk) matrix slice to SoA host buffers.
+    static void repackRowsQ40(const u8 *src, u32 cols, u32 r0, u32 nr, u32 c0, u32 nc, std::vector<u8> &qs,
+                              std::vector<u16> &d) {
+        const u32 nbAll = cols / kQBlock, nb0 = c0 / kQBlock, nb = nc / kQBlock;
+        for (u32 r = r0; r < r0 + nr; r++) {
+            const BlockQ40 *row = reinterpret_cast<const BlockQ40 *>(src) + (u64)r * nbAll + nb0;
+            for (u32 j = 0; j < nb; j++) {
+                qs.insert(qs.end(), row[j].qs, row[j].qs + 16);
+                d.push_back(row[j].d);
+            }
+        }
+    }
+
+    void uploadMat(DevMat &m, int rows, int n, const std::vector<u8> &qs, const std::vector<u16> &d,
+                   const std::vector<float> &f) {
+        m.rows = rows;
+        m.n = n;
+        if (q40_) {
+            DL_CHECK(qs.size() == (size_t)rows * n / 2 && d.size() == (size_t)rows * n / 32, "repack size");
+            m.qs = dalloc<uint8_t>(qs.size());
+            m.d = dalloc<uint16_t>(d.size());
+            DL_HIP(hipMemcpy(m.qs, qs.data(), qs.size(), hipMemcpyHostToDevice));
+            DL_HIP(hipMemcpy(m.d, d.data(), d.size() * 2, hipMemcpyHostToDevice));
+        } else {
+            DL_CHECK(f.size() == (size_t)rows * n, "f32 slice size");
+            m.f = dalloc<float>(f.size());
+            DL_HIP(hipMemcpy(m.f, f.data(), f.size() * 4, hipMemcpyHostToDevice));
+        }
+    }
+
+    // Build a device matrix from a list of (tensor, rowStart, nRows) row sources, optionally
+    // interleaving two sources row by row, restricted to input columns [c0, c0+nc).
+    struct RowSrc {
+        const TensorInfo *t;
+        u32 r0, nr;
+    };
+    void buildMat(DevMat &m, const std::vector<RowSrc> &srcs, bool interleave, u32 c0, u32 nc) {
+        std::vector<u8> qs;
+        std::vector<u16> d;
+        std::vector<float> f;
+        u32 rows = 0;
+        auto addRows = [&](const RowSrc &s, u32 r, u32 cnt) {
+            const u8 *base = file_->ptr(*s.t);
+            if (q40_) {
+                repackRowsQ40(base, s.t->cols, r, cnt, c0, nc, qs, d);
+            } else {
+                for (u32 rr = r; rr < r + cnt; rr++) {
+                    const float *row = reinterpret_cast<const float *>(base) + (u64)rr * s.t->cols + c0;
+                    f.insert(f.end(), row, row + nc);
+                }
+            }
+        };
+        if (interleave) {
+            DL_CHECK(srcs.size() == 2 && srcs[0].nr == srcs[1].nr, "interleave");
+            for (u32 i = 0; i < srcs[0].nr; i++) {
+                addRows(srcs[0], srcs[0].r0 + i, 1);
+                addRows(srcs[1], srcs[1].r0 + i, 1);
+            }
+            rows = 2 * srcs[0].nr;
+        } else {
+            for (const auto &s : srcs) {
+                addRows(s, s.r0, s.nr);
+                rows += s.nr;
+            }
+        }
+        uploadMat(m, rows, nc, qs, d, f);
+    }
+
+    float *uploadF32(const TensorInfo &t) {
+        float *p = dalloc<float>((size_t)t.rows * t.cols);
+        DL_HIP(hipMemcpy(p, file_->ptr(t), (size_t)t.rows * t.cols * 4, hipMemcpyHostToDevice));
+        return p;
+    }
+
+    void loadFromFile() {
+        const ShardPlan &p = plan_;
+        const ModelFile &f = *file_;
+        for (u32 l = 0; l < h_.nLayers; l++) {
+            DevLayer &L = layers_[l];
+            const TensorInfo &wq = f.find(TensorKind::WQ, l), &wk = f.find(TensorKind::WK, l),
+                             &wv = f.find(TensorKind::WV, l), &wo = f.find(TensorKind::WO, l),
+                             &w1 = f.find(TensorKind::W1, l), &w2 = f.find(TensorKind::W2, l),
+                             &w3 = f.find(TensorKind::W3, l);
+            buildMat(L.qkv, {{&wq, p.qStart(), p.q0}, {&wk, p.kvStart(), p.kv0}, {&wv, p.kvStart(), p.kv0}}, false, 0,
+                     h_.dim);
+            buildMat(L.wo, {{&wo, 0, h_.dim}}, false, p.qStart(), p.q0);
+            buildMat(L.w13, {{&w1, p.hiddenStart(), p.hidden0}, {&w3, p.hiddenStart(), p.hidden0}}, true, 0, h_.dim);
+            buildMat(L.w2, {{&w2, 0, h_.dim}}, false, p.hiddenStart(), p.hidden0);
+            L.rmsAtt = uploadF32(f.find(TensorKind::RMS_ATT, l));
+            L.rmsFfn = uploadF32(f.find(TensorKind::RMS_FFN, l));
+        }
+        emb_ = uploadF32(f.find(TensorKind::EMBEDDING, -1));
+        rmsFinal_ = uploadF32(f.find(TensorKind::RMS_FINAL, -1));
+        buildMat(wcls_, {{&f.find(TensorKind::WCLS, -1), p.vocabStart(), p.vocab0}}, false, 0, h_.dim);
+    }
+
+    void synthMat(DevMat &m, int rows, int n, u64 seed) {
+        m.rows = rows;
+        m.n = n;
+        const float scale = 1.0f / std::sqrt(21.5f * (float)n);
+        if (q40_) {
+            const size_t nBlocks = (size_t)rows * n / 32;
+            m.qs = dalloc<uint8_t>(nBlocks * 16);
+            m.d = dalloc<uint16_t>(nBlocks);
+            hipk::launchFillQ40(m.qs, m.d, nBlocks, scale, seed, stream_);
+        } else {
+            m.f = dalloc<float>((size_t)rows * n);
+            hipk::launchFillF32Uniform(m.f, (size_t)rows * n, std::sqrt(3.0f / (float)n), seed, stream_);
+        }
+        DL_HIP(hipGetLastError());
+    }
+
+    void loadSynthetic() {
+        const ShardPlan &p = plan_;
+        u64 seed = cfg_.seed * 1000003ull + (u64)p.rank * 7919ull;
+        for (u32 l = 0; l < h_.nLayers; l++) {
+            DevLayer &L = layers_[l];
+            synthMat(L.qkv, p.q0 + 2 * p.kv0, h_.dim, seed++);
+            synthMat(L.wo, h_.dim, p.q0, seed++);
+            synthMat(L.w13, 2 * p.hidden0, h_.dim, seed++);
+            synthMat(L.w2, h_.dim, p.hidden0, seed++);
+            L.rmsAtt = dalloc<float>(h_.dim);
+            L.rmsFfn = dalloc<float>(h_.dim);
+            hipk::launchFillF32Const(L.rmsAtt, h_.dim, 1.0f, stream_);
+            hipk::launchFillF32Const(L.rmsFfn, h_.dim, 1.0f, stream_);
+        }
+        emb_ = dalloc<float>((size_t)h_.vocabSize * h_.dim);
+        hipk::launchFillF32Uniform(emb_, (size_t)h_.vocabSize * h_.dim, 1.0f, cfg_.seed ^ 0xE3B, stream_);
+        rmsFinal_ = dalloc<float>(h_.dim);
+        hipk::launchFillF32Const(rmsFinal_, h_.dim, 1.0f, stream_);
+        synthMat(wcls_, p.vocab0, h_.dim, seed++);
+        DL_HIP(hipGetLastError());
+    }
+
+    // ---------------------------------------------------------------- forward schedule
+    void setInputs(int n, const int *tokens, const int *positions, const int *slots) {
+        DL_CHECK(n >= 1 && (u32)n <= cfg_.maxBatch, "batch size out of range");
+        for (int b = 0; b < n; b++) {
+            DL_CHECK(tokens[b] >= 0 && (u32)tokens[b] < h_.vocabSize, "token out of range");
+            DL_CHECK(positions[b] >= 0 && (u32)positions[b] < h_.seqLen, "position out of range");
+            DL_CHECK(slots[b] >= 0 && (u32)slots[b] < cfg_.nSlots, "slot out of range");
+        }
+        const u32 MB = cfg_.maxBatch;
+        // keep the pinned staging buffer stable while a previous copy may still read it
+        DL_HIP(hipStreamSynchronize(stream_));
+        std::memcpy(hIn_, tokens, n * sizeof(int));
+        std::memcpy(hIn_ + MB, positions, n * sizeof(int));
+        std::memcpy(hIn_ + 2 * MB, slots, n * sizeof(int));
+        DL_HIP(hipMemcpyAsync(dTok_, hIn_, n * sizeof(int), hipMemcpyHostToDevice, stream_));
+        DL_HIP(hipMemcpyAsync(dPos_, hIn_ + MB, n * sizeof(int), hipMemcpyHostToDevice, stream_));
+        DL_HIP(hipMemcpyAsync(dSlot_, hIn_ + 2 * MB, n * sizeof(int), hipMemcpyHostToDevice, stream_));
+    }
+
+    void runGraph(int n, GraphKind kind) {
+        if (!cfg_.useGraphs) {
+            enqueueForward(n, kind);
+            return;
+        }
+        const int key = n * 4 + (int)kind;
+        auto it = graphs_.find(key);
+        if (it == graphs_.end()) {
+            hipGraph_t g;
+            DL_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+            enqueueForward(n, kind);
+            DL_HIP(hipStreamEndCapture(stream_, &g));
+            hipGraphExec_t ge;
+            DL_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+            DL_HIP(hipGraphDestroy(g));
+            it = graphs_.emplace(key, ge).first;
+        }
+        DL_HIP(hipGraphLaunch(it->second, stream_));
+    }
+
+    // timing hook for profileForward (eager only)
+    struct ProfScope {
+        HipEngineImpl *e;
+        std::string name;
+        hipEvent_t a = nullptr, b = nullptr;
+        ProfScope(HipEngineImpl *e_, const char *n_) : e(e_), name(n_) {
+            if (e->profile_) {
+                (void)hipEventCreate(&a);
+                (void)hipEventCreate(&b);
+                (void)hipEventRecord(a, e->stream_);
+            }
+        }
+        ~ProfScope() {
+            if (e->profile_) {
+                (void)hipEventRecord(b, e->stream_);
+                e->profTimes_.push_back({name, {a, b}});
+            }
+        }
+    };
+
+    int batchChunk(int n) const {
+        // largest batch chunk (1/2/4) whose LDS footprint stays <= 64 KiB for this input width
+        int bc = 4;
+        while (bc > 1) {
+            const int L = hipk::gemvLanesPerRow(n, q40_);
+            if (hipk::gemvLdsBytes(n, bc, q40_, (256 / L) * 8) <= 64 * 1024) break;
+            bc >>= 1;
+        }
+        return bc;
+    }
+
+    int passesFor(const DevMat &m) const {
+        const int L = hipk::gemvLanesPerRow(m.n, q40_);
+        const int rp = 256 / L;
+        const int grid0 = (m.rows + rp - 1) / rp;
+        int passes = grid0 / 1024;
+        if (passes < 1) passes = 1;
+        if (passes > 8) passes = 8;
+        return passes;
+    }
+
+    // Launch a GEMV over all n rows, in batch chunks of <= 4.
+    void gemv(const DevMat &m, int n, int pro, int epi, const float *in, int ldIn, const float *add, float *xNext,
+              const float *normW, float *out, int ldOut, const DevLayer *L) {
+        const int bcMax = batchChunk(m.n);
+        for (int c0 = 0; c0 < n;) {
+            int bc = n - c0;
+            if (bc > bcMax) bc = bcMax;
+            if (bc == 3) bc = 2;
+            hipk::GemvArgs a;
+            a.qs = m.qs;
+            a.wd = m.d;
+            a.wf = m.f;
+            a.rows = m.rows;
+            a.n = m.n;
+            a.passes = passesFor(m);
+            a.in = in + (size_t)c0 * ldIn;
+            a.ldIn = ldIn;
+            a.addIn = add ? add + (size_t)c0 * ldIn : nullptr;
+            a.xNext = xNext ? xNext + (size_t)c0 * ldIn : nullptr;
+            a.normW = normW;
+            a.eps = h_.normEpsilon;
+            a.out = out + (size_t)c0 * ldOut;
+            a.ldOut = ldOut;
+            a.act = h_.hiddenAct == HiddenAct::GELU ? 0 : 1;
+            if (L) {
+                a.q0 = plan_.q0;
+                a.kv0 = plan_.kv0;
+                a.hs = plan_.headSize;
+                a.seqLen = h_.seqLen;
+                a.rope = dRope_;
+                a.pos = dPos_ + c0;
+                a.slot = dSlot_ + c0;
+                a.kcache = L->k;
+                a.vcache = L->v;
+                a.kvBf16 = kvBf16_ ? 1 : 0;
+            }
+            hipk::launchGemv(a, bc, pro, epi, q40_, stream_);
+            c0 += bc;
+        }
+    }
+
+    void allReduce(float *buf, size_t count) {
+        if (plan_.nRanks > 1) {
+            ProfScope ps(this, "allreduce");
+            comm_->allReduceSum(buf, count, stream_);
+        }
+    }
+
+    void enqueueForward(int n, GraphKind kind) {
+        const ShardPlan &p = plan_;
+        const int dim = h_.dim;
+        int cur = 0;
+        {
+            ProfScope ps(this, "embedding");
+            hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_);
+        }
+        for (u32 l = 0; l < h_.nLayers; l++) {
+            DevLayer &L = layers_[l];
+            const bool hasDelta = l > 0;
+            {
+                ProfScope ps(this, "gemv_qkv");
+                gemv(L.qkv, n, hipk::PRO_RESNORM, hipk::EPI_QKV, dX_[cur], dim, hasDelta ? dY_ : nullptr,
+                     hasDelta ? dX_[cur ^ 1] : nullptr, L.rmsAtt, dQ_, p.q0, &L);
+            }
+            if (hasDelta) cur ^= 1;
+            {
+                ProfScope ps(this, "attention");
+                hipk::AttnArgs a;
+                a.q = dQ_;
+                a.ldq = p.q0;
+                a.kcache = L.k;
+                a.vcache = L.v;
+                a.pos = dPos_;
+                a.slot = dSlot_;
+                a.nHeads0 = p.nHeads0;
+                a.kvMul = p.kvMul;
+                a.hs = p.headSize;
+                a.kv0 = p.kv0;
+                a.seqLen = h_.seqLen;
+                a.splitGrid = splitGrid_;
+                a.chunkMax = chunkMax_;
+                a.partO = dPartO_;
+                a.partML = dPartML_;
+                a.out = dAtt_;
+                a.ldOut = p.q0;
+                a.kvBf16 = kvBf16_ ? 1 : 0;
+                hipk::launchAttention(a, n, stream_);
+            }
+            {
+                ProfScope ps(this, "gemv_wo");
+                gemv(L.wo, n, hipk::PRO_QUANT, hipk::EPI_STORE, dAtt_, p.q0, nullptr, nullptr, nullptr, dY_, dim, nullptr);
+            }
+            allReduce(dY_, (size_t)n * dim);
+            {
+                ProfScope ps(this, "gemv_w13");
+                gemv(L.w13, n, hipk::PRO_RESNORM, hipk::EPI_ACT, dX_[cur], dim, dY_, dX_[cur ^ 1], L.rmsFfn, dH_,
+                     p.hidden0, nullptr);
+            }
+            cur ^= 1;
+            {
+                ProfScope ps(this, "gemv_w2");
+                gemv(L.w2, n, hipk::PRO_QUANT, hipk::EPI_STORE, dH_, p.hidden0, nullptr, nullptr, nullptr, dY_, dim,
+                     nullptr);
+            }
+            allReduce(dY_, (size_t)n * dim);
+        }
+        {
+            ProfScope ps(this, "gemv_logits");
+            gemv(wcls_, n, hipk::PRO_RESNORM, hipk::EPI_STORE, dX_[cur], dim, dY_, nullptr, rmsFinal_, dLogits_,
+                 p.vocab0, nullptr);
+        }
+        const float *full = dLogits_;
+        if (p.nRanks > 1) {
+            ProfScope ps(this, "allgather");
+            comm_->allGather(dLogits_, dLogitsAll_, (size_t)n * p.vocab0, stream_);
+            hipk::launchUnshardLogits(dLogitsAll_, dLogitsFull_, p.nRanks, n, p.vocab0, stream_);
+            full = dLogitsFull_;
+        }
+        if (kind != GraphKind::LOGITS) {
+            ProfScope ps(this, "argmax");
+            hipk::launchArgmax(full, h_.vocabSize, n, dIds_, stream_);
+        }
+        if (kind == GraphKind::CHAIN) {
+            // record into history at [b][pos], then feed back
+            recordHistory(n);
+            hipk::launchAdvance(dIds_, dTok_, dPos_, n, stream_);
+        }
+        DL_HIP(hipGetLastError());
+    }
+
+    void recordHistory(int n);
+
+    EngineConfig cfg_;
+    DeviceComm *comm_;
+    int dev_ = 0;
+    hipStream_t stream_ = nullptr;
+    std::unique_ptr<ModelFile> file_;
+    ModelHeader h_;
+    ShardPlan plan_;
+    bool q40_ = true, kvBf16_ = true;
+    std::vector<void *> allocs_, hostAllocs_;
+    size_t deviceBytes_ = 0;
+    std::vector<DevLayer> layers_;
+    DevMat wcls_;
+    float *emb_ = nullptr, *rmsFinal_ = nullptr;
+    int *dTok_ = nullptr, *dPos_ = nullptr, *dSlot_ = nullptr, *dIds_ = nullptr, *dHist_ = nullptr;
+    int *hIn_ = nullptr, *hIds_ = nullptr;
+    float *hLogits_ = nullptr;
+    float *dX_[2] = {nullptr, nullptr};
+    float *dY_ = nullptr, *dQ_ = nullptr, *dAtt_ = nullptr, *dH_ = nullptr, *dLogits_ = nullptr;
+    float *dLogitsAll_ = nullptr, *dLogitsFull_ = nullptr;
+    float *dPartO_ = nullptr, *dPartML_ = nullptr;
+    float2 *dRope_ = nullptr;
+    int splitGrid_ = 1, chunkMax_ = 256;
+    std::map<int, hipGraphExec_t> graphs_;
+    bool profile_ = false;
+    std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> profTimes_;
+};
+
+__global__ void recordHistoryKernel(const int *ids, const int *pos, int *hist, int seqLen, int B) {
+    const int b = threadIdx.x;
+    if (b < B) hist[(size_t)b * seqLen + pos[b]] = ids[b];
+}
+
+void HipEngineImpl::recordHistory(int n) {
+    hipLaunchKernelGGL(recordHistoryKernel, dim3(1), dim3(64), 0, stream_, dIds_, dPos_, dHist_, (int)h_.seqLen, n);
+}
+
+}  // namespace
+
+std::unique_ptr<HipEngine> makeHipEngine(const EngineConfig &cfg, DeviceComm *comm) {
+    return std::unique_ptr<HipEngine>(new HipEngineImpl(cfg, comm));
+}
+
+}  // namespace dl

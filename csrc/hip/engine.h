@@ -1,0 +1,32 @@
+// MI355X engine: one rank's shard resident in HBM, fused per-layer kernel schedule captured into
+// one hipGraph per batch size (replaces the reference's per-op executor + barrier).
+#pragma once
+
+#include <memory>
+
+#include "../runtime/backend.h"
+#include "device_comm.h"
+
+namespace dl {
+
+class HipEngine : public Backend {
+  public:
+    virtual ~HipEngine() = default;
+    // Greedy decode of `steps` tokens for one sequence entirely on device: the token produced by
+    // step i is fed to step i+1 without a host round trip (graph replay back to back).
+    // Writes the generated ids to `outTokens` (may be null). Returns device wall ms.
+    virtual double decodeGreedy(int steps, int token, int pos, int slot, int *outTokens) = 0;
+    // Same, for `nSeq` independent sequences decoded together (multi-user batch).
+    virtual double decodeGreedyBatch(int steps, int nSeq, const int *tokens, const int *pos, const int *slots,
+                                     int *outTokens) = 0;
+    virtual void synchronize() = 0;
+    virtual size_t deviceBytes() const = 0;
+    // Run one forward eagerly with a per-kernel-class timing breakdown (ms) printed to stdout.
+    virtual void profileForward(int n, const int *tokens, const int *positions, const int *slots) = 0;
+};
+
+// comm may be null (single GPU). The engine does not own comm.
+std::unique_ptr<HipEngine> makeHipEngine(const EngineConfig &cfg, DeviceComm *comm);
+int hipDeviceCount();
+
+}  // namespace dl

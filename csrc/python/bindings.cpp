@@ -1,0 +1,336 @@
+// Python bindings (pybind11) for tests, the torch oracle comparison and bench.py.
+// The hot path never goes through Python: a forward call is one C++ call that replays a hipGraph.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "../core/model_file.h"
+#include "../core/plan.h"
+#include "../core/quant.h"
+#include "../hip/engine.h"
+#include "../runtime/backend.h"
+#include "../text/tokenizer.h"
+
+namespace py = pybind11;
+using namespace dl;
+
+namespace {
+
+py::dict headerToDict(const ModelHeader &h) {
+    py::dict d;
+    d["header_size"] = h.headerSize;
+    d["file_size"] = h.fileSize;
+    d["version"] = h.version;
+    d["dim"] = h.dim;
+    d["hidden_dim"] = h.hiddenDim;
+    d["n_layers"] = h.nLayers;
+    d["n_heads"] = h.nHeads;
+    d["n_kv_heads"] = h.nKvHeads;
+    d["n_experts"] = h.nExperts;
+    d["vocab_size"] = h.vocabSize;
+    d["seq_len"] = h.seqLen;
+    d["orig_seq_len"] = h.origSeqLen;
+    d["hidden_act"] = (int)h.hiddenAct;
+    d["rope_theta"] = h.ropeTheta;
+    d["rope_type"] = (int)h.ropeType;
+    d["rope_scaling_factor"] = h.ropeScalingFactor;
+    d["rope_scaling_low_freq_factor"] = h.ropeScalingLowFreqFactor;
+    d["rope_scaling_high_freq_factor"] = h.ropeScalingHighFreqFactor;
+    d["rope_scaling_orig_max_seq_len"] = h.ropeScalingOrigMaxSeqLen;
+    d["norm_epsilon"] = h.normEpsilon;
+    d["weight_type"] = (int)h.weightType;
+    d["head_size"] = h.headSize();
+    d["kv_dim"] = h.kvDim();
+    return d;
+}
+
+ModelHeader dictToHeader(const py::dict &d) {
+    ModelHeader h;
+    h.dim = d["dim"].cast<u32>();
+    h.hiddenDim = d["hidden_dim"].cast<u32>();
+    h.nLayers = d["n_layers"].cast<u32>();
+    h.nHeads = d["n_heads"].cast<u32>();
+    h.nKvHeads = d["n_kv_heads"].cast<u32>();
+    h.vocabSize = d["vocab_size"].cast<u32>();
+    h.seqLen = d["seq_len"].cast<u32>();
+    h.origSeqLen = h.seqLen;
+    if (d.contains("rope_theta")) h.ropeTheta = d["rope_theta"].cast<float>();
+    if (d.contains("hidden_act")) h.hiddenAct = (HiddenAct)d["hidden_act"].cast<int>();
+    if (d.contains("rope_scaling_factor")) h.ropeScalingFactor = d["rope_scaling_factor"].cast<float>();
+    if (d.contains("rope_scaling_low_freq_factor"))
+        h.ropeScalingLowFreqFactor = d["rope_scaling_low_freq_factor"].cast<float>();
+    if (d.contains("rope_scaling_high_freq_factor"))
+        h.ropeScalingHighFreqFactor = d["rope_scaling_high_freq_factor"].cast<float>();
+    if (d.contains("rope_scaling_orig_max_seq_len"))
+        h.ropeScalingOrigMaxSeqLen = d["rope_scaling_orig_max_seq_len"].cast<u32>();
+    if (d.contains("rope_type")) h.ropeType = (RopeType)d["rope_type"].cast<int>();
+    h.weightType = d.contains("weight_type") ? (FloatType)d["weight_type"].cast<int>() : FloatType::Q40;
+    return h;
+}
+
+EngineConfig makeConfig(const std::string &model, const std::string &bufferType, int nThreads, u32 maxSeqLen,
+                        u32 maxBatch, u32 nSlots, int gpuIndex, bool useGraphs, bool kvBf16, py::object synthetic,
+                        u64 seed) {
+    EngineConfig c;
+    c.modelPath = model;
+    c.bufferType = parseFloatType(bufferType);
+    c.nThreads = nThreads;
+    c.maxSeqLen = maxSeqLen;
+    c.maxBatch = maxBatch;
+    c.nSlots = nSlots;
+    c.gpuIndex = gpuIndex;
+    c.useGraphs = useGraphs;
+    c.kvBf16 = kvBf16;
+    c.seed = seed;
+    if (!synthetic.is_none()) {
+        c.synthetic = true;
+        c.syntheticHeader = dictToHeader(synthetic.cast<py::dict>());
+    }
+    return c;
+}
+
+template <typename T>
+std::vector<int> toInts(const T &arr) {
+    std::vector<int> v;
+    for (auto x : arr) v.push_back(py::cast<int>(x));
+    return v;
+}
+
+py::array_t<float> runForward(Backend &b, const std::vector<int> &tokens, const std::vector<int> &positions,
+                              const std::vector<int> &slots) {
+    const int n = (int)tokens.size();
+    DL_CHECK(positions.size() == tokens.size() && slots.size() == tokens.size(), "input lengths");
+    py::array_t<float> out({n, (int)b.header().vocabSize});
+    {
+        py::gil_scoped_release rel;
+        b.forward(n, tokens.data(), positions.data(), slots.data(), out.mutable_data());
+    }
+    return out;
+}
+
+std::vector<int> runArgmax(Backend &b, const std::vector<int> &tokens, const std::vector<int> &positions,
+                           const std::vector<int> &slots) {
+    std::vector<int> out(tokens.size());
+    py::gil_scoped_release rel;
+    b.forwardArgmax((int)tokens.size(), tokens.data(), positions.data(), slots.data(), out.data());
+    return out;
+}
+
+// Keeps the device comm alive as long as the engine.
+struct PyHipEngine {
+    std::unique_ptr<DeviceComm> comm;
+    std::unique_ptr<HipEngine> engine;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+    m.doc() = "MI355X-native distributed Llama engine (native core)";
+    m.def("set_log_level", &setLogLevel);
+    m.def("hip_device_count", &hipDeviceCount);
+
+    m.def("f32_to_f16", &f32ToF16);
+    m.def("f16_to_f32", &f16ToF32);
+    m.def("quantize_q80", [](py::array_t<float, py::array::c_style | py::array::forcecast> x) {
+        const u64 n = (u64)x.size();
+        py::array_t<uint8_t> out((py::ssize_t)(n / kQBlock * kQ80BlockBytes));
+        quantizeQ80(x.data(), reinterpret_cast<BlockQ80 *>(out.mutable_data()), n);
+        return out;
+    });
+    m.def("quantize_q40", [](py::array_t<float, py::array::c_style | py::array::forcecast> x) {
+        const u64 n = (u64)x.size();
+        py::array_t<uint8_t> out((py::ssize_t)(n / kQBlock * kQ40BlockBytes));
+        quantizeQ40(x.data(), reinterpret_cast<BlockQ40 *>(out.mutable_data()), n);
+        return out;
+    });
+    m.def("dequantize_q80", [](py::array_t<uint8_t, py::array::c_style> b) {
+        const u64 n = (u64)b.size() / kQ80BlockBytes * kQBlock;
+        py::array_t<float> out((py::ssize_t)n);
+        dequantizeQ80(reinterpret_cast<const BlockQ80 *>(b.data()), out.mutable_data(), n);
+        return out;
+    });
+    m.def("dequantize_q40", [](py::array_t<uint8_t, py::array::c_style> b) {
+        const u64 n = (u64)b.size() / kQ40BlockBytes * kQBlock;
+        py::array_t<float> out((py::ssize_t)n);
+        dequantizeQ40(reinterpret_cast<const BlockQ40 *>(b.data()), out.mutable_data(), n);
+        return out;
+    });
+
+    m.def("load_header", [](const std::string &path, u32 maxSeqLen) { return headerToDict(loadModelHeader(path, maxSeqLen)); },
+          py::arg("path"), py::arg("max_seq_len") = 0);
+    m.def("tensor_table", [](const std::string &path) {
+        ModelHeader h = loadModelHeader(path);
+        py::list l;
+        for (const auto &t : buildTensorTable(h)) {
+            py::dict d;
+            d["name"] = tensorKindName(t.kind);
+            d["layer"] = t.layer;
+            d["offset"] = t.offset;
+            d["bytes"] = t.bytes;
+            d["type"] = (int)t.type;
+            d["rows"] = t.rows;
+            d["cols"] = t.cols;
+            l.append(d);
+        }
+        return l;
+    });
+    m.def("shard_plan", [](py::dict header, u32 nRanks, u32 rank) {
+        ShardPlan p = ShardPlan::make(dictToHeader(header), nRanks, rank);
+        py::dict d;
+        d["q0"] = p.q0;
+        d["kv0"] = p.kv0;
+        d["hidden0"] = p.hidden0;
+        d["vocab0"] = p.vocab0;
+        d["n_heads0"] = p.nHeads0;
+        d["n_kv_heads0"] = p.nKvHeads0;
+        d["kv_mul"] = p.kvMul;
+        return d;
+    });
+    m.def("rope_table", [](py::dict header) {
+        std::vector<float> t = buildRopeTable(dictToHeader(header));
+        return py::array_t<float>((py::ssize_t)t.size(), t.data());
+    });
+
+    py::class_<Tokenizer>(m, "Tokenizer")
+        .def(py::init<const std::string &, bool>(), py::arg("path"), py::arg("verbose") = false)
+        .def("encode",
+             [](const Tokenizer &t, const std::string &text, bool addBos, bool addSpecial) {
+                 return t.encode(text, addBos, addSpecial);
+             },
+             py::arg("text"), py::arg("add_bos") = true, py::arg("add_special_tokens") = false)
+        .def("decode",
+             [](Tokenizer &t, int token) -> py::object {
+                 std::string out;
+                 if (t.decode(token, out)) return py::bytes(out);
+                 return py::none();
+             })
+        .def("reset_decoder", &Tokenizer::resetDecoder)
+        .def("is_eos", &Tokenizer::isEos)
+        .def("piece", [](const Tokenizer &t, int id) { return py::bytes(t.piece(id)); })
+        .def_property_readonly("vocab_size", &Tokenizer::vocabSize)
+        .def_property_readonly("bos_id", &Tokenizer::bosId)
+        .def_property_readonly("eos_token_ids", &Tokenizer::eosTokenIds)
+        .def_property_readonly("chat_template", [](const Tokenizer &t) { return py::bytes(t.chatTemplate()); });
+
+    py::class_<Sampler>(m, "Sampler")
+        .def(py::init<int, float, float, u64>())
+        .def("sample",
+             [](Sampler &s, py::array_t<float, py::array::c_style | py::array::forcecast> logits) {
+                 std::vector<float> v(logits.data(), logits.data() + logits.size());
+                 return s.sample(v.data());
+             })
+        .def("set_temp", &Sampler::setTemp)
+        .def("set_seed", &Sampler::setSeed);
+
+    py::enum_<EosResult>(m, "EosResult")
+        .value("NOT_EOS", EosResult::NOT_EOS)
+        .value("MAYBE_EOS", EosResult::MAYBE_EOS)
+        .value("EOS", EosResult::EOS);
+    py::class_<EosDetector>(m, "EosDetector")
+        .def(py::init<std::vector<int>, std::vector<std::string>, int, int>())
+        .def("append",
+             [](EosDetector &d, int token, py::object piece) {
+                 if (piece.is_none()) return d.append(token, nullptr);
+                 std::string s = piece.cast<std::string>();
+                 return d.append(token, s.c_str());
+             })
+        .def("get_delta",
+             [](EosDetector &d) -> py::object {
+                 std::string out;
+                 if (d.getDelta(out)) return py::bytes(out);
+                 return py::none();
+             })
+        .def("reset", &EosDetector::reset);
+
+    py::class_<ChatTemplateGenerator>(m, "ChatTemplateGenerator")
+        .def(py::init([](const std::string &type, const std::string &tmpl, const std::string &eos) {
+                 return new ChatTemplateGenerator(type.empty() ? ChatTemplateType::UNKNOWN : parseChatTemplateType(type),
+                                                  tmpl, eos, false);
+             }),
+             py::arg("type"), py::arg("template"), py::arg("eos"))
+        .def_property_readonly("type", [](const ChatTemplateGenerator &g) { return chatTemplateTypeName(g.type()); })
+        .def("generate", [](const ChatTemplateGenerator &g, const std::vector<std::pair<std::string, std::string>> &items,
+                            bool appendGenerationPrompt) {
+            std::vector<ChatItem> its;
+            for (auto &p : items) its.push_back(ChatItem{p.first, p.second});
+            GeneratedChat c = g.generate(its, appendGenerationPrompt);
+            return py::make_tuple(py::bytes(c.content), py::bytes(c.publicPrompt));
+        });
+
+    py::class_<Backend>(m, "Backend")
+        .def_property_readonly("header", [](const Backend &b) { return headerToDict(b.header()); })
+        .def_property_readonly("name", &Backend::name)
+        .def("forward", [](Backend &b, std::vector<int> t, std::vector<int> p, std::vector<int> s) { return runForward(b, t, p, s); },
+             py::arg("tokens"), py::arg("positions"), py::arg("slots"))
+        .def("forward_argmax", [](Backend &b, std::vector<int> t, std::vector<int> p, std::vector<int> s) { return runArgmax(b, t, p, s); },
+             py::arg("tokens"), py::arg("positions"), py::arg("slots"))
+        .def("last_stats", [](const Backend &b) {
+            ForwardStats s = b.lastStats();
+            return py::make_tuple(s.computeMs, s.syncMs, s.sentBytes, s.recvBytes);
+        });
+
+    m.def("cpu_backend",
+          [](const std::string &model, const std::string &bufferType, int nThreads, u32 maxSeqLen, u32 maxBatch,
+             u32 nSlots) {
+              EngineConfig c = makeConfig(model, bufferType, nThreads, maxSeqLen, maxBatch, nSlots, -1, false, false,
+                                          py::none(), 1);
+              return makeCpuBackend(c, nullptr);
+          },
+          py::arg("model"), py::arg("buffer_type") = "q80", py::arg("nthreads") = 1, py::arg("max_seq_len") = 0,
+          py::arg("max_batch") = 32, py::arg("n_slots") = 1);
+
+    m.def("rccl_unique_id", []() {
+        auto v = rcclGetUniqueId();
+        return py::bytes(std::string(v.begin(), v.end()));
+    });
+
+    py::class_<PyHipEngine>(m, "HipEngine")
+        .def(py::init([](const std::string &model, const std::string &bufferType, u32 maxSeqLen, u32 maxBatch,
+                         u32 nSlots, int gpuIndex, bool useGraphs, bool kvBf16, py::object synthetic, u64 seed,
+                         int rank, int world, py::object uid) {
+                 EngineConfig c = makeConfig(model, bufferType, 1, maxSeqLen, maxBatch, nSlots, gpuIndex, useGraphs,
+                                             kvBf16, synthetic, seed);
+                 auto *e = new PyHipEngine();
+                 py::gil_scoped_release rel;
+                 if (world > 1) {
+                     std::string s;
+                     {
+                         py::gil_scoped_acquire acq;
+                         s = uid.cast<std::string>();
+                     }
+                     hipSetDevice(gpuIndex >= 0 ? gpuIndex : 0);
+                     e->comm = makeRcclComm(std::vector<unsigned char>(s.begin(), s.end()), rank, world);
+                 }
+                 e->engine = makeHipEngine(c, e->comm.get());
+                 return e;
+             }),
+             py::arg("model") = "", py::arg("buffer_type") = "q80", py::arg("max_seq_len") = 0,
+             py::arg("max_batch") = 32, py::arg("n_slots") = 1, py::arg("gpu_index") = 0, py::arg("use_graphs") = true,
+             py::arg("kv_bf16") = true, py::arg("synthetic") = py::none(), py::arg("seed") = 1234, py::arg("rank") = 0,
+             py::arg("world") = 1, py::arg("uid") = py::none())
+        .def_property_readonly("header", [](const PyHipEngine &e) { return headerToDict(e.engine->header()); })
+        .def_property_readonly("device_bytes", [](const PyHipEngine &e) { return e.engine->deviceBytes(); })
+        .def("forward", [](PyHipEngine &e, std::vector<int> t, std::vector<int> p, std::vector<int> s) { return runForward(*e.engine, t, p, s); },
+             py::arg("tokens"), py::arg("positions"), py::arg("slots"))
+        .def("forward_argmax", [](PyHipEngine &e, std::vector<int> t, std::vector<int> p, std::vector<int> s) { return runArgmax(*e.engine, t, p, s); },
+             py::arg("tokens"), py::arg("positions"), py::arg("slots"))
+        .def("decode_greedy",
+             [](PyHipEngine &e, int steps, std::vector<int> tokens, std::vector<int> pos, std::vector<int> slots) {
+                 const int nSeq = (int)tokens.size();
+                 std::vector<int> out((size_t)steps * nSeq);
+                 double ms;
+                 {
+                     py::gil_scoped_release rel;
+                     ms = e.engine->decodeGreedyBatch(steps, nSeq, tokens.data(), pos.data(), slots.data(), out.data());
+                 }
+                 return py::make_tuple(ms, out);
+             },
+             py::arg("steps"), py::arg("tokens"), py::arg("positions"), py::arg("slots"))
+        .def("profile_forward", [](PyHipEngine &e, std::vector<int> t, std::vector<int> p, std::vector<int> s) {
+            e.engine->profileForward((int)t.size(), t.data(), p.data(), s.data());
+        })
+        .def("synchronize", [](PyHipEngine &e) { e.engine->synchronize(); });
+
+}

@@ -1,0 +1,81 @@
+// Backend interface shared by the CPU reference backend and the HIP (MI355X) engine.
+//
+// One Backend instance = one rank's shard of the model. A forward call processes `n` rows;
+// every row carries its own token, position and KV slot, so rows of different requests
+// (multi-user batching) and rows of one prompt chunk (prefill) can be mixed in one call.
+// This replaces the reference's pipes + executor step list (nn-executor.cpp:124-187,
+// app.cpp:169-209) with a fixed per-layer schedule.
+#pragma once
+
+#include <memory>
+#include <string>
+
+#include "../core/model_file.h"
+#include "../core/plan.h"
+
+namespace dl {
+
+struct EngineConfig {
+    std::string modelPath;          // .m file (ignored when synthetic)
+    u32 maxSeqLen = 0;              // clamp of header seqLen (0 = model's)
+    u32 maxBatch = 32;              // max rows per forward (reference nBatches, app.cpp:37)
+    u32 nSlots = 1;                 // independent KV-cache slots (concurrent sequences)
+    FloatType bufferType = FloatType::F32;  // activation quantization: Q80 or F32
+    int nThreads = 1;               // CPU backend threads
+    int gpuIndex = -1;              // HIP device ordinal (-1 = CPU backend)
+    bool useGraphs = true;          // capture per-batch-size hipGraphs
+    bool kvBf16 = true;             // GPU KV cache dtype (bf16 default, f32 when false)
+    bool synthetic = false;         // random-init weights of the header's shape (no file)
+    ModelHeader syntheticHeader;    // used when synthetic
+    u64 seed = 1234;                // synthetic weight seed
+};
+
+struct ForwardStats {
+    double computeMs = 0;
+    double syncMs = 0;
+    u64 sentBytes = 0;
+    u64 recvBytes = 0;
+};
+
+class Backend {
+  public:
+    virtual ~Backend() = default;
+    virtual const ModelHeader &header() const = 0;
+    virtual const ShardPlan &plan() const = 0;
+    // logits (root only, may be null): [n][vocabSize] full vocabulary.
+    virtual void forward(int n, const int *tokens, const int *positions, const int *slots, float *logits) = 0;
+    // Greedy decode helper: out[i] = argmax over the full vocabulary (every rank gets it).
+    virtual void forwardArgmax(int n, const int *tokens, const int *positions, const int *slots, int *out) = 0;
+    virtual ForwardStats lastStats() const { return stats_; }
+    virtual std::string name() const = 0;
+
+  protected:
+    ForwardStats stats_;
+};
+
+// Host data plane used by the CPU backend for tensor parallelism.
+class HostComm {
+  public:
+    virtual ~HostComm() = default;
+    virtual int rank() const = 0;
+    virtual int size() const = 0;
+    virtual void allReduceSum(float *data, u64 n) = 0;
+    // every rank contributes nLocal floats; root receives size()*nLocal floats in rank order
+    virtual void gatherToRoot(const float *local, u64 nLocal, float *out) = 0;
+    virtual void stats(u64 &sent, u64 &recv) const {
+        sent = 0;
+        recv = 0;
+    }
+};
+
+class LocalComm : public HostComm {
+  public:
+    int rank() const override { return 0; }
+    int size() const override { return 1; }
+    void allReduceSum(float *, u64) override {}
+    void gatherToRoot(const float *local, u64 nLocal, float *out) override;
+};
+
+std::unique_ptr<Backend> makeCpuBackend(const EngineConfig &cfg, HostComm *comm);
+
+}  // namespace dl

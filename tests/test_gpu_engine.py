@@ -1,0 +1,118 @@
+"""HIP engine (gfx950 kernels) vs the CPU reference backend / torch oracle."""
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def medium(tmp_path_factory):
+    # wide enough to exercise the 32- and 64-lane GEMV row groups (n/32 >= 192 / 384)
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    d = str(tmp_path_factory.mktemp("medium"))
+    m, t, spec = make_test_assets(d, "tiny", FloatType.Q40, seq_len=512, seed=3, dim=1024, hidden_dim=12288,
+                                  n_heads=8, n_kv_heads=2, n_layers=2, vocab_size=2048)
+    return m
+
+
+def _rel(a, b):
+    return float(np.abs(a - b).max() / np.abs(b).max())
+
+
+def _seq(be, tokens, slot=0):
+    return np.stack([be.forward([t], [p], [slot])[0] for p, t in enumerate(tokens)])
+
+
+@pytest.mark.parametrize("kind,kv_bf16", [("q40", True), ("q40", False), ("f32", False), ("f32", True)])
+def test_engine_matches_cpu(C, assets, kind, kv_bf16):
+    buf = "q80" if kind == "q40" else "f32"
+    cpu = C.cpu_backend(assets[kind], buf, 4)
+    gpu = C.HipEngine(assets[kind], buf, kv_bf16=kv_bf16, max_batch=8)
+    tokens = [3, 17, 101, 7, 250, 9, 44, 300, 5, 6]
+    ref = _seq(cpu, tokens)
+    got = _seq(gpu, tokens)
+    tol = 3e-2 if kind == "q40" else (2e-2 if kv_bf16 else 1e-4)
+    assert _rel(got, ref) < tol
+    assert (got.argmax(-1) == ref.argmax(-1)).mean() >= 0.8
+
+
+def test_engine_medium_matches_cpu(C, medium):
+    cpu = C.cpu_backend(medium, "q80", 8)
+    gpu = C.HipEngine(medium, "q80", kv_bf16=False, max_batch=8)
+    tokens = [1, 2, 3, 500, 1000, 2000, 7]
+    assert _rel(_seq(gpu, tokens), _seq(cpu, tokens)) < 3e-2
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_engine_batched_prefill(C, assets, graphs):
+    """A prefill chunk of 7 rows (chunks 4+2+1 inside the GEMVs) == 7 sequential decodes."""
+    a = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=8, use_graphs=graphs)
+    b = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=8, use_graphs=graphs)
+    tokens = [9, 8, 7, 6, 5, 4, 3]
+    seq = _seq(a, tokens)
+    bat = b.forward(tokens, list(range(7)), [0] * 7)
+    assert _rel(bat, seq) < 1e-4
+
+
+def test_engine_slots_independent(C, assets):
+    g = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=4, n_slots=3)
+    x, y = [11, 12, 13, 14], [200, 201, 202, 203]
+    for p in range(4):
+        both = g.forward([x[p], y[p]], [p, p], [2, 0])
+    r1 = C.HipEngine(assets["q40"], "q80", kv_bf16=False)
+    r2 = C.HipEngine(assets["q40"], "q80", kv_bf16=False)
+    assert _rel(both[0], _seq(r1, x)[-1]) < 1e-4
+    assert _rel(both[1], _seq(r2, y)[-1]) < 1e-4
+
+
+def test_decode_greedy_chain_matches_stepwise(C, assets):
+    g1 = C.HipEngine(assets["q40"], "q80", kv_bf16=True)
+    g2 = C.HipEngine(assets["q40"], "q80", kv_bf16=True)
+    ms, chain = g1.decode_greedy(20, [42], [0], [0])
+    tok, step = 42, []
+    for p in range(20):
+        tok = g2.forward_argmax([tok], [p], [0])[0]
+        step.append(tok)
+    assert chain == step
+    assert ms > 0
+
+
+def test_argmax_matches_logits(C, assets):
+    g = C.HipEngine(assets["q40"], "q80")
+    lg = g.forward([1, 2, 3], [0, 1, 2], [0, 0, 0])
+    g2 = C.HipEngine(assets["q40"], "q80")
+    ids = g2.forward_argmax([1, 2, 3], [0, 1, 2], [0, 0, 0])
+    assert list(lg.argmax(-1)) == ids
+
+
+def test_long_context_split_attention(C, tmp_path):
+    """Positions beyond one 256-key chunk exercise the split-K attention + combine path."""
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    m, t, spec = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=1100, seed=5, n_layers=1)
+    cpu = C.cpu_backend(m, "q80", 8)
+    gpu = C.HipEngine(m, "q80", kv_bf16=False, max_batch=32)
+    rng = np.random.default_rng(0)
+    toks = rng.integers(0, spec.vocab_size, 1040).tolist()
+    # prefill in chunks of 32 rows, then compare the last rows
+    for s in range(0, 1024, 32):
+        c = cpu.forward(toks[s:s + 32], list(range(s, s + 32)), [0] * 32)
+        g = gpu.forward(toks[s:s + 32], list(range(s, s + 32)), [0] * 32)
+    assert _rel(g, c) < 3e-2
+    c = cpu.forward([toks[1024]], [1024], [0])
+    g = gpu.forward([toks[1024]], [1024], [0])
+    assert _rel(g, c) < 3e-2
+
+
+def test_synthetic_8b_shape_smoke(C):
+    """Random-init Llama-3.1-8B shapes on device; a few greedy steps must run and be finite."""
+    h = dict(dim=4096, hidden_dim=14336, n_layers=2, n_heads=32, n_kv_heads=8, vocab_size=128256, seq_len=256,
+             rope_theta=500000, weight_type=2)
+    g = C.HipEngine("", "q80", synthetic=h, max_seq_len=256)
+    lg = g.forward([1], [0], [0])
+    assert np.isfinite(lg).all() and lg.std() > 0
+    ms, toks = g.decode_greedy(8, [1], [1], [0])
+    assert len(toks) == 8 and all(0 <= t < 128256 for t in toks)
