@@ -1,2 +1,212 @@
+// `dllama inference | chat | worker` — CLI parity with the reference (src/dllama.cpp:11-239).
+//
+// inference: chunked prompt evaluation (<= --max-batch rows per forward), then decoding with
+//            per-token "🔷️ Eval" / "🔶 Pred" lines and the Evaluation/Prediction summary the
+//            benchmark harness parses (dllama.cpp:57-113).
+// chat:      interactive chat with template + stop-string detection (dllama.cpp:130-214).
+// worker:    serve a root (app.cpp:405-463).
+// Deliberate fix: the first decoded position is fed the LAST prompt token (the reference feeds
+// inputTokens[pos + 1], one past the prompt end, dllama.cpp:53 and :179).
 #include <cstdio>
-int main() { std::printf("not yet implemented\n"); return 1; }
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "../runtime/app.h"
+
+using namespace dl;
+
+static void printStatsLine(const char *kind, double ms, const ForwardStats &s, const std::string &tail) {
+    std::printf("%s%5u ms Sync%5u ms | Sent%6llu kB Recv%6llu kB | %s\n", kind, (unsigned)(ms - s.syncMs),
+                (unsigned)s.syncMs, (unsigned long long)(s.sentBytes / 1024), (unsigned long long)(s.recvBytes / 1024),
+                tail.c_str());
+}
+
+static int sampleOne(InferenceSession &sess, int token, int pos, std::vector<float> &logits, double &ms) {
+    Timer t;
+    const int slot = 0;
+    int next;
+    if (sess.sampler().temperature() == 0.0f) {
+        sess.forwardArgmax(1, &token, &pos, &slot, &next);
+    } else {
+        logits.resize(sess.header().vocabSize);
+        sess.forward(1, &token, &pos, &slot, logits.data());
+        next = sess.sampler().sample(logits.data());
+    }
+    ms = t.elapsedMs();
+    return next;
+}
+
+static void evalPrompt(InferenceSession &sess, const std::vector<int> &tokens, int startIndex, int &pos, int endPos,
+                       bool print, double *totalMs) {
+    const int nb = sess.maxBatch();
+    std::vector<int> positions, slots;
+    int i = startIndex;
+    while (pos < endPos) {
+        const int bs = std::min(nb, endPos - pos);
+        positions.resize(bs);
+        slots.assign(bs, 0);
+        for (int j = 0; j < bs; j++) positions[j] = pos + j;
+        Timer t;
+        std::vector<int> ids(bs);
+        sess.forwardArgmax(bs, &tokens[i], positions.data(), slots.data(), ids.data());
+        const double ms = t.elapsedMs();
+        if (print) {
+            char tail[32];
+            std::snprintf(tail, sizeof(tail), "(%d tokens)", bs);
+            printStatsLine("🔷️ Eval", ms, sess.lastStats(), tail);
+        }
+        if (totalMs) *totalMs += ms;
+        pos += bs;
+        i += bs;
+    }
+}
+
+static void inference(InferenceSession &sess, const AppArgs &args) {
+    if (args.prompt.empty()) throw Error("Prompt is required");
+    if (args.steps == 0) throw Error("Number of steps is required");
+    Tokenizer &tok = sess.tokenizer();
+    std::vector<int> input = tok.encode(args.prompt, true, false);
+    const int nInput = (int)input.size();
+    const u32 seqLen = sess.header().seqLen;
+    if ((u32)nInput > seqLen) throw Error("The number of prompt tokens is greater than the sequence length");
+    if (nInput > args.steps) throw Error("The number of prompt tokens is greater than the number of steps");
+    std::printf("%s\n", args.prompt.c_str());
+
+    int pos = 0;
+    double evalMs = 0, predMs = 0;
+    evalPrompt(sess, input, 0, pos, nInput - 1, true, &evalMs);
+    std::fflush(stdout);
+
+    int token = input[nInput - 1];
+    tok.resetDecoder();
+    const int maxPos = (int)std::min<u32>(seqLen, (u32)args.steps);
+    std::vector<float> logits;
+    std::string piece;
+    for (; pos < maxPos; pos++) {
+        double ms;
+        token = sampleOne(sess, token, pos, logits, ms);
+        const bool has = tok.decode(token, piece);
+        printStatsLine("🔶 Pred", ms, sess.lastStats(), has ? piece : std::string("~"));
+        std::fflush(stdout);
+        predMs += ms;
+    }
+    const int nEval = nInput - 1;
+    const int nPred = pos - nEval;
+    std::printf("\n");
+    std::printf("Evaluation\n");
+    std::printf("   nBatches: %d\n", sess.maxBatch());
+    std::printf("    nTokens: %d\n", nEval);
+    std::printf("   tokens/s: %3.2f (%3.2f ms/tok)\n", nEval > 0 ? nEval * 1000.0 / evalMs : 0.0,
+                nEval > 0 ? evalMs / nEval : 0.0);
+    std::printf("Prediction\n");
+    std::printf("    nTokens: %d\n", nPred);
+    std::printf("   tokens/s: %3.2f (%3.2f ms/tok)\n", nPred > 0 ? nPred * 1000.0 / predMs : 0.0,
+                nPred > 0 ? predMs / nPred : 0.0);
+}
+
+static bool readLine(const char *guide, std::string &out) {
+    std::printf("%s", guide);
+    std::fflush(stdout);
+    if (!std::getline(std::cin, out)) return false;
+    return true;
+}
+
+static void chat(InferenceSession &sess, const AppArgs &args) {
+    Tokenizer &tok = sess.tokenizer();
+    const u32 seqLen = sess.header().seqLen;
+    ChatStops stops(tok);
+    if (stops.stops.empty()) throw Error("The tokenizer has no EOS tokens");
+    ChatTemplateGenerator gen(args.chatTemplate, tok.chatTemplate(), stops.stops[0]);
+    EosDetector eos(tok.eosTokenIds(), stops.stops, (int)stops.maxStopLength, (int)stops.maxStopLength);
+
+    std::string line;
+    std::vector<ChatItem> delta;
+    if (!readLine("💻 System prompt (optional): ", line)) return;
+    if (!line.empty()) delta.push_back(ChatItem{"system", line});
+
+    int pos = 0;
+    std::vector<float> logits;
+    std::string piece, out;
+    do {
+        do {
+            if (!readLine("\n👱 User\n> ", line)) {
+                std::printf("\n");
+                return;
+            }
+        } while (line.empty());
+        delta.push_back(ChatItem{"user", line});
+        GeneratedChat prompt = gen.generate(delta, true);
+        std::vector<int> input = tok.encode(prompt.content, pos == 0, true);
+        const int endPos = (int)std::min<u32>(seqLen, (u32)(pos + (int)input.size() - 1));
+        evalPrompt(sess, input, 0, pos, endPos, false, nullptr);
+        int token = input[input.size() - 1];
+        tok.resetDecoder();
+        std::printf("\n🤖 Assistant\n");
+        if (!prompt.publicPrompt.empty()) std::printf("%s", prompt.publicPrompt.c_str());
+        while ((u32)pos < seqLen) {
+            double ms;
+            token = sampleOne(sess, token, pos, logits, ms);
+            const bool has = tok.decode(token, piece);
+            const EosResult r = eos.append(token, has ? piece.c_str() : nullptr);
+            if (r == EosResult::NOT_EOS || r == EosResult::EOS) {
+                if (eos.getDelta(out)) {
+                    std::printf("%s", out.c_str());
+                    std::fflush(stdout);
+                }
+                eos.reset();
+            }
+            pos++;
+            if (r == EosResult::EOS) break;
+        }
+        delta.clear();
+    } while ((u32)pos < seqLen);
+    std::printf("(end of context)\n");
+}
+
+static void usage() {
+    std::fprintf(stderr,
+                 "Usage: dllama {inference|chat|worker} {--model <path>} {--tokenizer <path>} [options]\n"
+                 "  --prompt <p> --steps <n>            (inference)\n"
+                 "  --buffer-float-type {f32|f16|q40|q80}\n"
+                 "  --workers <host:port> ...           (root of a tensor-parallel group)\n"
+                 "  --port <p>                          (worker)\n"
+                 "  --nthreads <n>                      (CPU backend threads)\n"
+                 "  --gpu-index <i>                     (MI355X device ordinal; -1 = CPU backend)\n"
+                 "  --temperature <t> --topp <p> --seed <s>\n"
+                 "  --chat-template {llama2|llama3|deepSeek3}\n"
+                 "  --max-seq-len <n> --max-batch <n> --slots <n>\n"
+                 "  --kv-dtype {bf16|f32} --graph {0|1} --log-level {0|1|2}\n"
+                 "  --synthetic {llama3_2_1b|llama3_1_8b|llama3_3_70b|llama3_1_405b}  (random-init weights)\n"
+                 "  --net-turbo {0|1} --gpu-segments <a:b>  (accepted for compatibility)\n");
+}
+
+int main(int argc, char **argv) {
+    try {
+        AppArgs args = AppArgs::parse(argc, argv, true);
+        if (args.help || args.mode.empty()) {
+            usage();
+            return args.help ? 0 : 1;
+        }
+        if (args.mode == "worker") {
+            runWorker(args);
+            return 0;
+        }
+        if (args.mode != "inference" && args.mode != "chat") {
+            usage();
+            return 1;
+        }
+        InferenceSession sess(args, args.slots > 0 ? args.slots : 1);
+        if (args.mode == "inference")
+            inference(sess, args);
+        else
+            chat(sess, args);
+        sess.finish();
+    } catch (const std::exception &e) {
+        std::printf("🚨 Critical error: %s\n", e.what());
+        std::fflush(stdout);
+        return 1;
+    }
+    return 0;
+}

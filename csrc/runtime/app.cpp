@@ -1,0 +1,290 @@
+#include "app.h"
+
+#include <cstdio>
+#include <cstring>
+#include <ctime>
+
+#include "../hip/engine.h"
+
+namespace dl {
+
+AppArgs AppArgs::parse(int argc, char **argv, bool requireMode) {
+    AppArgs a;
+    a.seed = (u64)std::time(nullptr);
+    int i = 1;
+    if (requireMode && argc > 1) {
+        a.mode = argv[1];
+        i++;
+    }
+    for (int x = 0; x < argc; x++) {
+        if (!std::strcmp(argv[x], "--usage") || !std::strcmp(argv[x], "--help") || !std::strcmp(argv[x], "-h")) {
+            a.help = true;
+            return a;
+        }
+    }
+    for (; i + 1 < argc; i += 2) {
+        const std::string name = argv[i];
+        const char *value = argv[i + 1];
+        if (name == "--model") a.modelPath = value;
+        else if (name == "--tokenizer") a.tokenizerPath = value;
+        else if (name == "--prompt") a.prompt = value;
+        else if (name == "--buffer-float-type") a.bufferType = parseFloatType(value);
+        else if (name == "--workers") {
+            int j = i + 1;
+            for (; j < argc && argv[j][0] != '-'; j++) {
+                const char *v = argv[j];
+                const char *sep = std::strchr(v, ':');
+                if (!sep) throw Error(std::string("Invalid worker address: ") + v);
+                a.workerHosts.emplace_back(v, sep - v);
+                a.workerPorts.push_back(std::atoi(sep + 1));
+            }
+            i = j - 2;
+        } else if (name == "--port") a.port = std::atoi(value);
+        else if (name == "--nthreads") a.nThreads = std::atoi(value);
+        else if (name == "--steps") a.steps = std::atoi(value);
+        else if (name == "--temperature") a.temperature = (float)std::atof(value);
+        else if (name == "--topp") a.topp = (float)std::atof(value);
+        else if (name == "--seed") a.seed = std::strtoull(value, nullptr, 10);
+        else if (name == "--chat-template") a.chatTemplate = parseChatTemplateType(value);
+        else if (name == "--max-seq-len") a.maxSeqLen = (u32)std::atoi(value);
+        else if (name == "--gpu-index") a.gpuIndex = std::atoi(value);
+        else if (name == "--gpu-segments") {
+            const char *sep = std::strchr(value, ':');
+            if (!sep) throw Error("GPU segments expected in the format <from>:<to>");
+            a.gpuSegmentFrom = std::atoi(value);
+            a.gpuSegmentTo = std::atoi(sep + 1);
+        } else if (name == "--net-turbo") a.netTurbo = std::atoi(value) == 1;
+        else if (name == "--max-batch") a.nBatches = std::atoi(value);
+        else if (name == "--slots") a.slots = std::atoi(value);
+        else if (name == "--kv-dtype") {
+            const std::string v = value;
+            if (v == "bf16") a.kvBf16 = true;
+            else if (v == "f32") a.kvBf16 = false;
+            else throw Error("Invalid --kv-dtype (bf16|f32): " + v);
+        } else if (name == "--graph") a.graphs = std::atoi(value) != 0;
+        else if (name == "--log-level") a.logLevel = std::atoi(value);
+        else if (name == "--synthetic") a.synthetic = value;
+        else throw Error("Unknown option: " + name);
+    }
+    setLogLevel(a.logLevel);
+    return a;
+}
+
+ModelHeader syntheticHeader(const std::string &name, u32 seqLen) {
+    ModelHeader h;
+    h.weightType = FloatType::Q40;
+    h.vocabSize = 128256;
+    h.nKvHeads = 8;
+    h.ropeTheta = 500000.f;
+    h.ropeType = RopeType::LLAMA3_1;
+    h.ropeScalingFactor = 8.f;
+    h.ropeScalingLowFreqFactor = 1.f;
+    h.ropeScalingHighFreqFactor = 4.f;
+    h.ropeScalingOrigMaxSeqLen = 8192;
+    if (name == "llama3_2_1b") { h.dim = 2048; h.hiddenDim = 8192; h.nLayers = 16; h.nHeads = 32; }
+    else if (name == "llama3_2_3b") { h.dim = 3072; h.hiddenDim = 8192; h.nLayers = 28; h.nHeads = 24; }
+    else if (name == "llama3_1_8b") { h.dim = 4096; h.hiddenDim = 14336; h.nLayers = 32; h.nHeads = 32; }
+    else if (name == "llama3_3_70b") { h.dim = 8192; h.hiddenDim = 28672; h.nLayers = 80; h.nHeads = 64; }
+    else if (name == "llama3_1_405b") { h.dim = 16384; h.hiddenDim = 53248; h.nLayers = 126; h.nHeads = 128; }
+    else throw Error("unknown synthetic model: " + name);
+    h.seqLen = seqLen > 0 ? seqLen : 8192;
+    h.origSeqLen = h.seqLen;
+    return h;
+}
+
+static EngineConfig engineConfigFrom(const AppArgs &a, int nSlots) {
+    EngineConfig c;
+    c.modelPath = a.modelPath;
+    c.maxSeqLen = a.maxSeqLen;
+    c.maxBatch = (u32)a.nBatches;
+    c.nSlots = (u32)nSlots;
+    c.bufferType = a.bufferType;
+    c.nThreads = a.nThreads;
+    c.gpuIndex = a.gpuIndex;
+    c.useGraphs = a.graphs;
+    c.kvBf16 = a.kvBf16;
+    if (!a.synthetic.empty()) {
+        c.synthetic = true;
+        c.syntheticHeader = syntheticHeader(a.synthetic, a.maxSeqLen);
+        c.bufferType = FloatType::Q80;
+    }
+    return c;
+}
+
+static std::unique_ptr<Backend> makeBackend(const EngineConfig &c, bool gpu, HostComm *hc, DeviceComm *dc) {
+    if (gpu) return std::unique_ptr<Backend>(makeHipEngine(c, dc).release());
+    return makeCpuBackend(c, hc);
+}
+
+InferenceSession::InferenceSession(const AppArgs &args, int nSlots) : args_(args), nSlots_(nSlots) {
+    maxBatch_ = args.nBatches;
+    gpu_ = args.gpuIndex >= 0 || !args.synthetic.empty();
+    AppArgs a = args;
+    if (gpu_ && a.gpuIndex < 0) a.gpuIndex = 0;
+    EngineConfig ec = engineConfigFrom(a, nSlots);
+    const int world = 1 + (int)args.workerHosts.size();
+
+    if (args.synthetic.empty()) {
+        ModelHeader h = loadModelHeader(args.modelPath, args.maxSeqLen);
+        if ((u32)world > h.nKvHeads)
+            throw Error("This version does not support more nodes than the number of KV heads in the model");
+        if (h.weightType == FloatType::Q40 && args.bufferType != FloatType::Q80)
+            throw Error("This version supports only Q40 weights with Q80 sync type");
+    }
+
+    WorkerConfig wc;
+    wc.world = (u32)world;
+    wc.gpu = gpu_;
+    wc.engine = ec;
+    if (world > 1) {
+        if (gpu_) wc.rcclUid = rcclGetUniqueId();
+        for (size_t i = 0; i < args.workerHosts.size(); i++) {
+            if (logLevel() >= 1)
+                std::printf("⭕ Connecting to worker %s:%d\n", args.workerHosts[i].c_str(), args.workerPorts[i]);
+            workers_.push_back(Socket::connectTo(args.workerHosts[i], args.workerPorts[i]));
+        }
+        for (size_t i = 0; i < workers_.size(); i++) {
+            wc.rank = (u32)(i + 1);
+            workers_[i].sendPod<u32>(kProtoMagic);
+            workers_[i].sendString(encodeWorkerConfig(wc));
+        }
+        std::vector<Socket *> peers;
+        for (auto &s : workers_) peers.push_back(&s);
+        if (gpu_) {
+            (void)hipDeviceCount();
+            devComm_ = makeRcclComm(wc.rcclUid, 0, world);
+        } else {
+            hostComm_.reset(new TcpHostComm(0, world, peers));
+        }
+        if (logLevel() >= 1) std::printf("⭕ Network is initialized (%d nodes)\n", world);
+    }
+    backend_ = makeBackend(ec, gpu_, hostComm_.get(), devComm_.get());
+    for (auto &s : workers_) {
+        const u32 ack = s.recvPod<u32>();
+        if (ack != kAck) throw NetError("worker failed to initialize: " + s.recvString());
+    }
+    if (logLevel() >= 1) printModelHeader(backend_->header());
+    if (!args.tokenizerPath.empty()) {
+        tokenizer_.reset(new Tokenizer(args.tokenizerPath, true));
+        if ((u32)tokenizer_->vocabSize() != backend_->header().vocabSize)
+            throw Error("Tokenizer vocab size does not match the model vocab size");
+    }
+    sampler_.reset(new Sampler((int)backend_->header().vocabSize, args.temperature, args.topp, args.seed));
+    for (auto &s : workers_) s.resetStats();
+}
+
+InferenceSession::~InferenceSession() {
+    try {
+        finish();
+    } catch (...) {
+    }
+}
+
+void InferenceSession::sendControl(Cmd cmd, int n, const int *tokens, const int *positions, const int *slots) {
+    if (workers_.empty()) return;
+    std::vector<int> buf(2 + 3 * (size_t)n);
+    buf[0] = (int)cmd;
+    buf[1] = n;
+    std::memcpy(&buf[2], tokens, n * sizeof(int));
+    std::memcpy(&buf[2 + n], positions, n * sizeof(int));
+    std::memcpy(&buf[2 + 2 * n], slots, n * sizeof(int));
+    for (auto &s : workers_) s.sendAll(buf.data(), buf.size() * sizeof(int));
+}
+
+void InferenceSession::forward(int n, const int *tokens, const int *positions, const int *slots, float *logits) {
+    sendControl(Cmd::FORWARD, n, tokens, positions, slots);
+    backend_->forward(n, tokens, positions, slots, logits);
+}
+
+void InferenceSession::forwardArgmax(int n, const int *tokens, const int *positions, const int *slots, int *out) {
+    sendControl(Cmd::FORWARD_ARGMAX, n, tokens, positions, slots);
+    backend_->forwardArgmax(n, tokens, positions, slots, out);
+}
+
+ForwardStats InferenceSession::lastStats() const {
+    ForwardStats s = backend_->lastStats();
+    if (!workers_.empty() && gpu_) {
+        // RCCL traffic is not visible to the sockets; report control bytes only
+        s.sentBytes = s.recvBytes = 0;
+        for (auto &w : workers_) {
+            s.sentBytes += w.sentBytes();
+            s.recvBytes += w.recvBytes();
+        }
+    }
+    return s;
+}
+
+void InferenceSession::finish() {
+    if (finished_) return;
+    finished_ = true;
+    int hdr[2] = {(int)Cmd::STOP, 0};
+    for (auto &s : workers_) {
+        try {
+            s.sendAll(hdr, sizeof(hdr));
+        } catch (...) {
+        }
+    }
+}
+
+void runWorker(const AppArgs &args) {
+    ServerSocket server(args.port);
+    while (true) {
+        if (logLevel() >= 1) std::printf("⭕ Listening on port %d...\n", args.port);
+        std::fflush(stdout);
+        Socket root = server.accept();
+        try {
+            if (root.recvPod<u32>() != kProtoMagic) throw NetError("bad magic from root");
+            WorkerConfig wc = decodeWorkerConfig(root.recvString());
+            if (logLevel() >= 1) std::printf("⭕ Root connected; rank %u of %u (%s)\n", wc.rank, wc.world, wc.gpu ? "gpu" : "cpu");
+            EngineConfig ec = wc.engine;
+            ec.nThreads = args.nThreads;
+            ec.gpuIndex = args.gpuIndex >= 0 ? args.gpuIndex : (wc.gpu ? (int)wc.rank : -1);
+            ec.useGraphs = ec.useGraphs && args.graphs;
+            std::unique_ptr<HostComm> hc;
+            std::unique_ptr<DeviceComm> dc;
+            std::unique_ptr<Backend> backend;
+            try {
+                if (wc.gpu) {
+                    (void)hipDeviceCount();
+                    dc = makeRcclComm(wc.rcclUid, (int)wc.rank, (int)wc.world);
+                } else {
+                    hc.reset(new TcpHostComm((int)wc.rank, (int)wc.world, {&root}));
+                }
+                backend = makeBackend(ec, wc.gpu, hc.get(), dc.get());
+            } catch (const std::exception &e) {
+                root.sendPod<u32>(0);
+                root.sendString(e.what());
+                throw;
+            }
+            root.sendPod<u32>(kAck);
+            if (logLevel() >= 1) std::printf("💿 Weights loaded\n");
+            std::fflush(stdout);
+            std::vector<int> buf, ids;
+            while (true) {
+                int hdr[2];
+                root.recvAll(hdr, sizeof(hdr));
+                const Cmd cmd = (Cmd)hdr[0];
+                const int n = hdr[1];
+                if (cmd == Cmd::STOP) {
+                    if (logLevel() >= 1) std::printf("🛑 Stop signal\n");
+                    break;
+                }
+                buf.resize(3 * (size_t)n);
+                root.recvAll(buf.data(), buf.size() * sizeof(int));
+                if (cmd == Cmd::FORWARD) {
+                    backend->forward(n, &buf[0], &buf[n], &buf[2 * n], nullptr);
+                } else if (cmd == Cmd::FORWARD_ARGMAX) {
+                    ids.resize(n);
+                    backend->forwardArgmax(n, &buf[0], &buf[n], &buf[2 * n], ids.data());
+                }
+            }
+        } catch (const NetError &e) {
+            std::printf("Network exception: %s\n", e.what());
+        } catch (const std::exception &e) {
+            std::printf("🚨 Worker error: %s\n", e.what());
+        }
+        std::fflush(stdout);
+    }
+}
+
+}  // namespace dl

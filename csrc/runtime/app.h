@@ -1,0 +1,88 @@
+// Application runtime shared by `dllama` and `dllama-api`.
+//
+// CLI parity with the reference (src/app.cpp:33-136; flag table SURVEY §5.6): every reference
+// flag is accepted with the same name and default; MI355X additions: --tp-gpus / --max-batch /
+// --slots / --kv-dtype / --graph / --log-level / --synthetic.
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../net/tcp.h"
+#include "../text/tokenizer.h"
+#include "backend.h"
+
+namespace dl {
+
+struct AppArgs {
+    bool help = false;
+    std::string mode;
+    std::string modelPath, tokenizerPath, prompt;
+    FloatType bufferType = FloatType::F32;
+    std::vector<std::string> workerHosts;
+    std::vector<int> workerPorts;
+    int port = 9990;
+    int nThreads = 1;
+    int nBatches = 32;  // max rows per forward (reference constant, now --max-batch)
+    int steps = 0;
+    float temperature = 0.8f;
+    float topp = 0.9f;
+    u64 seed = 0;
+    ChatTemplateType chatTemplate = ChatTemplateType::UNKNOWN;
+    u32 maxSeqLen = 0;
+    bool netTurbo = true;
+    int gpuIndex = -1;
+    int gpuSegmentFrom = -1, gpuSegmentTo = -1;  // accepted for CLI compatibility (no effect)
+    int slots = 0;                               // KV slots (0 = 1 for CLI modes, 8 for the API)
+    bool kvBf16 = true;
+    bool graphs = true;
+    int logLevel = 1;
+    std::string synthetic;                       // "llama3_1_8b" etc: random-init weights on device
+
+    static AppArgs parse(int argc, char **argv, bool requireMode);
+};
+
+
+// Root-side inference: local backend + (optional) remote workers in lockstep.
+class InferenceSession {
+  public:
+    explicit InferenceSession(const AppArgs &args, int nSlots);
+    ~InferenceSession();
+
+    const ModelHeader &header() const { return backend_->header(); }
+    Tokenizer &tokenizer() { return *tokenizer_; }
+    Sampler &sampler() { return *sampler_; }
+    int nSlots() const { return nSlots_; }
+    int maxBatch() const { return maxBatch_; }
+    bool isGpu() const { return gpu_; }
+    int nNodes() const { return 1 + (int)workers_.size(); }
+
+    // logits: [n][vocab]
+    void forward(int n, const int *tokens, const int *positions, const int *slots, float *logits);
+    void forwardArgmax(int n, const int *tokens, const int *positions, const int *slots, int *out);
+    ForwardStats lastStats() const;
+    void finish();  // stop workers (they return to listening)
+
+  private:
+    void sendControl(Cmd cmd, int n, const int *tokens, const int *positions, const int *slots);
+
+    AppArgs args_;
+    int nSlots_, maxBatch_;
+    bool gpu_ = false;
+    std::vector<Socket> workers_;
+    std::unique_ptr<HostComm> hostComm_;
+    std::unique_ptr<class DeviceComm> devComm_;
+    std::unique_ptr<Backend> backend_;
+    std::unique_ptr<Tokenizer> tokenizer_;
+    std::unique_ptr<Sampler> sampler_;
+    bool finished_ = false;
+};
+
+// `dllama worker`: serve forever; a root disconnect returns to listening.
+void runWorker(const AppArgs &args);
+
+// Builds the synthetic header for a named shape (see --synthetic).
+ModelHeader syntheticHeader(const std::string &name, u32 seqLen);
+
+}  // namespace dl
