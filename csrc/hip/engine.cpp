@@ -217,6 +217,16 @@ class HipEngineImpl : public HipEngine {
         dQ_ = dalloc<float>((size_t)MB * p.q0);
         dAtt_ = dalloc<float>((size_t)MB * p.q0);
         dH_ = dalloc<float>((size_t)MB * p.hidden0);
+        dAttQ_ = dalloc<int8_t>((size_t)MB * p.q0);
+        dAttS_ = dalloc<float2>((size_t)MB * p.q0 / 32);
+        dHQ_ = dalloc<int8_t>((size_t)MB * p.hidden0);
+        dHS_ = dalloc<float2>((size_t)MB * p.hidden0 / 32);
+        dAttCnt_ = dalloc<int>((size_t)MB * p.nHeads0);
+        DL_HIP(hipMemsetAsync(dAttCnt_, 0, sizeof(int) * (size_t)MB * p.nHeads0, stream_));
+        dArgV_ = dalloc<float>((size_t)MB * 64);
+        dArgI_ = dalloc<int>((size_t)MB * 64);
+        dArgCnt_ = dalloc<int>(MB);
+        DL_HIP(hipMemsetAsync(dArgCnt_, 0, sizeof(int) * MB, stream_));
         dLogits_ = dalloc<float>((size_t)MB * p.vocab0);
         if (p.nRanks > 1) {
             dLogitsAll_ = dalloc<float>((size_t)MB * h_.vocabSize);
@@ -441,31 +451,32 @@ class HipEngineImpl : public HipEngine {
         }
     };
 
-    int batchChunk(int n) const {
+    int batchChunk(const DevMat &m, int pro, int epi) const {
         // largest batch chunk (1/2/4) whose LDS footprint stays <= 64 KiB for this input width
         int bc = 4;
         while (bc > 1) {
-            const int L = hipk::gemvLanesPerRow(n, q40_);
-            if (hipk::gemvLdsBytes(n, bc, q40_, (256 / L) * 8) <= 64 * 1024) break;
+            const int rpw = hipk::gemvRowsPerPass(m.n, m.rows, bc, q40_) * passesFor(m, epi, bc);
+            if (hipk::gemvLdsBytes(m.n, bc, q40_, rpw, pro) <= 64 * 1024) break;
             bc >>= 1;
         }
         return bc;
     }
 
-    int passesFor(const DevMat &m) const {
-        const int L = hipk::gemvLanesPerRow(m.n, q40_);
-        const int rp = 256 / L;
+    int passesFor(const DevMat &m, int epi, int B) const {
+        const int rp = hipk::gemvRowsPerPass(m.n, m.rows, B, q40_);
+        if (epi == hipk::EPI_ACT_Q80) return 64 / rp;  // 32 hidden units (one Q80 block) per workgroup
         const int grid0 = (m.rows + rp - 1) / rp;
         int passes = grid0 / 1024;
         if (passes < 1) passes = 1;
-        if (passes > 8) passes = 8;
+        if (passes > 4) passes = 4;
         return passes;
     }
 
     // Launch a GEMV over all n rows, in batch chunks of <= 4.
     void gemv(const DevMat &m, int n, int pro, int epi, const float *in, int ldIn, const float *add, float *xNext,
-              const float *normW, float *out, int ldOut, const DevLayer *L) {
-        const int bcMax = batchChunk(m.n);
+              const float *normW, float *out, int ldOut, const DevLayer *L, const int8_t *aq = nullptr,
+              const float2 *as = nullptr, int8_t *oq = nullptr, float2 *os = nullptr) {
+        const int bcMax = batchChunk(m, pro, epi);
         for (int c0 = 0; c0 < n;) {
             int bc = n - c0;
             if (bc > bcMax) bc = bcMax;
@@ -476,14 +487,18 @@ class HipEngineImpl : public HipEngine {
             a.wf = m.f;
             a.rows = m.rows;
             a.n = m.n;
-            a.passes = passesFor(m);
-            a.in = in + (size_t)c0 * ldIn;
+            a.passes = passesFor(m, epi, bc);
+            a.in = in ? in + (size_t)c0 * ldIn : nullptr;
+            a.aq = aq ? aq + (size_t)c0 * m.n : nullptr;
+            a.as = as ? as + (size_t)c0 * (m.n / 32) : nullptr;
+            a.oq = oq ? oq + (size_t)c0 * ldOut : nullptr;
+            a.os = os ? os + (size_t)c0 * (ldOut / 32) : nullptr;
             a.ldIn = ldIn;
             a.addIn = add ? add + (size_t)c0 * ldIn : nullptr;
             a.xNext = xNext ? xNext + (size_t)c0 * ldIn : nullptr;
             a.normW = normW;
             a.eps = h_.normEpsilon;
-            a.out = out + (size_t)c0 * ldOut;
+            a.out = out ? out + (size_t)c0 * ldOut : nullptr;
             a.ldOut = ldOut;
             a.act = h_.hiddenAct == HiddenAct::GELU ? 0 : 1;
             if (L) {
@@ -546,25 +561,36 @@ class HipEngineImpl : public HipEngine {
                 a.partO = dPartO_;
                 a.partML = dPartML_;
                 a.out = dAtt_;
+                a.outQ = q40_ ? dAttQ_ : nullptr;
+                a.outS = q40_ ? dAttS_ : nullptr;
                 a.ldOut = p.q0;
                 a.kvBf16 = kvBf16_ ? 1 : 0;
+                a.counters = dAttCnt_;
                 hipk::launchAttention(a, n, stream_);
             }
             {
                 ProfScope ps(this, "gemv_wo");
-                gemv(L.wo, n, hipk::PRO_QUANT, hipk::EPI_STORE, dAtt_, p.q0, nullptr, nullptr, nullptr, dY_, dim, nullptr);
+                gemv(L.wo, n, hipk::PRO_GLOBAL, hipk::EPI_STORE, q40_ ? nullptr : dAtt_, p.q0, nullptr, nullptr,
+                     nullptr, dY_, dim, nullptr, dAttQ_, dAttS_);
             }
             allReduce(dY_, (size_t)n * dim);
+            // Q80 hand-off of h needs one workgroup per 32 hidden units; for skinny TP shards the
+            // w13 epilogue emits f32 and w2 quantizes in its prologue instead.
+            const bool hQ80 = q40_ && p.hidden0 / 32 >= 192;
             {
                 ProfScope ps(this, "gemv_w13");
-                gemv(L.w13, n, hipk::PRO_RESNORM, hipk::EPI_ACT, dX_[cur], dim, dY_, dX_[cur ^ 1], L.rmsFfn, dH_,
-                     p.hidden0, nullptr);
+                gemv(L.w13, n, hipk::PRO_RESNORM, hQ80 ? hipk::EPI_ACT_Q80 : hipk::EPI_ACT, dX_[cur], dim, dY_,
+                     dX_[cur ^ 1], L.rmsFfn, dH_, p.hidden0, nullptr, nullptr, nullptr, dHQ_, dHS_);
             }
             cur ^= 1;
             {
                 ProfScope ps(this, "gemv_w2");
-                gemv(L.w2, n, hipk::PRO_QUANT, hipk::EPI_STORE, dH_, p.hidden0, nullptr, nullptr, nullptr, dY_, dim,
-                     nullptr);
+                if (hQ80 || !q40_)
+                    gemv(L.w2, n, hipk::PRO_GLOBAL, hipk::EPI_STORE, q40_ ? nullptr : dH_, p.hidden0, nullptr,
+                         nullptr, nullptr, dY_, dim, nullptr, dHQ_, dHS_);
+                else
+                    gemv(L.w2, n, hipk::PRO_RESNORM, hipk::EPI_STORE, dH_, p.hidden0, nullptr, nullptr, nullptr, dY_,
+                         dim, nullptr);
             }
             allReduce(dY_, (size_t)n * dim);
         }
@@ -582,17 +608,24 @@ class HipEngineImpl : public HipEngine {
         }
         if (kind != GraphKind::LOGITS) {
             ProfScope ps(this, "argmax");
-            hipk::launchArgmax(full, h_.vocabSize, n, dIds_, stream_);
-        }
-        if (kind == GraphKind::CHAIN) {
-            // record into history at [b][pos], then feed back
-            recordHistory(n);
-            hipk::launchAdvance(dIds_, dTok_, dPos_, n, stream_);
+            hipk::ArgmaxArgs g;
+            g.logits = full;
+            g.vocab = h_.vocabSize;
+            g.ids = dIds_;
+            g.partV = dArgV_;
+            g.partI = dArgI_;
+            g.counters = dArgCnt_;
+            if (kind == GraphKind::CHAIN) {
+                // feed the sampled token back: tokens := ids, hist[b][pos] := ids, pos += 1
+                g.tokens = dTok_;
+                g.pos = dPos_;
+                g.hist = dHist_;
+                g.seqLen = h_.seqLen;
+            }
+            hipk::launchArgmax(g, n, stream_);
         }
         DL_HIP(hipGetLastError());
     }
-
-    void recordHistory(int n);
 
     EngineConfig cfg_;
     DeviceComm *comm_;
@@ -614,6 +647,10 @@ class HipEngineImpl : public HipEngine {
     float *dY_ = nullptr, *dQ_ = nullptr, *dAtt_ = nullptr, *dH_ = nullptr, *dLogits_ = nullptr;
     float *dLogitsAll_ = nullptr, *dLogitsFull_ = nullptr;
     float *dPartO_ = nullptr, *dPartML_ = nullptr;
+    int8_t *dAttQ_ = nullptr, *dHQ_ = nullptr;
+    float2 *dAttS_ = nullptr, *dHS_ = nullptr;
+    int *dAttCnt_ = nullptr, *dArgCnt_ = nullptr, *dArgI_ = nullptr;
+    float *dArgV_ = nullptr;
     float2 *dRope_ = nullptr;
     int splitGrid_ = 1, chunkMax_ = 256;
     std::map<int, hipGraphExec_t> graphs_;
@@ -621,16 +658,87 @@ class HipEngineImpl : public HipEngine {
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> profTimes_;
 };
 
-__global__ void recordHistoryKernel(const int *ids, const int *pos, int *hist, int seqLen, int B) {
-    const int b = threadIdx.x;
-    if (b < B) hist[(size_t)b * seqLen + pos[b]] = ids[b];
-}
-
-void HipEngineImpl::recordHistory(int n) {
-    hipLaunchKernelGGL(recordHistoryKernel, dim3(1), dim3(64), 0, stream_, dIds_, dPos_, dHist_, (int)h_.seqLen, n);
-}
-
 }  // namespace
+
+double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int passes, int copies, int iters) {
+    hipStream_t s;
+    DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const size_t nb = (size_t)rows * n / 32;
+    std::vector<void *> mem;
+    auto alloc = [&](size_t bytes) {
+        void *p;
+        DL_HIP(hipMalloc(&p, bytes));
+        mem.push_back(p);
+        return p;
+    };
+    std::vector<uint8_t *> qs(copies);
+    std::vector<uint16_t *> d(copies);
+    for (int c = 0; c < copies; c++) {
+        qs[c] = (uint8_t *)alloc(nb * 16);
+        d[c] = (uint16_t *)alloc(nb * 2);
+        hipk::launchFillQ40(qs[c], d[c], nb, 0.01f, 77 + c, s);
+    }
+    float *x = (float *)alloc((size_t)B * n * 4), *y = (float *)alloc((size_t)B * n * 4);
+    float *xn = (float *)alloc((size_t)B * n * 4), *w = (float *)alloc((size_t)n * 4);
+    hipk::launchFillF32Uniform(x, (size_t)B * n, 1.f, 1, s);
+    hipk::launchFillF32Uniform(y, (size_t)B * n, 1.f, 2, s);
+    hipk::launchFillF32Const(w, n, 1.f, s);
+    int8_t *aq = (int8_t *)alloc((size_t)B * n);
+    float2 *as = (float2 *)alloc((size_t)B * n / 32 * 8);
+    DL_HIP(hipMemsetAsync(aq, 1, (size_t)B * n, s));
+    DL_HIP(hipMemsetAsync(as, 0, (size_t)B * n / 32 * 8, s));
+    const int outRows = epi == hipk::EPI_ACT_Q80 ? rows / 2 : rows;
+    float *out = (float *)alloc((size_t)B * rows * 4);
+    int8_t *oq = (int8_t *)alloc((size_t)B * outRows);
+    float2 *os = (float2 *)alloc((size_t)B * outRows / 32 * 8);
+    hipk::GemvArgs a;
+    a.rows = rows;
+    a.n = n;
+    a.passes = passes;
+    a.lanes = lanes;
+    a.in = x;
+    a.ldIn = n;
+    a.addIn = y;
+    a.xNext = xn;
+    a.normW = w;
+    a.aq = aq;
+    a.as = as;
+    a.out = out;
+    a.ldOut = outRows;
+    a.oq = oq;
+    a.os = os;
+    auto launch = [&](int c) {
+        a.qs = qs[c % copies];
+        a.wd = d[c % copies];
+        hipk::launchGemv(a, B, pro, epi, true, s);
+    };
+    launch(0);
+    DL_HIP(hipGetLastError());
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    DL_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < iters; i++) launch(i);
+    DL_HIP(hipStreamEndCapture(s, &g));
+    DL_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    DL_HIP(hipGraphLaunch(ge, s));
+    DL_HIP(hipStreamSynchronize(s));
+    hipEvent_t e0, e1;
+    DL_HIP(hipEventCreate(&e0));
+    DL_HIP(hipEventCreate(&e1));
+    DL_HIP(hipEventRecord(e0, s));
+    DL_HIP(hipGraphLaunch(ge, s));
+    DL_HIP(hipEventRecord(e1, s));
+    DL_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    DL_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipGraphExecDestroy(ge);
+    (void)hipGraphDestroy(g);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    for (void *p : mem) (void)hipFree(p);
+    (void)hipStreamDestroy(s);
+    return ms * 1000.0 / iters;
+}
 
 std::unique_ptr<HipEngine> makeHipEngine(const EngineConfig &cfg, DeviceComm *comm) {
     return std::unique_ptr<HipEngine>(new HipEngineImpl(cfg, comm));

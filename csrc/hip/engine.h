@@ -29,4 +29,8 @@ class HipEngine : public Backend {
 std::unique_ptr<HipEngine> makeHipEngine(const EngineConfig &cfg, DeviceComm *comm);
 int hipDeviceCount();
 
+// Micro-benchmark of one Q40 GEMV configuration: `copies` weight matrices (to defeat the 256 MB
+// infinity cache) are cycled through a graph of `iters` launches. Returns microseconds per launch.
+double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int passes, int copies, int iters);
+
 }  // namespace dl

@@ -1,14 +1,17 @@
 // Host-visible launchers for the gfx950 kernels (csrc/hip/kernels.hip).
 //
 // Kernel map vs the reference op inventory:
-//   gemv<PRO_RESNORM, EPI_QKV>   OP_MERGE_ADD + OP_INV_RMS + OP_RMS_NORM + OP_CAST(Q80)
-//                                + 3x OP_MATMUL (q,k,v) + 2x OP_ROPE_LLAMA + 2x OP_SHIFT
-//   attention + attnCombine      OP_MULTIHEAD_ATT (flash-decoding split over the sequence)
-//   gemv<PRO_QUANT, EPI_STORE>   OP_CAST(Q80) + OP_MATMUL (wo, w2)
-//   gemv<PRO_RESNORM, EPI_ACT>   OP_MERGE_ADD + norm + OP_MATMUL (w1, w3) + OP_SILU/GELU + OP_MUL
-//   gemv<PRO_RESNORM, EPI_STORE> final norm + OP_MATMUL (logits)
-//   embedding                    OP_EMBEDDING
-//   argmaxRows                   greedy sampling on device
+//   gemv<PRO_RESNORM, EPI_QKV>     OP_MERGE_ADD + OP_INV_RMS + OP_RMS_NORM + OP_CAST(Q80)
+//                                  + 3x OP_MATMUL (q,k,v) + 2x OP_ROPE_LLAMA + 2x OP_SHIFT
+//   attention                      OP_MULTIHEAD_ATT (flash-decoding split over the sequence, the
+//                                  split combine done in-kernel by the last-arriving workgroup)
+//                                  + OP_CAST(Q80) of its output
+//   gemv<PRO_GLOBAL, EPI_STORE>    OP_MATMUL (wo, w2) on Q80 activations produced upstream
+//   gemv<PRO_RESNORM, EPI_ACT_Q80> OP_MERGE_ADD + norm + OP_MATMUL (w1, w3) + OP_SILU/GELU + OP_MUL
+//                                  + OP_CAST(Q80)
+//   gemv<PRO_RESNORM, EPI_STORE>   final norm + OP_MATMUL (logits)
+//   embedding                      OP_EMBEDDING
+//   argmax                         greedy sampling on device (+ token feedback for decode chains)
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -17,8 +20,13 @@
 namespace dl {
 namespace hipk {
 
-enum Prologue : int { PRO_QUANT = 0, PRO_RESNORM = 1 };
-enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2 };
+// PRO_GLOBAL: activations are read straight from global memory in the main loop (Q80 blocks for
+//             Q40 weights, f32 for F32 weights) - no prologue, no LDS, no barrier.
+// PRO_RESNORM: (x + delta) -> RMS norm -> Q80 (or f32) staged once per workgroup in LDS
+//             (normW == null: no norm, plain quantization of `in`).
+enum Prologue : int { PRO_GLOBAL = 0, PRO_RESNORM = 1 };
+// EPI_ACT_Q80: act(w1 x) * (w3 x), quantized to Q80 blocks for the next GEMV (32 hidden units/block).
+enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2, EPI_ACT_Q80 = 3 };
 
 struct GemvArgs {
     // weights: Q40 repacked (qs [rows][nb][16], d [rows][nb] f16) or F32 [rows][n]
@@ -27,7 +35,11 @@ struct GemvArgs {
     const float *wf = nullptr;
     int rows = 0, n = 0;
     int passes = 1;  // row passes per workgroup (rows per WG = passes * 256 / L)
-    // prologue
+    int lanes = 0;   // lanes per row (0 = auto from n)
+    // PRO_GLOBAL, Q40 weights: Q80 activations [B][n] int8 + [B][n/32] (d, sum of q)
+    const int8_t *aq = nullptr;
+    const float2 *as = nullptr;
+    // prologue / f32 input
     const float *in = nullptr;    // [B][ldIn]
     int ldIn = 0;
     const float *addIn = nullptr; // PRO_RESNORM: residual delta added to `in` (may be null)
@@ -38,6 +50,8 @@ struct GemvArgs {
     float *out = nullptr;
     int ldOut = 0;
     int act = 1;                  // EPI_ACT: 0 = GELU, 1 = SiLU
+    int8_t *oq = nullptr;         // EPI_ACT_Q80 outputs [B][ldOut] + [B][ldOut/32]
+    float2 *os = nullptr;
     // EPI_QKV
     int q0 = 0, kv0 = 0, hs = 0, seqLen = 0;
     const float2 *rope = nullptr; // [seqLen][hs/2] (cos, sin)
@@ -50,10 +64,16 @@ struct GemvArgs {
 
 // B = batch rows in this launch (1, 2 or 4); q40 = weight format.
 void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_t s);
-// Rows per workgroup for a given n (used by the host to size partial passes).
-int gemvLanesPerRow(int n, bool q40);
+// Rows handled by one lane group (2 at batch 1: the activation loads are shared by 2 rows).
+__host__ __device__ constexpr int gemvRowGroup(int B, bool q40) { return (B == 1 && q40) ? 2 : 1; }
+// Lanes cooperating on one weight row for a given input width, row count and batch.
+int gemvLanesPerRow(int n, int rows, int B, bool q40);
+// Rows per workgroup and pass.
+inline int gemvRowsPerPass(int n, int rows, int B, bool q40) {
+    return 256 / gemvLanesPerRow(n, rows, B, q40) * gemvRowGroup(B, q40);
+}
 // Dynamic LDS bytes a gemv launch needs.
-size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg);
+size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg, int pro);
 
 struct AttnArgs {
     const float *q = nullptr;   // [B][ldq], rotated queries
@@ -65,20 +85,33 @@ struct AttnArgs {
     int chunkMax = 256;         // LDS capacity in positions per split
     float *partO = nullptr;     // [B][nHeads0][splitGrid][hs]
     float *partML = nullptr;    // [B][nHeads0][splitGrid][2]
-    float *out = nullptr;       // [B][ldOut] (combined output)
+    float *out = nullptr;       // [B][ldOut] f32 output (when outQ is null)
+    int8_t *outQ = nullptr;     // [B][ldOut] Q80 output (+ outS [B][ldOut/32])
+    float2 *outS = nullptr;
     int ldOut = 0;
     int kvBf16 = 1;
+    int *counters = nullptr;    // [B][nHeads0/HG] arrival counters (zero-initialised, self-resetting)
 };
 void launchAttention(const AttnArgs &a, int B, hipStream_t s);
 int attnSplitGrid(int seqLen);
 int attnChunkMax(int seqLen, int splitGrid);
 
 void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s);
-void launchArgmax(const float *logits, int vocab, int B, int *outIds, hipStream_t s);
+// Parallel argmax over [B][vocab]; partials need B*256 floats + ints, counters B ints (zeroed).
+// When `tokens` is non-null the result is also fed back (tokens[b] = id; hist[b][pos] = id; pos += 1).
+struct ArgmaxArgs {
+    const float *logits = nullptr;
+    int vocab = 0;
+    int *ids = nullptr;
+    float *partV = nullptr;
+    int *partI = nullptr;
+    int *counters = nullptr;
+    int *tokens = nullptr, *pos = nullptr, *hist = nullptr;
+    int seqLen = 0;
+};
+void launchArgmax(const ArgmaxArgs &a, int B, hipStream_t s);
 // logits gathered rank-major [nRanks][B][vocab0] -> row-major [B][vocab]
 void launchUnshardLogits(const float *in, float *out, int nRanks, int B, int vocab0, hipStream_t s);
-// Decode chaining: tokens[b] = ids[b]; pos[b] += 1
-void launchAdvance(const int *ids, int *tokens, int *pos, int B, hipStream_t s);
 
 // Synthetic weights: random Q40 nibbles with scale ~ scale*(0.5..1.5), f32 uniform(-a,a), or constant.
 void launchFillQ40(uint8_t *qs, uint16_t *d, size_t nBlocks, float scale, uint64_t seed, hipStream_t s);

@@ -1,16 +1,23 @@
 // gfx950 (MI355X / CDNA4) kernels for decode and small-batch forward passes.
 //
 // Design notes (see csrc/hip/kernels.h for the op map):
-// * Weights stream straight from HBM into VGPRs (16 B per lane per Q40 block, several blocks in
-//   flight per lane); no LDS staging for operands that are read once (GEMV regime).
-// * Activations are quantized to Q80 ONCE per workgroup in the prologue and kept in LDS; the
-//   inner product is four v_dot4_i32_i8 per 16 weights with the "-8" nibble offset folded into a
-//   per-block activation sum: sum((q-8)*x) = dot(q, x) - 8*sum(x).
+// * Weights stream straight from HBM into VGPRs (16 B per lane per Q40 block); each lane's first
+//   KMAX blocks are issued BEFORE the prologue so HBM latency overlaps the norm/quant work
+//   (GEMV regime: operands read once, no LDS staging - cdna_hip_programming.md §5 table,
+//   "GEMV / M <= 16 decode weights"). Loads are non-temporal (read-once weights).
+// * Activations are Q80: either produced once per workgroup in LDS (norm prologue) or produced
+//   upstream in the epilogue of the previous kernel and read straight from global (L2-resident).
+//   The inner product is v_dot4_i32_i8 on nibbles with the "-8" folded into a per-block sum:
+//   sum((q-8)*x) = dot(q, x) - 8*sum(x).
 // * Row reductions use DPP (quad_perm / row_ror) inside 16-lane rows, shfl only across rows.
 // * Every per-token input (token id, position, KV slot) is read from device memory so the whole
-//   forward pass can be captured once in a hipGraph and replayed.
+//   forward pass is captured once per batch size in a hipGraph and replayed.
+// * Cross-workgroup hand-offs (attention split combine, argmax) follow the agent-scope
+//   release/acquire counter recipe (cdna_hip_programming.md §5 "In-launch split-K reduction").
 #include "device_common.h"
 #include "kernels.h"
+
+#include <cstdlib>
 
 namespace dl {
 namespace hipk {
@@ -18,6 +25,7 @@ namespace hipk {
 using namespace dl::dev;
 
 static constexpr int kThreads = 256;
+static constexpr int KMAX = 8;  // weight blocks per lane held in VGPRs (prefetched)
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -26,44 +34,222 @@ __device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<floa
 
 __host__ __device__ static inline size_t alignUp(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-int gemvLanesPerRow(int n, bool q40) {
+// Tuning knob (experiments only): DL_GEMV_MIN_LANES=32 forces at least 32 lanes per row.
+static int minLanesOverride() {
+    static const int v = [] {
+        const char *e = getenv("DL_GEMV_MIN_LANES");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
+int gemvLanesPerRow(int n, int rows, int B, bool q40) {
+    int L;
     if (q40) {
         const int nb = n / 32;
-        if (nb >= 384) return 64;
-        if (nb >= 192) return 32;
-        return 16;
+        L = nb <= 128 ? 16 : (nb <= 256 ? 32 : 64);
+    } else {
+        const int n4 = n / 4;
+        L = n4 >= 2048 ? 64 : (n4 >= 512 ? 32 : 16);
     }
-    const int n4 = n / 4;
-    if (n4 >= 2048) return 64;
-    if (n4 >= 512) return 32;
-    return 16;
+    // skinny shards (tensor parallel): fewer rows per workgroup so the grid still covers the CUs
+    while (L < 64 && rows / (kThreads / L * gemvRowGroup(B, q40)) < 256) L *= 2;
+    const int mo = minLanesOverride();
+    if (mo > L) L = mo > 64 ? 64 : mo;
+    return L;
 }
 
 struct GemvLds {
-    size_t scratch, res, act, sc, total;
+    size_t scratch, res, hbuf, act, sc, total;
 };
 
-__host__ __device__ static GemvLds gemvLayout(int n, int B, bool q40, int rowsPerWg) {
+__host__ __device__ static GemvLds gemvLayout(int n, int B, bool q40, int rowsPerWg, int pro) {
     GemvLds l;
     size_t off = 0;
     l.scratch = off;
     off += 64 * sizeof(float);
     l.res = off;
     off = alignUp(off + (size_t)B * rowsPerWg * sizeof(float), 16);
+    l.hbuf = off;
+    off = alignUp(off + (size_t)B * (rowsPerWg / 2) * sizeof(float), 16);
     l.act = off;
-    if (q40) {
-        off = alignUp(off + (size_t)B * n, 16);
-        l.sc = off;
-        off = alignUp(off + (size_t)B * (n / 32) * sizeof(float2), 16);
+    if (pro == PRO_RESNORM) {
+        if (q40) {
+            off = alignUp(off + (size_t)B * n, 16);
+            l.sc = off;
+            off = alignUp(off + (size_t)B * (n / 32) * sizeof(float2), 16);
+        } else {
+            off = alignUp(off + (size_t)B * n * sizeof(float), 16);
+            l.sc = off;
+        }
     } else {
-        off = alignUp(off + (size_t)B * n * sizeof(float), 16);
         l.sc = off;
     }
     l.total = off;
     return l;
 }
 
-size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg) { return gemvLayout(n, B, q40, rowsPerWg).total; }
+size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg, int pro) {
+    return gemvLayout(n, B, q40, rowsPerWg, pro).total;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Prologue: (x + delta) -> RMS norm -> Q80 blocks (or f32) in LDS; workgroup 0 writes x + delta.
+// ------------------------------------------------------------------------------------------------
+// Quantize (or store) one 8-element chunk c of row b into the LDS activation image.
+template <bool Q40>
+__device__ __forceinline__ void stageChunk(float (&v)[8], int b, int c, int n, int8_t *sq, float2 *ssc, float *sf) {
+    const int nb = n >> 5, tid = threadIdx.x;
+    if constexpr (Q40) {
+        float amax = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; i++) amax = fmaxf(amax, fabsf(v[i]));
+        amax = quadMax(amax);  // the 4 lanes of a quad hold one 32-element block
+        const float d = amax / 127.0f;
+        const float id = d != 0.f ? 1.0f / d : 0.f;
+        int q[8];
+        int qsum = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            q[i] = (int)rintf(v[i] * id);
+            q[i] = q[i] > 127 ? 127 : (q[i] < -127 ? -127 : q[i]);
+            qsum += q[i];
+        }
+        int2 packed;
+        packed.x = packI8x4(q[0], q[1], q[2], q[3]);
+        packed.y = packI8x4(q[4], q[5], q[6], q[7]);
+        *reinterpret_cast<int2 *>(sq + (size_t)b * n + c * 8) = packed;
+        qsum = quadSumI(qsum);
+        if ((tid & 3) == 0) ssc[b * nb + (c >> 2)] = make_float2(roundF16(d), (float)qsum);
+    } else {
+        float *dst = sf + (size_t)b * n + c * 8;
+        st4(dst, make_float4(v[0], v[1], v[2], v[3]));
+        st4(dst + 4, make_float4(v[4], v[5], v[6], v[7]));
+    }
+}
+
+// Single global pass: each thread keeps up to PMAX chunks of 8 elements per row in registers
+// (n <= 256 * 8 * PMAX); larger inputs fall back to a second pass over L2.
+template <int B, bool Q40>
+__device__ __forceinline__ void resNormPrologue(const GemvArgs &a, float *scratch, int8_t *sq, float2 *ssc, float *sf) {
+    constexpr int PMAX = 4;
+    const int n = a.n, tid = threadIdx.x;
+    const int nChunks = n >> 3;
+    const bool inReg = nChunks <= kThreads * PMAX;
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+        const float *xi = a.in + (size_t)b * a.ldIn;
+        const float *yi = a.addIn ? a.addIn + (size_t)b * a.ldIn : nullptr;
+        float *xo = (blockIdx.x == 0 && a.xNext) ? a.xNext + (size_t)b * a.ldIn : nullptr;
+        float v[PMAX][8];
+        float ss = 0.f;
+        if (inReg) {
+#pragma unroll
+            for (int k = 0; k < PMAX; k++) {
+                const int c = tid + k * kThreads;
+                if (c < nChunks) {
+                    float4 v0 = ld4(xi + c * 8), v1 = ld4(xi + c * 8 + 4);
+                    if (yi) {
+                        const float4 y0 = ld4(yi + c * 8), y1 = ld4(yi + c * 8 + 4);
+                        v0.x += y0.x; v0.y += y0.y; v0.z += y0.z; v0.w += y0.w;
+                        v1.x += y1.x; v1.y += y1.y; v1.z += y1.z; v1.w += y1.w;
+                    }
+                    if (xo) {
+                        st4(xo + c * 8, v0);
+                        st4(xo + c * 8 + 4, v1);
+                    }
+                    v[k][0] = v0.x; v[k][1] = v0.y; v[k][2] = v0.z; v[k][3] = v0.w;
+                    v[k][4] = v1.x; v[k][5] = v1.y; v[k][6] = v1.z; v[k][7] = v1.w;
+#pragma unroll
+                    for (int i = 0; i < 8; i++) ss += v[k][i] * v[k][i];
+                }
+            }
+        } else {
+            for (int i = tid * 4; i < n; i += kThreads * 4) {
+                float4 x = ld4(xi + i);
+                if (yi) {
+                    const float4 y = ld4(yi + i);
+                    x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w;
+                }
+                ss += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+                if (xo) st4(xo + i, x);
+            }
+        }
+        float inv = 1.0f;
+        if (a.normW) {
+            ss = blockSum<kThreads>(ss, scratch);
+            inv = 1.0f / sqrtf(ss / (float)n + a.eps);
+        }
+        if (inReg) {
+#pragma unroll
+            for (int k = 0; k < PMAX; k++) {
+                const int c = tid + k * kThreads;
+                if (c < nChunks) {
+                    if (a.normW) {
+                        const float4 w0 = ld4(a.normW + c * 8), w1 = ld4(a.normW + c * 8 + 4);
+                        const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+                        for (int i = 0; i < 8; i++) v[k][i] = wv[i] * (inv * v[k][i]);
+                    }
+                    stageChunk<Q40>(v[k], b, c, n, sq, ssc, sf);
+                }
+            }
+            continue;
+        }
+        for (int c = tid; c < nChunks; c += kThreads) {
+            float4 v0 = ld4(xi + c * 8), v1 = ld4(xi + c * 8 + 4);
+            if (yi) {
+                const float4 y0 = ld4(yi + c * 8), y1 = ld4(yi + c * 8 + 4);
+                v0.x += y0.x; v0.y += y0.y; v0.z += y0.z; v0.w += y0.w;
+                v1.x += y1.x; v1.y += y1.y; v1.z += y1.z; v1.w += y1.w;
+            }
+            float w8[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+            if (a.normW) {
+                const float4 w0 = ld4(a.normW + c * 8), w1 = ld4(a.normW + c * 8 + 4);
+                w8[0] = w0.x; w8[1] = w0.y; w8[2] = w0.z; w8[3] = w0.w;
+                w8[4] = w1.x; w8[5] = w1.y; w8[6] = w1.z; w8[7] = w1.w;
+            }
+            float vv[8] = {w8[0] * (inv * v0.x), w8[1] * (inv * v0.y), w8[2] * (inv * v0.z), w8[3] * (inv * v0.w),
+                           w8[4] * (inv * v1.x), w8[5] * (inv * v1.y), w8[6] * (inv * v1.z), w8[7] * (inv * v1.w)};
+            stageChunk<Q40>(vv, b, c, n, sq, ssc, sf);
+        }
+    }
+    __syncthreads();
+}
+
+// One Q40 block (32 weights) of RG rows against B activation blocks; the activation block is
+// loaded once and shared by the RG rows (halves activation traffic at batch 1).
+template <int B, int RG>
+__device__ __forceinline__ void q40Block(float (&acc)[RG][B], const u32x4 (&w)[RG], const float (&dw)[RG], int j,
+                                         int n, int nb, const int8_t *act, const float2 *asc) {
+    int lo[RG][4], hi[RG][4];
+#pragma unroll
+    for (int r = 0; r < RG; r++) {
+        lo[r][0] = w[r].x & 0x0F0F0F0F; hi[r][0] = (w[r].x >> 4) & 0x0F0F0F0F;
+        lo[r][1] = w[r].y & 0x0F0F0F0F; hi[r][1] = (w[r].y >> 4) & 0x0F0F0F0F;
+        lo[r][2] = w[r].z & 0x0F0F0F0F; hi[r][2] = (w[r].z >> 4) & 0x0F0F0F0F;
+        lo[r][3] = w[r].w & 0x0F0F0F0F; hi[r][3] = (w[r].w >> 4) & 0x0F0F0F0F;
+    }
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+        const int4 *xp = reinterpret_cast<const int4 *>(act + (size_t)b * n + j * 32);
+        const int4 xa = xp[0], xb = xp[1];
+        const float2 sc = asc[b * nb + j];
+        const int off8 = 8 * (int)sc.y;
+#pragma unroll
+        for (int r = 0; r < RG; r++) {
+            int s = dot4(lo[r][0], xa.x, 0);
+            s = dot4(lo[r][1], xa.y, s);
+            s = dot4(lo[r][2], xa.z, s);
+            s = dot4(lo[r][3], xa.w, s);
+            s = dot4(hi[r][0], xb.x, s);
+            s = dot4(hi[r][1], xb.y, s);
+            s = dot4(hi[r][2], xb.z, s);
+            s = dot4(hi[r][3], xb.w, s);
+            acc[r][b] += (dw[r] * sc.x) * (float)(s - off8);
+        }
+    }
+}
 
 // ------------------------------------------------------------------------------------------------
 // GEMV: out[b][row] = W[row,:] . act(in[b,:]), fused prologue/epilogue.
@@ -71,170 +257,138 @@ size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg) { return gemvLayout(n
 template <int L, int B, int PRO, int EPI, bool Q40>
 __global__ __launch_bounds__(kThreads) void gemvKernel(GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int RP = kThreads / L;  // rows per pass
+    constexpr int RG = gemvRowGroup(B, Q40);  // rows per lane group
+    constexpr int RP = kThreads / L * RG;     // rows per pass
     const int n = a.n, nb = n >> 5;
     const int R = RP * a.passes;
-    const GemvLds lay = gemvLayout(n, B, Q40, R);
+    const GemvLds lay = gemvLayout(n, B, Q40, R, PRO);
     float *scratch = reinterpret_cast<float *>(smem + lay.scratch);
     float *res = reinterpret_cast<float *>(smem + lay.res);
-    int8_t *sq = reinterpret_cast<int8_t *>(smem + lay.act);
-    float *sf = reinterpret_cast<float *>(smem + lay.act);
-    float2 *ssc = reinterpret_cast<float2 *>(smem + lay.sc);
+    float *hbuf = reinterpret_cast<float *>(smem + lay.hbuf);
     const int tid = threadIdx.x;
-
-    // ---- prologue: (residual add) + (rms norm) + quantize activations into LDS ----------------
-    float inv[B];
-#pragma unroll
-    for (int b = 0; b < B; b++) inv[b] = 1.0f;
-    if constexpr (PRO == PRO_RESNORM) {
-#pragma unroll
-        for (int b = 0; b < B; b++) {
-            const float *xi = a.in + (size_t)b * a.ldIn;
-            const float *yi = a.addIn ? a.addIn + (size_t)b * a.ldIn : nullptr;
-            float *xo = (blockIdx.x == 0 && a.xNext) ? a.xNext + (size_t)b * a.ldIn : nullptr;
-            float ss = 0.f;
-            for (int i = tid * 4; i < n; i += kThreads * 4) {
-                float4 v = ld4(xi + i);
-                if (yi) {
-                    const float4 y = ld4(yi + i);
-                    v.x += y.x;
-                    v.y += y.y;
-                    v.z += y.z;
-                    v.w += y.w;
-                }
-                ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-                if (xo) st4(xo + i, v);
-            }
-            if (a.normW) {
-                ss = blockSum<kThreads>(ss, scratch);
-                inv[b] = 1.0f / sqrtf(ss / (float)n + a.eps);
-            }
-        }
-    }
-#pragma unroll
-    for (int b = 0; b < B; b++) {
-        const float *xi = a.in + (size_t)b * a.ldIn;
-        const float *yi = (PRO == PRO_RESNORM && a.addIn) ? a.addIn + (size_t)b * a.ldIn : nullptr;
-        const float *w = (PRO == PRO_RESNORM) ? a.normW : nullptr;
-        for (int c = tid; c < (n >> 3); c += kThreads) {
-            float v[8];
-            float4 v0 = ld4(xi + c * 8), v1 = ld4(xi + c * 8 + 4);
-            if (yi) {
-                const float4 y0 = ld4(yi + c * 8), y1 = ld4(yi + c * 8 + 4);
-                v0.x += y0.x; v0.y += y0.y; v0.z += y0.z; v0.w += y0.w;
-                v1.x += y1.x; v1.y += y1.y; v1.z += y1.z; v1.w += y1.w;
-            }
-            v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
-            v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
-            if (w) {
-                const float4 w0 = ld4(w + c * 8), w1 = ld4(w + c * 8 + 4);
-                const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-#pragma unroll
-                for (int i = 0; i < 8; i++) v[i] = wv[i] * (inv[b] * v[i]);
-            }
-            if constexpr (Q40) {
-                float amax = 0.f;
-#pragma unroll
-                for (int i = 0; i < 8; i++) amax = fmaxf(amax, fabsf(v[i]));
-                amax = quadMax(amax);  // the 4 lanes of a quad hold one 32-element block
-                const float d = amax / 127.0f;
-                const float id = d != 0.f ? 1.0f / d : 0.f;
-                int q[8];
-                int qsum = 0;
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    q[i] = (int)rintf(v[i] * id);
-                    q[i] = q[i] > 127 ? 127 : (q[i] < -127 ? -127 : q[i]);
-                    qsum += q[i];
-                }
-                int2 packed;
-                packed.x = packI8x4(q[0], q[1], q[2], q[3]);
-                packed.y = packI8x4(q[4], q[5], q[6], q[7]);
-                *reinterpret_cast<int2 *>(sq + (size_t)b * n + c * 8) = packed;
-                qsum = quadSumI(qsum);
-                if ((tid & 3) == 0) ssc[b * nb + (c >> 2)] = make_float2(roundF16(d), (float)qsum);
-            } else {
-                float *dst = sf + (size_t)b * n + c * 8;
-                st4(dst, make_float4(v[0], v[1], v[2], v[3]));
-                st4(dst + 4, make_float4(v[4], v[5], v[6], v[7]));
-            }
-        }
-    }
-    __syncthreads();
-
-    // ---- main loop ------------------------------------------------------------------------------
     const int gi = tid / L, li = tid % L;
     const int rowBase = blockIdx.x * R;
+
+    // activation sources
+    const int8_t *act;
+    const float2 *asc;
+    const float *actF;
+    if constexpr (PRO == PRO_RESNORM) {
+        act = reinterpret_cast<const int8_t *>(smem + lay.act);
+        asc = reinterpret_cast<const float2 *>(smem + lay.sc);
+        actF = reinterpret_cast<const float *>(smem + lay.act);
+    } else {
+        act = a.aq;
+        asc = a.as;
+        actF = a.in;
+    }
+
+    // Q40: each lane's first KM blocks of its RG rows live in VGPRs; pass p+1's blocks are
+    // issued before pass p is computed (and pass 0's before the prologue).
+    constexpr int KM = KMAX / RG;  // prefetched blocks per row (KMAX loads in flight per lane)
+    auto rowOf = [&](int p, int r) { return rowBase + p * RP + gi * RG + r; };
+    u32x4 w[RG][KM], wn[RG][KM];
+    uint16_t dh[RG][KM], dn[RG][KM];
+    auto prefetch = [&](int p, u32x4(&wd)[RG][KM], uint16_t(&dd)[RG][KM]) {
+#pragma unroll
+        for (int r = 0; r < RG; r++) {
+            const int row = min(rowOf(p, r), a.rows - 1);
+            const u32x4 *wrow = reinterpret_cast<const u32x4 *>(a.qs + (size_t)row * nb * 16);
+            const uint16_t *drow = a.wd + (size_t)row * nb;
+#pragma unroll
+            for (int k = 0; k < KM; k++) {  // clamped: no divergent loads
+                const int j = min(li + k * L, nb - 1);
+                wd[r][k] = __builtin_nontemporal_load(wrow + j);
+                dd[r][k] = drow[j];
+            }
+        }
+    };
+    if constexpr (Q40) prefetch(0, w, dh);
     for (int p = 0; p < a.passes; p++) {
-        const int row = rowBase + p * RP + gi;
-        const int rowc = row < a.rows ? row : a.rows - 1;
-        float acc[B];
+        float acc[RG][B];
 #pragma unroll
-        for (int b = 0; b < B; b++) acc[b] = 0.f;
+        for (int r = 0; r < RG; r++)
+#pragma unroll
+            for (int b = 0; b < B; b++) acc[r][b] = 0.f;
         if constexpr (Q40) {
-            constexpr int U = 4;
-            const u32x4 *wrow = reinterpret_cast<const u32x4 *>(a.qs + (size_t)rowc * nb * 16);
-            const uint16_t *drow = a.wd + (size_t)rowc * nb;
-            for (int j0 = li; j0 < nb; j0 += L * U) {
-                u32x4 w[U];
-                float dw[U];
-                int jj[U];
+            if (PRO == PRO_RESNORM && p == 0) {
+                resNormPrologue<B, true>(a, scratch, reinterpret_cast<int8_t *>(smem + lay.act),
+                                         reinterpret_cast<float2 *>(smem + lay.sc), nullptr);
+            }
+            if (p + 1 < a.passes) prefetch(p + 1, wn, dn);
 #pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int j = j0 + u * L;
-                    jj[u] = j < nb ? j : nb - 1;  // clamp: loads always issue, tail masked by dw=0
-                    w[u] = __builtin_nontemporal_load(wrow + jj[u]);
-                    const uint16_t hb = drow[jj[u]];
-                    dw[u] = j < nb ? __half2float(__ushort_as_half(hb)) : 0.f;
+            for (int k = 0; k < KM; k++) {
+                const int j = li + k * L;
+                u32x4 wk[RG];
+                float dw[RG];
+#pragma unroll
+                for (int r = 0; r < RG; r++) {
+                    wk[r] = w[r][k];
+                    dw[r] = j < nb ? __half2float(__ushort_as_half(dh[r][k])) : 0.f;
                 }
+                q40Block<B, RG>(acc, wk, dw, min(j, nb - 1), n, nb, act, asc);
+            }
+            // remaining blocks (only when nb > KMAX * L), 2 in flight per row and lane
+            for (int j0 = li + KM * L; j0 < nb; j0 += 2 * L) {
+                u32x4 w2[2][RG];
+                float d2[2][RG];
 #pragma unroll
-                for (int u = 0; u < U; u++) {
-                    const int j = jj[u];
-                    const int lo0 = w[u].x & 0x0F0F0F0F, hi0 = (w[u].x >> 4) & 0x0F0F0F0F;
-                    const int lo1 = w[u].y & 0x0F0F0F0F, hi1 = (w[u].y >> 4) & 0x0F0F0F0F;
-                    const int lo2 = w[u].z & 0x0F0F0F0F, hi2 = (w[u].z >> 4) & 0x0F0F0F0F;
-                    const int lo3 = w[u].w & 0x0F0F0F0F, hi3 = (w[u].w >> 4) & 0x0F0F0F0F;
+                for (int u = 0; u < 2; u++) {
+                    const int j = j0 + u * L;
 #pragma unroll
-                    for (int b = 0; b < B; b++) {
-                        const int4 xa = *reinterpret_cast<const int4 *>(sq + (size_t)b * n + j * 32);
-                        const int4 xb = *reinterpret_cast<const int4 *>(sq + (size_t)b * n + j * 32 + 16);
-                        int s = dot4(lo0, xa.x, 0);
-                        s = dot4(lo1, xa.y, s);
-                        s = dot4(lo2, xa.z, s);
-                        s = dot4(lo3, xa.w, s);
-                        s = dot4(hi0, xb.x, s);
-                        s = dot4(hi1, xb.y, s);
-                        s = dot4(hi2, xb.z, s);
-                        s = dot4(hi3, xb.w, s);
-                        const float2 sc = ssc[b * nb + j];
-                        acc[b] += (dw[u] * sc.x) * (float)(s - 8 * (int)sc.y);
+                    for (int r = 0; r < RG; r++) {
+                        const int row = min(rowOf(p, r), a.rows - 1);
+                        const int jc = min(j, nb - 1);
+                        w2[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.qs + (size_t)row * nb * 16) + jc);
+                        const uint16_t hb = a.wd[(size_t)row * nb + jc];
+                        d2[u][r] = j < nb ? __half2float(__ushort_as_half(hb)) : 0.f;
                     }
                 }
+#pragma unroll
+                for (int u = 0; u < 2; u++) q40Block<B, RG>(acc, w2[u], d2[u], min(j0 + u * L, nb - 1), n, nb, act, asc);
             }
+#pragma unroll
+            for (int r = 0; r < RG; r++)
+#pragma unroll
+                for (int k = 0; k < KM; k++) {
+                    w[r][k] = wn[r][k];
+                    dh[r][k] = dn[r][k];
+                }
         } else {
+            if (PRO == PRO_RESNORM && p == 0) {
+                resNormPrologue<B, false>(a, scratch, nullptr, nullptr, reinterpret_cast<float *>(smem + lay.act));
+            }
+            const int rowc = min(rowOf(p, 0), a.rows - 1);
             const f32x4 *wrow = reinterpret_cast<const f32x4 *>(a.wf + (size_t)rowc * n);
             const int n4 = n >> 2;
+            const int ldx = PRO == PRO_RESNORM ? n : a.ldIn;
 #pragma unroll 4
             for (int k = li; k < n4; k += L) {
                 const f32x4 wv = __builtin_nontemporal_load(wrow + k);
 #pragma unroll
                 for (int b = 0; b < B; b++) {
-                    const float4 xv = *reinterpret_cast<const float4 *>(sf + (size_t)b * n + k * 4);
-                    acc[b] += wv.x * xv.x + wv.y * xv.y + wv.z * xv.z + wv.w * xv.w;
+                    const float4 xv = *reinterpret_cast<const float4 *>(actF + (size_t)b * ldx + k * 4);
+                    acc[0][b] += wv.x * xv.x + wv.y * xv.y + wv.z * xv.z + wv.w * xv.w;
                 }
             }
         }
 #pragma unroll
-        for (int b = 0; b < B; b++) acc[b] = groupSum<L>(acc[b]);
+        for (int r = 0; r < RG; r++)
+#pragma unroll
+            for (int b = 0; b < B; b++) acc[r][b] = groupSum<L>(acc[r][b]);
         if (li == 0) {
-            if constexpr (EPI == EPI_STORE) {
-                if (row < a.rows) {
 #pragma unroll
-                    for (int b = 0; b < B; b++) a.out[(size_t)b * a.ldOut + row] = acc[b];
+            for (int r = 0; r < RG; r++) {
+                const int row = rowOf(p, r);
+                if constexpr (EPI == EPI_STORE) {
+                    if (row < a.rows) {
+#pragma unroll
+                        for (int b = 0; b < B; b++) a.out[(size_t)b * a.ldOut + row] = acc[r][b];
+                    }
+                } else {
+#pragma unroll
+                    for (int b = 0; b < B; b++) res[b * R + (row - rowBase)] = acc[r][b];
                 }
-            } else {
-#pragma unroll
-                for (int b = 0; b < B; b++) res[b * R + p * RP + gi] = acc[b];
             }
         }
     }
@@ -246,9 +400,8 @@ __global__ __launch_bounds__(kThreads) void gemvKernel(GemvArgs a) {
     for (int i = tid; i < B * halfR; i += kThreads) {
         const int b = i / halfR, k = i % halfR;
         const int r0 = rowBase + 2 * k;
-        if (r0 >= a.rows) continue;
         const float v0 = res[b * R + 2 * k], v1 = res[b * R + 2 * k + 1];
-        if constexpr (EPI == EPI_ACT) {
+        if constexpr (EPI == EPI_ACT || EPI == EPI_ACT_Q80) {
             // interleaved rows: 2i = gate (w1), 2i+1 = up (w3)
             float g;
             if (a.act == 1) {
@@ -256,8 +409,13 @@ __global__ __launch_bounds__(kThreads) void gemvKernel(GemvArgs a) {
             } else {
                 g = 0.5f * v0 * (1.0f + tanhf(0.79788456080286535588f * v0 * (1.0f + 0.044715f * v0 * v0)));
             }
-            a.out[(size_t)b * a.ldOut + (r0 >> 1)] = g * v1;
+            if constexpr (EPI == EPI_ACT) {
+                if (r0 < a.rows) a.out[(size_t)b * a.ldOut + (r0 >> 1)] = g * v1;
+            } else {
+                hbuf[b * halfR + k] = g * v1;
+            }
         } else if constexpr (EPI == EPI_QKV) {
+            if (r0 >= a.rows) continue;
             const int p = a.pos[b];
             const int sl = a.slot[b];
             if (r0 < a.q0 + a.kv0) {
@@ -265,8 +423,7 @@ __global__ __launch_bounds__(kThreads) void gemvKernel(GemvArgs a) {
                 const float o0 = v0 * cs.x - v1 * cs.y;
                 const float o1 = v0 * cs.y + v1 * cs.x;
                 if (r0 < a.q0) {
-                    a.out[(size_t)b * a.ldOut + r0] = o0;
-                    a.out[(size_t)b * a.ldOut + r0 + 1] = o1;
+                    *reinterpret_cast<float2 *>(a.out + (size_t)b * a.ldOut + r0) = make_float2(o0, o1);
                 } else {
                     const size_t off = ((size_t)sl * a.seqLen + p) * a.kv0 + (r0 - a.q0);
                     if (a.kvBf16) {
@@ -287,6 +444,23 @@ __global__ __launch_bounds__(kThreads) void gemvKernel(GemvArgs a) {
             }
         }
     }
+    if constexpr (EPI == EPI_ACT_Q80) {
+        // quantize the workgroup's R/2 hidden units (a multiple of 32) into Q80 blocks
+        __syncthreads();
+        const int hBase = rowBase >> 1;
+        for (int i = tid; i < B * halfR; i += kThreads) {  // 32-lane groups = one block
+            const int b = i / halfR, k = i % halfR;
+            const float h = hbuf[b * halfR + k];
+            const float amax = groupMax<32>(fabsf(h));
+            const float d = amax / 127.0f;
+            const float id = d != 0.f ? 1.0f / d : 0.f;
+            int q = (int)rintf(h * id);
+            q = q > 127 ? 127 : (q < -127 ? -127 : q);
+            a.oq[(size_t)b * a.ldOut + hBase + k] = (int8_t)q;
+            const float qs = groupSum<32>((float)q);
+            if ((k & 31) == 0) a.os[(size_t)b * (a.ldOut >> 5) + ((hBase + k) >> 5)] = make_float2(roundF16(d), qs);
+        }
+    }
 }
 
 template <int L, int B, bool Q40>
@@ -296,11 +470,13 @@ static void gemvDispatchPE(const GemvArgs &a, int pro, int epi, size_t lds, int 
         hipLaunchKernelGGL((gemvKernel<L, B, P, E, Q40>), dim3(grid), dim3(kThreads), lds, s, a); \
         return;                                                                                \
     }
-    DL_GEMV_CASE(PRO_QUANT, EPI_STORE)
+    DL_GEMV_CASE(PRO_GLOBAL, EPI_STORE)
     DL_GEMV_CASE(PRO_RESNORM, EPI_STORE)
-    DL_GEMV_CASE(PRO_RESNORM, EPI_ACT)
     DL_GEMV_CASE(PRO_RESNORM, EPI_QKV)
-    DL_GEMV_CASE(PRO_QUANT, EPI_ACT)
+    DL_GEMV_CASE(PRO_RESNORM, EPI_ACT)
+    if constexpr (Q40) {
+        DL_GEMV_CASE(PRO_RESNORM, EPI_ACT_Q80)
+    }
 #undef DL_GEMV_CASE
 }
 
@@ -315,10 +491,10 @@ static void gemvDispatchB(const GemvArgs &a, int B, int pro, int epi, size_t lds
 }
 
 void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_t s) {
-    const int L = gemvLanesPerRow(a.n, q40);
-    const int R = (kThreads / L) * a.passes;
+    const int L = a.lanes > 0 ? a.lanes : gemvLanesPerRow(a.n, a.rows, B, q40);
+    const int R = (kThreads / L) * gemvRowGroup(B, q40) * a.passes;
     const int grid = (a.rows + R - 1) / R;
-    const size_t lds = gemvLdsBytes(a.n, B, q40, R);
+    const size_t lds = gemvLdsBytes(a.n, B, q40, R, pro);
     if (q40) {
         switch (L) {
             case 16: gemvDispatchB<16, true>(a, B, pro, epi, lds, grid, s); break;
@@ -336,7 +512,8 @@ void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_
 
 // ------------------------------------------------------------------------------------------------
 // Attention (decode / prefill rows): split the sequence [0, pos] into chunks, one workgroup per
-// (head group, chunk, row); online-softmax partials are merged by attnCombineKernel.
+// (head group, chunk, row). A single chunk writes the final output directly; with several chunks
+// each workgroup publishes its online-softmax partial and the last arriver combines them.
 // ------------------------------------------------------------------------------------------------
 int attnSplitGrid(int seqLen) {
     int g = (seqLen + 255) / 256;
@@ -389,11 +566,44 @@ __device__ __forceinline__ void loadKv(const void *base, size_t off, float (&v)[
     }
 }
 
+// Final output of HG heads from LDS fin[HG][HS] -> f32 or Q80 (32-element blocks) in global.
+template <int HG, int HS>
+__device__ __forceinline__ void attnWriteOut(const AttnArgs &a, int b, int head0, const float *fin) {
+    const int tid = threadIdx.x;
+    if (a.outQ) {
+        for (int i = tid; i < HG * HS; i += kThreads) {  // 32-lane groups = one Q80 block
+            const float v = fin[i];
+            const float amax = groupMax<32>(fabsf(v));
+            const float d = amax / 127.0f;
+            const float id = d != 0.f ? 1.0f / d : 0.f;
+            int q = (int)rintf(v * id);
+            q = q > 127 ? 127 : (q < -127 ? -127 : q);
+            const int col = head0 * HS + i;
+            a.outQ[(size_t)b * a.ldOut + col] = (int8_t)q;
+            const float qs = groupSum<32>((float)q);
+            if ((i & 31) == 0) a.outS[(size_t)b * (a.ldOut >> 5) + (col >> 5)] = make_float2(roundF16(d), qs);
+        }
+    } else {
+        for (int i = tid; i < HG * HS; i += kThreads) a.out[(size_t)b * a.ldOut + head0 * HS + i] = fin[i];
+    }
+}
+
+// Online-softmax merge of (m2, l2, o2) into (m, l, o).
+template <int D>
+__device__ __forceinline__ void softmaxMerge(float &m, float &l, float (&o)[D], float m2, float l2, const float (&o2)[D]) {
+    const float mn = fmaxf(m, m2);
+    const float c1 = mn == -INFINITY ? 0.f : __expf(m - mn);
+    const float c2 = mn == -INFINITY ? 0.f : __expf(m2 - mn);
+    l = l * c1 + l2 * c2;
+#pragma unroll
+    for (int i = 0; i < D; i++) o[i] = o[i] * c1 + o2[i] * c2;
+    m = mn;
+}
+
 template <int HG, int HS, bool BF16>
 __global__ __launch_bounds__(kThreads) void attnKernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int DPL = HS / 16;  // dims per lane in the score phase (16 lanes per position)
-    constexpr int DPV = HS / 64;  // dims per lane in the PV phase (one wave per position)
+    constexpr int DPL = HS / 16;  // dims per lane: 16 lanes cover one position's head vector
     const int b = blockIdx.z;
     const int pos = a.pos[b], sl = a.slot[b];
     const int len = pos + 1;
@@ -403,124 +613,166 @@ __global__ __launch_bounds__(kThreads) void attnKernel(AttnArgs a) {
     if (c >= nSplit) return;
     const int t0 = c * ch;
     const int t1 = min(t0 + ch, len);
-    const int nt = t1 - t0;
     const int head0 = blockIdx.x * HG;
     const int kvh = head0 / a.kvMul;
     const int tid = threadIdx.x, wave = tid / 64, lane = tid % 64;
-
-    float *qL = reinterpret_cast<float *>(smem);          // [HG][HS]
-    float *sL = qL + HG * HS;                              // [HG][chunkMax]
-    float *mlL = sL + HG * a.chunkMax;                     // [HG][2]
-    float *redL = mlL + 2 * HG + 2;                        // [4][HG][HS]
-
-    const float scale = 1.0f / sqrtf((float)HS);
-    for (int i = tid; i < HG * HS; i += kThreads) qL[i] = a.q[(size_t)b * a.ldq + head0 * HS + i] * scale;
-    __syncthreads();
-
-    // scores: 16 lanes per position
     const int g16 = tid / 16, l16 = tid % 16;
+
+    float *mW = reinterpret_cast<float *>(smem);    // [4][HG]
+    float *lW = mW + 4 * HG;                        // [4][HG]
+    float *oW = lW + 4 * HG;                        // [4][HG][HS]
+    float *redL = oW + 4 * HG * HS;                 // [HG][HS] final (unnormalized) o
+    float *mlL = redL + HG * HS;                    // [HG][2]
+    int *flagL = reinterpret_cast<int *>(mlL + 2 * HG);
+
+    // this lane's slice of the HG query heads (pre-scaled)
+    const float scale = 1.0f / sqrtf((float)HS);
     float qr[HG][DPL];
 #pragma unroll
-    for (int h = 0; h < HG; h++)
+    for (int h = 0; h < HG; h++) {
+        const float *qp = a.q + (size_t)b * a.ldq + (head0 + h) * HS + l16 * DPL;
 #pragma unroll
-        for (int i = 0; i < DPL; i++) qr[h][i] = qL[h * HS + l16 * DPL + i];
+        for (int i = 0; i < DPL; i++) qr[h][i] = qp[i] * scale;
+    }
+    float m[HG], l[HG], o[HG][DPL];
+#pragma unroll
+    for (int h = 0; h < HG; h++) {
+        m[h] = -INFINITY;
+        l[h] = 0.f;
+#pragma unroll
+        for (int i = 0; i < DPL; i++) o[h][i] = 0.f;
+    }
+    // each 16-lane group walks positions g16, g16+16, ... with a running softmax
     const size_t slotBase = (size_t)sl * a.seqLen;
-    for (int t = t0 + g16; t < t1; t += kThreads / 16) {
-        float kv[DPL];
-        loadKv<DPL, BF16>(a.kcache, (slotBase + t) * a.kv0 + kvh * HS + l16 * DPL, kv);
+    // 4 positions per group are loaded before any is consumed (one memory latency per 64 keys)
+    constexpr int TU = 4;
+    for (int tb = t0 + g16; tb < t1; tb += TU * (kThreads / 16)) {
+        float kv[TU][DPL], vv[TU][DPL];
+#pragma unroll
+        for (int u = 0; u < TU; u++) {
+            const int t = min(tb + u * (kThreads / 16), t1 - 1);  // clamped: no divergent loads
+            const size_t off = (slotBase + t) * a.kv0 + kvh * HS + l16 * DPL;
+            loadKv<DPL, BF16>(a.kcache, off, kv[u]);
+            loadKv<DPL, BF16>(a.vcache, off, vv[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < TU; u++) {
+            if (tb + u * (kThreads / 16) >= t1) break;  // uniform within the 16-lane group
+#pragma unroll
+            for (int h = 0; h < HG; h++) {
+                float d = 0.f;
+#pragma unroll
+                for (int i = 0; i < DPL; i++) d += qr[h][i] * kv[u][i];
+                d = groupSum<16>(d);
+                const float mn = fmaxf(m[h], d);
+                const float corr = __expf(m[h] - mn);  // m = -inf first time -> 0
+                const float p = __expf(d - mn);
+                l[h] = l[h] * corr + p;
+#pragma unroll
+                for (int i = 0; i < DPL; i++) o[h][i] = o[h][i] * corr + p * vv[u][i];
+                m[h] = mn;
+            }
+        }
+    }
+    // merge the 4 position groups of each wave (lanes l, l^16, l^32, l^48 share dims)
+#pragma unroll
+    for (int off = 16; off <= 32; off <<= 1) {
 #pragma unroll
         for (int h = 0; h < HG; h++) {
-            float d = 0.f;
+            const float m2 = __shfl_xor(m[h], off), l2 = __shfl_xor(l[h], off);
+            float o2[DPL];
 #pragma unroll
-            for (int i = 0; i < DPL; i++) d += qr[h][i] * kv[i];
-            d = groupSum<16>(d);
-            if (l16 == 0) sL[h * a.chunkMax + (t - t0)] = d;
+            for (int i = 0; i < DPL; i++) o2[i] = __shfl_xor(o[h][i], off);
+            softmaxMerge<DPL>(m[h], l[h], o[h], m2, l2, o2);
+        }
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int h = 0; h < HG; h++) {
+            if (lane == 0) {
+                mW[wave * HG + h] = m[h];
+                lW[wave * HG + h] = l[h];
+            }
+#pragma unroll
+            for (int i = 0; i < DPL; i++) oW[(wave * HG + h) * HS + lane * DPL + i] = o[h][i];
+        }
+    }
+    __syncthreads();
+    // merge the 4 waves
+    for (int i = tid; i < HG * HS; i += kThreads) {
+        const int h = i / HS;
+        float M = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < 4; w++) M = fmaxf(M, mW[w * HG + h]);
+        float acc = 0.f, Ls = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const float e = M == -INFINITY ? 0.f : __expf(mW[w * HG + h] - M);
+            acc += e * oW[(w * HG + h) * HS + (i % HS)];
+            Ls += e * lW[w * HG + h];
+        }
+        redL[i] = acc;
+        if (i % HS == 0) {
+            mlL[h * 2] = M;
+            mlL[h * 2 + 1] = Ls;
         }
     }
     __syncthreads();
 
-    // local softmax per head (one wave per head)
-    for (int h = wave; h < HG; h += kThreads / 64) {
-        float m = -INFINITY;
-        for (int i = lane; i < nt; i += 64) m = fmaxf(m, sL[h * a.chunkMax + i]);
-        m = waveMax(m);
-        float l = 0.f;
-        for (int i = lane; i < nt; i += 64) {
-            const float e = __expf(sL[h * a.chunkMax + i] - m);
-            sL[h * a.chunkMax + i] = e;
-            l += e;
-        }
-        l = waveSum(l);
-        if (lane == 0) {
-            mlL[h * 2] = m;
-            mlL[h * 2 + 1] = l;
-        }
+    if (nSplit == 1) {
+        for (int i = tid; i < HG * HS; i += kThreads) redL[i] = redL[i] / mlL[(i / HS) * 2 + 1];
+        __syncthreads();
+        attnWriteOut<HG, HS>(a, b, head0, redL);
+        return;
+    }
+
+    // publish this chunk's partial, count arrivals; the last workgroup combines
+    const size_t pbase = ((size_t)b * a.nHeads0 + head0) * a.splitGrid;
+    for (int i = tid; i < HG * HS; i += kThreads) {
+        const int h = i / HS, d = i % HS;
+        a.partO[((pbase + (size_t)h * a.splitGrid) + c) * HS + d] = redL[i];
+    }
+    if (tid < HG) {
+        a.partML[((pbase + (size_t)tid * a.splitGrid) + c) * 2] = mlL[tid * 2];
+        a.partML[((pbase + (size_t)tid * a.splitGrid) + c) * 2 + 1] = mlL[tid * 2 + 1];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int *cnt = a.counters + (size_t)b * gridDim.x + blockIdx.x;
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flagL[0] = old == nSplit - 1;
     }
     __syncthreads();
-
-    // P.V: wave w takes positions t0+w, t0+w+4, ...; lanes cover the head dims
-    float o[HG][DPV];
-#pragma unroll
-    for (int h = 0; h < HG; h++)
-#pragma unroll
-        for (int i = 0; i < DPV; i++) o[h][i] = 0.f;
-#pragma unroll 2
-    for (int t = wave; t < nt; t += kThreads / 64) {
-        float vv[DPV];
-        loadKv<DPV, BF16>(a.vcache, (slotBase + t0 + t) * a.kv0 + kvh * HS + lane * DPV, vv);
-#pragma unroll
-        for (int h = 0; h < HG; h++) {
-            const float p = sL[h * a.chunkMax + t];
-#pragma unroll
-            for (int i = 0; i < DPV; i++) o[h][i] += p * vv[i];
-        }
+    if (!flagL[0]) return;
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-#pragma unroll
-    for (int h = 0; h < HG; h++)
-#pragma unroll
-        for (int i = 0; i < DPV; i++) redL[(wave * HG + h) * HS + lane * DPV + i] = o[h][i];
     __syncthreads();
     for (int i = tid; i < HG * HS; i += kThreads) {
         const int h = i / HS, d = i % HS;
-        const float s = redL[(0 * HG + h) * HS + d] + redL[(1 * HG + h) * HS + d] + redL[(2 * HG + h) * HS + d] +
-                        redL[(3 * HG + h) * HS + d];
-        const size_t pidx = ((size_t)b * a.nHeads0 + head0 + h) * a.splitGrid + c;
-        a.partO[pidx * HS + d] = s;
-        if (d == 0) {
-            a.partML[pidx * 2] = mlL[h * 2];
-            a.partML[pidx * 2 + 1] = mlL[h * 2 + 1];
+        const float *ml = a.partML + (pbase + (size_t)h * a.splitGrid) * 2;
+        float M = -INFINITY;
+        for (int cc = 0; cc < nSplit; cc++) M = fmaxf(M, ml[cc * 2]);
+        float Ls = 0.f, acc = 0.f;
+        for (int cc = 0; cc < nSplit; cc++) {
+            const float w = M == -INFINITY ? 0.f : __expf(ml[cc * 2] - M);
+            Ls += w * ml[cc * 2 + 1];
+            acc += w * a.partO[((pbase + (size_t)h * a.splitGrid) + cc) * HS + d];
         }
+        redL[i] = acc / Ls;
     }
-}
-
-template <int HS>
-__global__ __launch_bounds__(64) void attnCombineKernel(AttnArgs a) {
-    constexpr int DPV = HS / 64;
-    const int head = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
-    const int len = a.pos[b] + 1;
-    int nSplit, ch;
-    attnSplit(len, a.splitGrid, nSplit, ch);
-    const size_t base = ((size_t)b * a.nHeads0 + head) * a.splitGrid;
-    float M = -INFINITY;
-    for (int c = 0; c < nSplit; c++) M = fmaxf(M, a.partML[(base + c) * 2]);
-    float o[DPV];
-#pragma unroll
-    for (int i = 0; i < DPV; i++) o[i] = 0.f;
-    float Lsum = 0.f;
-    for (int c = 0; c < nSplit; c++) {
-        const float w = __expf(a.partML[(base + c) * 2] - M);
-        Lsum += w * a.partML[(base + c) * 2 + 1];
-#pragma unroll
-        for (int i = 0; i < DPV; i++) o[i] += w * a.partO[(base + c) * HS + lane * DPV + i];
-    }
-    const float inv = 1.0f / Lsum;
-#pragma unroll
-    for (int i = 0; i < DPV; i++) a.out[(size_t)b * a.ldOut + head * HS + lane * DPV + i] = o[i] * inv;
+    __syncthreads();
+    attnWriteOut<HG, HS>(a, b, head0, redL);
 }
 
 template <int HS, bool BF16>
 static void attnDispatchHG(const AttnArgs &a, int B, int HG, hipStream_t s) {
-    const size_t lds = sizeof(float) * ((size_t)HG * HS + (size_t)HG * a.chunkMax + 2 * HG + 2 + 4 * HG * HS);
+    const size_t lds = sizeof(float) * (8 * HG + 4 * HG * HS + HG * HS + 2 * HG) + 16;
     const dim3 grid(a.nHeads0 / HG, a.splitGrid, B);
     switch (HG) {
         case 1: hipLaunchKernelGGL((attnKernel<1, HS, BF16>), grid, dim3(kThreads), lds, s, a); break;
@@ -528,7 +780,6 @@ static void attnDispatchHG(const AttnArgs &a, int B, int HG, hipStream_t s) {
         case 4: hipLaunchKernelGGL((attnKernel<4, HS, BF16>), grid, dim3(kThreads), lds, s, a); break;
         default: hipLaunchKernelGGL((attnKernel<8, HS, BF16>), grid, dim3(kThreads), lds, s, a); break;
     }
-    hipLaunchKernelGGL((attnCombineKernel<HS>), dim3(a.nHeads0, B), dim3(64), 0, s, a);
 }
 
 void launchAttention(const AttnArgs &a, int B, hipStream_t s) {
@@ -557,47 +808,74 @@ void launchEmbedding(const float *table, const int *tokens, float *x, int dim, i
     hipLaunchKernelGGL(embeddingKernel, dim3(B), dim3(256), 0, s, table, tokens, x, dim);
 }
 
-__global__ __launch_bounds__(1024) void argmaxKernel(const float *logits, int vocab, int *out) {
-    __shared__ float sv[16];
-    __shared__ int si[16];
-    const int b = blockIdx.x;
-    const float *x = logits + (size_t)b * vocab;
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int i = threadIdx.x; i < vocab; i += blockDim.x) {
-        const float v = x[i];
-        if (v > bv) {
-            bv = v;
-            bi = i;
-        }
+__device__ __forceinline__ void argBetter(float &bv, int &bi, float ov, int oi) {
+    if (ov > bv || (ov == bv && oi < bi)) {
+        bv = ov;
+        bi = oi;
     }
+}
+
+__device__ __forceinline__ void blockArgmax(float &bv, int &bi, float *sv, int *si) {
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const float ov = __shfl_xor(bv, off);
-        const int oi = __shfl_xor(bi, off);
-        if (ov > bv || (ov == bv && oi < bi)) {
-            bv = ov;
-            bi = oi;
-        }
-    }
+    for (int off = 32; off >= 1; off >>= 1) argBetter(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
     const int w = threadIdx.x / 64;
+    __syncthreads();
     if (threadIdx.x % 64 == 0) {
         sv[w] = bv;
         si[w] = bi;
     }
     __syncthreads();
+    if (threadIdx.x == 0)
+        for (int i = 1; i < (int)(blockDim.x / 64); i++) argBetter(bv, bi, sv[i], si[i]);
+}
+
+constexpr int kArgmaxBlocks = 64;
+
+// grid (kArgmaxBlocks, B): each workgroup reduces a slice; the last arriver reduces the partials.
+__global__ __launch_bounds__(256) void argmaxKernel(ArgmaxArgs a) {
+    __shared__ float sv[4];
+    __shared__ int si[4];
+    __shared__ int last;
+    const int b = blockIdx.y;
+    const float *x = a.logits + (size_t)b * a.vocab;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.vocab; i += gridDim.x * blockDim.x) argBetter(bv, bi, x[i], i);
+    blockArgmax(bv, bi, sv, si);
     if (threadIdx.x == 0) {
-        for (int i = 1; i < (int)(blockDim.x / 64); i++)
-            if (sv[i] > bv || (sv[i] == bv && si[i] < bi)) {
-                bv = sv[i];
-                bi = si[i];
-            }
-        out[b] = bi;
+        a.partV[b * kArgmaxBlocks + blockIdx.x] = bv;
+        a.partI[b * kArgmaxBlocks + blockIdx.x] = bi;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(a.counters + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = old == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(a.counters + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    bv = -INFINITY;
+    bi = 0x7fffffff;
+    for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x)
+        argBetter(bv, bi, a.partV[b * kArgmaxBlocks + i], a.partI[b * kArgmaxBlocks + i]);
+    blockArgmax(bv, bi, sv, si);
+    if (threadIdx.x == 0) {
+        a.ids[b] = bi;
+        if (a.tokens) {
+            const int p = a.pos[b];
+            a.hist[(size_t)b * a.seqLen + p] = bi;
+            a.tokens[b] = bi;
+            a.pos[b] = p + 1;
+        }
     }
 }
 
-void launchArgmax(const float *logits, int vocab, int B, int *outIds, hipStream_t s) {
-    hipLaunchKernelGGL(argmaxKernel, dim3(B), dim3(1024), 0, s, logits, vocab, outIds);
+void launchArgmax(const ArgmaxArgs &a, int B, hipStream_t s) {
+    hipLaunchKernelGGL(argmaxKernel, dim3(kArgmaxBlocks, B), dim3(256), 0, s, a);
 }
 
 __global__ void unshardKernel(const float *in, float *out, int nRanks, int B, int vocab0) {
@@ -612,18 +890,6 @@ __global__ void unshardKernel(const float *in, float *out, int nRanks, int B, in
 
 void launchUnshardLogits(const float *in, float *out, int nRanks, int B, int vocab0, hipStream_t s) {
     hipLaunchKernelGGL(unshardKernel, dim3(1024), dim3(256), 0, s, in, out, nRanks, B, vocab0);
-}
-
-__global__ void advanceKernel(const int *ids, int *tokens, int *pos, int B) {
-    const int b = threadIdx.x;
-    if (b < B) {
-        tokens[b] = ids[b];
-        pos[b] += 1;
-    }
-}
-
-void launchAdvance(const int *ids, int *tokens, int *pos, int B, hipStream_t s) {
-    hipLaunchKernelGGL(advanceKernel, dim3(1), dim3(64), 0, s, ids, tokens, pos, B);
 }
 
 __device__ __forceinline__ uint64_t splitmix(uint64_t x) {

@@ -281,6 +281,10 @@ PYBIND11_MODULE(_C, m) {
           py::arg("model"), py::arg("buffer_type") = "q80", py::arg("nthreads") = 1, py::arg("max_seq_len") = 0,
           py::arg("max_batch") = 32, py::arg("n_slots") = 1);
 
+    m.def("bench_gemv_q40", &benchGemvQ40, py::arg("rows"), py::arg("n"), py::arg("pro"), py::arg("epi"),
+          py::arg("batch") = 1, py::arg("lanes") = 0, py::arg("passes") = 1, py::arg("copies") = 8,
+          py::arg("iters") = 200, py::call_guard<py::gil_scoped_release>());
+
     m.def("rccl_unique_id", []() {
         auto v = rcclGetUniqueId();
         return py::bytes(std::string(v.begin(), v.end()));
