@@ -201,15 +201,15 @@ void InferenceSession::forwardArgmax(int n, const int *tokens, const int *positi
     backend_->forwardArgmax(n, tokens, positions, slots, out);
 }
 
-ForwardStats InferenceSession::lastStats() const {
+ForwardStats InferenceSession::lastStats() {
+    // bytes since the previous call (the reference resets its counters on read, nn-network.cpp:493-501);
+    // on GPUs the RCCL traffic is not visible here, only the control plane.
     ForwardStats s = backend_->lastStats();
-    if (!workers_.empty() && gpu_) {
-        // RCCL traffic is not visible to the sockets; report control bytes only
-        s.sentBytes = s.recvBytes = 0;
-        for (auto &w : workers_) {
-            s.sentBytes += w.sentBytes();
-            s.recvBytes += w.recvBytes();
-        }
+    s.sentBytes = s.recvBytes = 0;
+    for (auto &w : workers_) {
+        s.sentBytes += w.sentBytes();
+        s.recvBytes += w.recvBytes();
+        w.resetStats();
     }
     return s;
 }

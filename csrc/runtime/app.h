@@ -61,7 +61,7 @@ class InferenceSession {
     // logits: [n][vocab]
     void forward(int n, const int *tokens, const int *positions, const int *slots, float *logits);
     void forwardArgmax(int n, const int *tokens, const int *positions, const int *slots, int *out);
-    ForwardStats lastStats() const;
+    ForwardStats lastStats();
     void finish();  // stop workers (they return to listening)
 
   private:

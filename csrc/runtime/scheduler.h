@@ -1,0 +1,96 @@
+// Multi-user continuous-batching scheduler (replaces the reference's Request/RequestQueue +
+// inference_loop, src/Request.hpp:11-64, src/app.cpp:314-402).
+//
+// Fixes the reference defects SURVEY §2.9 Q1-Q5: every request owns a KV-cache slot and its own
+// positions; prompts are really prefilled (chunked, mixed with other requests' decode rows in the
+// same forward); each request has its own sampler/seed/temperature/stop strings and UTF-8 decoder;
+// the loop has a lifecycle (stop()) and the API front end is concurrent.
+#pragma once
+
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "app.h"
+
+namespace dl {
+
+struct GenParams {
+    int maxTokens = 128;      // reference default (Request.hpp:33); <= 0 = until EOS / context end
+    float temperature = 0.8f;
+    float topp = 0.9f;
+    u64 seed = 0;
+    std::vector<std::string> stop;  // extra stop strings
+};
+
+class GenRequest {
+  public:
+    u64 id = 0;
+    std::vector<int> prompt;
+    GenParams params;
+
+    // ---- results (guarded by mu) ----
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::string> deltas;  // streamed text pieces not yet consumed
+    std::string text;                // full generated text
+    std::string finishReason;        // "stop" | "length" | "error"
+    std::string error;
+    bool done = false;
+    int completionTokens = 0;
+
+    // Blocks until finished; returns the full text.
+    std::string wait();
+    // Pops the next delta (blocking); returns false once the request is done and drained.
+    bool nextDelta(std::string &out);
+
+  private:
+    friend class Scheduler;
+    int slot = -1;
+    size_t prefilled = 0;
+    std::vector<int> generated;
+    std::unique_ptr<Sampler> sampler;
+    std::unique_ptr<TokenDecoder> decoder;
+    std::unique_ptr<EosDetector> eos;
+    void emit(const std::string &d);
+    void finish(const std::string &reason);
+};
+
+struct SchedulerStats {
+    u64 forwards = 0, rows = 0, prefillRows = 0, decodeRows = 0, completed = 0, generatedTokens = 0;
+    double busyMs = 0;
+    int active = 0, queued = 0;
+};
+
+class Scheduler {
+  public:
+    explicit Scheduler(InferenceSession &sess);
+    ~Scheduler();
+    std::shared_ptr<GenRequest> submit(std::vector<int> prompt, const GenParams &params);
+    void stop();
+    SchedulerStats stats();
+
+  private:
+    void loop();
+    bool step();  // one batched forward; false when idle
+
+    InferenceSession &sess_;
+    Tokenizer &tok_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::shared_ptr<GenRequest>> queue_;
+    std::vector<std::shared_ptr<GenRequest>> active_;
+    std::vector<int> freeSlots_;
+    bool stop_ = false;
+    u64 nextId_ = 1;
+    SchedulerStats stats_;
+    std::vector<float> logits_;
+    std::thread thread_;
+};
+
+}  // namespace dl

@@ -268,6 +268,22 @@ bool Tokenizer::decode(int token, std::string &out) {
     return flushUtf8(pending_, out);
 }
 
+bool TokenDecoder::decode(int token, std::string &out) {
+    out.clear();
+    if (token == t_.bosId()) return false;
+    if (t_.isEos(token)) {
+        if (!pending_.empty()) {
+            out = pending_;
+            pending_.clear();
+            return true;
+        }
+        return false;
+    }
+    DL_CHECK(token >= 0 && token < t_.vocabSize(), "token id out of range");
+    pending_.append(t_.piece(token));
+    return flushUtf8(pending_, out);
+}
+
 // ---------------------------------------------------------------- sampler
 
 u32 randomU32(u64 *state) {

@@ -57,6 +57,19 @@ class Tokenizer {
     std::string pending_;
 };
 
+// Per-sequence streaming decoder (the Tokenizer's own decode() keeps one shared buffer, like the
+// reference; concurrent requests each need their own UTF-8 carry-over).
+class TokenDecoder {
+  public:
+    explicit TokenDecoder(const Tokenizer &t) : t_(t) {}
+    bool decode(int token, std::string &out);
+    void reset() { pending_.clear(); }
+
+  private:
+    const Tokenizer &t_;
+    std::string pending_;
+};
+
 class Sampler {
   public:
     Sampler(int vocabSize, float temperature, float topp, u64 seed);

@@ -1,0 +1,108 @@
+"""dllama-api end-to-end on the CPU backend: OpenAI + reference response shapes, SSE streaming,
+/v1/models, and concurrent requests batched by the scheduler giving the same tokens as solo runs
+(the reference's shared-KV multi-user loop could not)."""
+import concurrent.futures
+import json
+import os
+import socket
+import subprocess
+import time
+import urllib.request
+
+import pytest
+
+from conftest import REPO
+
+API = os.path.join(REPO, "build", "dllama-api")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def server(assets):
+    port = _free_port()
+    proc = subprocess.Popen([API, "--model", assets["q40"], "--tokenizer", assets["tok"], "--buffer-float-type", "q80",
+                             "--port", str(port), "--nthreads", "2", "--slots", "4", "--temperature", "0",
+                             "--max-seq-len", "128"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+    url = f"http://127.0.0.1:{port}"
+    for _ in range(200):
+        try:
+            urllib.request.urlopen(url + "/health", timeout=1).read()
+            break
+        except Exception:
+            time.sleep(0.05)
+    else:
+        proc.kill()
+        raise RuntimeError("server did not start: " + proc.stdout.read().decode(errors="replace"))
+    yield url
+    proc.kill()
+    proc.wait()
+
+
+def _post(url, body, timeout=60):
+    req = urllib.request.Request(url + "/v1/chat/completions", data=json.dumps(body).encode(),
+                                 headers={"Content-Type": "application/json"})
+    return urllib.request.urlopen(req, timeout=timeout)
+
+
+def _chat(url, content, max_tokens=12, **kw):
+    body = {"messages": [{"role": "user", "content": content}], "max_tokens": max_tokens, "temperature": 0}
+    body.update(kw)
+    return json.loads(_post(url, body).read())
+
+
+def test_models(server):
+    d = json.loads(urllib.request.urlopen(server + "/v1/models").read())
+    assert d["object"] == "list" and d["data"][0]["id"].endswith(".m")
+
+
+def test_completion_shapes(server):
+    d = _chat(server, "hello world")
+    assert "generated_text" in d  # web-ui / reference shape
+    assert d["object"] == "chat.completion"
+    assert d["choices"][0]["message"]["content"] == d["generated_text"]
+    assert d["usage"]["completion_tokens"] <= 12
+    assert d["usage"]["total_tokens"] == d["usage"]["prompt_tokens"] + d["usage"]["completion_tokens"]
+    assert d["choices"][0]["finish_reason"] in ("stop", "length")
+
+
+def test_streaming_matches_blocking(server):
+    full = _chat(server, "the world")["generated_text"]
+    r = _post(server, {"messages": [{"role": "user", "content": "the world"}], "max_tokens": 12, "temperature": 0,
+                       "stream": True})
+    assert r.headers["Content-Type"].startswith("text/event-stream")
+    text, done, reasons = "", False, []
+    for raw in r.read().decode().split("\r\n\r\n"):
+        if not raw.startswith("data: "):
+            continue
+        payload = raw[6:]
+        if payload == "[DONE]":
+            done = True
+            continue
+        ch = json.loads(payload)
+        assert ch["object"] == "chat.completion.chunk"
+        text += ch["choices"][0]["delta"].get("content", "")
+        reasons.append(ch["choices"][0]["finish_reason"])
+    assert done and text == full and reasons[-1] in ("stop", "length")
+
+
+def test_concurrent_requests_match_solo(server):
+    prompts = ["hello", "the world", "and the", "hello world the end"]
+    solo = [_chat(server, p)["generated_text"] for p in prompts]
+    with concurrent.futures.ThreadPoolExecutor(8) as ex:
+        conc = list(ex.map(lambda p: _chat(server, p)["generated_text"], prompts * 2))
+    assert conc == solo * 2
+    h = json.loads(urllib.request.urlopen(server + "/health").read())
+    assert h["completed"] >= 12 and h["decode_rows"] > 0 and h["prefill_rows"] > 0
+
+
+def test_bad_request(server):
+    with pytest.raises(urllib.error.HTTPError) as e:
+        _post(server, {"nope": 1})
+    assert e.value.code == 400

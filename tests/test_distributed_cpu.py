@@ -1,0 +1,145 @@
+"""Multi-process tensor parallelism on the CPU backend (root + `dllama worker` processes on
+127.0.0.1, the reference's examples/n-workers.sh pattern) and fault handling:
+  * TP=2/4 greedy tokens == TP=1 (the reference never tested this)
+  * CLI output lines used by the benchmark parser (dllama.cpp:57-113)
+  * a worker killed mid-run -> clean root error; a worker whose root died re-serves."""
+import os
+import re
+import signal
+import socket
+import subprocess
+import time
+
+import pytest
+
+from conftest import REPO
+
+DLLAMA = os.path.join(REPO, "build", "dllama")
+
+
+def _ports(n):
+    socks, ports = [], []
+    for _ in range(n):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        socks.append(s)
+        ports.append(s.getsockname()[1])
+    for s in socks:
+        s.close()
+    return ports
+
+
+def _workers(n, extra=()):
+    ports = _ports(n)
+    procs = [subprocess.Popen([DLLAMA, "worker", "--port", str(p), "--nthreads", "1", *extra],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for p in ports]
+    time.sleep(0.2)
+    return procs, [f"127.0.0.1:{p}" for p in ports]
+
+
+@pytest.fixture(scope="module")
+def kv4(tmp_path_factory, assets):
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    d = str(tmp_path_factory.mktemp("kv4"))
+    m, t, _ = make_test_assets(d, "tiny", FloatType.Q40, seq_len=128, seed=7, dim=512, n_heads=8, n_kv_heads=4,
+                               hidden_dim=1024)
+    return {"q40": m, "tok": t}
+
+
+def _inference(assets, workers=(), steps=16, extra=()):
+    cmd = [DLLAMA, "inference", "--model", assets["q40"], "--tokenizer", assets["tok"], "--buffer-float-type", "q80",
+           "--prompt", "hello world the", "--steps", str(steps), "--nthreads", "1", "--temperature", "0", *extra]
+    if workers:
+        cmd += ["--workers", *workers]
+    r = subprocess.run(cmd, capture_output=True, timeout=120)
+    return r.returncode, r.stdout.decode("utf-8", errors="replace")
+
+
+def _preds(out):
+    return [l.split("|")[-1] for l in out.splitlines() if l.startswith("🔶 Pred")]
+
+
+def test_cli_output_lines(assets):
+    rc, out = _inference(assets, steps=12)
+    assert rc == 0, out
+    assert re.search(r"🔷️ Eval\s+\d+ ms Sync\s+\d+ ms \| Sent\s+\d+ kB Recv\s+\d+ kB \| \(\d+ tokens\)", out)
+    n_eval = int(re.search(r"Evaluation\n\s+nBatches: \d+\n\s+nTokens: (\d+)", out).group(1))
+    assert len(_preds(out)) == 12 - n_eval
+    assert re.search(r"Evaluation\n\s+nBatches: 32\n\s+nTokens: \d+\n\s+tokens/s: [\d.]+ \([\d.]+ ms/tok\)", out)
+    assert re.search(r"Prediction\n\s+nTokens: \d+\n\s+tokens/s: [\d.]+ \([\d.]+ ms/tok\)", out)
+
+
+@pytest.mark.parametrize("n_workers", [1, 3])
+def test_tensor_parallel_matches_single(kv4, n_workers):
+    assets = kv4
+    rc, ref = _inference(assets)
+    assert rc == 0, ref
+    procs, addrs = _workers(n_workers)
+    try:
+        rc, out = _inference(assets, addrs)
+        assert rc == 0, out
+        assert _preds(out) == _preds(ref)
+        # the workers got the stop signal and went back to listening
+        time.sleep(0.3)
+        for p in procs:
+            assert p.poll() is None
+    finally:
+        for p in procs:
+            p.kill()
+        logs = [p.communicate()[0].decode(errors="replace") for p in procs]
+    for l in logs:
+        assert "Stop signal" in l and l.count("Listening on port") >= 2
+
+
+def test_worker_killed_mid_run_gives_clean_error(assets):
+    procs, addrs = _workers(1)
+    try:
+        cmd = [DLLAMA, "inference", "--model", assets["q40"], "--tokenizer", assets["tok"], "--buffer-float-type",
+               "q80", "--prompt", "hello", "--steps", "127", "--nthreads", "1", "--temperature", "0", "--workers",
+               *addrs]
+        root = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+        # wait for decoding to start, then kill the worker
+        deadline = time.time() + 30
+        buf = b""
+        while time.time() < deadline and b"Pred" not in buf:
+            buf += root.stdout.read1(4096) if hasattr(root.stdout, "read1") else root.stdout.read(1)
+        procs[0].send_signal(signal.SIGKILL)
+        out = buf + root.communicate(timeout=60)[0]
+        text = out.decode(errors="replace")
+        assert root.returncode != 0 or "Prediction" in text
+        if root.returncode != 0:
+            assert "Critical error" in text
+    finally:
+        for p in procs:
+            p.kill()
+
+
+def test_worker_reserves_after_root_dies(assets):
+    procs, addrs = _workers(1)
+    try:
+        root = subprocess.Popen([DLLAMA, "inference", "--model", assets["q40"], "--tokenizer", assets["tok"],
+                                 "--buffer-float-type", "q80", "--prompt", "hello", "--steps", "127", "--nthreads", "1",
+                                 "--temperature", "0", "--workers", *addrs], stdout=subprocess.PIPE,
+                                stderr=subprocess.STDOUT)
+        time.sleep(1.0)
+        root.kill()
+        root.wait()
+        time.sleep(0.5)
+        # the same worker serves a fresh root
+        rc, out = _inference(assets, addrs, steps=8)
+        assert rc == 0, out
+    finally:
+        for p in procs:
+            p.kill()
+
+
+def test_too_many_nodes_rejected(assets):
+    # tiny model has 2 kv heads: 3 nodes must be refused (app.cpp:237-238)
+    procs, addrs = _workers(2)
+    try:
+        rc, out = _inference(assets, addrs)
+        assert rc != 0 and "more nodes than the number of KV heads" in out
+    finally:
+        for p in procs:
+            p.kill()
