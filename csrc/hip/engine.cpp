@@ -412,23 +412,50 @@ class HipEngineImpl : public HipEngine {
     }
 
     void runGraph(int n, GraphKind kind) {
-        if (!cfg_.useGraphs) {
+        if (!cfg_.useGraphs || graphsBroken_) {
             enqueueForward(n, kind);
             return;
         }
         const int key = n * 4 + (int)kind;
         auto it = graphs_.find(key);
         if (it == graphs_.end()) {
-            hipGraph_t g;
-            DL_HIP(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
-            enqueueForward(n, kind);
-            DL_HIP(hipStreamEndCapture(stream_, &g));
-            hipGraphExec_t ge;
-            DL_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-            DL_HIP(hipGraphDestroy(g));
+            hipGraphExec_t ge = captureForward(n, kind);
+            if (!ge) {
+                // e.g. a collective library build that cannot be stream-captured: stay correct, run eagerly
+                graphsBroken_ = true;
+                std::fprintf(stderr, "⚠️  hipGraph capture failed; falling back to eager launches\n");
+                enqueueForward(n, kind);
+                return;
+            }
             it = graphs_.emplace(key, ge).first;
         }
         DL_HIP(hipGraphLaunch(it->second, stream_));
+    }
+
+    hipGraphExec_t captureForward(int n, GraphKind kind) {
+        hipGraph_t g = nullptr;
+        hipGraphExec_t ge = nullptr;
+        if (hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal) != hipSuccess) return nullptr;
+        bool ok = true;
+        try {
+            enqueueForward(n, kind);
+        } catch (const std::exception &e) {
+            std::fprintf(stderr, "capture error: %s\n", e.what());
+            ok = false;
+        }
+        const hipError_t ec = hipStreamEndCapture(stream_, &g);
+        if (ec != hipSuccess || !ok || !g) {
+            if (g) (void)hipGraphDestroy(g);
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        const hipError_t ei = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        if (ei != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        return ge;
     }
 
     // timing hook for profileForward (eager only)
@@ -655,6 +682,7 @@ class HipEngineImpl : public HipEngine {
     int splitGrid_ = 1, chunkMax_ = 256;
     std::map<int, hipGraphExec_t> graphs_;
     bool profile_ = false;
+    bool graphsBroken_ = false;
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> profTimes_;
 };
 

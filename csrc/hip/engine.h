@@ -3,6 +3,7 @@
 #pragma once
 
 #include <memory>
+#include <vector>
 
 #include "../runtime/backend.h"
 #include "device_comm.h"
@@ -33,4 +34,10 @@ int hipDeviceCount();
 // infinity cache) are cycled through a graph of `iters` launches. Returns microseconds per launch.
 double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int passes, int copies, int iters);
 
+}  // namespace dl
+
+namespace dl {
+// Test helper: `world` tensor-parallel ranks simulated on one GPU (host-staged collectives).
+// Returns rank 0's logits for single-token forwards of `tokens` at positions 0.., [n][vocab].
+std::vector<float> simulateTensorParallel(const EngineConfig &cfg, int world, const std::vector<int> &tokens);
 }  // namespace dl

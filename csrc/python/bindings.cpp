@@ -285,6 +285,23 @@ PYBIND11_MODULE(_C, m) {
           py::arg("batch") = 1, py::arg("lanes") = 0, py::arg("passes") = 1, py::arg("copies") = 8,
           py::arg("iters") = 200, py::call_guard<py::gil_scoped_release>());
 
+    m.def("simulate_tp",
+          [](const std::string &model, const std::string &bufferType, int world, std::vector<int> tokens, bool kvBf16,
+             int gpuIndex) {
+              EngineConfig c = makeConfig(model, bufferType, 1, 0, 8, 1, gpuIndex, false, kvBf16, py::none(), 1);
+              std::vector<float> out;
+              {
+                  py::gil_scoped_release rel;
+                  out = simulateTensorParallel(c, world, tokens);
+              }
+              const size_t vocab = out.size() / tokens.size();
+              py::array_t<float> a({(py::ssize_t)tokens.size(), (py::ssize_t)vocab});
+              std::memcpy(a.mutable_data(), out.data(), out.size() * 4);
+              return a;
+          },
+          py::arg("model"), py::arg("buffer_type"), py::arg("world"), py::arg("tokens"), py::arg("kv_bf16") = false,
+          py::arg("gpu_index") = 0);
+
     m.def("rccl_unique_id", []() {
         auto v = rcclGetUniqueId();
         return py::bytes(std::string(v.begin(), v.end()));

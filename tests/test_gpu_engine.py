@@ -116,3 +116,25 @@ def test_synthetic_8b_shape_smoke(C):
     assert np.isfinite(lg).all() and lg.std() > 0
     ms, toks = g.decode_greedy(8, [1], [1], [0])
     assert len(toks) == 8 and all(0 <= t < 128256 for t in toks)
+
+
+@pytest.fixture(scope="module")
+def kv4_gpu(tmp_path_factory):
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    d = str(tmp_path_factory.mktemp("kv4g"))
+    # head size 64, 4 kv heads, hidden shard 1024/4 = 256: exercises Q80 and f32 h hand-offs
+    m, t, _ = make_test_assets(d, "tiny", FloatType.Q40, seq_len=128, seed=9, dim=512, n_heads=8, n_kv_heads=4,
+                               hidden_dim=1024, vocab_size=1024)
+    return m
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_simulated_tensor_parallel_matches_single(C, kv4_gpu, world):
+    """N ranks (threads) on one GPU with host-staged collectives: same logits as TP=1."""
+    tokens = [5, 99, 300, 7, 1000, 2]
+    single = C.HipEngine(kv4_gpu, "q80", kv_bf16=False)
+    ref = np.stack([single.forward([t], [p], [0])[0] for p, t in enumerate(tokens)])
+    got = C.simulate_tp(kv4_gpu, "q80", world, tokens)
+    assert _rel(got, ref) < 3e-2
+    assert (got.argmax(-1) == ref.argmax(-1)).all()
