@@ -567,11 +567,11 @@ __device__ __forceinline__ void loadKv(const void *base, size_t off, float (&v)[
 }
 
 // Final output of HG heads from LDS fin[HG][HS] -> f32 or Q80 (32-element blocks) in global.
-template <int HG, int HS>
+template <int HG, int HS, int AT>
 __device__ __forceinline__ void attnWriteOut(const AttnArgs &a, int b, int head0, const float *fin) {
     const int tid = threadIdx.x;
     if (a.outQ) {
-        for (int i = tid; i < HG * HS; i += kThreads) {  // 32-lane groups = one Q80 block
+        for (int i = tid; i < HG * HS; i += AT) {  // 32-lane groups = one Q80 block
             const float v = fin[i];
             const float amax = groupMax<32>(fabsf(v));
             const float d = amax / 127.0f;
@@ -584,7 +584,7 @@ __device__ __forceinline__ void attnWriteOut(const AttnArgs &a, int b, int head0
             if ((i & 31) == 0) a.outS[(size_t)b * (a.ldOut >> 5) + (col >> 5)] = make_float2(roundF16(d), qs);
         }
     } else {
-        for (int i = tid; i < HG * HS; i += kThreads) a.out[(size_t)b * a.ldOut + head0 * HS + i] = fin[i];
+        for (int i = tid; i < HG * HS; i += AT) a.out[(size_t)b * a.ldOut + head0 * HS + i] = fin[i];
     }
 }
 
@@ -600,10 +600,15 @@ __device__ __forceinline__ void softmaxMerge(float &m, float &l, float (&o)[D], 
     m = mn;
 }
 
+static constexpr int kAttnThreads = 512;  // 8 waves = 32 groups of 16 lanes, one key per group
+
 template <int HG, int HS, bool BF16>
-__global__ __launch_bounds__(kThreads) void attnKernel(AttnArgs a) {
+__global__ __launch_bounds__(kAttnThreads) void attnKernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int DPL = HS / 16;  // dims per lane: 16 lanes cover one position's head vector
+    constexpr int AT = kAttnThreads, NW = AT / 64, NG = AT / 16;
+    constexpr int DPL = HS / 16;           // dims per lane: 16 lanes cover one position's head vector
+    constexpr int TU = BF16 ? 8 : 4;       // keys per group loaded before any is consumed
+    constexpr int RW = BF16 ? DPL / 2 : DPL;  // 32-bit words per lane per key (packed bf16 pairs)
     const int b = blockIdx.z;
     const int pos = a.pos[b], sl = a.slot[b];
     const int len = pos + 1;
@@ -618,21 +623,27 @@ __global__ __launch_bounds__(kThreads) void attnKernel(AttnArgs a) {
     const int tid = threadIdx.x, wave = tid / 64, lane = tid % 64;
     const int g16 = tid / 16, l16 = tid % 16;
 
-    float *mW = reinterpret_cast<float *>(smem);    // [4][HG]
-    float *lW = mW + 4 * HG;                        // [4][HG]
-    float *oW = lW + 4 * HG;                        // [4][HG][HS]
-    float *redL = oW + 4 * HG * HS;                 // [HG][HS] final (unnormalized) o
+    float *mW = reinterpret_cast<float *>(smem);    // [NW][HG]
+    float *lW = mW + NW * HG;                       // [NW][HG]
+    float *oW = lW + NW * HG;                       // [NW][HG][HS]
+    float *redL = oW + NW * HG * HS;                // [HG][HS] final (unnormalized) o
     float *mlL = redL + HG * HS;                    // [HG][2]
     int *flagL = reinterpret_cast<int *>(mlL + 2 * HG);
 
-    // this lane's slice of the HG query heads (pre-scaled)
+    // this lane's slice of the HG query heads (pre-scaled), vector loads
     const float scale = 1.0f / sqrtf((float)HS);
     float qr[HG][DPL];
 #pragma unroll
     for (int h = 0; h < HG; h++) {
         const float *qp = a.q + (size_t)b * a.ldq + (head0 + h) * HS + l16 * DPL;
 #pragma unroll
-        for (int i = 0; i < DPL; i++) qr[h][i] = qp[i] * scale;
+        for (int i = 0; i < DPL; i += 4) {
+            const float4 v = ld4(qp + i);
+            qr[h][i] = v.x * scale;
+            qr[h][i + 1] = v.y * scale;
+            qr[h][i + 2] = v.z * scale;
+            qr[h][i + 3] = v.w * scale;
+        }
     }
     float m[HG], l[HG], o[HG][DPL];
 #pragma unroll
@@ -642,34 +653,66 @@ __global__ __launch_bounds__(kThreads) void attnKernel(AttnArgs a) {
 #pragma unroll
         for (int i = 0; i < DPL; i++) o[h][i] = 0.f;
     }
-    // each 16-lane group walks positions g16, g16+16, ... with a running softmax
+    // each 16-lane group walks keys g16, g16+NG, ... with a running softmax; TU keys per group are
+    // in flight at once (NG*TU = 256 keys per memory round trip for bf16 caches)
     const size_t slotBase = (size_t)sl * a.seqLen;
-    // 4 positions per group are loaded before any is consumed (one memory latency per 64 keys)
-    constexpr int TU = 4;
-    for (int tb = t0 + g16; tb < t1; tb += TU * (kThreads / 16)) {
-        float kv[TU][DPL], vv[TU][DPL];
+    for (int tb = t0 + g16; tb < t1; tb += TU * NG) {
+        uint32_t kr[TU][RW], vr[TU][RW];
 #pragma unroll
         for (int u = 0; u < TU; u++) {
-            const int t = min(tb + u * (kThreads / 16), t1 - 1);  // clamped: no divergent loads
+            const int t = min(tb + u * NG, t1 - 1);  // clamped: no divergent loads
             const size_t off = (slotBase + t) * a.kv0 + kvh * HS + l16 * DPL;
-            loadKv<DPL, BF16>(a.kcache, off, kv[u]);
-            loadKv<DPL, BF16>(a.vcache, off, vv[u]);
+            const uint32_t *kp = reinterpret_cast<const uint32_t *>(
+                BF16 ? (const void *)(reinterpret_cast<const uint16_t *>(a.kcache) + off)
+                     : (const void *)(reinterpret_cast<const float *>(a.kcache) + off));
+            const uint32_t *vp = reinterpret_cast<const uint32_t *>(
+                BF16 ? (const void *)(reinterpret_cast<const uint16_t *>(a.vcache) + off)
+                     : (const void *)(reinterpret_cast<const float *>(a.vcache) + off));
+            if constexpr (RW == 4) {
+                const uint4 k4 = *reinterpret_cast<const uint4 *>(kp), v4 = *reinterpret_cast<const uint4 *>(vp);
+                kr[u][0] = k4.x; kr[u][1] = k4.y; kr[u][2] = k4.z; kr[u][3] = k4.w;
+                vr[u][0] = v4.x; vr[u][1] = v4.y; vr[u][2] = v4.z; vr[u][3] = v4.w;
+            } else if constexpr (RW == 8) {
+                const uint4 k0 = reinterpret_cast<const uint4 *>(kp)[0], k1 = reinterpret_cast<const uint4 *>(kp)[1];
+                const uint4 v0 = reinterpret_cast<const uint4 *>(vp)[0], v1 = reinterpret_cast<const uint4 *>(vp)[1];
+                kr[u][0] = k0.x; kr[u][1] = k0.y; kr[u][2] = k0.z; kr[u][3] = k0.w;
+                kr[u][4] = k1.x; kr[u][5] = k1.y; kr[u][6] = k1.z; kr[u][7] = k1.w;
+                vr[u][0] = v0.x; vr[u][1] = v0.y; vr[u][2] = v0.z; vr[u][3] = v0.w;
+                vr[u][4] = v1.x; vr[u][5] = v1.y; vr[u][6] = v1.z; vr[u][7] = v1.w;
+            } else {
+                const uint2 k2 = *reinterpret_cast<const uint2 *>(kp), v2 = *reinterpret_cast<const uint2 *>(vp);
+                kr[u][0] = k2.x; kr[u][1] = k2.y;
+                vr[u][0] = v2.x; vr[u][1] = v2.y;
+            }
         }
 #pragma unroll
         for (int u = 0; u < TU; u++) {
-            if (tb + u * (kThreads / 16) >= t1) break;  // uniform within the 16-lane group
+            if (tb + u * NG >= t1) break;  // uniform within the 16-lane group
+            float kv[DPL], vv[DPL];
+#pragma unroll
+            for (int w = 0; w < RW; w++) {
+                if constexpr (BF16) {
+                    kv[2 * w] = __uint_as_float(kr[u][w] << 16);
+                    kv[2 * w + 1] = __uint_as_float(kr[u][w] & 0xFFFF0000u);
+                    vv[2 * w] = __uint_as_float(vr[u][w] << 16);
+                    vv[2 * w + 1] = __uint_as_float(vr[u][w] & 0xFFFF0000u);
+                } else {
+                    kv[w] = __uint_as_float(kr[u][w]);
+                    vv[w] = __uint_as_float(vr[u][w]);
+                }
+            }
 #pragma unroll
             for (int h = 0; h < HG; h++) {
                 float d = 0.f;
 #pragma unroll
-                for (int i = 0; i < DPL; i++) d += qr[h][i] * kv[u][i];
+                for (int i = 0; i < DPL; i++) d += qr[h][i] * kv[i];
                 d = groupSum<16>(d);
                 const float mn = fmaxf(m[h], d);
                 const float corr = __expf(m[h] - mn);  // m = -inf first time -> 0
                 const float p = __expf(d - mn);
                 l[h] = l[h] * corr + p;
 #pragma unroll
-                for (int i = 0; i < DPL; i++) o[h][i] = o[h][i] * corr + p * vv[u][i];
+                for (int i = 0; i < DPL; i++) o[h][i] = o[h][i] * corr + p * vv[i];
                 m[h] = mn;
             }
         }
@@ -698,15 +741,15 @@ __global__ __launch_bounds__(kThreads) void attnKernel(AttnArgs a) {
         }
     }
     __syncthreads();
-    // merge the 4 waves
-    for (int i = tid; i < HG * HS; i += kThreads) {
+    // merge the NW waves
+    for (int i = tid; i < HG * HS; i += AT) {
         const int h = i / HS;
         float M = -INFINITY;
 #pragma unroll
-        for (int w = 0; w < 4; w++) M = fmaxf(M, mW[w * HG + h]);
+        for (int w = 0; w < NW; w++) M = fmaxf(M, mW[w * HG + h]);
         float acc = 0.f, Ls = 0.f;
 #pragma unroll
-        for (int w = 0; w < 4; w++) {
+        for (int w = 0; w < NW; w++) {
             const float e = M == -INFINITY ? 0.f : __expf(mW[w * HG + h] - M);
             acc += e * oW[(w * HG + h) * HS + (i % HS)];
             Ls += e * lW[w * HG + h];
@@ -720,15 +763,15 @@ __global__ __launch_bounds__(kThreads) void attnKernel(AttnArgs a) {
     __syncthreads();
 
     if (nSplit == 1) {
-        for (int i = tid; i < HG * HS; i += kThreads) redL[i] = redL[i] / mlL[(i / HS) * 2 + 1];
+        for (int i = tid; i < HG * HS; i += AT) redL[i] = redL[i] / mlL[(i / HS) * 2 + 1];
         __syncthreads();
-        attnWriteOut<HG, HS>(a, b, head0, redL);
+        attnWriteOut<HG, HS, AT>(a, b, head0, redL);
         return;
     }
 
     // publish this chunk's partial, count arrivals; the last workgroup combines
     const size_t pbase = ((size_t)b * a.nHeads0 + head0) * a.splitGrid;
-    for (int i = tid; i < HG * HS; i += kThreads) {
+    for (int i = tid; i < HG * HS; i += AT) {
         const int h = i / HS, d = i % HS;
         a.partO[((pbase + (size_t)h * a.splitGrid) + c) * HS + d] = redL[i];
     }
@@ -753,7 +796,7 @@ __global__ __launch_bounds__(kThreads) void attnKernel(AttnArgs a) {
         __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    for (int i = tid; i < HG * HS; i += kThreads) {
+    for (int i = tid; i < HG * HS; i += AT) {
         const int h = i / HS, d = i % HS;
         const float *ml = a.partML + (pbase + (size_t)h * a.splitGrid) * 2;
         float M = -INFINITY;
@@ -767,18 +810,19 @@ __global__ __launch_bounds__(kThreads) void attnKernel(AttnArgs a) {
         redL[i] = acc / Ls;
     }
     __syncthreads();
-    attnWriteOut<HG, HS>(a, b, head0, redL);
+    attnWriteOut<HG, HS, AT>(a, b, head0, redL);
 }
 
 template <int HS, bool BF16>
 static void attnDispatchHG(const AttnArgs &a, int B, int HG, hipStream_t s) {
-    const size_t lds = sizeof(float) * (8 * HG + 4 * HG * HS + HG * HS + 2 * HG) + 16;
+    constexpr int NW = kAttnThreads / 64;
+    const size_t lds = sizeof(float) * (2 * NW * HG + NW * HG * HS + HG * HS + 2 * HG) + 16;
     const dim3 grid(a.nHeads0 / HG, a.splitGrid, B);
     switch (HG) {
-        case 1: hipLaunchKernelGGL((attnKernel<1, HS, BF16>), grid, dim3(kThreads), lds, s, a); break;
-        case 2: hipLaunchKernelGGL((attnKernel<2, HS, BF16>), grid, dim3(kThreads), lds, s, a); break;
-        case 4: hipLaunchKernelGGL((attnKernel<4, HS, BF16>), grid, dim3(kThreads), lds, s, a); break;
-        default: hipLaunchKernelGGL((attnKernel<8, HS, BF16>), grid, dim3(kThreads), lds, s, a); break;
+        case 1: hipLaunchKernelGGL((attnKernel<1, HS, BF16>), grid, dim3(kAttnThreads), lds, s, a); break;
+        case 2: hipLaunchKernelGGL((attnKernel<2, HS, BF16>), grid, dim3(kAttnThreads), lds, s, a); break;
+        case 4: hipLaunchKernelGGL((attnKernel<4, HS, BF16>), grid, dim3(kAttnThreads), lds, s, a); break;
+        default: hipLaunchKernelGGL((attnKernel<8, HS, BF16>), grid, dim3(kAttnThreads), lds, s, a); break;
     }
 }
 
