@@ -321,7 +321,7 @@ PYBIND11_MODULE(_C, m) {
                          py::gil_scoped_acquire acq;
                          s = uid.cast<std::string>();
                      }
-                     hipSetDevice(gpuIndex >= 0 ? gpuIndex : 0);
+                     (void)hipSetDevice(gpuIndex >= 0 ? gpuIndex : 0);
                      e->comm = makeRcclComm(std::vector<unsigned char>(s.begin(), s.end()), rank, world);
                  }
                  e->engine = makeHipEngine(c, e->comm.get());

@@ -110,10 +110,32 @@ void Tokenizer::parse(const u8 *data, u64 size, bool verbose) {
         DL_CHECK(len >= 0, "negative token length");
         vocab_[i] = r.bytes((u64)len);
     }
-    // The reference assumes bosId splits regular and special tokens (tokenizer.cpp:137-138).
-    regularVocabSize_ = bosId_ >= 0 ? std::min(bosId_, vocabSize) : vocabSize;
-    regular_.reserve(regularVocabSize_ * 2);
-    for (int i = 0; i < regularVocabSize_; i++) regular_.emplace(vocab_[i], i);  // first id wins
+    // The reference assumes bosId splits regular and special tokens (tokenizer.cpp:137-138): that
+    // holds for Llama-3-style vocabularies whose specials are appended at the end. Tokenizers that
+    // put their control tokens first (HF-trained BPE, sentencepiece <unk>/<s>/</s>) get the leading
+    // run of bos/eos/"<...>" marker tokens as the special set instead.
+    std::vector<bool> special(vocabSize, false);
+    if (bosId_ < 0 || bosId_ >= vocabSize / 2) {
+        for (int i = std::max(bosId_, 0); bosId_ >= 0 && i < vocabSize; i++) special[i] = true;
+    } else {
+        auto isMarker = [&](int i) {
+            const std::string &v = vocab_[i];
+            if (i == bosId_ || std::find(eos_.begin(), eos_.end(), i) != eos_.end()) return true;
+            return v.size() >= 3 && v.front() == '<' && v.back() == '>';
+        };
+        for (int i = 0; i < vocabSize && isMarker(i); i++) special[i] = true;
+        for (int e : eos_)
+            if (e >= 0 && e < vocabSize) special[e] = true;
+        special[bosId_] = true;
+    }
+    regular_.reserve(vocabSize * 2);
+    for (int i = 0; i < vocabSize; i++) {
+        if (special[i])
+            specialIds_.push_back(i);
+        else
+            regular_.emplace(vocab_[i], i);  // first id wins
+    }
+    regularVocabSize_ = vocabSize - (int)specialIds_.size();
     if (verbose && logLevel() >= 1) {
         if (bosId_ >= 0 && bosId_ < vocabSize) std::printf("📄 BosId: %d (%s)\n", bosId_, vocab_[bosId_].c_str());
         if (!eos_.empty()) {
@@ -123,7 +145,7 @@ void Tokenizer::parse(const u8 *data, u64 size, bool verbose) {
             std::printf("\n");
         }
         std::printf("📄 RegularVocabSize: %d\n", regularVocabSize_);
-        std::printf("📄 SpecialVocabSize: %d\n", vocabSize - regularVocabSize_);
+        std::printf("📄 SpecialVocabSize: %d\n", (int)specialIds_.size());
     }
 }
 
@@ -133,7 +155,7 @@ int Tokenizer::findRegular(const std::string &s) const {
 }
 
 int Tokenizer::findSpecialPrefix(const char *text, size_t remaining) const {
-    for (int id = regularVocabSize_; id < (int)vocab_.size(); id++) {
+    for (int id : specialIds_) {
         const std::string &v = vocab_[id];
         if (v.size() <= remaining && std::memcmp(v.data(), text, v.size()) == 0) return id;
     }

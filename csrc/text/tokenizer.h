@@ -53,6 +53,7 @@ class Tokenizer {
     int bosId_ = -1;
     u32 maxTokenLength_ = 0;
     int regularVocabSize_ = 0;
+    std::vector<int> specialIds_;
     std::unordered_map<std::string, int> regular_;
     std::string pending_;
 };
