@@ -8,10 +8,13 @@
 //           "stream": true -> server-sent events with chat.completion.chunk objects + [DONE]
 //   GET  /v1/models            {"object":"list","data":[{"id":<model file name>, ...}]}
 //   GET  /health               scheduler counters
+//   GET  /, /app.js, /style.css  the chat web UI (--web-ui <dir>, default ./web-ui when present)
 // Requests run concurrently (thread per connection); the scheduler batches them into shared forwards.
 #include <csignal>
 #include <cstdio>
 #include <ctime>
+#include <fstream>
+#include <sstream>
 #include <string>
 
 #include "../net/http.h"
@@ -190,6 +193,31 @@ struct Api {
     }
 };
 
+bool readFile(const std::string &path, std::string &out) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    std::ostringstream ss;
+    ss << f.rdbuf();
+    out = ss.str();
+    return true;
+}
+
+void serveWebUi(HttpServer &server, const std::string &dir) {
+    static const char *files[][3] = {{"/", "index.html", "text/html; charset=utf-8"},
+                                     {"/app.js", "app.js", "application/javascript"},
+                                     {"/style.css", "style.css", "text/css"}};
+    for (auto &f : files) {
+        const std::string path = dir + "/" + f[1], type = f[2];
+        server.route("GET", f[0], [path, type](const HttpRequest &, HttpConnection &c) {
+            std::string body;
+            if (readFile(path, body))
+                c.writeResponse(200, type, body);
+            else
+                c.writeJson(404, "{\"error\":\"web ui file missing\"}");
+        });
+    }
+}
+
 void usage() {
     std::fprintf(stderr,
                  "Usage: dllama-api {--model <path>} {--tokenizer <path>} [--port <p>]\n"
@@ -197,7 +225,8 @@ void usage() {
                  "        [--max-seq-len <max>] [--slots <n>] [--max-batch <n>]\n"
                  "        [--nthreads <n>] [--gpu-index <i>]\n"
                  "        [--workers <ip:port> ...]\n"
-                 "        [--temperature <temp>] [--topp <t>] [--seed <s>] [--chat-template <t>]\n");
+                 "        [--temperature <temp>] [--topp <t>] [--seed <s>] [--chat-template <t>]\n"
+                 "        [--web-ui <dir>]\n");
 }
 
 }  // namespace
@@ -231,6 +260,13 @@ int main(int argc, char **argv) {
         server.route("POST", "/v1/chat/completions", [&](const HttpRequest &r, HttpConnection &c) { api.complete(r, c); });
         server.route("GET", "/v1/models", [&](const HttpRequest &r, HttpConnection &c) { api.models(r, c); });
         server.route("GET", "/health", [&](const HttpRequest &r, HttpConnection &c) { api.health(r, c); });
+        std::string ui = args.webUi;
+        std::string probe;
+        if (ui.empty() && readFile("web-ui/index.html", probe)) ui = "web-ui";
+        if (!ui.empty()) {
+            serveWebUi(server, ui);
+            std::printf("Web UI: http://127.0.0.1:%d/\n", args.port);
+        }
         std::printf("Server URL: http://127.0.0.1:%d/v1/\n", args.port);
         std::fflush(stdout);
         server.serveForever();

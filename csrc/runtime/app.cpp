@@ -64,6 +64,7 @@ AppArgs AppArgs::parse(int argc, char **argv, bool requireMode) {
         } else if (name == "--graph") a.graphs = std::atoi(value) != 0;
         else if (name == "--log-level") a.logLevel = std::atoi(value);
         else if (name == "--synthetic") a.synthetic = value;
+        else if (name == "--web-ui") a.webUi = value;
         else throw Error("Unknown option: " + name);
     }
     setLogLevel(a.logLevel);

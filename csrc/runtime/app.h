@@ -39,6 +39,7 @@ struct AppArgs {
     bool graphs = true;
     int logLevel = 1;
     std::string synthetic;                       // "llama3_1_8b" etc: random-init weights on device
+    std::string webUi;                           // dllama-api: directory served at GET /
 
     static AppArgs parse(int argc, char **argv, bool requireMode);
 };

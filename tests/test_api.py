@@ -29,7 +29,7 @@ def server(assets):
     port = _free_port()
     proc = subprocess.Popen([API, "--model", assets["q40"], "--tokenizer", assets["tok"], "--buffer-float-type", "q80",
                              "--port", str(port), "--nthreads", "2", "--slots", "4", "--temperature", "0",
-                             "--max-seq-len", "128"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+                             "--max-seq-len", "128", "--web-ui", os.path.join(REPO, "web-ui")], stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
     url = f"http://127.0.0.1:{port}"
     for _ in range(200):
         try:
@@ -106,3 +106,21 @@ def test_bad_request(server):
     with pytest.raises(urllib.error.HTTPError) as e:
         _post(server, {"nope": 1})
     assert e.value.code == 400
+
+
+def test_web_ui_served(server):
+    html = urllib.request.urlopen(server + "/", timeout=5).read().decode()
+    assert "app.js" in html
+    js = urllib.request.urlopen(server + "/app.js", timeout=5).read().decode()
+    assert "generated_text" in js and "/chat/completions" in js
+
+
+def test_launcher_writes_tp_script(tmp_path):
+    import sys
+    sys.path.insert(0, REPO)
+    import launch
+    assert launch.main(["llama3_1_8b_instruct_q40", "--gpus", "4", "--no-download", "--dir", str(tmp_path)]) == 0
+    script = (tmp_path / "run_llama3_1_8b_instruct_q40_tp4.sh").read_text()
+    assert script.count("build/dllama worker") == 3 and "--gpu-index 3" in script
+    assert "--workers 127.0.0.1:9997 127.0.0.1:9996 127.0.0.1:9995" in script
+    assert len(launch.MODELS["llama3_1_405b_instruct_q40"].urls) == 56
