@@ -37,10 +37,10 @@ int hipDeviceCount() {
 namespace {
 
 struct DevMat {
-    uint8_t *qs = nullptr;
+    uint8_t *qs = nullptr;  // Q40: tiled for `lanes` lanes per row (hipk::Q40Tiling)
     uint16_t *d = nullptr;
     float *f = nullptr;
-    int rows = 0, n = 0;
+    int rows = 0, n = 0, lanes = 0;
 };
 
 struct DevLayer {
@@ -277,10 +277,15 @@ class HipEngineImpl : public HipEngine {
         m.n = n;
         if (q40_) {
             DL_CHECK(qs.size() == (size_t)rows * n / 2 && d.size() == (size_t)rows * n / 32, "repack size");
-            m.qs = dalloc<uint8_t>(qs.size());
-            m.d = dalloc<uint16_t>(d.size());
-            DL_HIP(hipMemcpy(m.qs, qs.data(), qs.size(), hipMemcpyHostToDevice));
-            DL_HIP(hipMemcpy(m.d, d.data(), d.size() * 2, hipMemcpyHostToDevice));
+            m.lanes = hipk::gemvLanesPerRow(n, rows, 1, true);
+            const hipk::Q40Tiling t = hipk::q40Tiling(rows, n, m.lanes);
+            std::vector<u8> qt(t.qsBytes);
+            std::vector<uint32_t> dt(t.dBytes / 4);
+            hipk::tileQ40(qs.data(), d.data(), rows, n, m.lanes, qt.data(), dt.data());
+            m.qs = dalloc<uint8_t>(qt.size());
+            m.d = dalloc<uint16_t>(t.dBytes / 2);
+            DL_HIP(hipMemcpy(m.qs, qt.data(), qt.size(), hipMemcpyHostToDevice));
+            DL_HIP(hipMemcpy(m.d, dt.data(), t.dBytes, hipMemcpyHostToDevice));
         } else {
             DL_CHECK(f.size() == (size_t)rows * n, "f32 slice size");
             m.f = dalloc<float>(f.size());
@@ -359,8 +364,10 @@ class HipEngineImpl : public HipEngine {
         m.n = n;
         const float scale = 1.0f / std::sqrt(21.5f * (float)n);
         if (q40_) {
-            const size_t nBlocks = (size_t)rows * n / 32;
-            m.qs = dalloc<uint8_t>(nBlocks * 16);
+            m.lanes = hipk::gemvLanesPerRow(n, rows, 1, true);
+            const hipk::Q40Tiling t = hipk::q40Tiling(rows, n, m.lanes);
+            const size_t nBlocks = t.qsBytes / 16;  // == t.dBytes / 2 f16 scales
+            m.qs = dalloc<uint8_t>(t.qsBytes);
             m.d = dalloc<uint16_t>(nBlocks);
             hipk::launchFillQ40(m.qs, m.d, nBlocks, scale, seed, stream_);
         } else {
@@ -490,13 +497,7 @@ class HipEngineImpl : public HipEngine {
     }
 
     int passesFor(const DevMat &m, int epi, int B) const {
-        const int rp = hipk::gemvRowsPerPass(m.n, m.rows, B, q40_);
-        if (epi == hipk::EPI_ACT_Q80) return 64 / rp;  // 32 hidden units (one Q80 block) per workgroup
-        const int grid0 = (m.rows + rp - 1) / rp;
-        int passes = grid0 / 1024;
-        if (passes < 1) passes = 1;
-        if (passes > 4) passes = 4;
-        return passes;
+        return hipk::gemvDefaultPasses(m.n, m.rows, B, q40_, epi);
     }
 
     // Launch a GEMV over all n rows, in batch chunks of <= 4.
@@ -515,6 +516,7 @@ class HipEngineImpl : public HipEngine {
             a.rows = m.rows;
             a.n = m.n;
             a.passes = passesFor(m, epi, bc);
+            a.lanes = m.lanes;
             a.in = in ? in + (size_t)c0 * ldIn : nullptr;
             a.aq = aq ? aq + (size_t)c0 * m.n : nullptr;
             a.as = as ? as + (size_t)c0 * (m.n / 32) : nullptr;
@@ -691,7 +693,6 @@ class HipEngineImpl : public HipEngine {
 double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int passes, int copies, int iters) {
     hipStream_t s;
     DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    const size_t nb = (size_t)rows * n / 32;
     std::vector<void *> mem;
     auto alloc = [&](size_t bytes) {
         void *p;
@@ -699,12 +700,14 @@ double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int pas
         mem.push_back(p);
         return p;
     };
+    const int L = lanes > 0 ? lanes : hipk::gemvLanesPerRow(n, rows, B, true);
+    const hipk::Q40Tiling t = hipk::q40Tiling(rows, n, L);
     std::vector<uint8_t *> qs(copies);
     std::vector<uint16_t *> d(copies);
     for (int c = 0; c < copies; c++) {
-        qs[c] = (uint8_t *)alloc(nb * 16);
-        d[c] = (uint16_t *)alloc(nb * 2);
-        hipk::launchFillQ40(qs[c], d[c], nb, 0.01f, 77 + c, s);
+        qs[c] = (uint8_t *)alloc(t.qsBytes);
+        d[c] = (uint16_t *)alloc(t.dBytes);
+        hipk::launchFillQ40(qs[c], d[c], t.qsBytes / 16, 0.01f, 77 + c, s);
     }
     float *x = (float *)alloc((size_t)B * n * 4), *y = (float *)alloc((size_t)B * n * 4);
     float *xn = (float *)alloc((size_t)B * n * 4), *w = (float *)alloc((size_t)n * 4);
@@ -722,8 +725,14 @@ double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int pas
     hipk::GemvArgs a;
     a.rows = rows;
     a.n = n;
-    a.passes = passes;
-    a.lanes = lanes;
+    a.lanes = L;
+    a.passes = passes > 0 ? passes : hipk::gemvDefaultPasses(n, rows, B, true, epi);
+    if (passes <= 0 && lanes > 0) {  // forced lane count: same residency rule with its rows/pass
+        const int rp = 256 / lanes * 2, grid0 = (rows + rp - 1) / rp;
+        a.passes = (grid0 + 511) / 512;
+        if (epi == hipk::EPI_ACT_Q80)
+            while ((rp * a.passes) % 64) a.passes++;
+    }
     a.in = x;
     a.ldIn = n;
     a.addIn = y;

@@ -28,8 +28,23 @@ enum Prologue : int { PRO_GLOBAL = 0, PRO_RESNORM = 1 };
 // EPI_ACT_Q80: act(w1 x) * (w3 x), quantized to Q80 blocks for the next GEMV (32 hidden units/block).
 enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2, EPI_ACT_Q80 = 3 };
 
+// Q40 weights live on the device TILED in the ring GEMV's consumption order, for a lanes-per-row
+// count L fixed per matrix (NG = 256/L row pairs per workgroup pass, K = ceil(nb/L) steps):
+//   chunk c = pass group g (2*NG consecutive rows) x step k (blocks j = li + k*L), c = g*K + k
+//   qs: [c][r in {0,1}][256 threads] x 16 B    thread tid = gi*L + li -> row 2*(g*NG+gi) + r
+//   d : [c][256 threads] x u32                 {lo: f16 scale of the even row, hi: odd row}
+// so a workgroup streams one contiguous region (8 KB of nibbles + 1 KB of scales per step).
+// Padding (rows past the end, j >= nb) is zero.
+struct Q40Tiling {
+    int L = 16, NG = 16, K = 0, groups = 0;
+    size_t chunks = 0, qsBytes = 0, dBytes = 0;
+};
+Q40Tiling q40Tiling(int rows, int n, int L);
+// Host repack of row-major SoA blocks (qs [rows][nb][16], d [rows][nb] f16) into the tiled layout.
+void tileQ40(const uint8_t *qs, const uint16_t *d, int rows, int n, int L, uint8_t *qsOut, uint32_t *dOut);
+
 struct GemvArgs {
-    // weights: Q40 repacked (qs [rows][nb][16], d [rows][nb] f16) or F32 [rows][n]
+    // weights: Q40 tiled (see Q40Tiling; `lanes` must be the tiling's L) or F32 [rows][n]
     const uint8_t *qs = nullptr;
     const uint16_t *wd = nullptr;
     const float *wf = nullptr;
@@ -65,7 +80,7 @@ struct GemvArgs {
 // B = batch rows in this launch (1, 2 or 4); q40 = weight format.
 void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_t s);
 // Rows handled by one lane group (2 at batch 1: the activation loads are shared by 2 rows).
-__host__ __device__ constexpr int gemvRowGroup(int B, bool q40) { return (B == 1 && q40) ? 2 : 1; }
+__host__ __device__ constexpr int gemvRowGroup(int B, bool q40) { return q40 ? 2 : 1; }
 // Lanes cooperating on one weight row for a given input width, row count and batch.
 int gemvLanesPerRow(int n, int rows, int B, bool q40);
 // Rows per workgroup and pass.
@@ -74,6 +89,9 @@ inline int gemvRowsPerPass(int n, int rows, int B, bool q40) {
 }
 // Dynamic LDS bytes a gemv launch needs.
 size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg, int pro);
+// Passes (row groups per lane group) for a launch: Q40 ring kernel -> enough that the whole grid is
+// resident at once (DL_GEMV_RESIDENT workgroups, default 512); ACT_Q80 -> whole Q80 blocks per WG.
+int gemvDefaultPasses(int n, int rows, int B, bool q40, int epi);
 
 struct AttnArgs {
     const float *q = nullptr;   // [B][ldq], rotated queries

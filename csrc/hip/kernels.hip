@@ -18,6 +18,7 @@
 #include "kernels.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace dl {
 namespace hipk {
@@ -25,6 +26,7 @@ namespace hipk {
 using namespace dl::dev;
 
 static constexpr int kThreads = 256;
+static constexpr int kMaxHeadSize = 128;  // RoPE rows staged in LDS by the QKV epilogue
 static constexpr int KMAX = 8;  // weight blocks per lane held in VGPRs (prefetched)
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -46,21 +48,24 @@ static int minLanesOverride() {
 int gemvLanesPerRow(int n, int rows, int B, bool q40) {
     int L;
     if (q40) {
-        const int nb = n / 32;
-        L = nb <= 128 ? 16 : (nb <= 256 ? 32 : 64);
+        // Ring kernel: the fewest lanes per row (longest per-lane block sequence, cheapest
+        // reduction) that still gives >= 256 workgroups, i.e. every CU streams.
+        const int groups = (rows + 1) / 2;
+        L = 16;
+        while (L < 64 && (size_t)groups * L / kThreads < 256) L *= 2;
     } else {
         const int n4 = n / 4;
         L = n4 >= 2048 ? 64 : (n4 >= 512 ? 32 : 16);
+        // skinny shards (tensor parallel): fewer rows per workgroup so the grid still covers the CUs
+        while (L < 64 && rows / (kThreads / L * gemvRowGroup(B, q40)) < 256) L *= 2;
     }
-    // skinny shards (tensor parallel): fewer rows per workgroup so the grid still covers the CUs
-    while (L < 64 && rows / (kThreads / L * gemvRowGroup(B, q40)) < 256) L *= 2;
     const int mo = minLanesOverride();
     if (mo > L) L = mo > 64 ? 64 : mo;
     return L;
 }
 
 struct GemvLds {
-    size_t scratch, res, hbuf, act, sc, total;
+    size_t scratch, rope, res, hbuf, act, sc, total;
 };
 
 __host__ __device__ static GemvLds gemvLayout(int n, int B, bool q40, int rowsPerWg, int pro) {
@@ -68,12 +73,14 @@ __host__ __device__ static GemvLds gemvLayout(int n, int B, bool q40, int rowsPe
     size_t off = 0;
     l.scratch = off;
     off += 64 * sizeof(float);
+    l.rope = off;  // RoPE rows of the batch's positions (QKV epilogue of the Q40 ring kernel)
+    off += (size_t)B * (kMaxHeadSize / 2) * sizeof(float2);
     l.res = off;
     off = alignUp(off + (size_t)B * rowsPerWg * sizeof(float), 16);
     l.hbuf = off;
     off = alignUp(off + (size_t)B * (rowsPerWg / 2) * sizeof(float), 16);
     l.act = off;
-    if (pro == PRO_RESNORM) {
+    if (pro == PRO_RESNORM || q40) {
         if (q40) {
             off = alignUp(off + (size_t)B * n, 16);
             l.sc = off;
@@ -87,6 +94,65 @@ __host__ __device__ static GemvLds gemvLayout(int n, int B, bool q40, int rowsPe
     }
     l.total = off;
     return l;
+}
+
+Q40Tiling q40Tiling(int rows, int n, int L) {
+    Q40Tiling t;
+    t.L = L;
+    t.NG = kThreads / L;
+    const int nb = n / 32;
+    t.K = (nb + L - 1) / L;
+    t.groups = (rows + 2 * t.NG - 1) / (2 * t.NG);
+    t.chunks = (size_t)t.groups * t.K;
+    t.qsBytes = t.chunks * 2 * kThreads * 16;
+    t.dBytes = t.chunks * kThreads * 4;
+    return t;
+}
+
+void tileQ40(const uint8_t *qs, const uint16_t *d, int rows, int n, int L, uint8_t *qsOut, uint32_t *dOut) {
+    const Q40Tiling t = q40Tiling(rows, n, L);
+    const int nb = n / 32;
+    for (int g = 0; g < t.groups; g++)
+        for (int k = 0; k < t.K; k++) {
+            const size_t c = (size_t)g * t.K + k;
+            for (int tid = 0; tid < kThreads; tid++) {
+                const int gi = tid / L, li = tid % L, j = li + k * L;
+                const int row0 = 2 * (g * t.NG + gi);
+                uint32_t dd = 0;
+                for (int r = 0; r < 2; r++) {
+                    uint8_t *dst = qsOut + ((c * 2 + r) * kThreads + tid) * 16;
+                    const int row = row0 + r;
+                    if (row < rows && j < nb) {
+                        const size_t blk = (size_t)row * nb + j;
+                        for (int i = 0; i < 16; i++) dst[i] = qs[blk * 16 + i];
+                        dd |= (uint32_t)d[blk] << (16 * r);
+                    } else {
+                        for (int i = 0; i < 16; i++) dst[i] = 0;
+                    }
+                }
+                dOut[c * kThreads + tid] = dd;
+            }
+        }
+}
+
+int gemvDefaultPasses(int n, int rows, int B, bool q40, int epi) {
+    static const int resident = [] {
+        const char *e = getenv("DL_GEMV_RESIDENT");
+        return e ? atoi(e) : 512;
+    }();
+    const int rp = gemvRowsPerPass(n, rows, B, q40);
+    const int grid0 = (rows + rp - 1) / rp;
+    int passes;
+    if (q40) {
+        passes = (grid0 + resident - 1) / resident;
+        if (epi == EPI_ACT_Q80)
+            while ((rp * passes) % 64) passes++;
+    } else {
+        if (epi == EPI_ACT_Q80) return 64 / rp;
+        passes = grid0 / 1024;
+        passes = passes < 1 ? 1 : (passes > 4 ? 4 : passes);
+    }
+    return passes;
 }
 
 size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg, int pro) {
@@ -251,6 +317,238 @@ __device__ __forceinline__ void q40Block(float (&acc)[RG][B], const u32x4 (&w)[R
     }
 }
 
+// Fused epilogues of a row pair (2k, 2k+1) --------------------------------------------------------
+__device__ __forceinline__ float gateAct(const GemvArgs &a, float v) {
+    if (a.act == 1) return v / (1.0f + __expf(-v));
+    return 0.5f * v * (1.0f + tanhf(0.79788456080286535588f * v * (1.0f + 0.044715f * v * v)));
+}
+
+// Rows [0, q0) are Q, [q0, q0+kv0) K, then V. Q and K pairs are rotated (RoPE at this row's
+// position); K and V are appended to the KV cache at [slot][pos].
+__device__ __forceinline__ void qkvPairStore(const GemvArgs &a, int r0, float v0, float v1, const float2 *ropeRow,
+                                             int p, int sl, float *qRow) {
+    if (r0 < a.q0 + a.kv0) {
+        const float2 cs = ropeRow[(r0 % a.hs) >> 1];
+        const float o0 = v0 * cs.x - v1 * cs.y;
+        const float o1 = v0 * cs.y + v1 * cs.x;
+        if (r0 < a.q0) {
+            *reinterpret_cast<float2 *>(qRow + r0) = make_float2(o0, o1);
+        } else {
+            const size_t off = ((size_t)sl * a.seqLen + p) * a.kv0 + (r0 - a.q0);
+            if (a.kvBf16) {
+                const uint32_t pk = (uint32_t)f32ToBf16(o0) | ((uint32_t)f32ToBf16(o1) << 16);
+                *reinterpret_cast<uint32_t *>(reinterpret_cast<uint16_t *>(a.kcache) + off) = pk;
+            } else {
+                *reinterpret_cast<float2 *>(reinterpret_cast<float *>(a.kcache) + off) = make_float2(o0, o1);
+            }
+        }
+    } else {
+        const size_t off = ((size_t)sl * a.seqLen + p) * a.kv0 + (r0 - a.q0 - a.kv0);
+        if (a.kvBf16) {
+            const uint32_t pk = (uint32_t)f32ToBf16(v0) | ((uint32_t)f32ToBf16(v1) << 16);
+            *reinterpret_cast<uint32_t *>(reinterpret_cast<uint16_t *>(a.vcache) + off) = pk;
+        } else {
+            *reinterpret_cast<float2 *>(reinterpret_cast<float *>(a.vcache) + off) = make_float2(v0, v1);
+        }
+    }
+}
+
+// Quantize a workgroup's `halfR` hidden units (multiple of 32, in LDS) to Q80 blocks in global.
+template <int B>
+__device__ __forceinline__ void storeHiddenQ80(const GemvArgs &a, const float *hbuf, int halfR, int hBase) {
+    for (int i = threadIdx.x; i < B * halfR; i += kThreads) {  // 32-lane groups = one block
+        const int b = i / halfR, k = i % halfR;
+        if (hBase + k >= (a.rows >> 1)) continue;  // whole 32-unit blocks: uniform per lane group
+        const float h = hbuf[b * halfR + k];
+        const float amax = groupMax<32>(fabsf(h));
+        const float d = amax / 127.0f;
+        const float id = d != 0.f ? 1.0f / d : 0.f;
+        int q = (int)rintf(h * id);
+        q = q > 127 ? 127 : (q < -127 ? -127 : q);
+        a.oq[(size_t)b * a.ldOut + hBase + k] = (int8_t)q;
+        const float qs = groupSum<32>((float)q);
+        if ((k & 31) == 0) a.os[(size_t)b * (a.ldOut >> 5) + ((hBase + k) >> 5)] = make_float2(roundF16(d), qs);
+    }
+}
+
+// Copy B rows of Q80 activations (n int8 + n/32 scale pairs) from global into the LDS image.
+template <int B>
+__device__ __forceinline__ void stageQ80(const GemvArgs &a, int8_t *sq, float2 *ssc) {
+    const int n = a.n, nb = n >> 5;
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+        const int4 *src = reinterpret_cast<const int4 *>(a.aq + (size_t)b * n);
+        int4 *dst = reinterpret_cast<int4 *>(sq + (size_t)b * n);
+        for (int i = threadIdx.x; i < (n >> 4); i += kThreads) dst[i] = src[i];
+        for (int i = threadIdx.x; i < nb; i += kThreads) ssc[b * nb + i] = a.as[(size_t)b * nb + i];
+    }
+    __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Q40 GEMV, register-ring pipeline.
+//   Each lane group (L lanes) owns row pairs; lane li walks blocks j = li, li+L, ... of its rows
+//   for every pass (row pair) of the workgroup as ONE flat sequence of T = passes * K steps
+//   (K = ceil(nb / L)). kRing steps are kept in flight in a ring of VGPR slots: step t is
+//   consumed from slot t % kRing and the slot is immediately refilled with step t + kRing, so the
+//   HBM stream never drains between blocks, row pairs or passes (the previous design issued
+//   4 blocks, computed, then issued the rest 2 at a time: ~1.6x the streaming floor measured by
+//   scripts/microbench_stream.hip). Activations always come from LDS (norm prologue or a copy
+//   of upstream Q80), row-pair epilogues (SwiGLU, RoPE + KV append) run in registers.
+// ------------------------------------------------------------------------------------------------
+static constexpr int kRing = 8;
+
+template <int L, int B, int PRO, int EPI>
+__global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int RG = 2, NG = kThreads / L, RP = NG * RG, D = kRing;
+    const int n = a.n, nb = n >> 5, K = (nb + L - 1) / L, P = a.passes, T = P * K;
+    const int R = RP * P;
+    const GemvLds lay = gemvLayout(n, B, true, R, PRO_RESNORM);
+    float *scratch = reinterpret_cast<float *>(smem + lay.scratch);
+    float *hbuf = reinterpret_cast<float *>(smem + lay.hbuf);
+    int8_t *sq = reinterpret_cast<int8_t *>(smem + lay.act);
+    float2 *ssc = reinterpret_cast<float2 *>(smem + lay.sc);
+    const int tid = threadIdx.x, gi = tid / L, li = tid % L;
+    const int rowBase = blockIdx.x * R;
+
+    // slot = 2 rows x 16 B of nibbles + the pair's two f16 scales in one 32-bit word
+    u32x4 w[D][RG];
+    uint32_t dh[D];
+    const uint32_t *wd2 = reinterpret_cast<const uint32_t *>(a.wd);  // tiled pair scales
+    // this workgroup's chunks are [blockIdx.x * T, blockIdx.x * T + T) of the tiled matrix
+    const size_t cBase = (size_t)blockIdx.x * T;
+    const size_t cLast = (size_t)((a.rows + RP - 1) / RP) * K - 1;
+    int it = 0;  // issue cursor (steps)
+    // The ring's loads are inline asm with explicit vmcnt waits (cdna_hip_programming.md §5.7,
+    // form ii): hipcc's own waitcnt pass flushes vmcnt(0) at the loop header, which turns the ring
+    // into bulk-synchronous rounds. Each step is 3 loads; consuming a slot waits until only the
+    // loads issued after it are outstanding. Refills past the last step re-read this workgroup's
+    // last chunk (L2), keeping every slot unconditionally defined (no phi copies of in-flight
+    // registers).
+    auto issue = [&](u32x4(&ws)[RG], uint32_t &ds) {
+        const size_t c = min(cBase + (size_t)min(it, T - 1), cLast);
+        const u32x4 *p0 = reinterpret_cast<const u32x4 *>(a.qs) + (c * 2) * kThreads + tid;
+        const u32x4 *p1 = p0 + kThreads;
+        const uint32_t *pd = wd2 + c * kThreads + tid;
+        asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(ws[0]) : "v"(p0));
+        asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(ws[1]) : "v"(p1));
+        asm volatile("global_load_dword %0, %1, off" : "=v"(ds) : "v"(pd));
+        ++it;
+    };
+    // sched_barrier keeps issue order == slot order, so each step waits for exactly its own slot
+    // (vmcnt = loads of the other kRing-1 slots) instead of the scheduler batching the ring.
+#pragma unroll
+    for (int s = 0; s < D; s++) {
+        issue(w[s], dh[s]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    float2 *sRope = reinterpret_cast<float2 *>(smem + lay.rope);
+    int posB[B], slotB[B];  // uniform: scalar loads, kept out of the ring's vmcnt accounting
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+        posB[b] = EPI == EPI_QKV ? a.pos[b] : 0;
+        slotB[b] = EPI == EPI_QKV ? a.slot[b] : 0;
+    }
+    if constexpr (EPI == EPI_QKV) {  // the prologue's __syncthreads publishes these
+        const int h2 = a.hs >> 1;
+        for (int i = tid; i < B * h2; i += kThreads) {
+            const int b = i / h2;
+            sRope[b * (kMaxHeadSize / 2) + i % h2] = a.rope[(size_t)a.pos[b] * h2 + i % h2];
+        }
+    }
+    if constexpr (PRO == PRO_RESNORM)
+        resNormPrologue<B, true>(a, scratch, sq, ssc, nullptr);
+    else
+        stageQ80<B>(a, sq, ssc);
+    // The prologue's own loads were issued after the ring's, so waiting for them already drained
+    // the ring; this explicit wait pins every slot register before the compiler may copy one.
+    auto waitAll = [&]() {
+#pragma unroll
+        for (int s = 0; s < D; s++) asm volatile("s_waitcnt vmcnt(0)" : "+v"(w[s][0]), "+v"(w[s][1]), "+v"(dh[s]));
+    };
+    waitAll();
+
+    float acc[RG][B];
+#pragma unroll
+    for (int r = 0; r < RG; r++)
+#pragma unroll
+        for (int b = 0; b < B; b++) acc[r][b] = 0.f;
+    int cp = 0, ck = 0;  // consume cursor
+    // consume the step held in slot (ws, ds)
+    auto consume = [&](const u32x4(&ws)[RG], uint32_t ds, bool live) {
+        const int j = li + ck * L;
+        const bool use = live && j < nb;
+        float dw[RG];
+        dw[0] = use ? __half2float(__ushort_as_half((uint16_t)(ds & 0xFFFFu))) : 0.f;
+        dw[1] = use ? __half2float(__ushort_as_half((uint16_t)(ds >> 16))) : 0.f;
+        q40Block<B, RG>(acc, ws, dw, min(j, nb - 1), n, nb, sq, ssc);
+    };
+    // after a step: at the end of a row pair, reduce over the lane group and run the fused
+    // epilogue on its lane 0
+    auto advance = [&]() {
+        if (++ck < K) return;
+#pragma unroll
+        for (int r = 0; r < RG; r++)
+#pragma unroll
+            for (int b = 0; b < B; b++) acc[r][b] = groupSum<L>(acc[r][b]);
+        const int r0 = rowBase + cp * RP + gi * RG;
+        if (li == 0 && r0 < a.rows) {
+#pragma unroll
+            for (int b = 0; b < B; b++) {
+                const float v0 = acc[0][b], v1 = acc[1][b];
+                if constexpr (EPI == EPI_STORE) {
+                    float *o = a.out + (size_t)b * a.ldOut + r0;
+                    o[0] = v0;
+                    if (r0 + 1 < a.rows) o[1] = v1;
+                } else if constexpr (EPI == EPI_ACT) {
+                    a.out[(size_t)b * a.ldOut + (r0 >> 1)] = gateAct(a, v0) * v1;
+                } else if constexpr (EPI == EPI_ACT_Q80) {
+                    hbuf[b * (R >> 1) + ((r0 - rowBase) >> 1)] = gateAct(a, v0) * v1;
+                } else {
+                    qkvPairStore(a, r0, v0, v1, sRope + b * (kMaxHeadSize / 2), posB[b], slotB[b],
+                                 a.out + (size_t)b * a.ldOut);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RG; r++)
+#pragma unroll
+            for (int b = 0; b < B; b++) acc[r][b] = 0.f;
+        ck = 0;
+        ++cp;
+    };
+    // Full rounds: every slot is consumed and refilled, so the slots stay in fixed registers and
+    // consuming slot s waits until only the other kRing-1 slots are in flight.
+    int t0 = 0;
+    for (; t0 + D < T; t0 += D) {
+#pragma unroll
+        for (int s = 0; s < D; s++) {
+            asm volatile("s_waitcnt vmcnt(%3)" : "+v"(w[s][0]), "+v"(w[s][1]), "+v"(dh[s]) : "i"(3 * (D - 1)));
+            consume(w[s], dh[s], true);
+            issue(w[s], dh[s]);
+            advance();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    // Last round: no refills; slot s waits for the loads issued after it (slots s+1..kRing-1), so
+    // every load has landed when the workgroup ends.
+#pragma unroll
+    for (int s = 0; s < D; s++) {
+        asm volatile("s_waitcnt vmcnt(%3)" : "+v"(w[s][0]), "+v"(w[s][1]), "+v"(dh[s]) : "i"(3 * (D - 1 - s)));
+        if (t0 + s < T) {
+            consume(w[s], dh[s], true);
+            advance();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (EPI == EPI_ACT_Q80) {
+        __syncthreads();
+        storeHiddenQ80<B>(a, hbuf, R >> 1, rowBase >> 1);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // GEMV: out[b][row] = W[row,:] . act(in[b,:]), fused prologue/epilogue.
 // ------------------------------------------------------------------------------------------------
@@ -283,78 +581,14 @@ __global__ __launch_bounds__(kThreads) void gemvKernel(GemvArgs a) {
         actF = a.in;
     }
 
-    // Q40: each lane's first KM blocks of its RG rows live in VGPRs; pass p+1's blocks are
-    // issued before pass p is computed (and pass 0's before the prologue).
-    constexpr int KM = KMAX / RG;  // prefetched blocks per row (KMAX loads in flight per lane)
     auto rowOf = [&](int p, int r) { return rowBase + p * RP + gi * RG + r; };
-    u32x4 w[RG][KM], wn[RG][KM];
-    uint16_t dh[RG][KM], dn[RG][KM];
-    auto prefetch = [&](int p, u32x4(&wd)[RG][KM], uint16_t(&dd)[RG][KM]) {
-#pragma unroll
-        for (int r = 0; r < RG; r++) {
-            const int row = min(rowOf(p, r), a.rows - 1);
-            const u32x4 *wrow = reinterpret_cast<const u32x4 *>(a.qs + (size_t)row * nb * 16);
-            const uint16_t *drow = a.wd + (size_t)row * nb;
-#pragma unroll
-            for (int k = 0; k < KM; k++) {  // clamped: no divergent loads
-                const int j = min(li + k * L, nb - 1);
-                wd[r][k] = __builtin_nontemporal_load(wrow + j);
-                dd[r][k] = drow[j];
-            }
-        }
-    };
-    if constexpr (Q40) prefetch(0, w, dh);
     for (int p = 0; p < a.passes; p++) {
         float acc[RG][B];
 #pragma unroll
         for (int r = 0; r < RG; r++)
 #pragma unroll
             for (int b = 0; b < B; b++) acc[r][b] = 0.f;
-        if constexpr (Q40) {
-            if (PRO == PRO_RESNORM && p == 0) {
-                resNormPrologue<B, true>(a, scratch, reinterpret_cast<int8_t *>(smem + lay.act),
-                                         reinterpret_cast<float2 *>(smem + lay.sc), nullptr);
-            }
-            if (p + 1 < a.passes) prefetch(p + 1, wn, dn);
-#pragma unroll
-            for (int k = 0; k < KM; k++) {
-                const int j = li + k * L;
-                u32x4 wk[RG];
-                float dw[RG];
-#pragma unroll
-                for (int r = 0; r < RG; r++) {
-                    wk[r] = w[r][k];
-                    dw[r] = j < nb ? __half2float(__ushort_as_half(dh[r][k])) : 0.f;
-                }
-                q40Block<B, RG>(acc, wk, dw, min(j, nb - 1), n, nb, act, asc);
-            }
-            // remaining blocks (only when nb > KMAX * L), 2 in flight per row and lane
-            for (int j0 = li + KM * L; j0 < nb; j0 += 2 * L) {
-                u32x4 w2[2][RG];
-                float d2[2][RG];
-#pragma unroll
-                for (int u = 0; u < 2; u++) {
-                    const int j = j0 + u * L;
-#pragma unroll
-                    for (int r = 0; r < RG; r++) {
-                        const int row = min(rowOf(p, r), a.rows - 1);
-                        const int jc = min(j, nb - 1);
-                        w2[u][r] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a.qs + (size_t)row * nb * 16) + jc);
-                        const uint16_t hb = a.wd[(size_t)row * nb + jc];
-                        d2[u][r] = j < nb ? __half2float(__ushort_as_half(hb)) : 0.f;
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < 2; u++) q40Block<B, RG>(acc, w2[u], d2[u], min(j0 + u * L, nb - 1), n, nb, act, asc);
-            }
-#pragma unroll
-            for (int r = 0; r < RG; r++)
-#pragma unroll
-                for (int k = 0; k < KM; k++) {
-                    w[r][k] = wn[r][k];
-                    dh[r][k] = dn[r][k];
-                }
-        } else {
+        {
             if (PRO == PRO_RESNORM && p == 0) {
                 resNormPrologue<B, false>(a, scratch, nullptr, nullptr, reinterpret_cast<float *>(smem + lay.act));
             }
@@ -403,72 +637,32 @@ __global__ __launch_bounds__(kThreads) void gemvKernel(GemvArgs a) {
         const float v0 = res[b * R + 2 * k], v1 = res[b * R + 2 * k + 1];
         if constexpr (EPI == EPI_ACT || EPI == EPI_ACT_Q80) {
             // interleaved rows: 2i = gate (w1), 2i+1 = up (w3)
-            float g;
-            if (a.act == 1) {
-                g = v0 / (1.0f + __expf(-v0));
-            } else {
-                g = 0.5f * v0 * (1.0f + tanhf(0.79788456080286535588f * v0 * (1.0f + 0.044715f * v0 * v0)));
-            }
+            const float g = gateAct(a, v0);
             if constexpr (EPI == EPI_ACT) {
                 if (r0 < a.rows) a.out[(size_t)b * a.ldOut + (r0 >> 1)] = g * v1;
             } else {
                 hbuf[b * halfR + k] = g * v1;
             }
         } else if constexpr (EPI == EPI_QKV) {
-            if (r0 >= a.rows) continue;
-            const int p = a.pos[b];
-            const int sl = a.slot[b];
-            if (r0 < a.q0 + a.kv0) {
-                const float2 cs = a.rope[(size_t)p * (a.hs >> 1) + ((r0 % a.hs) >> 1)];
-                const float o0 = v0 * cs.x - v1 * cs.y;
-                const float o1 = v0 * cs.y + v1 * cs.x;
-                if (r0 < a.q0) {
-                    *reinterpret_cast<float2 *>(a.out + (size_t)b * a.ldOut + r0) = make_float2(o0, o1);
-                } else {
-                    const size_t off = ((size_t)sl * a.seqLen + p) * a.kv0 + (r0 - a.q0);
-                    if (a.kvBf16) {
-                        uint32_t pk = (uint32_t)f32ToBf16(o0) | ((uint32_t)f32ToBf16(o1) << 16);
-                        *reinterpret_cast<uint32_t *>(reinterpret_cast<uint16_t *>(a.kcache) + off) = pk;
-                    } else {
-                        *reinterpret_cast<float2 *>(reinterpret_cast<float *>(a.kcache) + off) = make_float2(o0, o1);
-                    }
-                }
-            } else {
-                const size_t off = ((size_t)sl * a.seqLen + p) * a.kv0 + (r0 - a.q0 - a.kv0);
-                if (a.kvBf16) {
-                    uint32_t pk = (uint32_t)f32ToBf16(v0) | ((uint32_t)f32ToBf16(v1) << 16);
-                    *reinterpret_cast<uint32_t *>(reinterpret_cast<uint16_t *>(a.vcache) + off) = pk;
-                } else {
-                    *reinterpret_cast<float2 *>(reinterpret_cast<float *>(a.vcache) + off) = make_float2(v0, v1);
-                }
-            }
+            if (r0 < a.rows) qkvPairStore(a, r0, v0, v1, a.rope + (size_t)a.pos[b] * (a.hs >> 1), a.pos[b], a.slot[b],
+                                          a.out + (size_t)b * a.ldOut);
         }
     }
     if constexpr (EPI == EPI_ACT_Q80) {
-        // quantize the workgroup's R/2 hidden units (a multiple of 32) into Q80 blocks
         __syncthreads();
-        const int hBase = rowBase >> 1;
-        for (int i = tid; i < B * halfR; i += kThreads) {  // 32-lane groups = one block
-            const int b = i / halfR, k = i % halfR;
-            const float h = hbuf[b * halfR + k];
-            const float amax = groupMax<32>(fabsf(h));
-            const float d = amax / 127.0f;
-            const float id = d != 0.f ? 1.0f / d : 0.f;
-            int q = (int)rintf(h * id);
-            q = q > 127 ? 127 : (q < -127 ? -127 : q);
-            a.oq[(size_t)b * a.ldOut + hBase + k] = (int8_t)q;
-            const float qs = groupSum<32>((float)q);
-            if ((k & 31) == 0) a.os[(size_t)b * (a.ldOut >> 5) + ((hBase + k) >> 5)] = make_float2(roundF16(d), qs);
-        }
+        storeHiddenQ80<B>(a, hbuf, halfR, rowBase >> 1);
     }
 }
 
 template <int L, int B, bool Q40>
 static void gemvDispatchPE(const GemvArgs &a, int pro, int epi, size_t lds, int grid, hipStream_t s) {
-#define DL_GEMV_CASE(P, E)                                                                     \
-    if (pro == P && epi == E) {                                                                \
-        hipLaunchKernelGGL((gemvKernel<L, B, P, E, Q40>), dim3(grid), dim3(kThreads), lds, s, a); \
-        return;                                                                                \
+#define DL_GEMV_CASE(P, E)                                                                          \
+    if (pro == P && epi == E) {                                                                     \
+        if constexpr (Q40)                                                                          \
+            hipLaunchKernelGGL((gemvQ40Kernel<L, B, P, E>), dim3(grid), dim3(kThreads), lds, s, a); \
+        else                                                                                        \
+            hipLaunchKernelGGL((gemvKernel<L, B, P, E, false>), dim3(grid), dim3(kThreads), lds, s, a); \
+        return;                                                                                     \
     }
     DL_GEMV_CASE(PRO_GLOBAL, EPI_STORE)
     DL_GEMV_CASE(PRO_RESNORM, EPI_STORE)

@@ -27,14 +27,9 @@ for name, rows, n, pro, epi in shapes:
     mb = rows * n * 0.5625 / 1e6
     line = f"{name} {rows:6d}x{n:5d} {mb:7.1f} MB |"
     for v in variants:
-        lanes, passes = 0, 1
+        lanes, passes = 0, 0  # 0 = engine default (lanes per row / residency rule)
         if v != "auto":
             lanes, passes = [int(x) for x in v.split("x")]
-        if epi == EPI_ACT_Q80:
-            L = lanes or (16 if n // 32 <= 128 else (32 if n // 32 <= 256 else 64))  # rows >= 65536 here
-            passes = max(passes, 64 // (256 // L * 2))
-        elif v == "auto":
-            passes = max(1, min(4, rows // (256 // (lanes or 16) * 2) // 1024))
         us = C.bench_gemv_q40(rows, n, pro, epi, 1, lanes, passes, 8, 200)
         line += f" {v}: {us:6.2f} us {mb / us:5.2f} TB/s |"
     print(line, flush=True)
