@@ -54,23 +54,37 @@ def main() -> int:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     dist = None
     uid = None
+    comm = None
+    max_batch = max(32, args.batch)
+    comm_kind = os.environ.get("DL_TP_COMM", "xgmi")
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as tdist
         dist = tdist
-        # control plane only (barriers, timing max, RCCL id exchange); the data plane is the
-        # engine's own RCCL communicator
+        # control plane only (barriers, timing max, IPC handle / RCCL id exchange); the data plane
+        # is the engine's own device communicator
         dist.init_process_group("gloo")
-        obj = [C.rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        uid = obj[0]
-    torch.cuda.set_device(local)
+        if comm_kind == "xgmi":
+            # one-shot collectives over IPC-mapped peer buffers (csrc/hip/xgmi_comm.cpp)
+            hdr = C.load_header(args.model) if args.model else LLAMA31_8B
+            vocab0 = -(-hdr["vocab_size"] // world)
+            max_floats = max_batch * max(hdr["dim"], vocab0)
+            comm = C.XgmiComm(rank, world, max_floats, local)
+            handles = [None] * world
+            dist.all_gather_object(handles, comm.handle())
+            comm.connect(handles)
+            dist.barrier()
+        else:
+            obj = [C.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            uid = obj[0]
 
     seq_len = args.prompt + args.warmup + args.steps + 8
     synthetic = None if args.model else dict(LLAMA31_8B, seq_len=seq_len)
     t0 = time.time()
-    eng = C.HipEngine(args.model, "q80", max_seq_len=seq_len, max_batch=max(32, args.batch), n_slots=args.batch,
+    eng = C.HipEngine(args.model, "q80", max_seq_len=seq_len, max_batch=max_batch, n_slots=args.batch,
                       gpu_index=local, use_graphs=not args.no_graphs, synthetic=synthetic, seed=1234, rank=rank,
-                      world=world, uid=uid)
+                      world=world, uid=uid, comm=comm)
     load_s = time.time() - t0
     B = args.batch
 
@@ -136,6 +150,7 @@ def main() -> int:
             "device_ms_per_step": round(dev_ms / args.steps, 4),
             "load_s": round(load_s, 2),
             "hip_graphs": not args.no_graphs,
+            "tp_comm": comm_kind if world > 1 else None,
         },
     }
     if rank == 0:

@@ -30,4 +30,18 @@ std::vector<unsigned char> rcclGetUniqueId();
 // Must be called with the HIP device of this rank already selected.
 std::unique_ptr<DeviceComm> makeRcclComm(const std::vector<unsigned char> &uid, int rank, int size);
 
+#define DL_HIP(x)                                                                                        \
+    do {                                                                                                 \
+        hipError_t e_ = (x);                                                                             \
+        if (e_ != hipSuccess) throw Error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x); \
+    } while (0)
+
+// One-shot xGMI collectives over IPC-shared buffers (xgmi_comm.cpp). Bootstrap: create on every
+// rank (device selected), exchange xgmiHandle() bytes over the control plane, xgmiConnect() with
+// all ranks' handles, barrier, then use. maxFloats bounds any single message (per rank).
+std::unique_ptr<DeviceComm> makeXgmiComm(int rank, int world, size_t maxFloats);
+std::string xgmiHandle(DeviceComm *c);
+void xgmiConnect(DeviceComm *c, const std::vector<std::string> &handles);
+bool xgmiTimedOut(DeviceComm *c);
+
 }  // namespace dl

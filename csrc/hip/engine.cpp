@@ -22,11 +22,6 @@
 
 namespace dl {
 
-#define DL_HIP(x)                                                                                        \
-    do {                                                                                                 \
-        hipError_t e_ = (x);                                                                             \
-        if (e_ != hipSuccess) throw Error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x); \
-    } while (0)
 
 int hipDeviceCount() {
     int n = 0;
@@ -744,6 +739,22 @@ double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int pas
     a.ldOut = outRows;
     a.oq = oq;
     a.os = os;
+    if (epi == hipk::EPI_QKV) {  // Llama-like split: q = 2/3 of the rows, k = v = 1/6, one position
+        a.hs = 128;
+        a.kv0 = rows / 6;
+        a.q0 = rows - 2 * a.kv0;
+        a.seqLen = 1;
+        a.kvBf16 = 1;
+        float2 *rope = (float2 *)alloc(64 * sizeof(float2));
+        int *zeros = (int *)alloc(64 * sizeof(int));
+        DL_HIP(hipMemsetAsync(rope, 0, 64 * sizeof(float2), s));
+        DL_HIP(hipMemsetAsync(zeros, 0, 64 * sizeof(int), s));
+        a.rope = rope;
+        a.pos = zeros;
+        a.slot = zeros;
+        a.kcache = alloc((size_t)a.kv0 * 2);
+        a.vcache = alloc((size_t)a.kv0 * 2);
+    }
     auto launch = [&](int c) {
         a.qs = qs[c % copies];
         a.wd = d[c % copies];

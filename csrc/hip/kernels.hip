@@ -48,11 +48,13 @@ static int minLanesOverride() {
 int gemvLanesPerRow(int n, int rows, int B, bool q40) {
     int L;
     if (q40) {
-        // Ring kernel: the fewest lanes per row (longest per-lane block sequence, cheapest
-        // reduction) that still gives >= 256 workgroups, i.e. every CU streams.
+        // Ring kernel: the fewest lanes per row (longest per-lane step sequence, so the whole
+        // ring is real work, cheapest reduction, fewest redundant prologues) that still spreads
+        // over >= 3/4 of the CUs (measured: qkv 6144x4096 7.1 us at L=16 / 192 WGs vs 8.3 us at
+        // L=32 / 384 WGs; wo 4096x4096 4.2 us at L=32 / 256 WGs vs 4.9 us at L=16 / 128 WGs).
         const int groups = (rows + 1) / 2;
         L = 16;
-        while (L < 64 && (size_t)groups * L / kThreads < 256) L *= 2;
+        while (L < 64 && (size_t)groups * L / kThreads < 192) L *= 2;
     } else {
         const int n4 = n / 4;
         L = n4 >= 2048 ? 64 : (n4 >= 512 ? 32 : 16);
@@ -208,12 +210,17 @@ __device__ __forceinline__ void resNormPrologue(const GemvArgs &a, float *scratc
         const float *yi = a.addIn ? a.addIn + (size_t)b * a.ldIn : nullptr;
         float *xo = (blockIdx.x == 0 && a.xNext) ? a.xNext + (size_t)b * a.ldIn : nullptr;
         float v[PMAX][8];
+        float4 nw[PMAX][2];  // norm weights, fetched in the same round trip as x and delta
         float ss = 0.f;
         if (inReg) {
 #pragma unroll
             for (int k = 0; k < PMAX; k++) {
                 const int c = tid + k * kThreads;
                 if (c < nChunks) {
+                    if (a.normW) {
+                        nw[k][0] = ld4(a.normW + c * 8);
+                        nw[k][1] = ld4(a.normW + c * 8 + 4);
+                    }
                     float4 v0 = ld4(xi + c * 8), v1 = ld4(xi + c * 8 + 4);
                     if (yi) {
                         const float4 y0 = ld4(yi + c * 8), y1 = ld4(yi + c * 8 + 4);
@@ -252,7 +259,7 @@ __device__ __forceinline__ void resNormPrologue(const GemvArgs &a, float *scratc
                 const int c = tid + k * kThreads;
                 if (c < nChunks) {
                     if (a.normW) {
-                        const float4 w0 = ld4(a.normW + c * 8), w1 = ld4(a.normW + c * 8 + 4);
+                        const float4 w0 = nw[k][0], w1 = nw[k][1];
                         const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
                         for (int i = 0; i < 8; i++) v[k][i] = wv[i] * (inv * v[k][i]);

@@ -1,0 +1,240 @@
+// One-shot all-reduce / all-gather over xGMI peer-to-peer, for the small per-layer tensor-parallel
+// exchanges of decode (16 KB per all-reduce at batch 1 for an 8B model).
+//
+// Replaces both the reference's star all-gather over TCP (nn-network.cpp:537-569) and, on the
+// hot path, RCCL's ring/LL collectives: for a few KB the cost is latency, so every rank publishes
+// its vector once in its own HBM and every rank reads all peers' copies directly over xGMI
+// (one hop, all links in parallel) and reduces them locally in rank order, so the results are
+// bitwise identical on all ranks.
+//
+// Buffers (one hipMalloc per rank, shared with peers through IPC handles):
+//   pub[2][maxFloats]   published vectors, double-buffered by epoch parity
+//   flags[W][kSlots]    flags[p][g] = last epoch rank p published for slot g (written remotely)
+//   epochs[kSlots]      local epoch per slot
+//   error               set when a wait timed out
+// Elements are owned by fixed slots: chunk c (kChunk floats) belongs to slot c % kSlots, for
+// every message size, so a slot only ever races with the same slot on other ranks. Protocol per
+// call and slot (workgroup g): e = ++epochs[g]; write my chunks to pub[e&1]; release (system);
+// store e into every peer's flags[me][g]; wait until my flags[p][g] >= e for all peers; acquire;
+// read the chunks from every rank's pub[e&1]. A rank can only reuse pub[e&1] at epoch e+2 after
+// every peer published e+1 for that slot, i.e. after they finished reading epoch e.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstring>
+#include <thread>
+
+#include "../core/common.h"
+#include "device_comm.h"
+
+namespace dl {
+
+namespace {
+
+constexpr int kSlots = 64;          // workgroups per call (max)
+constexpr int kChunk = 1024;        // floats per chunk (256 threads x float4)
+constexpr int kMaxRanks = 16;
+constexpr int kThreads = 256;
+
+struct XgmiPeers {
+    float *pub[kMaxRanks];          // each rank's pub base (pub[p] + parity * maxFloats)
+    int *flags[kMaxRanks];          // each rank's flags base: [W][kSlots]
+};
+
+struct XgmiCall {
+    XgmiPeers peers;
+    int *epochs;                    // local
+    int *error;                     // local
+    const float *in;                // local input (n floats)
+    float *out;                     // local output (n floats for reduce, W*n for gather)
+    long long maxFloats;
+    long long n;
+    int rank, world, gather;
+    long long timeoutTicks;         // s_memrealtime ticks (100 MHz)
+};
+
+__device__ __forceinline__ long long rtClock() { return (long long)__builtin_amdgcn_s_memrealtime(); }
+
+__global__ __launch_bounds__(kThreads) void xgmiKernel(XgmiCall a) {
+    const int g = blockIdx.x, tid = threadIdx.x;
+    const long long nChunks = (a.n + kChunk - 1) / kChunk;
+    if (g >= nChunks) return;  // no chunk for this slot at this size (same on every rank)
+    __shared__ int sEpoch;
+    if (tid == 0) sEpoch = a.epochs[g] + 1;
+    __syncthreads();
+    const int e = sEpoch, q = e & 1;
+    float *myPub = a.peers.pub[a.rank] + (long long)q * a.maxFloats;
+    // 1. publish my chunks
+    for (long long c = g; c < nChunks; c += kSlots) {
+        const long long i = c * kChunk + tid * 4;
+        if (i + 3 < a.n) {
+            *reinterpret_cast<float4 *>(myPub + i) = *reinterpret_cast<const float4 *>(a.in + i);
+        } else {
+            for (long long k = i; k < a.n; k++) myPub[k] = a.in[k];
+        }
+    }
+    __syncthreads();
+    // 2. signal every peer, then wait for every peer's signal (one lane per peer)
+    if (tid < a.world) {
+        __threadfence_system();  // release: my chunks are visible at system scope
+        if (tid != a.rank) {
+            int *remote = a.peers.flags[tid] + a.rank * kSlots + g;
+            __hip_atomic_store(remote, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            int *local = a.peers.flags[a.rank] + tid * kSlots + g;
+            const long long t0 = rtClock();
+            while (__hip_atomic_load(local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+                __builtin_amdgcn_s_sleep(1);
+                if (rtClock() - t0 > a.timeoutTicks) {  // a peer never arrived: give up, flag it
+                    __hip_atomic_store(a.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system-scope acquire: drop stale lines
+    }
+    __syncthreads();
+    // 3. reduce (rank order, identical on every rank) or gather
+    for (long long c = g; c < nChunks; c += kSlots) {
+        const long long i = c * kChunk + tid * 4;
+        const long long cnt = i + 3 < a.n ? 4 : (i < a.n ? a.n - i : 0);
+        if (cnt <= 0) continue;
+        if (!a.gather) {
+            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (cnt == 4) {
+                float4 v[kMaxRanks];  // all peers' loads in flight at once
+#pragma unroll
+                for (int p = 0; p < kMaxRanks; p++)
+                    if (p < a.world)
+                        v[p] = *reinterpret_cast<const float4 *>(a.peers.pub[p] + (long long)q * a.maxFloats + i);
+#pragma unroll
+                for (int p = 0; p < kMaxRanks; p++)
+                    if (p < a.world) {
+                        acc.x += v[p].x;
+                        acc.y += v[p].y;
+                        acc.z += v[p].z;
+                        acc.w += v[p].w;
+                    }
+                *reinterpret_cast<float4 *>(a.out + i) = acc;
+            } else {
+                for (long long k = 0; k < cnt; k++) {
+                    float s = 0.f;
+                    for (int p = 0; p < a.world; p++) s += a.peers.pub[p][(long long)q * a.maxFloats + i + k];
+                    a.out[i + k] = s;
+                }
+            }
+        } else {
+            for (int p = 0; p < a.world; p++) {
+                const float *src = a.peers.pub[p] + (long long)q * a.maxFloats + i;
+                float *dst = a.out + (long long)p * a.n + i;
+                if (cnt == 4)
+                    *reinterpret_cast<float4 *>(dst) = *reinterpret_cast<const float4 *>(src);
+                else
+                    for (long long k = 0; k < cnt; k++) dst[k] = src[k];
+            }
+        }
+    }
+    if (tid == 0) a.epochs[g] = e;
+}
+
+class XgmiComm : public DeviceComm {
+  public:
+    XgmiComm(int rank, int world, size_t maxFloats) : rank_(rank), world_(world), maxFloats_(maxFloats) {
+        DL_CHECK(world >= 1 && world <= kMaxRanks, "xgmi comm: world size must be 1..16");
+        DL_CHECK(rank >= 0 && rank < world, "xgmi comm: bad rank");
+        maxFloats_ = (maxFloats_ + kChunk - 1) / kChunk * kChunk;
+        pubBytes_ = 2 * maxFloats_ * sizeof(float);
+        flagsBytes_ = (size_t)kMaxRanks * kSlots * sizeof(int);
+        const size_t total = pubBytes_ + flagsBytes_ + kSlots * sizeof(int) + 64;
+        DL_HIP(hipMalloc(&base_, total));
+        DL_HIP(hipMemset(base_, 0, total));
+        DL_HIP(hipDeviceSynchronize());
+        epochs_ = reinterpret_cast<int *>(static_cast<char *>(base_) + pubBytes_ + flagsBytes_);
+        error_ = epochs_ + kSlots;
+        hipIpcMemHandle_t h;
+        DL_HIP(hipIpcGetMemHandle(&h, base_));
+        handle_.assign(reinterpret_cast<const char *>(&h), reinterpret_cast<const char *>(&h) + sizeof(h));
+    }
+    ~XgmiComm() override {
+        for (int p = 0; p < world_; p++)
+            if (p != rank_ && peerBase_[p]) (void)hipIpcCloseMemHandle(peerBase_[p]);
+        if (base_) (void)hipFree(base_);
+    }
+    const std::string &handle() const { return handle_; }
+    // handles[p] = rank p's handle() bytes; call on every rank after all ranks were created.
+    void connect(const std::vector<std::string> &handles) {
+        DL_CHECK((int)handles.size() == world_, "xgmi comm: need one handle per rank");
+        for (int p = 0; p < world_; p++) {
+            if (p == rank_) {
+                peerBase_[p] = base_;
+            } else {
+                DL_CHECK(handles[p].size() == sizeof(hipIpcMemHandle_t), "xgmi comm: bad handle size");
+                hipIpcMemHandle_t h;
+                std::memcpy(&h, handles[p].data(), sizeof(h));
+                DL_HIP(hipIpcOpenMemHandle(&peerBase_[p], h, hipIpcMemLazyEnablePeerAccess));
+            }
+            peers_.pub[p] = static_cast<float *>(peerBase_[p]);
+            peers_.flags[p] = reinterpret_cast<int *>(static_cast<char *>(peerBase_[p]) + pubBytes_);
+        }
+        connected_ = true;
+    }
+    int rank() const override { return rank_; }
+    int size() const override { return world_; }
+    std::string name() const override { return "xgmi"; }
+    void allReduceSum(float *buf, size_t n, hipStream_t s) override { launch(buf, buf, n, false, s); }
+    void allGather(const float *send, float *recv, size_t nPerRank, hipStream_t s) override {
+        launch(send, recv, nPerRank, true, s);
+    }
+    void broadcastInts(int *, size_t, int, hipStream_t) override {
+        throw Error("xgmi comm: broadcastInts is not used on the device data plane");
+    }
+    bool timedOut() {
+        int v = 0;
+        DL_HIP(hipMemcpy(&v, error_, sizeof(int), hipMemcpyDeviceToHost));
+        return v != 0;
+    }
+
+  private:
+    void launch(const float *in, float *out, size_t n, bool gather, hipStream_t s) {
+        DL_CHECK(connected_, "xgmi comm: connect() was not called");
+        DL_CHECK(n <= maxFloats_, "xgmi comm: message larger than the published buffer");
+        XgmiCall c;
+        c.peers = peers_;
+        c.epochs = epochs_;
+        c.error = error_;
+        c.in = in;
+        c.out = out;
+        c.maxFloats = (long long)maxFloats_;
+        c.n = (long long)n;
+        c.rank = rank_;
+        c.world = world_;
+        c.gather = gather ? 1 : 0;
+        c.timeoutTicks = 200LL * 1000 * 1000;  // 2 s at 100 MHz
+        const long long chunks = ((long long)n + kChunk - 1) / kChunk;
+        const int grid = (int)(chunks < kSlots ? chunks : kSlots);
+        if (grid == 0) return;
+        hipLaunchKernelGGL(xgmiKernel, dim3(grid), dim3(kThreads), 0, s, c);
+        DL_HIP(hipGetLastError());
+    }
+
+    int rank_, world_;
+    size_t maxFloats_, pubBytes_ = 0, flagsBytes_ = 0;
+    void *base_ = nullptr;
+    void *peerBase_[kMaxRanks] = {};
+    XgmiPeers peers_{};
+    int *epochs_ = nullptr, *error_ = nullptr;
+    std::string handle_;
+    bool connected_ = false;
+};
+
+}  // namespace
+
+std::unique_ptr<DeviceComm> makeXgmiComm(int rank, int world, size_t maxFloats) {
+    return std::unique_ptr<DeviceComm>(new XgmiComm(rank, world, maxFloats));
+}
+std::string xgmiHandle(DeviceComm *c) { return static_cast<XgmiComm *>(c)->handle(); }
+void xgmiConnect(DeviceComm *c, const std::vector<std::string> &handles) {
+    static_cast<XgmiComm *>(c)->connect(handles);
+}
+bool xgmiTimedOut(DeviceComm *c) { return static_cast<XgmiComm *>(c)->timedOut(); }
+
+}  // namespace dl

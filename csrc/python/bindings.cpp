@@ -118,9 +118,14 @@ std::vector<int> runArgmax(Backend &b, const std::vector<int> &tokens, const std
     return out;
 }
 
+// Device communicator owned from Python (xGMI one-shot collectives); shared with engines.
+struct PyComm {
+    std::shared_ptr<DeviceComm> comm;
+};
+
 // Keeps the device comm alive as long as the engine.
 struct PyHipEngine {
-    std::unique_ptr<DeviceComm> comm;
+    std::shared_ptr<DeviceComm> comm;
     std::unique_ptr<HipEngine> engine;
 };
 
@@ -307,22 +312,82 @@ PYBIND11_MODULE(_C, m) {
         return py::bytes(std::string(v.begin(), v.end()));
     });
 
+    py::class_<PyComm>(m, "XgmiComm")
+        .def(py::init([](int rank, int world, size_t maxFloats, int gpuIndex) {
+                 auto *c = new PyComm();
+                 py::gil_scoped_release rel;
+                 (void)hipSetDevice(gpuIndex);
+                 c->comm = std::shared_ptr<DeviceComm>(makeXgmiComm(rank, world, maxFloats).release());
+                 return c;
+             }),
+             py::arg("rank"), py::arg("world"), py::arg("max_floats"), py::arg("gpu_index") = 0)
+        .def("handle", [](PyComm &c) { return py::bytes(xgmiHandle(c.comm.get())); })
+        .def("connect",
+             [](PyComm &c, const std::vector<py::bytes> &handles) {
+                 std::vector<std::string> hs;
+                 for (auto &h : handles) hs.push_back(std::string(h));
+                 py::gil_scoped_release rel;
+                 xgmiConnect(c.comm.get(), hs);
+             })
+        .def("timed_out", [](PyComm &c) { return xgmiTimedOut(c.comm.get()); })
+        .def_property_readonly("rank", [](PyComm &c) { return c.comm->rank(); })
+        .def_property_readonly("world", [](PyComm &c) { return c.comm->size(); })
+        // test helpers: host vector in, collective result out (device round trip on the null stream)
+        .def("all_reduce",
+             [](PyComm &c, py::array_t<float, py::array::c_style | py::array::forcecast> x) {
+                 const size_t n = (size_t)x.size();
+                 py::array_t<float> out((py::ssize_t)n);
+                 std::vector<float> h(x.data(), x.data() + n);
+                 {
+                     py::gil_scoped_release rel;
+                     float *d;
+                     DL_HIP(hipMalloc(&d, n * 4));
+                     DL_HIP(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+                     c.comm->allReduceSum(d, n, nullptr);
+                     DL_HIP(hipMemcpy(h.data(), d, n * 4, hipMemcpyDeviceToHost));
+                     DL_HIP(hipFree(d));
+                 }
+                 std::memcpy(out.mutable_data(), h.data(), n * 4);
+                 return out;
+             })
+        .def("all_gather", [](PyComm &c, py::array_t<float, py::array::c_style | py::array::forcecast> x) {
+            const size_t n = (size_t)x.size();
+            const int w = c.comm->size();
+            py::array_t<float> out((py::ssize_t)(n * w));
+            std::vector<float> h(x.data(), x.data() + n), r(n * w);
+            {
+                py::gil_scoped_release rel;
+                float *d, *o;
+                DL_HIP(hipMalloc(&d, n * 4));
+                DL_HIP(hipMalloc(&o, n * w * 4));
+                DL_HIP(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+                c.comm->allGather(d, o, n, nullptr);
+                DL_HIP(hipMemcpy(r.data(), o, n * w * 4, hipMemcpyDeviceToHost));
+                DL_HIP(hipFree(d));
+                DL_HIP(hipFree(o));
+            }
+            std::memcpy(out.mutable_data(), r.data(), n * w * 4);
+            return out;
+        });
+
     py::class_<PyHipEngine>(m, "HipEngine")
         .def(py::init([](const std::string &model, const std::string &bufferType, u32 maxSeqLen, u32 maxBatch,
                          u32 nSlots, int gpuIndex, bool useGraphs, bool kvBf16, py::object synthetic, u64 seed,
-                         int rank, int world, py::object uid) {
+                         int rank, int world, py::object uid, py::object comm) {
                  EngineConfig c = makeConfig(model, bufferType, 1, maxSeqLen, maxBatch, nSlots, gpuIndex, useGraphs,
                                              kvBf16, synthetic, seed);
                  auto *e = new PyHipEngine();
+                 if (!comm.is_none()) e->comm = comm.cast<PyComm &>().comm;
                  py::gil_scoped_release rel;
-                 if (world > 1) {
+                 if (world > 1 && !e->comm) {
                      std::string s;
                      {
                          py::gil_scoped_acquire acq;
                          s = uid.cast<std::string>();
                      }
                      (void)hipSetDevice(gpuIndex >= 0 ? gpuIndex : 0);
-                     e->comm = makeRcclComm(std::vector<unsigned char>(s.begin(), s.end()), rank, world);
+                     e->comm = std::shared_ptr<DeviceComm>(
+                         makeRcclComm(std::vector<unsigned char>(s.begin(), s.end()), rank, world).release());
                  }
                  e->engine = makeHipEngine(c, e->comm.get());
                  return e;
@@ -330,7 +395,7 @@ PYBIND11_MODULE(_C, m) {
              py::arg("model") = "", py::arg("buffer_type") = "q80", py::arg("max_seq_len") = 0,
              py::arg("max_batch") = 32, py::arg("n_slots") = 1, py::arg("gpu_index") = 0, py::arg("use_graphs") = true,
              py::arg("kv_bf16") = true, py::arg("synthetic") = py::none(), py::arg("seed") = 1234, py::arg("rank") = 0,
-             py::arg("world") = 1, py::arg("uid") = py::none())
+             py::arg("world") = 1, py::arg("uid") = py::none(), py::arg("comm") = py::none())
         .def_property_readonly("header", [](const PyHipEngine &e) { return headerToDict(e.engine->header()); })
         .def_property_readonly("device_bytes", [](const PyHipEngine &e) { return e.engine->deviceBytes(); })
         .def("forward", [](PyHipEngine &e, std::vector<int> t, std::vector<int> p, std::vector<int> s) { return runForward(*e.engine, t, p, s); },

@@ -11,6 +11,8 @@ EPI_STORE, EPI_ACT, EPI_QKV, EPI_ACT_Q80 = 0, 1, 2, 3
 shapes = [
     # name, rows, n, pro, epi
     ("qkv  tp1", 6144, 4096, PRO_RESNORM, EPI_STORE),
+    ("qkvQ tp1", 6144, 4096, PRO_RESNORM, EPI_QKV),
+    ("qkvG tp1", 6144, 4096, PRO_GLOBAL, EPI_STORE),
     ("wo   tp1", 4096, 4096, PRO_GLOBAL, EPI_STORE),
     ("w13  tp1", 28672, 4096, PRO_RESNORM, EPI_ACT_Q80),
     ("w2   tp1", 4096, 14336, PRO_GLOBAL, EPI_STORE),
@@ -30,6 +32,7 @@ for name, rows, n, pro, epi in shapes:
         lanes, passes = 0, 0  # 0 = engine default (lanes per row / residency rule)
         if v != "auto":
             lanes, passes = [int(x) for x in v.split("x")]
-        us = C.bench_gemv_q40(rows, n, pro, epi, 1, lanes, passes, 8, 200)
+        us = C.bench_gemv_q40(rows, n, pro, epi, int(os.environ.get("BATCH", "1")), lanes, passes,
+                              int(os.environ.get("COPIES", "8")), 200)
         line += f" {v}: {us:6.2f} us {mb / us:5.2f} TB/s |"
     print(line, flush=True)
