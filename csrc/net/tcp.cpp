@@ -187,7 +187,7 @@ std::string encodeWorkerConfig(const WorkerConfig &c) {
       << "\nh_theta=" << h.ropeTheta << "\nh_wtype=" << (int)h.weightType << "\nh_act=" << (int)h.hiddenAct
       << "\nh_rsf=" << h.ropeScalingFactor << "\nh_rlo=" << h.ropeScalingLowFreqFactor
       << "\nh_rhi=" << h.ropeScalingHighFreqFactor << "\nh_rorig=" << h.ropeScalingOrigMaxSeqLen
-      << "\nuid=" << hexOf(c.rcclUid) << "\n";
+      << "\nuid=" << hexOf(c.rcclUid) << "\ndev_comm=" << c.devComm << "\nxgmi_max=" << c.xgmiMaxFloats << "\n";
     return o.str();
 }
 
@@ -231,6 +231,8 @@ WorkerConfig decodeWorkerConfig(const std::string &s) {
         else if (k == "h_rhi") h.ropeScalingHighFreqFactor = std::stof(v);
         else if (k == "h_rorig") h.ropeScalingOrigMaxSeqLen = std::stoul(v);
         else if (k == "uid") c.rcclUid = unhex(v);
+        else if (k == "dev_comm") c.devComm = v;
+        else if (k == "xgmi_max") c.xgmiMaxFloats = std::stoull(v);
     }
     if (!magicOk) throw NetError("bad control-plane magic");
     h.origSeqLen = h.seqLen;

@@ -91,6 +91,8 @@ struct WorkerConfig {
     bool gpu = false;
     EngineConfig engine;
     std::vector<unsigned char> rcclUid;
+    std::string devComm = "xgmi";  // GPU data plane: "xgmi" (IPC one-shot) or "rccl"
+    u64 xgmiMaxFloats = 0;          // largest single message per rank (xgmi)
 };
 std::string encodeWorkerConfig(const WorkerConfig &c);
 WorkerConfig decodeWorkerConfig(const std::string &s);

@@ -1,5 +1,7 @@
 #include "app.h"
 
+#include <cstdlib>
+
 #include <cstdio>
 #include <cstring>
 #include <ctime>
@@ -138,7 +140,15 @@ InferenceSession::InferenceSession(const AppArgs &args, int nSlots) : args_(args
     wc.gpu = gpu_;
     wc.engine = ec;
     if (world > 1) {
-        if (gpu_) wc.rcclUid = rcclGetUniqueId();
+        if (gpu_) {
+            const char *dcEnv = std::getenv("DL_TP_COMM");
+            wc.devComm = dcEnv && *dcEnv ? dcEnv : "xgmi";
+            const ModelHeader h = args.synthetic.empty() ? loadModelHeader(args.modelPath, args.maxSeqLen)
+                                                         : syntheticHeader(args.synthetic, args.maxSeqLen);
+            const u64 vocab0 = (h.vocabSize + world - 1) / world;
+            wc.xgmiMaxFloats = (u64)maxBatch_ * std::max<u64>(h.dim, vocab0);
+            if (wc.devComm == "rccl") wc.rcclUid = rcclGetUniqueId();
+        }
         for (size_t i = 0; i < args.workerHosts.size(); i++) {
             if (logLevel() >= 1)
                 std::printf("⭕ Connecting to worker %s:%d\n", args.workerHosts[i].c_str(), args.workerPorts[i]);
@@ -152,8 +162,21 @@ InferenceSession::InferenceSession(const AppArgs &args, int nSlots) : args_(args
         std::vector<Socket *> peers;
         for (auto &s : workers_) peers.push_back(&s);
         if (gpu_) {
-            (void)hipDeviceCount();
-            devComm_ = makeRcclComm(wc.rcclUid, 0, world);
+            DL_HIP(hipSetDevice(a.gpuIndex));
+            if (wc.devComm == "xgmi") {
+                // every rank publishes an IPC handle of its buffers; the root redistributes them
+                devComm_ = makeXgmiComm(0, world, wc.xgmiMaxFloats);
+                std::vector<std::string> handles{xgmiHandle(devComm_.get())};
+                for (auto &s : workers_) {
+                    if (s.recvPod<u32>() != kAck) throw NetError("worker failed to create its device comm: " + s.recvString());
+                    handles.push_back(s.recvString());
+                }
+                for (auto &s : workers_)
+                    for (auto &hnd : handles) s.sendString(hnd);
+                xgmiConnect(devComm_.get(), handles);
+            } else {
+                devComm_ = makeRcclComm(wc.rcclUid, 0, world);
+            }
         } else {
             hostComm_.reset(new TcpHostComm(0, world, peers));
         }
@@ -246,8 +269,17 @@ void runWorker(const AppArgs &args) {
             std::unique_ptr<Backend> backend;
             try {
                 if (wc.gpu) {
-                    (void)hipDeviceCount();
-                    dc = makeRcclComm(wc.rcclUid, (int)wc.rank, (int)wc.world);
+                    DL_HIP(hipSetDevice(ec.gpuIndex));
+                    if (wc.devComm == "xgmi") {
+                        dc = makeXgmiComm((int)wc.rank, (int)wc.world, wc.xgmiMaxFloats);  // failure: reported below
+                        root.sendPod<u32>(kAck);
+                        root.sendString(xgmiHandle(dc.get()));
+                        std::vector<std::string> handles(wc.world);
+                        for (auto &hnd : handles) hnd = root.recvString();
+                        xgmiConnect(dc.get(), handles);
+                    } else {
+                        dc = makeRcclComm(wc.rcclUid, (int)wc.rank, (int)wc.world);
+                    }
                 } else {
                     hc.reset(new TcpHostComm((int)wc.rank, (int)wc.world, {&root}));
                 }

@@ -122,3 +122,36 @@ def test_xgmi_engine_tp2_matches_single(C, tmp_path):
     rel = np.abs(got - ref).max() / np.abs(ref).max()
     assert rel < 3e-2, rel
     assert (got.argmax(-1) == ref.argmax(-1)).all()
+
+
+@pytest.mark.parametrize("n_workers", [1, 3])
+def test_cli_root_workers_over_xgmi(tmp_path, n_workers):
+    """`dllama inference` root + `dllama worker` processes (all on GPU 0 here): the TCP control plane
+    carries the IPC handles, collectives run over xGMI; greedy tokens == single process."""
+    import subprocess
+    import time
+    from conftest import REPO
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    dllama = os.path.join(REPO, "build", "dllama")
+    m, t, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=7, dim=512, n_heads=8,
+                               n_kv_heads=4, hidden_dim=1024)
+    base = [dllama, "inference", "--model", m, "--tokenizer", t, "--buffer-float-type", "q80", "--prompt",
+            "hello world the", "--steps", "24", "--temperature", "0", "--gpu-index", "0"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", DL_TP_COMM="xgmi")
+    ref = subprocess.run(base, capture_output=True, timeout=120, env=env)
+    assert ref.returncode == 0, ref.stdout.decode(errors="replace")
+    preds = lambda out: [l.split("|")[-1] for l in out.decode(errors="replace").splitlines() if l.startswith("🔶 Pred")]
+    ports = [_port() for _ in range(n_workers)]
+    procs = [subprocess.Popen([dllama, "worker", "--port", str(p), "--gpu-index", "0"], stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, env=env) for p in ports]
+    try:
+        time.sleep(0.5)
+        r = subprocess.run(base + ["--workers", *[f"127.0.0.1:{p}" for p in ports]], capture_output=True,
+                           timeout=180, env=env)
+        assert r.returncode == 0, r.stdout.decode(errors="replace")
+        assert preds(r.stdout) == preds(ref.stdout) and len(preds(ref.stdout)) > 0
+    finally:
+        for p in procs:
+            p.kill()
+            p.wait()
