@@ -9,6 +9,8 @@
 //   W1/W3 row slices interleaved      -> one GEMV whose epilogue computes act(w1 x) * (w3 x)
 #include "engine.h"
 
+#include <cstdlib>
+
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -216,6 +218,23 @@ class HipEngineImpl : public HipEngine {
         dAttS_ = dalloc<float2>((size_t)MB * p.q0 / 32);
         dHQ_ = dalloc<int8_t>((size_t)MB * p.hidden0);
         dHS_ = dalloc<float2>((size_t)MB * p.hidden0 / 32);
+        if (q40_) {  // batched (MFMA) path: normalized Q80 activations, split-K partials, counters
+            const size_t wq = std::max<size_t>({(size_t)h_.dim, (size_t)p.hidden0, (size_t)p.q0});
+            dXq_ = dalloc<int8_t>((size_t)MB * wq);
+            dXs_ = dalloc<float2>((size_t)MB * wq / 32);
+            const int mt = std::min((int)MB, kGemmMaxTokens);
+            size_t part = 0;
+            auto acc = [&](int rows, int n) { part = std::max(part, hipk::gemmPartFloats(rows, n, mt)); };
+            acc(p.q0 + 2 * p.kv0, h_.dim);
+            acc(h_.dim, p.q0);
+            acc(2 * p.hidden0, h_.dim);
+            acc(h_.dim, p.hidden0);
+            acc(p.vocab0, h_.dim);
+            if (part) dPart_ = dalloc<float>(part);
+            const int maxTiles = (std::max<int>({(int)(p.q0 + 2 * p.kv0), (int)h_.dim, (int)(2 * p.hidden0), (int)p.vocab0}) + 63) / 64;
+            dGemmCnt_ = dalloc<int>(maxTiles);
+            DL_HIP(hipMemsetAsync(dGemmCnt_, 0, sizeof(int) * maxTiles, stream_));
+        }
         dAttCnt_ = dalloc<int>((size_t)MB * p.nHeads0);
         DL_HIP(hipMemsetAsync(dAttCnt_, 0, sizeof(int) * (size_t)MB * p.nHeads0, stream_));
         dArgV_ = dalloc<float>((size_t)MB * 64);
@@ -499,6 +518,10 @@ class HipEngineImpl : public HipEngine {
     void gemv(const DevMat &m, int n, int pro, int epi, const float *in, int ldIn, const float *add, float *xNext,
               const float *normW, float *out, int ldOut, const DevLayer *L, const int8_t *aq = nullptr,
               const float2 *as = nullptr, int8_t *oq = nullptr, float2 *os = nullptr) {
+        if (q40_ && n >= gemmMinTokens()) {
+            gemmBatched(m, n, pro, epi, in, ldIn, add, xNext, normW, out, ldOut, L, aq, as, oq, os);
+            return;
+        }
         const int bcMax = batchChunk(m, pro, epi);
         for (int c0 = 0; c0 < n;) {
             int bc = n - c0;
@@ -539,6 +562,70 @@ class HipEngineImpl : public HipEngine {
             }
             hipk::launchGemv(a, bc, pro, epi, q40_, stream_);
             c0 += bc;
+        }
+    }
+
+    // rows per forward from which the MFMA GEMM replaces the GEMV (DL_GEMM_MIN, read per call so
+    // tests can compare both paths in one process)
+    static int gemmMinTokens() {
+        const char *e = std::getenv("DL_GEMM_MIN");
+        return e && *e ? std::atoi(e) : 2;
+    }
+
+    // Batched path (>= gemmMinTokens rows): per chunk of <= 32 tokens, an optional norm/quant
+    // kernel (RESNORM) then the MFMA GEMM with the same fused epilogue.
+    void gemmBatched(const DevMat &m, int n, int pro, int epi, const float *in, int ldIn, const float *add,
+                     float *xNext, const float *normW, float *out, int ldOut, const DevLayer *L, const int8_t *aq,
+                     const float2 *as, int8_t *oq, float2 *os) {
+        for (int c0 = 0; c0 < n; c0 += kGemmMaxTokens) {
+            const int bc = std::min(kGemmMaxTokens, n - c0);
+            hipk::GemmArgs g;
+            hipk::GemvArgs &a = g.e;
+            a.qs = m.qs;
+            a.wd = m.d;
+            a.rows = m.rows;
+            a.n = m.n;
+            a.lanes = m.lanes;
+            if (pro == hipk::PRO_RESNORM) {
+                hipk::GemvArgs nq;
+                nq.n = m.n;
+                nq.in = in + (size_t)c0 * ldIn;
+                nq.ldIn = ldIn;
+                nq.addIn = add ? add + (size_t)c0 * ldIn : nullptr;
+                nq.xNext = xNext ? xNext + (size_t)c0 * ldIn : nullptr;
+                nq.normW = normW;
+                nq.eps = h_.normEpsilon;
+                nq.oq = dXq_;
+                nq.os = dXs_;
+                hipk::launchNormQ80(nq, bc, stream_);
+                a.aq = dXq_;
+                a.as = dXs_;
+            } else {
+                a.aq = aq + (size_t)c0 * m.n;
+                a.as = as + (size_t)c0 * (m.n / 32);
+            }
+            a.out = out ? out + (size_t)c0 * ldOut : nullptr;
+            a.ldOut = ldOut;
+            a.oq = oq ? oq + (size_t)c0 * ldOut : nullptr;
+            a.os = os ? os + (size_t)c0 * (ldOut / 32) : nullptr;
+            a.act = h_.hiddenAct == HiddenAct::GELU ? 0 : 1;
+            if (L) {
+                a.q0 = plan_.q0;
+                a.kv0 = plan_.kv0;
+                a.hs = plan_.headSize;
+                a.seqLen = h_.seqLen;
+                a.rope = dRope_;
+                a.pos = dPos_ + c0;
+                a.slot = dSlot_ + c0;
+                a.kcache = L->k;
+                a.vcache = L->v;
+                a.kvBf16 = kvBf16_ ? 1 : 0;
+            }
+            g.M = bc;
+            g.splits = hipk::gemmSplits(m.rows, m.n);
+            g.part = dPart_;
+            g.counters = dGemmCnt_;
+            hipk::launchGemmQ40(g, epi, stream_);
         }
     }
 
@@ -650,6 +737,12 @@ class HipEngineImpl : public HipEngine {
         }
         DL_HIP(hipGetLastError());
     }
+
+    static constexpr int kGemmMaxTokens = 32;
+    int8_t *dXq_ = nullptr;
+    float2 *dXs_ = nullptr;
+    float *dPart_ = nullptr;
+    int *dGemmCnt_ = nullptr;
 
     EngineConfig cfg_;
     DeviceComm *comm_;

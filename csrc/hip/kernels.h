@@ -77,6 +77,23 @@ struct GemvArgs {
     int kvBf16 = 1;
 };
 
+// Batched Q40 matmul on MFMA (2..32 tokens): GemvArgs `e` carries weights (tiled), Q80
+// activations (aq/as [M][n]) and the epilogue fields; split-K partials + per-tile counters
+// (zero-initialised, reset by the kernel) when splits > 1.
+struct GemmArgs {
+    GemvArgs e;
+    int M = 0;
+    int splits = 1;
+    float *part = nullptr;
+    int *counters = nullptr;
+};
+void launchGemmQ40(const GemmArgs &a, int epi, hipStream_t s);
+int gemmSplits(int rows, int n);
+size_t gemmPartFloats(int rows, int n, int maxTokens);
+// Residual add + RMS norm (normW may be null: plain quantization) + Q80 of M rows:
+// in/addIn/xNext [M][ldIn] f32 -> oq [M][n] int8, os [M][n/32] (d, sum q).
+void launchNormQ80(const GemvArgs &a, int M, hipStream_t s);
+
 // B = batch rows in this launch (1, 2 or 4); q40 = weight format.
 void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_t s);
 // Rows handled by one lane group (2 at batch 1: the activation loads are shared by 2 rows).

@@ -27,7 +27,6 @@ using namespace dl::dev;
 
 static constexpr int kThreads = 256;
 static constexpr int kMaxHeadSize = 128;  // RoPE rows staged in LDS by the QKV epilogue
-static constexpr int KMAX = 8;  // weight blocks per lane held in VGPRs (prefetched)
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -199,7 +198,8 @@ __device__ __forceinline__ void stageChunk(float (&v)[8], int b, int c, int n, i
 // Single global pass: each thread keeps up to PMAX chunks of 8 elements per row in registers
 // (n <= 256 * 8 * PMAX); larger inputs fall back to a second pass over L2.
 template <int B, bool Q40>
-__device__ __forceinline__ void resNormPrologue(const GemvArgs &a, float *scratch, int8_t *sq, float2 *ssc, float *sf) {
+__device__ __forceinline__ void resNormPrologue(const GemvArgs &a, float *scratch, int8_t *sq, float2 *ssc, float *sf,
+                                                bool writeX = false) {
     constexpr int PMAX = 4;
     const int n = a.n, tid = threadIdx.x;
     const int nChunks = n >> 3;
@@ -208,7 +208,7 @@ __device__ __forceinline__ void resNormPrologue(const GemvArgs &a, float *scratc
     for (int b = 0; b < B; b++) {
         const float *xi = a.in + (size_t)b * a.ldIn;
         const float *yi = a.addIn ? a.addIn + (size_t)b * a.ldIn : nullptr;
-        float *xo = (blockIdx.x == 0 && a.xNext) ? a.xNext + (size_t)b * a.ldIn : nullptr;
+        float *xo = ((blockIdx.x == 0 || writeX) && a.xNext) ? a.xNext + (size_t)b * a.ldIn : nullptr;
         float v[PMAX][8];
         float4 nw[PMAX][2];  // norm weights, fetched in the same round trip as x and delta
         float ss = 0.f;
@@ -557,14 +557,16 @@ __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// GEMV: out[b][row] = W[row,:] . act(in[b,:]), fused prologue/epilogue.
+// F32-weight GEMV: out[b][row] = W[row,:] . act(in[b,:]), fused prologue/epilogue (Q40 weights use
+// gemvQ40Kernel / gemmQ40Kernel).
 // ------------------------------------------------------------------------------------------------
 template <int L, int B, int PRO, int EPI, bool Q40>
 __global__ __launch_bounds__(kThreads) void gemvKernel(GemvArgs a) {
+    static_assert(!Q40, "Q40 weights go through gemvQ40Kernel");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int RG = gemvRowGroup(B, Q40);  // rows per lane group
     constexpr int RP = kThreads / L * RG;     // rows per pass
-    const int n = a.n, nb = n >> 5;
+    const int n = a.n;
     const int R = RP * a.passes;
     const GemvLds lay = gemvLayout(n, B, Q40, R, PRO);
     float *scratch = reinterpret_cast<float *>(smem + lay.scratch);
@@ -574,19 +576,8 @@ __global__ __launch_bounds__(kThreads) void gemvKernel(GemvArgs a) {
     const int gi = tid / L, li = tid % L;
     const int rowBase = blockIdx.x * R;
 
-    // activation sources
-    const int8_t *act;
-    const float2 *asc;
-    const float *actF;
-    if constexpr (PRO == PRO_RESNORM) {
-        act = reinterpret_cast<const int8_t *>(smem + lay.act);
-        asc = reinterpret_cast<const float2 *>(smem + lay.sc);
-        actF = reinterpret_cast<const float *>(smem + lay.act);
-    } else {
-        act = a.aq;
-        asc = a.as;
-        actF = a.in;
-    }
+    // activation source: normalized copy in LDS or the caller's f32 rows
+    const float *actF = PRO == PRO_RESNORM ? reinterpret_cast<const float *>(smem + lay.act) : a.in;
 
     auto rowOf = [&](int p, int r) { return rowBase + p * RP + gi * RG + r; };
     for (int p = 0; p < a.passes; p++) {
@@ -709,6 +700,227 @@ void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_
             default: gemvDispatchB<64, false>(a, B, pro, epi, lds, grid, s); break;
         }
     }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Batched Q40 x Q80 matmul on MFMA (prefill / multi-user decode, 2..32 tokens per launch).
+//   out[t][row] = sum_k W[row][k] * x[t][k]   with W Q40 (tiled GEMV layout, see Q40Tiling) and
+//   x Q80. Each workgroup owns 64 weight rows (4 waves x 16) and one K split; per Q40 block a
+//   lane dequantizes 8 nibbles of its row into an f16 B fragment (((1024+q) - 1032) * d, one
+//   rounding) and multiplies the 16-token A fragments, staged per 16-block chunk in LDS as f16,
+//   with v_mfma_f32_16x16x32_f16 (f32 accumulate). Split-K partials are combined in split order
+//   by the last-arriving workgroup (agent-scope release/acquire counter, deterministic), which
+//   then runs the same fused epilogues as the GEMV (store / SwiGLU / SwiGLU+Q80 / RoPE+KV).
+// ------------------------------------------------------------------------------------------------
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+static constexpr int kGemmRows = 64;
+static constexpr int kGemmCh = 16;  // Q40 blocks per staged activation chunk
+
+int gemmSplits(int rows, int n) {
+    const int tiles = (rows + kGemmRows - 1) / kGemmRows, nb = n / 32;
+    int S = 1;
+    while (S < 8 && tiles * S < 256 && nb % (2 * S) == 0) S *= 2;
+    return S;
+}
+
+size_t gemmPartFloats(int rows, int n, int maxTokens) {
+    const int tiles = (rows + kGemmRows - 1) / kGemmRows, S = gemmSplits(rows, n);
+    const int mp = (maxTokens + 15) / 16 * 16;
+    return S > 1 ? (size_t)S * tiles * mp * kGemmRows : 0;
+}
+
+static size_t gemmLds(int MT) { return (size_t)MT * 16 * (kGemmCh * 32 + 8) * 2 + (size_t)MT * 16 * kGemmRows * 4 + 16; }
+
+// 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d via the 0x6400 | q magic (1024 + q)
+__device__ __forceinline__ half8 dequantQ40x8(uint2 wv, int nibHi, uint32_t d16) {
+    const uint32_t lo = nibHi ? (wv.x >> 4) & 0x0F0F0F0Fu : wv.x & 0x0F0F0F0Fu;
+    const uint32_t hi = nibHi ? (wv.y >> 4) & 0x0F0F0F0Fu : wv.y & 0x0F0F0F0Fu;
+    // bytes b0..b3 of a word -> f16 pairs 0x64bb: 1024 + nibble
+    const uint32_t p0 = __builtin_amdgcn_perm(0x64646464u, lo, 0x07010700u);
+    const uint32_t p1 = __builtin_amdgcn_perm(0x64646464u, lo, 0x07030702u);
+    const uint32_t p2 = __builtin_amdgcn_perm(0x64646464u, hi, 0x07010700u);
+    const uint32_t p3 = __builtin_amdgcn_perm(0x64646464u, hi, 0x07030702u);
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const _Float16 d = __builtin_bit_cast(_Float16, (uint16_t)d16);
+    // (1024 + q) - 1032 = q - 8 is exact in f16; one rounding in the multiply by d
+    const h2 dd = {d, d};
+    const h2 off = {(_Float16)-1032.0f, (_Float16)-1032.0f};
+    const h2 r0 = (__builtin_bit_cast(h2, p0) + off) * dd;
+    const h2 r1 = (__builtin_bit_cast(h2, p1) + off) * dd;
+    const h2 r2 = (__builtin_bit_cast(h2, p2) + off) * dd;
+    const h2 r3 = (__builtin_bit_cast(h2, p3) + off) * dd;
+    half8 out;
+    out[0] = r0[0]; out[1] = r0[1]; out[2] = r1[0]; out[3] = r1[1];
+    out[4] = r2[0]; out[5] = r2[1]; out[6] = r3[0]; out[7] = r3[1];
+    return out;
+}
+
+template <int MT, int EPI>
+__global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
+    const GemvArgs &a = ga.e;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int MP = MT * 16;
+    constexpr int AST = kGemmCh * 32 + 8;  // f16 per staged token row (+16 B: conflict-free reads)
+    _Float16 *sa = reinterpret_cast<_Float16 *>(smem);
+    float *tile = reinterpret_cast<float *>(smem + (size_t)MP * AST * 2);  // [MP][64]
+    int *flag = reinterpret_cast<int *>(tile + MP * kGemmRows);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int col = lane & 15, h = lane >> 4;
+    const int n = a.n, nb = n >> 5, L = a.lanes, NG = kThreads / L, KS = (nb + L - 1) / L;
+    const int lgL = 31 - __builtin_clz(L);
+    const int tileIdx = blockIdx.x, sp = blockIdx.y, S = ga.splits;
+    const int R0 = tileIdx * kGemmRows;
+    const int row = min(R0 + wave * 16 + col, a.rows - 1);
+    const int g = row / (2 * NG), rem = row % (2 * NG), gi = rem >> 1, rpar = rem & 1;
+    const size_t gBase = (size_t)g * KS;
+    const int bps = nb / S, j0 = sp * bps, j1 = j0 + bps;
+    const int byteHalf = h & 1, nibHi = h >> 1;
+    const uint8_t *qs = a.qs;
+    const uint32_t *wd2 = reinterpret_cast<const uint32_t *>(a.wd);
+
+    f32x4 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int c0 = j0; c0 < j1; c0 += kGemmCh) {
+        const int cn = min(kGemmCh, j1 - c0);
+        __syncthreads();  // previous chunk consumed
+        // stage x[t][c0*32 .. (c0+cn)*32) as f16, 16 elements per item
+        for (int i = tid; i < MP * cn * 2; i += kThreads) {
+            const int t = i / (cn * 2), rest = i % (cn * 2), jb = rest >> 1, hf = rest & 1;
+            typedef _Float16 h16 __attribute__((ext_vector_type(16)));
+            h16 v;
+            if (t < ga.M) {
+                const int4 q = *reinterpret_cast<const int4 *>(a.aq + (size_t)t * n + (size_t)(c0 + jb) * 32 + hf * 16);
+                const float d = a.as[(size_t)t * nb + c0 + jb].x;
+                const int w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int e = 0; e < 16; e++) v[e] = (_Float16)((float)(int8_t)(w4[e >> 2] >> (8 * (e & 3))) * d);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 16; e++) v[e] = (_Float16)0.f;
+            }
+            *reinterpret_cast<h16 *>(sa + (size_t)t * AST + jb * 32 + hf * 16) = v;
+        }
+        __syncthreads();
+        // 4 blocks per step: weight loads first, then dequant + MFMA
+        for (int jj = 0; jj < cn; jj += 4) {
+            uint2 wv[4];
+            uint32_t dw[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int j = min(c0 + jj + u, j1 - 1);
+                const int k = j >> lgL, li = j & (L - 1);
+                const size_t idx = (gBase + k) * kThreads + gi * L + li;
+                const size_t unit = ((gBase + k) * 2 + rpar) * kThreads + gi * L + li;  // 16-B block
+                wv[u] = *reinterpret_cast<const uint2 *>(qs + unit * 16 + byteHalf * 8);
+                dw[u] = wd2[idx];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (jj + u >= cn) break;
+                const uint32_t d16 = rpar ? dw[u] >> 16 : dw[u] & 0xFFFFu;
+                const half8 b = dequantQ40x8(wv[u], nibHi, d16);
+#pragma unroll
+                for (int t = 0; t < MT; t++) {
+                    const half8 av = *reinterpret_cast<const half8 *>(sa + (size_t)(t * 16 + col) * AST + (jj + u) * 32 + 8 * h);
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b, acc[t], 0, 0, 0);
+                }
+            }
+        }
+    }
+    // C layout: weight row (local) wave*16 + col, token t*16 + h*4 + i
+    if (S == 1) {
+#pragma unroll
+        for (int t = 0; t < MT; t++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) tile[(t * 16 + h * 4 + i) * kGemmRows + wave * 16 + col] = acc[t][i];
+    } else {
+        const int tiles = gridDim.x;
+        float *part = ga.part + ((size_t)sp * tiles + tileIdx) * MP * kGemmRows;
+#pragma unroll
+        for (int t = 0; t < MT; t++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) part[(t * 16 + h * 4 + i) * kGemmRows + wave * 16 + col] = acc[t][i];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            const int old = __hip_atomic_fetch_add(ga.counters + tileIdx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            flag[0] = old == S - 1;
+        }
+        __syncthreads();
+        if (!flag[0]) return;
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __hip_atomic_store(ga.counters + tileIdx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        for (int i = tid; i < MP * kGemmRows; i += kThreads) {
+            float v = 0.f;
+            for (int s2 = 0; s2 < S; s2++) v += ga.part[((size_t)s2 * tiles + tileIdx) * MP * kGemmRows + i];
+            tile[i] = v;
+        }
+    }
+    __syncthreads();
+    // fused epilogues on row pairs (2k, 2k+1) of the tile, 32 pairs per token
+    for (int i = tid; i < ga.M * 32; i += kThreads) {
+        const int t = i >> 5, k = i & 31, r0 = R0 + 2 * k;
+        const float v0 = tile[t * kGemmRows + 2 * k], v1 = tile[t * kGemmRows + 2 * k + 1];
+        if constexpr (EPI == EPI_STORE) {
+            if (r0 < a.rows) a.out[(size_t)t * a.ldOut + r0] = v0;
+            if (r0 + 1 < a.rows) a.out[(size_t)t * a.ldOut + r0 + 1] = v1;
+        } else if constexpr (EPI == EPI_ACT) {
+            if (r0 < a.rows) a.out[(size_t)t * a.ldOut + (r0 >> 1)] = gateAct(a, v0) * v1;
+        } else if constexpr (EPI == EPI_ACT_Q80) {
+            const int hBase = R0 >> 1;
+            if (hBase >= (a.rows >> 1)) continue;  // whole 32-unit block: uniform per lane group
+            const float hv = gateAct(a, v0) * v1;
+            const float amax = groupMax<32>(fabsf(hv));
+            const float d = amax / 127.0f;
+            const float id = d != 0.f ? 1.0f / d : 0.f;
+            int q = (int)rintf(hv * id);
+            q = q > 127 ? 127 : (q < -127 ? -127 : q);
+            a.oq[(size_t)t * a.ldOut + hBase + k] = (int8_t)q;
+            const float qsum = groupSum<32>((float)q);
+            if (k == 0) a.os[(size_t)t * (a.ldOut >> 5) + (hBase >> 5)] = make_float2(roundF16(d), qsum);
+        } else {
+            if (r0 < a.rows)
+                qkvPairStore(a, r0, v0, v1, a.rope + (size_t)a.pos[t] * (a.hs >> 1), a.pos[t], a.slot[t],
+                             a.out + (size_t)t * a.ldOut);
+        }
+    }
+}
+
+void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
+    const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
+    const int MT = ga.M <= 16 ? 1 : 2;
+    const dim3 grid(tiles, ga.splits);
+    const size_t lds = gemmLds(MT);
+#define DL_GEMM_CASE(M_, E)                                                                   \
+    if (MT == M_ && epi == E) {                                                               \
+        hipLaunchKernelGGL((gemmQ40Kernel<M_, E>), grid, dim3(kThreads), lds, s, ga);         \
+        return;                                                                               \
+    }
+    DL_GEMM_CASE(1, EPI_STORE) DL_GEMM_CASE(1, EPI_ACT) DL_GEMM_CASE(1, EPI_ACT_Q80) DL_GEMM_CASE(1, EPI_QKV)
+    DL_GEMM_CASE(2, EPI_STORE) DL_GEMM_CASE(2, EPI_ACT) DL_GEMM_CASE(2, EPI_ACT_Q80) DL_GEMM_CASE(2, EPI_QKV)
+#undef DL_GEMM_CASE
+}
+
+// Residual add + RMS norm + Q80 for M token rows (one workgroup per row); the batched path's
+// replacement for the GEMV's per-workgroup norm prologue.
+__global__ __launch_bounds__(kThreads) void normQ80Kernel(GemvArgs a) {
+    __shared__ float scratch[64];
+    const int b = blockIdx.x, nb = a.n >> 5;
+    GemvArgs r = a;
+    r.in = a.in + (size_t)b * a.ldIn;
+    r.addIn = a.addIn ? a.addIn + (size_t)b * a.ldIn : nullptr;
+    r.xNext = a.xNext ? a.xNext + (size_t)b * a.ldIn : nullptr;
+    resNormPrologue<1, true>(r, scratch, a.oq + (size_t)b * a.n, a.os + (size_t)b * nb, nullptr, true);
+}
+
+void launchNormQ80(const GemvArgs &a, int M, hipStream_t s) {
+    hipLaunchKernelGGL(normQ80Kernel, dim3(M), dim3(kThreads), 0, s, a);
 }
 
 // ------------------------------------------------------------------------------------------------

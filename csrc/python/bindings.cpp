@@ -330,6 +330,39 @@ PYBIND11_MODULE(_C, m) {
                  xgmiConnect(c.comm.get(), hs);
              })
         .def("timed_out", [](PyComm &c) { return xgmiTimedOut(c.comm.get()); })
+        // µs per in-graph all-reduce of n floats (iters back-to-back collectives in one hipGraph)
+        .def("bench_all_reduce",
+             [](PyComm &c, size_t n, int iters) {
+                 py::gil_scoped_release rel;
+                 float *d;
+                 hipStream_t s;
+                 DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+                 DL_HIP(hipMalloc(&d, n * 4));
+                 DL_HIP(hipMemset(d, 0, n * 4));
+                 hipGraph_t g;
+                 hipGraphExec_t ge;
+                 DL_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+                 for (int i = 0; i < iters; i++) c.comm->allReduceSum(d, n, s);
+                 DL_HIP(hipStreamEndCapture(s, &g));
+                 DL_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+                 DL_HIP(hipGraphLaunch(ge, s));
+                 DL_HIP(hipStreamSynchronize(s));
+                 hipEvent_t e0, e1;
+                 DL_HIP(hipEventCreate(&e0));
+                 DL_HIP(hipEventCreate(&e1));
+                 DL_HIP(hipEventRecord(e0, s));
+                 DL_HIP(hipGraphLaunch(ge, s));
+                 DL_HIP(hipEventRecord(e1, s));
+                 DL_HIP(hipEventSynchronize(e1));
+                 float ms = 0;
+                 DL_HIP(hipEventElapsedTime(&ms, e0, e1));
+                 (void)hipGraphExecDestroy(ge);
+                 (void)hipGraphDestroy(g);
+                 (void)hipFree(d);
+                 (void)hipStreamDestroy(s);
+                 return (double)ms * 1000.0 / iters;
+             },
+             py::arg("n"), py::arg("iters") = 200)
         .def_property_readonly("rank", [](PyComm &c) { return c.comm->rank(); })
         .def_property_readonly("world", [](PyComm &c) { return c.comm->size(); })
         // test helpers: host vector in, collective result out (device round trip on the null stream)

@@ -47,8 +47,9 @@ def test_engine_medium_matches_cpu(C, medium):
 
 
 @pytest.mark.parametrize("graphs", [True, False])
-def test_engine_batched_prefill(C, assets, graphs):
-    """A prefill chunk of 7 rows (chunks 4+2+1 inside the GEMVs) == 7 sequential decodes."""
+def test_engine_batched_prefill_gemv_chunks(C, assets, graphs, monkeypatch):
+    """GEMV batch path (chunks 4+2+1 of the same int8 kernels) == 7 sequential decodes."""
+    monkeypatch.setenv("DL_GEMM_MIN", "1000")
     a = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=8, use_graphs=graphs)
     b = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=8, use_graphs=graphs)
     tokens = [9, 8, 7, 6, 5, 4, 3]
@@ -57,15 +58,37 @@ def test_engine_batched_prefill(C, assets, graphs):
     assert _rel(bat, seq) < 1e-4
 
 
-def test_engine_slots_independent(C, assets):
+@pytest.mark.parametrize("graphs", [True, False])
+@pytest.mark.parametrize("n", [2, 7, 16, 23, 40])
+def test_engine_batched_prefill_mfma(C, assets, graphs, n):
+    """MFMA GEMM batch path (f16 dequantized Q40 x Q80, split-K, fused epilogues; 40 rows = two
+    chunks) vs sequential int8 GEMV decodes and vs the CPU reference backend."""
+    rng = np.random.default_rng(n)
+    tokens = [int(t) for t in rng.integers(0, 512, n)]
+    a = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=64, use_graphs=graphs)
+    b = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=64, use_graphs=graphs)
+    seq = _seq(a, tokens)
+    bat = b.forward(tokens, list(range(n)), [0] * n)
+    assert _rel(bat, seq) < 2e-2
+    assert (bat.argmax(-1) == seq.argmax(-1)).mean() >= 0.85
+    cpu = C.cpu_backend(assets["q40"], "q80", 2, max_batch=64)
+    ref = cpu.forward(tokens, list(range(n)), [0] * n)
+    assert _rel(bat, ref) < 3e-2
+
+
+@pytest.mark.parametrize("gemm_min,tol", [("1000", 1e-4), ("2", 2e-2)])
+def test_engine_slots_independent(C, assets, monkeypatch, gemm_min, tol):
+    """Two sequences in different KV slots in one batch == each alone (GEMV batch path exactly,
+    MFMA batch path within f16 dequant tolerance)."""
+    monkeypatch.setenv("DL_GEMM_MIN", gemm_min)
     g = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=4, n_slots=3)
     x, y = [11, 12, 13, 14], [200, 201, 202, 203]
     for p in range(4):
         both = g.forward([x[p], y[p]], [p, p], [2, 0])
     r1 = C.HipEngine(assets["q40"], "q80", kv_bf16=False)
     r2 = C.HipEngine(assets["q40"], "q80", kv_bf16=False)
-    assert _rel(both[0], _seq(r1, x)[-1]) < 1e-4
-    assert _rel(both[1], _seq(r2, y)[-1]) < 1e-4
+    assert _rel(both[0], _seq(r1, x)[-1]) < tol
+    assert _rel(both[1], _seq(r2, y)[-1]) < tol
 
 
 def test_decode_greedy_chain_matches_stepwise(C, assets):
