@@ -92,8 +92,12 @@ def main() -> int:
         if dist is not None:
             dist.barrier()
 
-    # eval: prefill the prompt (chunks of 32 rows per forward, like the reference nBatches=32)
+    # eval: prefill the prompt (chunks of 32 rows per forward, like the reference nBatches=32);
+    # one untimed chunk first so the batch-32 graph is captured outside the timed region
     prompt = [(i * 7919 + 13) % 128000 for i in range(args.prompt)]
+    if len(prompt) >= 32:
+        for b in range(B):
+            eng.forward_argmax(prompt[:32], list(range(32)), [b] * 32)
     torch.cuda.synchronize()
     barrier()
     te = time.perf_counter()

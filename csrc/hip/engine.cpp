@@ -218,10 +218,14 @@ class HipEngineImpl : public HipEngine {
         dAttS_ = dalloc<float2>((size_t)MB * p.q0 / 32);
         dHQ_ = dalloc<int8_t>((size_t)MB * p.hidden0);
         dHS_ = dalloc<float2>((size_t)MB * p.hidden0 / 32);
-        if (q40_) {  // batched (MFMA) path: normalized Q80 activations, split-K partials, counters
-            const size_t wq = std::max<size_t>({(size_t)h_.dim, (size_t)p.hidden0, (size_t)p.q0});
-            dXq_ = dalloc<int8_t>((size_t)MB * wq);
-            dXs_ = dalloc<float2>((size_t)MB * wq / 32);
+        if (q40_) {  // batched (MFMA) path: f16 activations, split-K partials, counters
+            const size_t rowsH = ((size_t)MB + 2 * kGemmMaxTokens - 1) / kGemmMaxTokens * kGemmMaxTokens;
+            dXh_ = dalloc<_Float16>(rowsH * h_.dim);
+            dAttH_ = dalloc<_Float16>(rowsH * p.q0);
+            dHh_ = dalloc<_Float16>(rowsH * p.hidden0);
+            DL_HIP(hipMemsetAsync(dXh_, 0, rowsH * h_.dim * 2, stream_));
+            DL_HIP(hipMemsetAsync(dAttH_, 0, rowsH * p.q0 * 2, stream_));
+            DL_HIP(hipMemsetAsync(dHh_, 0, rowsH * p.hidden0 * 2, stream_));
             const int mt = std::min((int)MB, kGemmMaxTokens);
             size_t part = 0;
             auto acc = [&](int rows, int n) { part = std::max(part, hipk::gemmPartFloats(rows, n, mt)); };
@@ -518,10 +522,6 @@ class HipEngineImpl : public HipEngine {
     void gemv(const DevMat &m, int n, int pro, int epi, const float *in, int ldIn, const float *add, float *xNext,
               const float *normW, float *out, int ldOut, const DevLayer *L, const int8_t *aq = nullptr,
               const float2 *as = nullptr, int8_t *oq = nullptr, float2 *os = nullptr) {
-        if (q40_ && n >= gemmMinTokens()) {
-            gemmBatched(m, n, pro, epi, in, ldIn, add, xNext, normW, out, ldOut, L, aq, as, oq, os);
-            return;
-        }
         const int bcMax = batchChunk(m, pro, epi);
         for (int c0 = 0; c0 < n;) {
             int bc = n - c0;
@@ -572,11 +572,13 @@ class HipEngineImpl : public HipEngine {
         return e && *e ? std::atoi(e) : 2;
     }
 
-    // Batched path (>= gemmMinTokens rows): per chunk of <= 32 tokens, an optional norm/quant
-    // kernel (RESNORM) then the MFMA GEMM with the same fused epilogue.
-    void gemmBatched(const DevMat &m, int n, int pro, int epi, const float *in, int ldIn, const float *add,
-                     float *xNext, const float *normW, float *out, int ldOut, const DevLayer *L, const int8_t *aq,
-                     const float2 *as, int8_t *oq, float2 *os) {
+    bool batchedPath(int n) const { return q40_ && n >= gemmMinTokens(); }
+
+    // Batched path (>= gemmMinTokens rows, Q40): per chunk of <= 32 tokens, a norm kernel (f32 ->
+    // f16, RESNORM) or the producer's f16 rows (xh) feed the MFMA GEMM with the fused epilogue.
+    void gemmBatched(const DevMat &m, int n, int epi, const float *in, int ldIn, const float *add, float *xNext,
+                     const float *normW, const _Float16 *xh, float *out, int ldOut, _Float16 *outH,
+                     const DevLayer *L) {
         for (int c0 = 0; c0 < n; c0 += kGemmMaxTokens) {
             const int bc = std::min(kGemmMaxTokens, n - c0);
             hipk::GemmArgs g;
@@ -586,7 +588,7 @@ class HipEngineImpl : public HipEngine {
             a.rows = m.rows;
             a.n = m.n;
             a.lanes = m.lanes;
-            if (pro == hipk::PRO_RESNORM) {
+            if (!xh) {
                 hipk::GemvArgs nq;
                 nq.n = m.n;
                 nq.in = in + (size_t)c0 * ldIn;
@@ -595,19 +597,14 @@ class HipEngineImpl : public HipEngine {
                 nq.xNext = xNext ? xNext + (size_t)c0 * ldIn : nullptr;
                 nq.normW = normW;
                 nq.eps = h_.normEpsilon;
-                nq.oq = dXq_;
-                nq.os = dXs_;
-                hipk::launchNormQ80(nq, bc, stream_);
-                a.aq = dXq_;
-                a.as = dXs_;
+                hipk::launchNormF16(nq, dXh_, bc, stream_);
+                g.x = dXh_;
             } else {
-                a.aq = aq + (size_t)c0 * m.n;
-                a.as = as + (size_t)c0 * (m.n / 32);
+                g.x = xh + (size_t)c0 * m.n;
             }
             a.out = out ? out + (size_t)c0 * ldOut : nullptr;
+            g.outH = outH ? outH + (size_t)c0 * ldOut : nullptr;
             a.ldOut = ldOut;
-            a.oq = oq ? oq + (size_t)c0 * ldOut : nullptr;
-            a.os = os ? os + (size_t)c0 * (ldOut / 32) : nullptr;
             a.act = h_.hiddenAct == HiddenAct::GELU ? 0 : 1;
             if (L) {
                 a.q0 = plan_.q0;
@@ -644,13 +641,18 @@ class HipEngineImpl : public HipEngine {
             ProfScope ps(this, "embedding");
             hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_);
         }
+        const bool bat = batchedPath(n);  // MFMA GEMMs on f16 activations instead of GEMVs
         for (u32 l = 0; l < h_.nLayers; l++) {
             DevLayer &L = layers_[l];
             const bool hasDelta = l > 0;
             {
                 ProfScope ps(this, "gemv_qkv");
-                gemv(L.qkv, n, hipk::PRO_RESNORM, hipk::EPI_QKV, dX_[cur], dim, hasDelta ? dY_ : nullptr,
-                     hasDelta ? dX_[cur ^ 1] : nullptr, L.rmsAtt, dQ_, p.q0, &L);
+                if (bat)
+                    gemmBatched(L.qkv, n, hipk::EPI_QKV, dX_[cur], dim, hasDelta ? dY_ : nullptr,
+                                hasDelta ? dX_[cur ^ 1] : nullptr, L.rmsAtt, nullptr, dQ_, p.q0, nullptr, &L);
+                else
+                    gemv(L.qkv, n, hipk::PRO_RESNORM, hipk::EPI_QKV, dX_[cur], dim, hasDelta ? dY_ : nullptr,
+                         hasDelta ? dX_[cur ^ 1] : nullptr, L.rmsAtt, dQ_, p.q0, &L);
             }
             if (hasDelta) cur ^= 1;
             {
@@ -672,8 +674,9 @@ class HipEngineImpl : public HipEngine {
                 a.partO = dPartO_;
                 a.partML = dPartML_;
                 a.out = dAtt_;
-                a.outQ = q40_ ? dAttQ_ : nullptr;
-                a.outS = q40_ ? dAttS_ : nullptr;
+                a.outQ = q40_ && !bat ? dAttQ_ : nullptr;
+                a.outS = q40_ && !bat ? dAttS_ : nullptr;
+                a.outH = bat ? dAttH_ : nullptr;
                 a.ldOut = p.q0;
                 a.kvBf16 = kvBf16_ ? 1 : 0;
                 a.counters = dAttCnt_;
@@ -681,8 +684,12 @@ class HipEngineImpl : public HipEngine {
             }
             {
                 ProfScope ps(this, "gemv_wo");
-                gemv(L.wo, n, hipk::PRO_GLOBAL, hipk::EPI_STORE, q40_ ? nullptr : dAtt_, p.q0, nullptr, nullptr,
-                     nullptr, dY_, dim, nullptr, dAttQ_, dAttS_);
+                if (bat)
+                    gemmBatched(L.wo, n, hipk::EPI_STORE, nullptr, 0, nullptr, nullptr, nullptr, dAttH_, dY_, dim,
+                                nullptr, nullptr);
+                else
+                    gemv(L.wo, n, hipk::PRO_GLOBAL, hipk::EPI_STORE, q40_ ? nullptr : dAtt_, p.q0, nullptr, nullptr,
+                         nullptr, dY_, dim, nullptr, dAttQ_, dAttS_);
             }
             allReduce(dY_, (size_t)n * dim);
             // Q80 hand-off of h needs one workgroup per 32 hidden units; for skinny TP shards the
@@ -690,13 +697,20 @@ class HipEngineImpl : public HipEngine {
             const bool hQ80 = q40_ && p.hidden0 / 32 >= 192;
             {
                 ProfScope ps(this, "gemv_w13");
-                gemv(L.w13, n, hipk::PRO_RESNORM, hQ80 ? hipk::EPI_ACT_Q80 : hipk::EPI_ACT, dX_[cur], dim, dY_,
-                     dX_[cur ^ 1], L.rmsFfn, dH_, p.hidden0, nullptr, nullptr, nullptr, dHQ_, dHS_);
+                if (bat)
+                    gemmBatched(L.w13, n, hipk::EPI_ACT_F16, dX_[cur], dim, dY_, dX_[cur ^ 1], L.rmsFfn, nullptr,
+                                nullptr, p.hidden0, dHh_, nullptr);
+                else
+                    gemv(L.w13, n, hipk::PRO_RESNORM, hQ80 ? hipk::EPI_ACT_Q80 : hipk::EPI_ACT, dX_[cur], dim, dY_,
+                         dX_[cur ^ 1], L.rmsFfn, dH_, p.hidden0, nullptr, nullptr, nullptr, dHQ_, dHS_);
             }
             cur ^= 1;
             {
                 ProfScope ps(this, "gemv_w2");
-                if (hQ80 || !q40_)
+                if (bat)
+                    gemmBatched(L.w2, n, hipk::EPI_STORE, nullptr, 0, nullptr, nullptr, nullptr, dHh_, dY_, dim,
+                                nullptr, nullptr);
+                else if (hQ80 || !q40_)
                     gemv(L.w2, n, hipk::PRO_GLOBAL, hipk::EPI_STORE, q40_ ? nullptr : dH_, p.hidden0, nullptr,
                          nullptr, nullptr, dY_, dim, nullptr, dHQ_, dHS_);
                 else
@@ -707,8 +721,12 @@ class HipEngineImpl : public HipEngine {
         }
         {
             ProfScope ps(this, "gemv_logits");
-            gemv(wcls_, n, hipk::PRO_RESNORM, hipk::EPI_STORE, dX_[cur], dim, dY_, nullptr, rmsFinal_, dLogits_,
-                 p.vocab0, nullptr);
+            if (bat)
+                gemmBatched(wcls_, n, hipk::EPI_STORE, dX_[cur], dim, dY_, nullptr, rmsFinal_, nullptr, dLogits_,
+                            p.vocab0, nullptr, nullptr);
+            else
+                gemv(wcls_, n, hipk::PRO_RESNORM, hipk::EPI_STORE, dX_[cur], dim, dY_, nullptr, rmsFinal_, dLogits_,
+                     p.vocab0, nullptr);
         }
         const float *full = dLogits_;
         if (p.nRanks > 1) {
@@ -739,8 +757,7 @@ class HipEngineImpl : public HipEngine {
     }
 
     static constexpr int kGemmMaxTokens = 32;
-    int8_t *dXq_ = nullptr;
-    float2 *dXs_ = nullptr;
+    _Float16 *dXh_ = nullptr, *dAttH_ = nullptr, *dHh_ = nullptr;
     float *dPart_ = nullptr;
     int *dGemmCnt_ = nullptr;
 

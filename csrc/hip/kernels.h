@@ -26,7 +26,7 @@ namespace hipk {
 //             (normW == null: no norm, plain quantization of `in`).
 enum Prologue : int { PRO_GLOBAL = 0, PRO_RESNORM = 1 };
 // EPI_ACT_Q80: act(w1 x) * (w3 x), quantized to Q80 blocks for the next GEMV (32 hidden units/block).
-enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2, EPI_ACT_Q80 = 3 };
+enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2, EPI_ACT_Q80 = 3, EPI_ACT_F16 = 4 };
 
 // Q40 weights live on the device TILED in the ring GEMV's consumption order, for a lanes-per-row
 // count L fixed per matrix (NG = 256/L row pairs per workgroup pass, K = ceil(nb/L) steps):
@@ -77,11 +77,14 @@ struct GemvArgs {
     int kvBf16 = 1;
 };
 
-// Batched Q40 matmul on MFMA (2..32 tokens): GemvArgs `e` carries weights (tiled), Q80
-// activations (aq/as [M][n]) and the epilogue fields; split-K partials + per-tile counters
-// (zero-initialised, reset by the kernel) when splits > 1.
+// Batched Q40 matmul on MFMA (2..32 tokens per launch): GemvArgs `e` carries the weights (tiled,
+// `lanes` = tiling L) and the epilogue fields; activations are f16 [>= roundup(M,16)][n] (`x`,
+// rows past M are read but their outputs dropped); split-K partials + per-tile counters
+// (zero-initialised, reset by the kernel) when splits > 1. EPI_ACT_F16 writes SwiGLU as f16 to outH.
 struct GemmArgs {
     GemvArgs e;
+    const _Float16 *x = nullptr;
+    _Float16 *outH = nullptr;
     int M = 0;
     int splits = 1;
     float *part = nullptr;
@@ -90,9 +93,9 @@ struct GemmArgs {
 void launchGemmQ40(const GemmArgs &a, int epi, hipStream_t s);
 int gemmSplits(int rows, int n);
 size_t gemmPartFloats(int rows, int n, int maxTokens);
-// Residual add + RMS norm (normW may be null: plain quantization) + Q80 of M rows:
-// in/addIn/xNext [M][ldIn] f32 -> oq [M][n] int8, os [M][n/32] (d, sum q).
-void launchNormQ80(const GemvArgs &a, int M, hipStream_t s);
+// Residual add + RMS norm (normW may be null: no norm) of M rows -> f16:
+// in/addIn/xNext [M][ldIn] f32 -> out [M][n] f16 (xNext = in + addIn when set).
+void launchNormF16(const GemvArgs &a, _Float16 *out, int M, hipStream_t s);
 
 // B = batch rows in this launch (1, 2 or 4); q40 = weight format.
 void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_t s);
@@ -120,7 +123,8 @@ struct AttnArgs {
     int chunkMax = 256;         // LDS capacity in positions per split
     float *partO = nullptr;     // [B][nHeads0][splitGrid][hs]
     float *partML = nullptr;    // [B][nHeads0][splitGrid][2]
-    float *out = nullptr;       // [B][ldOut] f32 output (when outQ is null)
+    float *out = nullptr;       // [B][ldOut] f32 output (when outQ and outH are null)
+    _Float16 *outH = nullptr;   // [B][ldOut] f16 output (batched path)
     int8_t *outQ = nullptr;     // [B][ldOut] Q80 output (+ outS [B][ldOut/32])
     float2 *outS = nullptr;
     int ldOut = 0;

@@ -703,23 +703,27 @@ void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_
 }
 
 // ------------------------------------------------------------------------------------------------
-// Batched Q40 x Q80 matmul on MFMA (prefill / multi-user decode, 2..32 tokens per launch).
-//   out[t][row] = sum_k W[row][k] * x[t][k]   with W Q40 (tiled GEMV layout, see Q40Tiling) and
-//   x Q80. Each workgroup owns 64 weight rows (4 waves x 16) and one K split; per Q40 block a
-//   lane dequantizes 8 nibbles of its row into an f16 B fragment (((1024+q) - 1032) * d, one
-//   rounding) and multiplies the 16-token A fragments, staged per 16-block chunk in LDS as f16,
-//   with v_mfma_f32_16x16x32_f16 (f32 accumulate). Split-K partials are combined in split order
-//   by the last-arriving workgroup (agent-scope release/acquire counter, deterministic), which
-//   then runs the same fused epilogues as the GEMV (store / SwiGLU / SwiGLU+Q80 / RoPE+KV).
+// Batched Q40 matmul on MFMA (prefill / multi-user decode, 2..32 tokens per launch).
+//   out[t][row] = sum_k W[row][k] * x[t][k], W Q40 (the GEMV's tiled layout), x f16.
+// Each workgroup owns 64 weight rows (4 waves x 16) and one K split, streamed in chunks of 16
+// Q40 blocks. Both operands are copied HBM/L2 -> LDS with global_load_lds_dwordx4 (no VGPR
+// staging; one 16-B unit per lane, contiguous 256-B+ runs per wave instruction), multi-buffered
+// with counted vmcnt waits and raw barriers (3 stages: two chunks in flight), into XOR-swizzled images so the fragment reads are
+// bank-conflict free. Per block a lane dequantizes 8 nibbles of its row ((1024+q) - 1032 exact in
+// f16, times d) into the B fragment of v_mfma_f32_16x16x32_f16; A fragments are read as is.
+// Split-K partials are combined in split order by the last-arriving workgroup (agent-scope
+// release/acquire counter: deterministic), which runs the fused epilogues (store / SwiGLU /
+// SwiGLU -> f16 / SwiGLU -> Q80 / RoPE + KV append).
 // ------------------------------------------------------------------------------------------------
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 static constexpr int kGemmRows = 64;
-static constexpr int kGemmCh = 16;  // Q40 blocks per staged activation chunk
+static constexpr int kGemmCh = 8;  // Q40 blocks per pipeline stage (~25 KB at 32 tokens)
 
 int gemmSplits(int rows, int n) {
     const int tiles = (rows + kGemmRows - 1) / kGemmRows, nb = n / 32;
     int S = 1;
-    while (S < 8 && tiles * S < 256 && nb % (2 * S) == 0) S *= 2;
+    while (S < 8 && tiles * S < 256 && nb % (2 * S) == 0 && nb / (2 * S) >= kGemmCh) S *= 2;
     return S;
 }
 
@@ -729,13 +733,16 @@ size_t gemmPartFloats(int rows, int n, int maxTokens) {
     return S > 1 ? (size_t)S * tiles * mp * kGemmRows : 0;
 }
 
-static size_t gemmLds(int MT) { return (size_t)MT * 16 * (kGemmCh * 32 + 8) * 2 + (size_t)MT * 16 * kGemmRows * 4 + 16; }
+// stage layout (bytes): weights [64 rows][8 units] x 16 B | scales [32 pairs][8] u32 | x [MP][32 units] x 16 B
+static constexpr int kStW = kGemmRows * kGemmCh * 16, kStD = (kGemmRows / 2) * kGemmCh * 4;
+__host__ __device__ static constexpr int gemmStageBytes(int MT) { return kStW + kStD + MT * 16 * kGemmCh * 64; }
+static constexpr int kGemmStages = 3;  // chunks c+1, c+2 in flight while c is consumed
+static size_t gemmLds(int MT) { return kGemmStages * (size_t)gemmStageBytes(MT) + 16; }
 
 // 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d via the 0x6400 | q magic (1024 + q)
-__device__ __forceinline__ half8 dequantQ40x8(uint2 wv, int nibHi, uint32_t d16) {
+__device__ __forceinline__ half8 dequantQ40x8(u32x2 wv, int nibHi, uint32_t d16) {
     const uint32_t lo = nibHi ? (wv.x >> 4) & 0x0F0F0F0Fu : wv.x & 0x0F0F0F0Fu;
     const uint32_t hi = nibHi ? (wv.y >> 4) & 0x0F0F0F0Fu : wv.y & 0x0F0F0F0Fu;
-    // bytes b0..b3 of a word -> f16 pairs 0x64bb: 1024 + nibble
     const uint32_t p0 = __builtin_amdgcn_perm(0x64646464u, lo, 0x07010700u);
     const uint32_t p1 = __builtin_amdgcn_perm(0x64646464u, lo, 0x07030702u);
     const uint32_t p2 = __builtin_amdgcn_perm(0x64646464u, hi, 0x07010700u);
@@ -755,93 +762,128 @@ __device__ __forceinline__ half8 dequantQ40x8(uint2 wv, int nibHi, uint32_t d16)
     return out;
 }
 
+// one 16-B global -> LDS copy per lane; `lds` = this wave's base (lane l lands at lds + 16 l)
+__device__ __forceinline__ void glds16(const void *g, void *lds) {
+    __builtin_amdgcn_global_load_lds(const_cast<void *>(g), reinterpret_cast<__attribute__((address_space(3))) void *>(
+                                         reinterpret_cast<uintptr_t>(lds)), 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void *g, void *lds) {
+    __builtin_amdgcn_global_load_lds(const_cast<void *>(g), reinterpret_cast<__attribute__((address_space(3))) void *>(
+                                         reinterpret_cast<uintptr_t>(lds)), 4, 0, 0);
+}
+
 template <int MT, int EPI>
 __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     const GemvArgs &a = ga.e;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int MP = MT * 16;
-    constexpr int AST = kGemmCh * 32 + 8;  // f16 per staged token row (+16 B: conflict-free reads)
-    _Float16 *sa = reinterpret_cast<_Float16 *>(smem);
-    float *tile = reinterpret_cast<float *>(smem + (size_t)MP * AST * 2);  // [MP][64]
-    int *flag = reinterpret_cast<int *>(tile + MP * kGemmRows);
+    constexpr int SB = gemmStageBytes(MT);
+    constexpr int NW = kGemmRows * kGemmCh / kThreads, NX = MT * 16 * kGemmCh * 4 / kThreads;
+    constexpr int NLD = NW + 1 + NX;  // glds instructions per thread per stage
+    int *flag = reinterpret_cast<int *>(smem + kGemmStages * SB);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int col = lane & 15, h = lane >> 4;
     const int n = a.n, nb = n >> 5, L = a.lanes, NG = kThreads / L, KS = (nb + L - 1) / L;
     const int lgL = 31 - __builtin_clz(L);
     const int tileIdx = blockIdx.x, sp = blockIdx.y, S = ga.splits;
     const int R0 = tileIdx * kGemmRows;
-    const int row = min(R0 + wave * 16 + col, a.rows - 1);
-    const int g = row / (2 * NG), rem = row % (2 * NG), gi = rem >> 1, rpar = rem & 1;
-    const size_t gBase = (size_t)g * KS;
     const int bps = nb / S, j0 = sp * bps, j1 = j0 + bps;
-    const int byteHalf = h & 1, nibHi = h >> 1;
+    const int nch = (bps + kGemmCh - 1) / kGemmCh;
     const uint8_t *qs = a.qs;
     const uint32_t *wd2 = reinterpret_cast<const uint32_t *>(a.wd);
+    auto unitOf = [&](int row, int j) -> size_t {  // tiled 16-B unit of (row, block j), clamped
+        row = min(row, a.rows - 1);
+        j = min(j, j1 - 1);
+        const int g = row / (2 * NG), rem = row % (2 * NG), gi = rem >> 1, rpar = rem & 1;
+        const int k = j >> lgL, li = j & (L - 1);
+        return (((size_t)g * KS + k) * 2 + rpar) * kThreads + gi * L + li;
+    };
+    auto scaleIdx = [&](int pairRow, int j) -> size_t {  // tiled u32 pair scale of (row pair, block j)
+        const int row = min(pairRow, a.rows - 1);
+        j = min(j, j1 - 1);
+        const int g = row / (2 * NG), rem = row % (2 * NG), gi = rem >> 1;
+        const int k = j >> lgL, li = j & (L - 1);
+        return ((size_t)g * KS + k) * kThreads + gi * L + li;
+    };
+    // issue the copies of chunk c into stage buffer b
+    auto issue = [&](int c, int b) {
+        char *st = smem + b * SB;
+        const int c0 = j0 + c * kGemmCh;
+        // weights: unit u = s*256 + tid -> (row_l = u/8, position p = u%8) holds block p ^ (row_l&7)
+#pragma unroll
+        for (int s = 0; s < NW; s++) {
+            const int u = s * kThreads + tid, rl = u / kGemmCh, pp = u % kGemmCh;
+            const size_t unit = unitOf(R0 + rl, c0 + (pp ^ (rl & (kGemmCh - 1))));
+            glds16(qs + unit * 16, st + (size_t)(s * kThreads + wave * 64) * 16);
+        }
+        // pair scales: u = tid -> (pair_l = u/8, block u%8), 4 B each
+        {
+            const int pl = tid / kGemmCh, jj = tid % kGemmCh;
+            glds4(wd2 + scaleIdx(R0 + 2 * pl, c0 + jj), st + kStW + (size_t)(wave * 64) * 4);
+        }
+        // activations: token row t = 4*kGemmCh units of 8 f16; position p holds unit p ^ (t&15)
+#pragma unroll
+        for (int s = 0; s < NX; s++) {
+            const int u = s * kThreads + tid, t = u / (4 * kGemmCh), pp = u % (4 * kGemmCh);
+            const int uu = pp ^ (t & 15);
+            const int cb = min(c0 + (uu >> 2), j1 - 1);  // block of this unit (clamped)
+            const _Float16 *src = ga.x + (size_t)t * n + (size_t)cb * 32 + (uu & 3) * 8;
+            glds16(src, st + kStW + kStD + (size_t)(s * kThreads + wave * 64) * 16);
+        }
+    };
 
     f32x4 acc[MT];
 #pragma unroll
     for (int t = 0; t < MT; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int rl = wave * 16 + col;  // this lane's weight row (local)
+    const int byteHalf = h & 1, nibHi = h >> 1;
 
-    for (int c0 = j0; c0 < j1; c0 += kGemmCh) {
-        const int cn = min(kGemmCh, j1 - c0);
-        __syncthreads();  // previous chunk consumed
-        // stage x[t][c0*32 .. (c0+cn)*32) as f16, 16 elements per item
-        for (int i = tid; i < MP * cn * 2; i += kThreads) {
-            const int t = i / (cn * 2), rest = i % (cn * 2), jb = rest >> 1, hf = rest & 1;
-            typedef _Float16 h16 __attribute__((ext_vector_type(16)));
-            h16 v;
-            if (t < ga.M) {
-                const int4 q = *reinterpret_cast<const int4 *>(a.aq + (size_t)t * n + (size_t)(c0 + jb) * 32 + hf * 16);
-                const float d = a.as[(size_t)t * nb + c0 + jb].x;
-                const int w4[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-                for (int e = 0; e < 16; e++) v[e] = (_Float16)((float)(int8_t)(w4[e >> 2] >> (8 * (e & 3))) * d);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 16; e++) v[e] = (_Float16)0.f;
-            }
-            *reinterpret_cast<h16 *>(sa + (size_t)t * AST + jb * 32 + hf * 16) = v;
+    issue(0, 0);
+    if (nch > 1) issue(1, 1);
+    for (int c = 0; c < nch; c++) {
+        if (c + 2 < nch) {
+            issue(c + 2, (c + 2) % kGemmStages);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * NLD) : "memory");  // chunk c landed (this thread)
+        } else if (c + 1 < nch) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NLD) : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
-        __syncthreads();
-        // 4 blocks per step: weight loads first, then dequant + MFMA
-        for (int jj = 0; jj < cn; jj += 4) {
-            uint2 wv[4];
-            uint32_t dw[4];
+        __builtin_amdgcn_s_barrier();  // ... and for every thread
+        const char *st = smem + (c % kGemmStages) * SB;
+        const int cn = min(kGemmCh, bps - c * kGemmCh);
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int j = min(c0 + jj + u, j1 - 1);
-                const int k = j >> lgL, li = j & (L - 1);
-                const size_t idx = (gBase + k) * kThreads + gi * L + li;
-                const size_t unit = ((gBase + k) * 2 + rpar) * kThreads + gi * L + li;  // 16-B block
-                wv[u] = *reinterpret_cast<const uint2 *>(qs + unit * 16 + byteHalf * 8);
-                dw[u] = wd2[idx];
-            }
+        for (int jj = 0; jj < kGemmCh; jj++) {
+            const int pp = jj ^ (rl & (kGemmCh - 1));
+            const u32x2 wv = *reinterpret_cast<const u32x2 *>(st + (size_t)(rl * kGemmCh + pp) * 16 + byteHalf * 8);
+            const uint32_t dw = *reinterpret_cast<const uint32_t *>(st + kStW + (size_t)((rl >> 1) * kGemmCh + jj) * 4);
+            const uint32_t d16 = jj < cn ? ((rl & 1) ? dw >> 16 : dw & 0xFFFFu) : 0u;
+            const half8 b = dequantQ40x8(wv, nibHi, d16);
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                if (jj + u >= cn) break;
-                const uint32_t d16 = rpar ? dw[u] >> 16 : dw[u] & 0xFFFFu;
-                const half8 b = dequantQ40x8(wv[u], nibHi, d16);
-#pragma unroll
-                for (int t = 0; t < MT; t++) {
-                    const half8 av = *reinterpret_cast<const half8 *>(sa + (size_t)(t * 16 + col) * AST + (jj + u) * 32 + 8 * h);
-                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b, acc[t], 0, 0, 0);
-                }
+            for (int t = 0; t < MT; t++) {
+                const int tok = t * 16 + col, up = (jj * 4 + h) ^ (tok & 15);
+                const half8 av = *reinterpret_cast<const half8 *>(st + kStW + kStD + (size_t)(tok * 4 * kGemmCh + up) * 16);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b, acc[t], 0, 0, 0);
             }
         }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // stage c % kGemmStages is refilled at iteration c + 1
     }
+
+    float *tile = reinterpret_cast<float *>(smem);  // [MP][64], stages are free now
     // C layout: weight row (local) wave*16 + col, token t*16 + h*4 + i
     if (S == 1) {
 #pragma unroll
         for (int t = 0; t < MT; t++)
 #pragma unroll
-            for (int i = 0; i < 4; i++) tile[(t * 16 + h * 4 + i) * kGemmRows + wave * 16 + col] = acc[t][i];
+            for (int i = 0; i < 4; i++) tile[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
     } else {
         const int tiles = gridDim.x;
         float *part = ga.part + ((size_t)sp * tiles + tileIdx) * MP * kGemmRows;
 #pragma unroll
         for (int t = 0; t < MT; t++)
 #pragma unroll
-            for (int i = 0; i < 4; i++) part[(t * 16 + h * 4 + i) * kGemmRows + wave * 16 + col] = acc[t][i];
+            for (int i = 0; i < 4; i++) part[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
@@ -872,6 +914,8 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
             if (r0 + 1 < a.rows) a.out[(size_t)t * a.ldOut + r0 + 1] = v1;
         } else if constexpr (EPI == EPI_ACT) {
             if (r0 < a.rows) a.out[(size_t)t * a.ldOut + (r0 >> 1)] = gateAct(a, v0) * v1;
+        } else if constexpr (EPI == EPI_ACT_F16) {
+            if (r0 < a.rows) ga.outH[(size_t)t * a.ldOut + (r0 >> 1)] = (_Float16)(gateAct(a, v0) * v1);
         } else if constexpr (EPI == EPI_ACT_Q80) {
             const int hBase = R0 >> 1;
             if (hBase >= (a.rows >> 1)) continue;  // whole 32-unit block: uniform per lane group
@@ -903,24 +947,82 @@ void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
         return;                                                                               \
     }
     DL_GEMM_CASE(1, EPI_STORE) DL_GEMM_CASE(1, EPI_ACT) DL_GEMM_CASE(1, EPI_ACT_Q80) DL_GEMM_CASE(1, EPI_QKV)
+    DL_GEMM_CASE(1, EPI_ACT_F16)
     DL_GEMM_CASE(2, EPI_STORE) DL_GEMM_CASE(2, EPI_ACT) DL_GEMM_CASE(2, EPI_ACT_Q80) DL_GEMM_CASE(2, EPI_QKV)
+    DL_GEMM_CASE(2, EPI_ACT_F16)
 #undef DL_GEMM_CASE
 }
 
-// Residual add + RMS norm + Q80 for M token rows (one workgroup per row); the batched path's
-// replacement for the GEMV's per-workgroup norm prologue.
-__global__ __launch_bounds__(kThreads) void normQ80Kernel(GemvArgs a) {
+// Residual add + RMS norm (optional) of M rows -> f16 (one workgroup per row): the batched
+// path's replacement for the GEMV's per-workgroup norm prologue.
+__global__ __launch_bounds__(kThreads) void normF16Kernel(GemvArgs a, _Float16 *out) {
     __shared__ float scratch[64];
-    const int b = blockIdx.x, nb = a.n >> 5;
-    GemvArgs r = a;
-    r.in = a.in + (size_t)b * a.ldIn;
-    r.addIn = a.addIn ? a.addIn + (size_t)b * a.ldIn : nullptr;
-    r.xNext = a.xNext ? a.xNext + (size_t)b * a.ldIn : nullptr;
-    resNormPrologue<1, true>(r, scratch, a.oq + (size_t)b * a.n, a.os + (size_t)b * nb, nullptr, true);
+    constexpr int PV = 8;  // float4 per thread kept in registers (n <= 8192 in one pass)
+    const int b = blockIdx.x, n = a.n, tid = threadIdx.x;
+    const float *x = a.in + (size_t)b * a.ldIn;
+    const float *y = a.addIn ? a.addIn + (size_t)b * a.ldIn : nullptr;
+    float *xo = a.xNext ? a.xNext + (size_t)b * a.ldIn : nullptr;
+    _Float16 *o = out + (size_t)b * n;
+    const bool inReg = n <= kThreads * 4 * PV;
+    float4 v[PV];
+    float ss = 0.f;
+    if (inReg) {
+#pragma unroll
+        for (int k = 0; k < PV; k++) {
+            const int i = (tid + k * kThreads) * 4;
+            if (i < n) {
+                v[k] = ld4(x + i);
+                if (y) {
+                    const float4 w = ld4(y + i);
+                    v[k].x += w.x; v[k].y += w.y; v[k].z += w.z; v[k].w += w.w;
+                }
+                if (xo) st4(xo + i, v[k]);
+                ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+            }
+        }
+    } else {
+        for (int i = tid * 4; i < n; i += kThreads * 4) {
+            float4 u = ld4(x + i);
+            if (y) {
+                const float4 w = ld4(y + i);
+                u.x += w.x; u.y += w.y; u.z += w.z; u.w += w.w;
+            }
+            if (xo) st4(xo + i, u);
+            ss += u.x * u.x + u.y * u.y + u.z * u.z + u.w * u.w;
+        }
+    }
+    float inv = 1.0f;
+    if (a.normW) {
+        ss = blockSum<kThreads>(ss, scratch);
+        inv = 1.0f / sqrtf(ss / (float)n + a.eps);
+    }
+    auto emit = [&](int i, float4 u) {
+        const float4 g = a.normW ? ld4(a.normW + i) : make_float4(1.f, 1.f, 1.f, 1.f);
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        const h4 r = {(_Float16)(g.x * (inv * u.x)), (_Float16)(g.y * (inv * u.y)), (_Float16)(g.z * (inv * u.z)),
+                      (_Float16)(g.w * (inv * u.w))};
+        *reinterpret_cast<h4 *>(o + i) = r;
+    };
+    if (inReg) {
+#pragma unroll
+        for (int k = 0; k < PV; k++) {
+            const int i = (tid + k * kThreads) * 4;
+            if (i < n) emit(i, v[k]);
+        }
+    } else {
+        for (int i = tid * 4; i < n; i += kThreads * 4) {
+            float4 u = xo ? ld4(xo + i) : ld4(x + i);
+            if (!xo && y) {
+                const float4 w = ld4(y + i);
+                u.x += w.x; u.y += w.y; u.z += w.z; u.w += w.w;
+            }
+            emit(i, u);
+        }
+    }
 }
 
-void launchNormQ80(const GemvArgs &a, int M, hipStream_t s) {
-    hipLaunchKernelGGL(normQ80Kernel, dim3(M), dim3(kThreads), 0, s, a);
+void launchNormF16(const GemvArgs &a, _Float16 *out, int M, hipStream_t s) {
+    hipLaunchKernelGGL(normF16Kernel, dim3(M), dim3(kThreads), 0, s, a, out);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -996,6 +1098,8 @@ __device__ __forceinline__ void attnWriteOut(const AttnArgs &a, int b, int head0
             const float qs = groupSum<32>((float)q);
             if ((i & 31) == 0) a.outS[(size_t)b * (a.ldOut >> 5) + (col >> 5)] = make_float2(roundF16(d), qs);
         }
+    } else if (a.outH) {
+        for (int i = tid; i < HG * HS; i += AT) a.outH[(size_t)b * a.ldOut + head0 * HS + i] = (_Float16)fin[i];
     } else {
         for (int i = tid; i < HG * HS; i += AT) a.out[(size_t)b * a.ldOut + head0 * HS + i] = fin[i];
     }

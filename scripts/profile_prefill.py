@@ -1,0 +1,31 @@
+"""Batched-forward profiling helper: per-class eager breakdown + repeated graph-replayed forwards of
+`--tokens` rows (run under `rocprofv3 --kernel-trace --stats` for per-kernel device time)."""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--model", default="llama3_1_8b")
+ap.add_argument("--tokens", type=int, default=32)
+ap.add_argument("--reps", type=int, default=8)
+args = ap.parse_args()
+
+import distributed_llama_multiusers_amd as dl
+from distributed_llama_multiusers_amd.models.synthetic import LLAMA_SHAPES
+
+C = dl.native()
+h = dict(LLAMA_SHAPES[args.model], seq_len=1024, rope_theta=500000, weight_type=2)
+eng = C.HipEngine("", "q80", synthetic=h, max_seq_len=1024, n_slots=1, max_batch=max(32, args.tokens))
+n = args.tokens
+toks = [(i * 31 + 7) % 1000 for i in range(n)]
+eng.forward_argmax(toks, list(range(n)), [0] * n)
+eng.profile_forward(toks, list(range(n)), [0] * n)
+t = time.perf_counter()
+for r in range(args.reps):
+    eng.forward_argmax(toks, list(range(n)), [0] * n)
+eng.synchronize()
+wall = (time.perf_counter() - t) * 1000 / args.reps
+print(f"prefill {args.model} {n} tokens: {wall:.3f} ms per forward, {wall / n:.4f} ms/token")
