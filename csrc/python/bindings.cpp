@@ -11,6 +11,7 @@
 #include "../core/quant.h"
 #include "../hip/engine.h"
 #include "../runtime/backend.h"
+#include "../runtime/weight_stream.h"
 #include "../text/tokenizer.h"
 
 namespace py = pybind11;
@@ -306,6 +307,16 @@ PYBIND11_MODULE(_C, m) {
           },
           py::arg("model"), py::arg("buffer_type"), py::arg("world"), py::arg("tokens"), py::arg("kv_bf16") = false,
           py::arg("gpu_index") = 0);
+
+    m.def("shard_bytes",
+          [](const std::string &model, u32 world, u32 rank) {
+              ModelFile f(model);
+              const auto ranges = shardByteRanges(f.header(), f.tensors(), ShardPlan::make(f.header(), world, rank));
+              u64 t = 0;
+              for (auto &r : ranges) t += r.length;
+              return t;
+          },
+          py::arg("model"), py::arg("world"), py::arg("rank"));
 
     m.def("rccl_unique_id", []() {
         auto v = rcclGetUniqueId();

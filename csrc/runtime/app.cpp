@@ -6,7 +6,10 @@
 #include <cstring>
 #include <ctime>
 
+#include <unistd.h>
+
 #include "../hip/engine.h"
+#include "weight_stream.h"
 
 namespace dl {
 
@@ -67,6 +70,8 @@ AppArgs AppArgs::parse(int argc, char **argv, bool requireMode) {
         else if (name == "--log-level") a.logLevel = std::atoi(value);
         else if (name == "--synthetic") a.synthetic = value;
         else if (name == "--web-ui") a.webUi = value;
+        else if (name == "--stream-weights") a.streamWeights = std::atoi(value) != 0;
+        else if (name == "--weights-cache") a.weightsCache = value;
         else throw Error("Unknown option: " + name);
     }
     setLogLevel(a.logLevel);
@@ -158,6 +163,16 @@ InferenceSession::InferenceSession(const AppArgs &args, int nSlots) : args_(args
             wc.rank = (u32)(i + 1);
             workers_[i].sendPod<u32>(kProtoMagic);
             workers_[i].sendString(encodeWorkerConfig(wc));
+        }
+        // workers without the model file get their slices streamed
+        for (size_t i = 0; i < workers_.size(); i++) {
+            const u32 st = workers_[i].recvPod<u32>();
+            if (st == kWantWeights) {
+                if (logLevel() >= 1) std::printf("💿 Streaming weights to worker %zu\n", i + 1);
+                serveWeights(workers_[i], args.modelPath);
+            } else if (st != kHaveWeights) {
+                throw NetError("worker failed before loading weights");
+            }
         }
         std::vector<Socket *> peers;
         for (auto &s : workers_) peers.push_back(&s);
@@ -261,6 +276,26 @@ void runWorker(const AppArgs &args) {
             WorkerConfig wc = decodeWorkerConfig(root.recvString());
             if (logLevel() >= 1) std::printf("⭕ Root connected; rank %u of %u (%s)\n", wc.rank, wc.world, wc.gpu ? "gpu" : "cpu");
             EngineConfig ec = wc.engine;
+            std::string streamedFile;
+            if (!ec.synthetic && (args.streamWeights || ::access(ec.modelPath.c_str(), R_OK) != 0)) {
+                root.sendPod<u32>(kWantWeights);
+                const size_t slash = ec.modelPath.find_last_of('/');
+                streamedFile = args.weightsCache + "/dllama_r" + std::to_string(wc.rank) + "_" +
+                               (slash == std::string::npos ? ec.modelPath : ec.modelPath.substr(slash + 1));
+                const u64 got = fetchWeights(root, streamedFile, wc.rank, wc.world);
+                if (logLevel() >= 1)
+                    std::printf("💿 Received %llu MB of weight slices -> %s\n", (unsigned long long)(got >> 20),
+                                streamedFile.c_str());
+                ec.modelPath = streamedFile;
+            } else {
+                root.sendPod<u32>(kHaveWeights);
+            }
+            struct Cleanup {
+                std::string path;
+                ~Cleanup() {
+                    if (!path.empty()) ::unlink(path.c_str());
+                }
+            } cleanup{streamedFile};
             ec.nThreads = args.nThreads;
             ec.gpuIndex = args.gpuIndex >= 0 ? args.gpuIndex : (wc.gpu ? (int)wc.rank : -1);
             ec.useGraphs = ec.useGraphs && args.graphs;

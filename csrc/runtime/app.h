@@ -40,6 +40,8 @@ struct AppArgs {
     int logLevel = 1;
     std::string synthetic;                       // "llama3_1_8b" etc: random-init weights on device
     std::string webUi;                           // dllama-api: directory served at GET /
+    bool streamWeights = false;                  // worker: always fetch slices from the root
+    std::string weightsCache = "/tmp";           // worker: directory for streamed weight files
 
     static AppArgs parse(int argc, char **argv, bool requireMode);
 };

@@ -92,6 +92,37 @@ def test_tensor_parallel_matches_single(kv4, n_workers):
         assert "Stop signal" in l and l.count("Listening on port") >= 2
 
 
+def test_workers_without_model_file_get_streamed_slices(kv4, tmp_path):
+    """Workers that do not have the model (forced with --stream-weights 1) receive exactly their
+    row/column slices from the root (reference NnRootWeightLoader); same tokens."""
+    rc, ref = _inference(kv4)
+    assert rc == 0, ref
+    procs, addrs = _workers(3, ("--stream-weights", "1", "--weights-cache", str(tmp_path)))
+    try:
+        rc, out = _inference(kv4, addrs)
+        assert rc == 0, out
+        assert _preds(out) == _preds(ref)
+    finally:
+        for p in procs:
+            p.kill()
+        logs = [p.communicate()[0].decode(errors="replace") for p in procs]
+    for l in logs:
+        assert "Received" in l and "weight slices" in l, l
+    assert not list(tmp_path.glob("dllama_r*")), "streamed weight files are removed after the session"
+
+
+def test_shard_byte_ranges_cover_a_quarter(C, kv4):
+    """Each of 4 ranks requests ~1/4 of the matmul bytes (+ embedding and norms)."""
+    import os
+    h = C.load_header(kv4["q40"])
+    size = os.path.getsize(kv4["q40"])
+    tot = [C.shard_bytes(kv4["q40"], 4, r) for r in range(4)]
+    emb = h["vocab_size"] * h["dim"] * 4
+    for t in tot:
+        assert t < (size - emb) / 4 * 1.1 + emb
+    assert sum(tot) >= size - 3 * emb - 1
+
+
 def test_worker_killed_mid_run_gives_clean_error(assets):
     procs, addrs = _workers(1)
     try:
