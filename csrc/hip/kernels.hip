@@ -708,7 +708,7 @@ void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_
 // Each workgroup owns 64 weight rows (4 waves x 16) and one K split, streamed in chunks of 16
 // Q40 blocks. Both operands are copied HBM/L2 -> LDS with global_load_lds_dwordx4 (no VGPR
 // staging; one 16-B unit per lane, contiguous 256-B+ runs per wave instruction), multi-buffered
-// with counted vmcnt waits and raw barriers (3 stages: two chunks in flight), into XOR-swizzled images so the fragment reads are
+// with counted vmcnt waits and raw barriers (kGemmStages buffers), into XOR-swizzled images so the fragment reads are
 // bank-conflict free. Per block a lane dequantizes 8 nibbles of its row ((1024+q) - 1032 exact in
 // f16, times d) into the B fragment of v_mfma_f32_16x16x32_f16; A fragments are read as is.
 // Split-K partials are combined in split order by the last-arriving workgroup (agent-scope
@@ -736,7 +736,7 @@ size_t gemmPartFloats(int rows, int n, int maxTokens) {
 // stage layout (bytes): weights [64 rows][8 units] x 16 B | scales [32 pairs][8] u32 | x [MP][32 units] x 16 B
 static constexpr int kStW = kGemmRows * kGemmCh * 16, kStD = (kGemmRows / 2) * kGemmCh * 4;
 __host__ __device__ static constexpr int gemmStageBytes(int MT) { return kStW + kStD + MT * 16 * kGemmCh * 64; }
-static constexpr int kGemmStages = 3;  // chunks c+1, c+2 in flight while c is consumed
+static constexpr int kGemmStages = 2;  // stage buffers (kGemmStages-1 chunks in flight); 2 -> 3 WGs/CU
 static size_t gemmLds(int MT) { return kGemmStages * (size_t)gemmStageBytes(MT) + 16; }
 
 // 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d via the 0x6400 | q magic (1024 + q)
@@ -838,17 +838,18 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     const int rl = wave * 16 + col;  // this lane's weight row (local)
     const int byteHalf = h & 1, nibHi = h >> 1;
 
-    issue(0, 0);
-    if (nch > 1) issue(1, 1);
+    constexpr int PF = kGemmStages - 1;  // chunks in flight ahead of the one consumed
+    for (int c = 0; c < PF && c < nch; c++) issue(c, c);
     for (int c = 0; c < nch; c++) {
-        if (c + 2 < nch) {
-            issue(c + 2, (c + 2) % kGemmStages);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * NLD) : "memory");  // chunk c landed (this thread)
-        } else if (c + 1 < nch) {
+        if (c + PF < nch) issue(c + PF, (c + PF) % kGemmStages);
+        // wait until chunk c landed (this thread): the chunks issued after it may stay in flight
+        const int after = min(nch - 1, c + PF) - c;
+        if (after >= 2)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * NLD) : "memory");
+        else if (after == 1)
             asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NLD) : "memory");
-        } else {
+        else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
         __builtin_amdgcn_s_barrier();  // ... and for every thread
         const char *st = smem + (c % kGemmStages) * SB;
         const int cn = min(kGemmCh, bps - c * kGemmCh);

@@ -82,7 +82,9 @@ __global__ __launch_bounds__(kThreads) void xgmiKernel(XgmiCall a) {
             __hip_atomic_store(remote, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             int *local = a.peers.flags[a.rank] + tid * kSlots + g;
             const long long t0 = rtClock();
-            while (__hip_atomic_load(local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+            // after a first timeout every later call fails fast instead of waiting again
+            const bool failed = __hip_atomic_load(a.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+            while (!failed && __hip_atomic_load(local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
                 __builtin_amdgcn_s_sleep(1);
                 if (rtClock() - t0 > a.timeoutTicks) {  // a peer never arrived: give up, flag it
                     __hip_atomic_store(a.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
