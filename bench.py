@@ -40,6 +40,8 @@ def main() -> int:
     ap.add_argument("--prompt", type=int, default=64, help="prompt tokens prefilled before decoding (eval)")
     ap.add_argument("--batch", type=int, default=1, help="concurrent sequences decoded together")
     ap.add_argument("--model", default="", help="optional .m file instead of synthetic 8B weights")
+    ap.add_argument("--shape", default="llama3_1_8b",
+                    help="synthetic shape (models/synthetic.py LLAMA_SHAPES); the headline metric is llama3_1_8b")
     ap.add_argument("--no-graphs", action="store_true")
     args = ap.parse_args()
 
@@ -50,6 +52,8 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("DL_BENCH_SAME_GPU") == "1":  # rehearsal of the multi-rank path on one GPU
+        local = 0
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     dist = None
@@ -69,7 +73,9 @@ def main() -> int:
             # rank cannot set them up, every rank falls back to RCCL
             ok = 1
             try:
-                hdr = C.load_header(args.model) if args.model else LLAMA31_8B
+                hdr = C.load_header(args.model) if args.model else (
+                    dict(LLAMA31_8B, **__import__("distributed_llama_multiusers_amd.models.synthetic",
+                                                  fromlist=["LLAMA_SHAPES"]).LLAMA_SHAPES[args.shape]))
                 vocab0 = -(-hdr["vocab_size"] // world)
                 max_floats = max_batch * max(hdr["dim"], vocab0)
                 comm = C.XgmiComm(rank, world, max_floats, local)
@@ -97,7 +103,11 @@ def main() -> int:
             uid = obj[0]
 
     seq_len = args.prompt + args.warmup + args.steps + 8
-    synthetic = None if args.model else dict(LLAMA31_8B, seq_len=seq_len)
+    shape = LLAMA31_8B
+    if args.shape != "llama3_1_8b":
+        from distributed_llama_multiusers_amd.models.synthetic import LLAMA_SHAPES
+        shape = dict(LLAMA31_8B, **LLAMA_SHAPES[args.shape])
+    synthetic = None if args.model else dict(shape, seq_len=seq_len)
     t0 = time.time()
     eng = C.HipEngine(args.model, "q80", max_seq_len=seq_len, max_batch=max_batch, n_slots=args.batch,
                       gpu_index=local, use_graphs=not args.no_graphs, synthetic=synthetic, seed=1234, rank=rank,
@@ -161,7 +171,8 @@ def main() -> int:
         "dtype": "q40-weights/q80-activations (f32 accumulate)",
         "data": "synthetic: random-init Llama-3.1-8B weights on device, synthetic prompt",
         "config": {
-            "model": "Llama-3.1-8B" if not args.model else os.path.basename(args.model),
+            "model": ({"llama3_1_8b": "Llama-3.1-8B"}.get(args.shape, args.shape) if not args.model
+                      else os.path.basename(args.model)),
             "global_batch": B,
             "seq_len": seq_len,
             "prompt_tokens": args.prompt,

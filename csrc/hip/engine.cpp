@@ -55,6 +55,7 @@ class HipEngineImpl : public HipEngine {
         DL_CHECK(dev_ < nDev, "gpu index out of range");
         DL_HIP(hipSetDevice(dev_));
         DL_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+
         const u32 nRanks = comm_ ? comm_->size() : 1, rank = comm_ ? comm_->rank() : 0;
         if (cfg.synthetic) {
             h_ = cfg.syntheticHeader;
@@ -508,7 +509,7 @@ class HipEngineImpl : public HipEngine {
         int bc = 4;
         while (bc > 1) {
             const int rpw = hipk::gemvRowsPerPass(m.n, m.rows, bc, q40_) * passesFor(m, epi, bc);
-            if (hipk::gemvLdsBytes(m.n, bc, q40_, rpw, pro) <= 64 * 1024) break;
+            if (hipk::gemvLdsBytes(m.n, bc, q40_, rpw, pro) <= 64 * 1024) break;  // B > 1 only; B = 1 may use up to 160 KB
             bc >>= 1;
         }
         return bc;
@@ -573,6 +574,17 @@ class HipEngineImpl : public HipEngine {
     }
 
     bool batchedPath(int n) const { return q40_ && n >= gemmMinTokens(); }
+
+    // MALL warm-up of wo + the head of w13 beside attention (DL_MALL_PREFETCH=1 enables;
+    // DL_MALL_PREFETCH_MB sets the w13 head size)
+    static bool mallPrefetch() {  // opt-in: measured slower on MI355X (profiles/r1_mall_prefetch.md)
+        const char *e = std::getenv("DL_MALL_PREFETCH");
+        return e && *e == '1';
+    }
+    static size_t mallPrefetchBytes() {
+        const char *e = std::getenv("DL_MALL_PREFETCH_MB");
+        return (size_t)(e && *e ? std::atoi(e) : 24) << 20;
+    }
 
     // Batched path (>= gemmMinTokens rows, Q40): per chunk of <= 32 tokens, a norm kernel (f32 ->
     // f16, RESNORM) or the producer's f16 rows (xh) feed the MFMA GEMM with the fused epilogue.
@@ -655,6 +667,7 @@ class HipEngineImpl : public HipEngine {
                          hasDelta ? dX_[cur ^ 1] : nullptr, L.rmsAtt, dQ_, p.q0, &L);
             }
             if (hasDelta) cur ^= 1;
+            const bool pf = mallPrefetch() && q40_ && !profile_;
             {
                 ProfScope ps(this, "attention");
                 hipk::AttnArgs a;
@@ -680,6 +693,17 @@ class HipEngineImpl : public HipEngine {
                 a.ldOut = p.q0;
                 a.kvBf16 = kvBf16_ ? 1 : 0;
                 a.counters = dAttCnt_;
+                if (pf) {
+                    // attention keeps a handful of CUs busy for several µs while HBM idles: extra
+                    // workgroups of the same launch pull wo and the head of w13 into the MALL
+                    const hipk::Q40Tiling two = hipk::q40Tiling(L.wo.rows, L.wo.n, L.wo.lanes);
+                    const hipk::Q40Tiling t13 = hipk::q40Tiling(L.w13.rows, L.w13.n, L.w13.lanes);
+                    a.pf0 = L.wo.qs;
+                    a.pf0Bytes = two.qsBytes;
+                    a.pf1 = L.w13.qs;
+                    a.pf1Bytes = std::min(t13.qsBytes, mallPrefetchBytes());
+                    a.pfBlocks = 256;
+                }
                 hipk::launchAttention(a, n, stream_);
             }
             {
@@ -765,6 +789,7 @@ class HipEngineImpl : public HipEngine {
     DeviceComm *comm_;
     int dev_ = 0;
     hipStream_t stream_ = nullptr;
+
     std::unique_ptr<ModelFile> file_;
     ModelHeader h_;
     ShardPlan plan_;

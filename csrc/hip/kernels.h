@@ -97,6 +97,7 @@ size_t gemmPartFloats(int rows, int n, int maxTokens);
 // in/addIn/xNext [M][ldIn] f32 -> out [M][n] f16 (xNext = in + addIn when set).
 void launchNormF16(const GemvArgs &a, _Float16 *out, int M, hipStream_t s);
 
+
 // B = batch rows in this launch (1, 2 or 4); q40 = weight format.
 void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_t s);
 // Rows handled by one lane group (2 at batch 1: the activation loads are shared by 2 rows).
@@ -130,6 +131,10 @@ struct AttnArgs {
     int ldOut = 0;
     int kvBf16 = 1;
     int *counters = nullptr;    // [B][nHeads0/HG] arrival counters (zero-initialised, self-resetting)
+    // optional MALL warm-up run by extra workgroups of the same launch (weights of the next GEMVs)
+    const void *pf0 = nullptr, *pf1 = nullptr;
+    size_t pf0Bytes = 0, pf1Bytes = 0;
+    int pfBlocks = 0;
 };
 void launchAttention(const AttnArgs &a, int B, hipStream_t s);
 int attnSplitGrid(int seqLen);

@@ -652,14 +652,22 @@ __global__ __launch_bounds__(kThreads) void gemvKernel(GemvArgs a) {
     }
 }
 
+// Dynamic LDS above 64 KB (up to the CU's 160 KB) has to be opted into per kernel.
+static void allowLds(const void *fn, size_t bytes) {
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
 template <int L, int B, bool Q40>
 static void gemvDispatchPE(const GemvArgs &a, int pro, int epi, size_t lds, int grid, hipStream_t s) {
 #define DL_GEMV_CASE(P, E)                                                                          \
     if (pro == P && epi == E) {                                                                     \
-        if constexpr (Q40)                                                                          \
+        if constexpr (Q40) {                                                                        \
+            if (lds > 65536) allowLds((const void *)gemvQ40Kernel<L, B, P, E>, lds);                 \
             hipLaunchKernelGGL((gemvQ40Kernel<L, B, P, E>), dim3(grid), dim3(kThreads), lds, s, a); \
-        else                                                                                        \
+        } else {                                                                                    \
+            if (lds > 65536) allowLds((const void *)gemvKernel<L, B, P, E, false>, lds);             \
             hipLaunchKernelGGL((gemvKernel<L, B, P, E, false>), dim3(grid), dim3(kThreads), lds, s, a); \
+        }                                                                                           \
         return;                                                                                     \
     }
     DL_GEMV_CASE(PRO_GLOBAL, EPI_STORE)
@@ -1127,6 +1135,32 @@ __global__ __launch_bounds__(kAttnThreads) void attnKernel(AttnArgs a) {
     constexpr int DPL = HS / 16;           // dims per lane: 16 lanes cover one position's head vector
     constexpr int TU = BF16 ? 8 : 4;       // keys per group loaded before any is consumed
     constexpr int RW = BF16 ? DPL / 2 : DPL;  // 32-bit words per lane per key (packed bf16 pairs)
+    const int hgx = a.nHeads0 / HG;  // attention workgroups per (split, row) slice
+    if ((int)blockIdx.x >= hgx) {
+        // MALL warm-up role: every extra workgroup of every slice streams its share of the next
+        // GEMVs' weights with plain loads (allocating in the Infinity Cache) and discards them
+        const int pfx = gridDim.x - hgx;
+        const int id = (blockIdx.z * gridDim.y + blockIdx.y) * pfx + (blockIdx.x - hgx);
+        const int nPf = pfx * gridDim.y * gridDim.z;
+        typedef unsigned int u32x4l __attribute__((ext_vector_type(4)));
+        const size_t n0 = a.pf0Bytes / 16, n1 = a.pf1Bytes / 16, tot = n0 + n1;
+        const size_t per = (tot + nPf - 1) / nPf;
+        const size_t i0 = (size_t)id * per, i1 = min(i0 + per, tot);
+        const u32x4l *p0 = reinterpret_cast<const u32x4l *>(a.pf0), *p1 = reinterpret_cast<const u32x4l *>(a.pf1);
+        u32x4l acc = {0u, 0u, 0u, 0u};
+        for (size_t i = i0 + threadIdx.x; i < i1; i += 4 * kAttnThreads) {
+            u32x4l v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const size_t j = min(i + (size_t)u * kAttnThreads, i1 - 1);
+                v[u] = j < n0 ? p0[j] : p1[j - n0];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) acc ^= v[u];
+        }
+        asm volatile("" ::"v"(acc.x), "v"(acc.y), "v"(acc.z), "v"(acc.w));
+        return;
+    }
     const int b = blockIdx.z;
     const int pos = a.pos[b], sl = a.slot[b];
     const int len = pos + 1;
@@ -1299,7 +1333,7 @@ __global__ __launch_bounds__(kAttnThreads) void attnKernel(AttnArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    int *cnt = a.counters + (size_t)b * gridDim.x + blockIdx.x;
+    int *cnt = a.counters + (size_t)b * hgx + blockIdx.x;
     if (tid == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1335,7 +1369,9 @@ template <int HS, bool BF16>
 static void attnDispatchHG(const AttnArgs &a, int B, int HG, hipStream_t s) {
     constexpr int NW = kAttnThreads / 64;
     const size_t lds = sizeof(float) * (2 * NW * HG + NW * HG * HS + HG * HS + 2 * HG) + 16;
-    const dim3 grid(a.nHeads0 / HG, a.splitGrid, B);
+    int pfx = 0;  // extra MALL warm-up workgroups per slice (see attnKernel)
+    if (a.pfBlocks > 0 && (a.pf0Bytes + a.pf1Bytes) >= 16) pfx = (a.pfBlocks + a.splitGrid * B - 1) / (a.splitGrid * B);
+    const dim3 grid(a.nHeads0 / HG + pfx, a.splitGrid, B);
     switch (HG) {
         case 1: hipLaunchKernelGGL((attnKernel<1, HS, BF16>), grid, dim3(kAttnThreads), lds, s, a); break;
         case 2: hipLaunchKernelGGL((attnKernel<2, HS, BF16>), grid, dim3(kAttnThreads), lds, s, a); break;
