@@ -24,6 +24,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 BASELINE_MS = {1: 1312.50, 2: 793.69, 4: 494.00, 8: 588.19}  # BASELINE.md (Llama 2 7B, RPi 4B cluster)
+BASELINE_MS_70B = {8: 4842.81}  # BASELINE.md (Llama 2 70B, 8x RPi 4B)
 METRIC = "avg eval+pred ms/token (= tokens/sec) for Llama-3.1-8B Q40 at 1/2/4/8 MI355X"
 
 LLAMA31_8B = dict(dim=4096, hidden_dim=14336, n_layers=32, n_heads=32, n_kv_heads=8, vocab_size=128256,
@@ -156,7 +157,9 @@ def main() -> int:
 
     ms_per_step = elapsed * 1000.0 / args.steps
     tok_s = B * 1000.0 / ms_per_step
-    base = BASELINE_MS.get(world)
+    # the published baselines are per model family: 7B/8B at 1/2/4/8 devices, 70B at 8 devices
+    base = (BASELINE_MS.get(world) if args.shape == "llama3_1_8b" and not args.model
+            else BASELINE_MS_70B.get(world) if args.shape == "llama3_3_70b" and not args.model else None)
     result = {
         "metric": METRIC,
         "value": round(tok_s, 3),
@@ -169,7 +172,8 @@ def main() -> int:
         "scaling": "strong",
         "vs_baseline": round(tok_s / (1000.0 / base), 2) if base else None,
         "dtype": "q40-weights/q80-activations (f32 accumulate)",
-        "data": "synthetic: random-init Llama-3.1-8B weights on device, synthetic prompt",
+        "data": (f"synthetic: random-init {args.shape} weights on device, synthetic prompt" if not args.model
+                 else "model file weights, synthetic prompt"),
         "config": {
             "model": ({"llama3_1_8b": "Llama-3.1-8B"}.get(args.shape, args.shape) if not args.model
                       else os.path.basename(args.model)),

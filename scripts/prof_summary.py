@@ -29,6 +29,7 @@ def from_db(path):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("path")
+    ap.add_argument("--by-grid", action="store_true", help="separate rows per launch grid (wo vs w2, ...)")
     ap.add_argument("--skip-first", type=int, default=0, help="ignore the first N dispatches overall (warmup)")
     args = ap.parse_args()
     path = args.path
@@ -40,7 +41,7 @@ def main():
     rows = rows[args.skip_first:]
     agg = collections.OrderedDict()
     for r in rows:
-        k = short(r["name"])
+        k = short(r["name"]) + (f" [{r['grid']}]" if args.by_grid else "")
         a = agg.setdefault(k, dict(calls=0, ns=0, vgpr=r["vgpr"], lds=r["lds"], grid=r["grid"], wg=r["wg"]))
         a["calls"] += 1
         a["ns"] += r["end"] - r["start"]
