@@ -28,6 +28,7 @@ using namespace dl::dev;
 static constexpr int kThreads = 256;
 static constexpr int kMaxHeadSize = 128;  // RoPE rows staged in LDS by the QKV epilogue
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
@@ -427,29 +428,44 @@ __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
     const size_t cBase = (size_t)blockIdx.x * T;
     const size_t cLast = (size_t)((a.rows + RP - 1) / RP) * K - 1;
     int it = 0;  // issue cursor (steps)
-    // The ring's loads are inline asm with explicit vmcnt waits (cdna_hip_programming.md §5.7,
+    auto stepPtrs = [&](const u32x4 *&p0, const uint32_t *&pd) {
+        const size_t c = min(cBase + (size_t)min(it, T - 1), cLast);
+        p0 = reinterpret_cast<const u32x4 *>(a.qs) + (c * 2) * kThreads + tid;
+        pd = wd2 + c * kThreads + tid;
+        ++it;
+    };
+    // The ring's refills are inline asm with explicit vmcnt waits (cdna_hip_programming.md §5.7,
     // form ii): hipcc's own waitcnt pass flushes vmcnt(0) at the loop header, which turns the ring
     // into bulk-synchronous rounds. Each step is 3 loads; consuming a slot waits until only the
     // loads issued after it are outstanding. Refills past the last step re-read this workgroup's
     // last chunk (L2), keeping every slot unconditionally defined (no phi copies of in-flight
     // registers).
     auto issue = [&](u32x4(&ws)[RG], uint32_t &ds) {
-        const size_t c = min(cBase + (size_t)min(it, T - 1), cLast);
-        const u32x4 *p0 = reinterpret_cast<const u32x4 *>(a.qs) + (c * 2) * kThreads + tid;
-        const u32x4 *p1 = p0 + kThreads;
-        const uint32_t *pd = wd2 + c * kThreads + tid;
+        const u32x4 *p0;
+        const uint32_t *pd;
+        stepPtrs(p0, pd);
         asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(ws[0]) : "v"(p0));
-        asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(ws[1]) : "v"(p1));
+        asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(ws[1]) : "v"(p0 + kThreads));
         asm volatile("global_load_dword %0, %1, off" : "=v"(ds) : "v"(pd));
-        ++it;
     };
-    // sched_barrier keeps issue order == slot order, so each step waits for exactly its own slot
-    // (vmcnt = loads of the other kRing-1 slots) instead of the scheduler batching the ring.
+    // The same step as compiler-visible loads (first round of the early-prologue path): the
+    // waitcnt pass then counts them, so the prologue's own (older) loads are waited for with
+    // vmcnt(3 * kRing) while the ring's first round is still in flight.
+    auto issueVisible = [&](u32x4(&ws)[RG], uint32_t &ds) {
+        const u32x4 *p0;
+        const uint32_t *pd;
+        stepPtrs(p0, pd);
+        ws[0] = __builtin_nontemporal_load(p0);
+        ws[1] = __builtin_nontemporal_load(p0 + kThreads);
+        ds = *pd;
+    };
+    // The prologue's loads were issued after the ring's (late path), or the ring's first round is
+    // compiler-visible (early path); either way this explicit wait pins every slot register before
+    // the loop, so no copy of an in-flight register can be made.
+    auto waitAll = [&]() {
 #pragma unroll
-    for (int s = 0; s < D; s++) {
-        issue(w[s], dh[s]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
+        for (int s = 0; s < D; s++) asm volatile("s_waitcnt vmcnt(0)" : "+v"(w[s][0]), "+v"(w[s][1]), "+v"(dh[s]));
+    };
 
     float2 *sRope = reinterpret_cast<float2 *>(smem + lay.rope);
     int posB[B], slotB[B];  // uniform: scalar loads, kept out of the ring's vmcnt accounting
@@ -458,24 +474,129 @@ __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
         posB[b] = EPI == EPI_QKV ? a.pos[b] : 0;
         slotB[b] = EPI == EPI_QKV ? a.slot[b] : 0;
     }
-    if constexpr (EPI == EPI_QKV) {  // the prologue's __syncthreads publishes these
-        const int h2 = a.hs >> 1;
-        for (int i = tid; i < B * h2; i += kThreads) {
-            const int b = i / h2;
-            sRope[b * (kMaxHeadSize / 2) + i % h2] = a.rope[(size_t)a.pos[b] * h2 + i % h2];
-        }
-    }
-    if constexpr (PRO == PRO_RESNORM)
-        resNormPrologue<B, true>(a, scratch, sq, ssc, nullptr);
-    else
-        stageQ80<B>(a, sq, ssc);
-    // The prologue's own loads were issued after the ring's, so waiting for them already drained
-    // the ring; this explicit wait pins every slot register before the compiler may copy one.
-    auto waitAll = [&]() {
+    // Early prologue (batch 1, activations small enough to sit in registers): the activation /
+    // residual / norm-weight loads go out BEFORE the ring's first round, so the norm + Q80 work
+    // overlaps the ring's HBM round trip instead of following it (~1 us per kernel).
+    // PK = 8-float chunks (resnorm) or 16-byte Q80 units (copy) per thread, sized from n so no
+    // load is wasted: resnorm n <= 2048 * PK, Q80 copy n <= 4096 * PK.
+    auto earlyPath = [&](auto pkTag) {
+        constexpr int PK = decltype(pkTag)::value, PS = (PK + 1) / 2;
+        const int nChunks = n >> 3, n16 = n >> 4;
+        float4 ex[PK][2], ey[PK][2], ew[PK][2];
+        u32x4 eq[PK];
+        u32x2 es[PS];
+        // unconditional, clamped loads in one basic block: a branch here would let the compiler
+        // pull the arithmetic up to the loads and wait for them before the ring is issued
+        float2 ropeV = make_float2(0.f, 0.f);
+        if constexpr (EPI == EPI_QKV) ropeV = a.rope[(size_t)posB[0] * (a.hs >> 1) + min(tid, (a.hs >> 1) - 1)];
+        if constexpr (PRO == PRO_RESNORM) {
+            const float *yp = a.addIn ? a.addIn : a.in;
+            const float *wp = a.normW ? a.normW : a.in;
 #pragma unroll
-        for (int s = 0; s < D; s++) asm volatile("s_waitcnt vmcnt(0)" : "+v"(w[s][0]), "+v"(w[s][1]), "+v"(dh[s]));
+            for (int k = 0; k < PK; k++) {
+                const int c = min(tid + k * kThreads, nChunks - 1);
+                ex[k][0] = ld4(a.in + c * 8);
+                ex[k][1] = ld4(a.in + c * 8 + 4);
+                ey[k][0] = ld4(yp + c * 8);
+                ey[k][1] = ld4(yp + c * 8 + 4);
+                ew[k][0] = ld4(wp + c * 8);
+                ew[k][1] = ld4(wp + c * 8 + 4);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < PK; k++) eq[k] = reinterpret_cast<const u32x4 *>(a.aq)[min(tid + k * kThreads, n16 - 1)];
+#pragma unroll
+            for (int k = 0; k < PS; k++) es[k] = reinterpret_cast<const u32x2 *>(a.as)[min(tid + k * kThreads, nb - 1)];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < D; s++) {
+            issueVisible(w[s], dh[s]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (EPI == EPI_QKV)
+            if (tid < (a.hs >> 1)) sRope[tid] = ropeV;
+        if constexpr (PRO == PRO_RESNORM) {
+            float *xo = (blockIdx.x == 0 && a.xNext) ? a.xNext : nullptr;
+            float v[PK][8];
+            float ss = 0.f;
+#pragma unroll
+            for (int k = 0; k < PK; k++) {
+                const int c = tid + k * kThreads;
+                float4 v0 = ex[k][0], v1 = ex[k][1];
+                if (a.addIn) {
+                    v0.x += ey[k][0].x; v0.y += ey[k][0].y; v0.z += ey[k][0].z; v0.w += ey[k][0].w;
+                    v1.x += ey[k][1].x; v1.y += ey[k][1].y; v1.z += ey[k][1].z; v1.w += ey[k][1].w;
+                }
+                if (xo && c < nChunks) {
+                    st4(xo + c * 8, v0);
+                    st4(xo + c * 8 + 4, v1);
+                }
+                v[k][0] = v0.x; v[k][1] = v0.y; v[k][2] = v0.z; v[k][3] = v0.w;
+                v[k][4] = v1.x; v[k][5] = v1.y; v[k][6] = v1.z; v[k][7] = v1.w;
+                if (c < nChunks) {
+#pragma unroll
+                    for (int i = 0; i < 8; i++) ss += v[k][i] * v[k][i];
+                }
+            }
+            float inv = 1.0f;
+            if (a.normW) {
+                ss = blockSum<kThreads>(ss, scratch);
+                inv = 1.0f / sqrtf(ss / (float)n + a.eps);
+            }
+#pragma unroll
+            for (int k = 0; k < PK; k++) {
+                const int c = tid + k * kThreads;
+                if (c < nChunks) {
+                    if (a.normW) {
+                        const float wv[8] = {ew[k][0].x, ew[k][0].y, ew[k][0].z, ew[k][0].w,
+                                             ew[k][1].x, ew[k][1].y, ew[k][1].z, ew[k][1].w};
+#pragma unroll
+                        for (int i = 0; i < 8; i++) v[k][i] = wv[i] * (inv * v[k][i]);
+                    }
+                    stageChunk<true>(v[k], 0, c, n, sq, ssc, nullptr);
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < PK; k++)
+                if (tid + k * kThreads < n16) reinterpret_cast<u32x4 *>(sq)[tid + k * kThreads] = eq[k];
+#pragma unroll
+            for (int k = 0; k < PS; k++)
+                if (tid + k * kThreads < nb) reinterpret_cast<u32x2 *>(ssc)[tid + k * kThreads] = es[k];
+        }
+        __syncthreads();
+        waitAll();
     };
-    waitAll();
+    const int unitsPerThread = PRO == PRO_RESNORM ? (n + 8 * kThreads - 1) / (8 * kThreads)
+                                                  : (n + 16 * kThreads - 1) / (16 * kThreads);
+    if (B == 1 && unitsPerThread <= 1) {
+        earlyPath(std::integral_constant<int, 1>{});
+    } else if (B == 1 && unitsPerThread <= 2) {
+        earlyPath(std::integral_constant<int, 2>{});
+    } else if (B == 1 && unitsPerThread <= 4) {
+        earlyPath(std::integral_constant<int, 4>{});
+    } else {
+        // sched_barrier keeps issue order == slot order, so each step waits for exactly its own
+        // slot (vmcnt = loads of the other kRing-1 slots) instead of the scheduler batching the ring.
+#pragma unroll
+        for (int s = 0; s < D; s++) {
+            issue(w[s], dh[s]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (EPI == EPI_QKV) {  // the prologue's __syncthreads publishes these
+            const int h2 = a.hs >> 1;
+            for (int i = tid; i < B * h2; i += kThreads) {
+                const int b = i / h2;
+                sRope[b * (kMaxHeadSize / 2) + i % h2] = a.rope[(size_t)a.pos[b] * h2 + i % h2];
+            }
+        }
+        if constexpr (PRO == PRO_RESNORM)
+            resNormPrologue<B, true>(a, scratch, sq, ssc, nullptr);
+        else
+            stageQ80<B>(a, sq, ssc);
+        waitAll();
+    }
 
     float acc[RG][B];
 #pragma unroll
@@ -724,7 +845,6 @@ void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_
 // SwiGLU -> f16 / SwiGLU -> Q80 / RoPE + KV append).
 // ------------------------------------------------------------------------------------------------
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 static constexpr int kGemmRows = 64;
 static constexpr int kGemmCh = 8;  // Q40 blocks per pipeline stage (~25 KB at 32 tokens)
 
