@@ -923,6 +923,87 @@ double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int pas
     return ms * 1000.0 / iters;
 }
 
+double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B, int copies, int iters) {
+    hipStream_t s;
+    DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<void *> mem;
+    auto alloc = [&](size_t bytes) {
+        void *p;
+        DL_HIP(hipMalloc(&p, bytes));
+        DL_HIP(hipMemsetAsync(p, 0, bytes, s));
+        mem.push_back(p);
+        return p;
+    };
+    DL_CHECK(kvMul >= 1 && nHeads0 % kvMul == 0 && pos >= 0 && pos < seqLen && B >= 1, "bad attention bench shape");
+    const int kv0 = nHeads0 / kvMul * hs, q0 = nHeads0 * hs;
+    const size_t kvElems = (size_t)B * seqLen * kv0;  // one slot per row
+    std::vector<void *> kc(copies), vc(copies);
+    for (int c = 0; c < copies; c++) {
+        kc[c] = alloc(kvElems * 2);
+        vc[c] = alloc(kvElems * 2);
+        hipk::launchFillF32Uniform((float *)kc[c], kvElems / 2, 1.f, 5 + c, s);  // bf16 pairs of small values
+        hipk::launchFillF32Uniform((float *)vc[c], kvElems / 2, 1.f, 9 + c, s);
+    }
+    float *q = (float *)alloc((size_t)B * q0 * 4);
+    hipk::launchFillF32Uniform(q, (size_t)B * q0, 1.f, 3, s);
+    std::vector<int> hp(B), hsl(B);
+    for (int b = 0; b < B; b++) hp[b] = pos, hsl[b] = b;
+    int *dpos = (int *)alloc(B * 4), *dslot = (int *)alloc(B * 4);
+    DL_HIP(hipMemcpyAsync(dpos, hp.data(), B * 4, hipMemcpyHostToDevice, s));
+    DL_HIP(hipMemcpyAsync(dslot, hsl.data(), B * 4, hipMemcpyHostToDevice, s));
+    hipk::AttnArgs a;
+    a.q = q;
+    a.ldq = q0;
+    a.pos = dpos;
+    a.slot = dslot;
+    a.nHeads0 = nHeads0;
+    a.kvMul = kvMul;
+    a.hs = hs;
+    a.kv0 = kv0;
+    a.seqLen = seqLen;
+    a.splitGrid = hipk::attnSplitGrid(seqLen);
+    a.chunkMax = hipk::attnChunkMax(seqLen, a.splitGrid);
+    a.partO = (float *)alloc((size_t)B * nHeads0 * a.splitGrid * hs * 4);
+    a.partML = (float *)alloc((size_t)B * nHeads0 * a.splitGrid * 2 * 4);
+    a.outQ = (int8_t *)alloc((size_t)B * q0);
+    a.outS = (float2 *)alloc((size_t)B * q0 / 32 * 8);
+    a.ldOut = q0;
+    a.kvBf16 = 1;
+    a.counters = (int *)alloc((size_t)B * nHeads0 * 4);
+    DL_HIP(hipStreamSynchronize(s));
+    auto launch = [&](int c) {
+        a.kcache = kc[c % copies];
+        a.vcache = vc[c % copies];
+        hipk::launchAttention(a, B, s);
+    };
+    launch(0);
+    DL_HIP(hipGetLastError());
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    DL_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < iters; i++) launch(i);
+    DL_HIP(hipStreamEndCapture(s, &g));
+    DL_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    DL_HIP(hipGraphLaunch(ge, s));
+    DL_HIP(hipStreamSynchronize(s));
+    hipEvent_t e0, e1;
+    DL_HIP(hipEventCreate(&e0));
+    DL_HIP(hipEventCreate(&e1));
+    DL_HIP(hipEventRecord(e0, s));
+    DL_HIP(hipGraphLaunch(ge, s));
+    DL_HIP(hipEventRecord(e1, s));
+    DL_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    DL_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipGraphExecDestroy(ge);
+    (void)hipGraphDestroy(g);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    for (void *p : mem) (void)hipFree(p);
+    (void)hipStreamDestroy(s);
+    return ms * 1000.0 / iters;
+}
+
 std::unique_ptr<HipEngine> makeHipEngine(const EngineConfig &cfg, DeviceComm *comm) {
     return std::unique_ptr<HipEngine>(new HipEngineImpl(cfg, comm));
 }

@@ -1248,6 +1248,91 @@ __device__ __forceinline__ void softmaxMerge(float &m, float &l, float (&o)[D], 
 
 static constexpr int kAttnThreads = 512;  // 8 waves = 32 groups of 16 lanes, one key per group
 
+// Split epilogue of the attention kernel: redL [HG][HS] holds the unnormalised output of this
+// workgroup's chunk, mlL [HG][2] its (max, sum). One chunk: normalise and write. Several: publish
+// the partial and count arrivals; the last workgroup combines all chunks. The combine stages every
+// chunk's (max, sum) in LDS (`scratch`, >= 2 * HG * splitGrid floats) with one load per thread and
+// keeps 8 partial-output loads in flight per thread: a serial loop over the chunks costs one
+// cross-XCD round trip per chunk (~30 us at 32 chunks).
+template <int HG, int HS, int AT>
+__device__ __forceinline__ void attnFinish(const AttnArgs &a, int b, int head0, int c, int nSplit, float *redL,
+                                           float *mlL, int *flagL, float *scratch) {
+    const int tid = threadIdx.x;
+    if (nSplit == 1) {
+        for (int i = tid; i < HG * HS; i += AT) redL[i] = redL[i] / mlL[(i / HS) * 2 + 1];
+        __syncthreads();
+        attnWriteOut<HG, HS, AT>(a, b, head0, redL);
+        return;
+    }
+    const int G = a.splitGrid;
+    const size_t pbase = ((size_t)b * a.nHeads0 + head0) * G;  // [HG][G] chunks of this head group
+    for (int i = tid; i < HG * HS; i += AT) {
+        const int h = i / HS, d = i % HS;
+        a.partO[((pbase + (size_t)h * G) + c) * HS + d] = redL[i];
+    }
+    if (tid < HG) {
+        a.partML[((pbase + (size_t)tid * G) + c) * 2] = mlL[tid * 2];
+        a.partML[((pbase + (size_t)tid * G) + c) * 2 + 1] = mlL[tid * 2 + 1];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int *cnt = a.counters + (size_t)b * (a.nHeads0 / HG) + blockIdx.x;
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flagL[0] = old == nSplit - 1;
+    }
+    __syncthreads();
+    if (!flagL[0]) return;
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    // every chunk's (max, sum) -> LDS, then per head: global max and chunk weights w = exp(m - M)
+    for (int i = tid; i < HG * nSplit; i += AT) {
+        const int h = i / nSplit, cc = i % nSplit;
+        const float2 ml = *reinterpret_cast<const float2 *>(a.partML + ((pbase + (size_t)h * G) + cc) * 2);
+        scratch[2 * (h * G + cc)] = ml.x;
+        scratch[2 * (h * G + cc) + 1] = ml.y;
+    }
+    __syncthreads();
+    if (tid < HG) {
+        float M = -INFINITY;
+        for (int cc = 0; cc < nSplit; cc++) M = fmaxf(M, scratch[2 * (tid * G + cc)]);
+        float Ls = 0.f;
+        for (int cc = 0; cc < nSplit; cc++) {
+            float *ml = scratch + 2 * (tid * G + cc);
+            const float w = M == -INFINITY ? 0.f : __expf(ml[0] - M);
+            ml[0] = w;
+            Ls += w * ml[1];
+        }
+        mlL[tid * 2 + 1] = Ls;
+    }
+    __syncthreads();
+    constexpr int U = 8;
+    for (int i = tid; i < HG * HS; i += AT) {
+        const int h = i / HS, d = i % HS;
+        const float *po = a.partO + (pbase + (size_t)h * G) * HS + d;
+        const float *wv = scratch + 2 * h * G;
+        float acc = 0.f;
+        int cc = 0;
+        for (; cc + U <= nSplit; cc += U) {
+            float v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) v[u] = po[(size_t)(cc + u) * HS];
+#pragma unroll
+            for (int u = 0; u < U; u++) acc += wv[2 * (cc + u)] * v[u];
+        }
+        for (; cc < nSplit; cc++) acc += wv[2 * cc] * po[(size_t)cc * HS];
+        redL[i] = acc / mlL[h * 2 + 1];
+    }
+    __syncthreads();
+    attnWriteOut<HG, HS, AT>(a, b, head0, redL);
+}
+
 template <int HG, int HS, bool BF16>
 __global__ __launch_bounds__(kAttnThreads) void attnKernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1434,63 +1519,15 @@ __global__ __launch_bounds__(kAttnThreads) void attnKernel(AttnArgs a) {
     }
     __syncthreads();
 
-    if (nSplit == 1) {
-        for (int i = tid; i < HG * HS; i += AT) redL[i] = redL[i] / mlL[(i / HS) * 2 + 1];
-        __syncthreads();
-        attnWriteOut<HG, HS, AT>(a, b, head0, redL);
-        return;
-    }
-
-    // publish this chunk's partial, count arrivals; the last workgroup combines
-    const size_t pbase = ((size_t)b * a.nHeads0 + head0) * a.splitGrid;
-    for (int i = tid; i < HG * HS; i += AT) {
-        const int h = i / HS, d = i % HS;
-        a.partO[((pbase + (size_t)h * a.splitGrid) + c) * HS + d] = redL[i];
-    }
-    if (tid < HG) {
-        a.partML[((pbase + (size_t)tid * a.splitGrid) + c) * 2] = mlL[tid * 2];
-        a.partML[((pbase + (size_t)tid * a.splitGrid) + c) * 2 + 1] = mlL[tid * 2 + 1];
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int *cnt = a.counters + (size_t)b * hgx + blockIdx.x;
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        flagL[0] = old == nSplit - 1;
-    }
-    __syncthreads();
-    if (!flagL[0]) return;
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    for (int i = tid; i < HG * HS; i += AT) {
-        const int h = i / HS, d = i % HS;
-        const float *ml = a.partML + (pbase + (size_t)h * a.splitGrid) * 2;
-        float M = -INFINITY;
-        for (int cc = 0; cc < nSplit; cc++) M = fmaxf(M, ml[cc * 2]);
-        float Ls = 0.f, acc = 0.f;
-        for (int cc = 0; cc < nSplit; cc++) {
-            const float w = M == -INFINITY ? 0.f : __expf(ml[cc * 2] - M);
-            Ls += w * ml[cc * 2 + 1];
-            acc += w * a.partO[((pbase + (size_t)h * a.splitGrid) + cc) * HS + d];
-        }
-        redL[i] = acc / Ls;
-    }
-    __syncthreads();
-    attnWriteOut<HG, HS, AT>(a, b, head0, redL);
+    attnFinish<HG, HS, AT>(a, b, head0, c, nSplit, redL, mlL, flagL, oW);
 }
 
 template <int HS, bool BF16>
 static void attnDispatchHG(const AttnArgs &a, int B, int HG, hipStream_t s) {
     constexpr int NW = kAttnThreads / 64;
-    const size_t lds = sizeof(float) * (2 * NW * HG + NW * HG * HS + HG * HS + 2 * HG) + 16;
     int pfx = 0;  // extra MALL warm-up workgroups per slice (see attnKernel)
     if (a.pfBlocks > 0 && (a.pf0Bytes + a.pf1Bytes) >= 16) pfx = (a.pfBlocks + a.splitGrid * B - 1) / (a.splitGrid * B);
+    const size_t lds = sizeof(float) * (2 * NW * HG + NW * HG * HS + HG * HS + 2 * HG) + 16;
     const dim3 grid(a.nHeads0 / HG + pfx, a.splitGrid, B);
     switch (HG) {
         case 1: hipLaunchKernelGGL((attnKernel<1, HS, BF16>), grid, dim3(kAttnThreads), lds, s, a); break;
@@ -1501,8 +1538,19 @@ static void attnDispatchHG(const AttnArgs &a, int B, int HG, hipStream_t s) {
 }
 
 void launchAttention(const AttnArgs &a, int B, hipStream_t s) {
-    int HG = a.kvMul < 8 ? a.kvMul : 8;
-    if (HG == 3 || HG == 5 || HG == 6 || HG == 7) HG = 1;
+    static const int hgOverride = [] {  // experiments: DL_ATTN_HG forces query heads per workgroup
+        const char *e = getenv("DL_ATTN_HG");
+        return e ? atoi(e) : 0;
+    }();
+    // Query heads per workgroup: sharing a KV head's loads between HG heads costs HG x the serial
+    // work per workgroup, so take the fewest heads per workgroup that keep the grid (at the
+    // longest context this launch can see) within one workgroup per CU. Measured on MI355X
+    // (scripts/bench_attn.py, profiles/r1_attention.md): short contexts 7.9 -> 5.9 us (TP1) and
+    // 7.7 -> 4.4 us (TP8) with one head per workgroup; long contexts keep 2-4 heads per workgroup.
+    const int hgMax = (a.kvMul & (a.kvMul - 1)) == 0 ? (a.kvMul < 8 ? a.kvMul : 8) : 1;
+    int HG = 1;
+    while (HG < hgMax && (long)(a.nHeads0 / HG) * a.splitGrid * B > 256) HG *= 2;
+    if (hgOverride > 0 && hgOverride <= hgMax && hgMax % hgOverride == 0) HG = hgOverride;
     if (a.hs == 128) {
         if (a.kvBf16) attnDispatchHG<128, true>(a, B, HG, s);
         else attnDispatchHG<128, false>(a, B, HG, s);

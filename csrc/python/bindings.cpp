@@ -290,6 +290,9 @@ PYBIND11_MODULE(_C, m) {
     m.def("bench_gemv_q40", &benchGemvQ40, py::arg("rows"), py::arg("n"), py::arg("pro"), py::arg("epi"),
           py::arg("batch") = 1, py::arg("lanes") = 0, py::arg("passes") = 1, py::arg("copies") = 8,
           py::arg("iters") = 200, py::call_guard<py::gil_scoped_release>());
+    m.def("bench_attention", &benchAttention, py::arg("n_heads0"), py::arg("kv_mul"), py::arg("head_size"),
+          py::arg("seq_len"), py::arg("pos"), py::arg("batch") = 1, py::arg("copies") = 32, py::arg("iters") = 200,
+          py::call_guard<py::gil_scoped_release>());
 
     m.def("simulate_tp",
           [](const std::string &model, const std::string &bufferType, int world, std::vector<int> tokens, bool kvBf16,

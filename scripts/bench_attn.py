@@ -1,0 +1,30 @@
+#!/usr/bin/env python3
+"""Decode-attention micro-benchmark: microseconds per launch of the attention kernel (bf16 KV cache,
+Q80 output) inside a hipGraph of back-to-back launches, for the Llama-3.1-8B head layout at each
+tensor-parallel degree (heads and KV heads per rank shrink with TP).
+
+    python scripts/bench_attn.py                # default sweep
+    DL_ATTN_HG=1 python scripts/bench_attn.py   # force query heads per workgroup
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import distributed_llama_multiusers_amd as dl
+    C = dl.native()
+    copies = 32  # one KV cache per layer: a decode step revisits a layer's KV only every token
+    iters = 200
+    print(f"attention µs/launch (graph of {iters}, {copies} KV copies), env DL_ATTN_HG={os.environ.get('DL_ATTN_HG', '')}")
+    for tp in (1, 2, 4, 8):
+        nh, kvm = 32 // tp, 4
+        for seq, pos in ((256, 150), (2048, 1500), (8192, 8000)):
+            for B in (1, 4):
+                us = C.bench_attention(nh, kvm, 128, seq, pos, B, copies, iters)
+                print(f"tp{tp} heads {nh:2d} kvMul {kvm} seqLen {seq:5d} pos {pos:5d} B {B}: {us:7.2f} us", flush=True)
+
+
+if __name__ == "__main__":
+    main()
