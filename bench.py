@@ -69,39 +69,13 @@ def main() -> int:
         # control plane only (barriers, timing max, IPC handle / RCCL id exchange); the data plane
         # is the engine's own device communicator
         dist.init_process_group("gloo")
-        if comm_kind == "xgmi":
-            # one-shot collectives over IPC-mapped peer buffers (csrc/hip/xgmi_comm.cpp); if any
-            # rank cannot set them up, every rank falls back to RCCL
-            ok = 1
-            try:
-                hdr = C.load_header(args.model) if args.model else (
-                    dict(LLAMA31_8B, **__import__("distributed_llama_multiusers_amd.models.synthetic",
-                                                  fromlist=["LLAMA_SHAPES"]).LLAMA_SHAPES[args.shape]))
-                vocab0 = -(-hdr["vocab_size"] // world)
-                max_floats = max_batch * max(hdr["dim"], vocab0)
-                comm = C.XgmiComm(rank, world, max_floats, local)
-                handles = [None] * world
-                dist.all_gather_object(handles, comm.handle())
-                comm.connect(handles)
-                dist.barrier()
-                # pre-flight: one exact all-reduce across the real GPUs before trusting the path
-                import numpy as np
-                got = comm.all_reduce(np.full(4096, rank + 1, np.float32))
-                want = world * (world + 1) / 2
-                if comm.timed_out() or not np.all(got == want):
-                    raise RuntimeError(f"self-test failed (got {got[:4]}, want {want})")
-            except Exception as e:  # noqa: BLE001 - reported, then the collective fallback
-                print(f"rank {rank}: xgmi comm unavailable ({e}); falling back to rccl", file=sys.stderr)
-                ok = 0
-            flag = torch.tensor([ok], dtype=torch.int32)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            if int(flag[0]) == 0:
-                comm, comm_kind = None, "rccl"
-            dist.barrier()
-        if comm_kind != "xgmi":
-            obj = [C.rccl_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(obj, src=0)
-            uid = obj[0]
+        from distributed_llama_multiusers_amd.parallel import init_device_comm
+        hdr = C.load_header(args.model) if args.model else dict(
+            LLAMA31_8B, **__import__("distributed_llama_multiusers_amd.models.synthetic",
+                                     fromlist=["LLAMA_SHAPES"]).LLAMA_SHAPES[args.shape])
+        vocab0 = -(-hdr["vocab_size"] // world)
+        comm, uid, comm_kind = init_device_comm(C, dist, rank, world, max_batch * max(hdr["dim"], vocab0), local,
+                                                comm_kind)
 
     seq_len = args.prompt + args.warmup + args.steps + 8
     shape = LLAMA31_8B

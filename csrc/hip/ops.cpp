@@ -1,0 +1,352 @@
+// Single-kernel entry points (see ops.h). Host staging is deliberately simple: synchronous copies,
+// one allocation per operand, freed on return.
+#include "ops.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "../core/quant.h"
+#include "device_comm.h"
+#include "kernels.h"
+
+namespace dl {
+namespace ops {
+
+namespace {
+
+// Device allocations of one op call, released on scope exit.
+class Scratch {
+  public:
+    Scratch() { DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking)); }
+    ~Scratch() {
+        for (void *p : mem_) (void)hipFree(p);
+        (void)hipStreamDestroy(s);
+    }
+    template <typename T>
+    T *alloc(size_t count) {
+        void *p = nullptr;
+        const size_t bytes = count * sizeof(T) < 16 ? 16 : count * sizeof(T);
+        DL_HIP(hipMalloc(&p, bytes));
+        DL_HIP(hipMemsetAsync(p, 0, bytes, s));
+        mem_.push_back(p);
+        return static_cast<T *>(p);
+    }
+    template <typename T>
+    T *upload(const std::vector<T> &v) {
+        if (v.empty()) return nullptr;
+        T *p = alloc<T>(v.size());
+        DL_HIP(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+        return p;
+    }
+    template <typename T>
+    std::vector<T> download(const T *p, size_t count) {
+        std::vector<T> v(count);
+        DL_HIP(hipMemcpyAsync(v.data(), p, count * sizeof(T), hipMemcpyDeviceToHost, s));
+        DL_HIP(hipStreamSynchronize(s));
+        return v;
+    }
+    void sync() {
+        DL_HIP(hipGetLastError());
+        DL_HIP(hipStreamSynchronize(s));
+    }
+    hipStream_t s = nullptr;
+
+  private:
+    std::vector<void *> mem_;
+};
+
+// File-layout Q40 blocks -> the engine's tiled device layout (csrc/hip/kernels.h Q40Tiling).
+struct DevQ40 {
+    uint8_t *qs = nullptr;
+    uint16_t *d = nullptr;
+    int lanes = 0;
+};
+
+DevQ40 uploadQ40(Scratch &sc, const std::vector<uint8_t> &blocks, int rows, int n) {
+    DL_CHECK(n % 32 == 0 && rows > 0, "Q40 shape");
+    const size_t nb = (size_t)rows * (n / 32);
+    DL_CHECK(blocks.size() == nb * sizeof(BlockQ40), "Q40 blocks size");
+    std::vector<uint8_t> qs(nb * 16);
+    std::vector<uint16_t> d(nb);
+    const BlockQ40 *b = reinterpret_cast<const BlockQ40 *>(blocks.data());
+    for (size_t i = 0; i < nb; i++) {
+        std::memcpy(&qs[i * 16], b[i].qs, 16);
+        d[i] = b[i].d;
+    }
+    DevQ40 m;
+    m.lanes = hipk::gemvLanesPerRow(n, rows, 1, true);
+    const hipk::Q40Tiling t = hipk::q40Tiling(rows, n, m.lanes);
+    std::vector<uint8_t> qt(t.qsBytes);
+    std::vector<uint32_t> dt(t.dBytes / 4);
+    hipk::tileQ40(qs.data(), d.data(), rows, n, m.lanes, qt.data(), dt.data());
+    m.qs = sc.upload(qt);
+    m.d = reinterpret_cast<uint16_t *>(sc.upload(dt));
+    return m;
+}
+
+void checkRows(const std::vector<float> &v, size_t want, const char *what) {
+    DL_CHECK(v.empty() || v.size() == want, std::string("ops: bad size of ") + what);
+}
+
+}  // namespace
+
+std::vector<float> gemvQ40(const std::vector<uint8_t> &blocks, int rows, int n, const std::vector<float> &in,
+                           const std::vector<float> &residual, const std::vector<float> &normW, float eps, int B,
+                           int epi, std::vector<float> *xNext) {
+    DL_CHECK(B == 1 || B == 2 || B == 4, "gemv batch must be 1, 2 or 4");
+    DL_CHECK(epi == 0 || (epi == 1 && rows % 2 == 0), "gemv epilogue");
+    DL_CHECK(in.size() == (size_t)B * n, "gemv input size");
+    checkRows(residual, (size_t)B * n, "residual");
+    checkRows(normW, (size_t)n, "norm weights");
+    Scratch sc;
+    const DevQ40 w = uploadQ40(sc, blocks, rows, n);
+    const int outRows = epi == 1 ? rows / 2 : rows;
+    hipk::GemvArgs a;
+    a.qs = w.qs;
+    a.wd = w.d;
+    a.rows = rows;
+    a.n = n;
+    a.lanes = w.lanes;
+    const int ep = epi == 1 ? hipk::EPI_ACT : hipk::EPI_STORE;
+    a.passes = hipk::gemvDefaultPasses(n, rows, B, true, ep);
+    a.in = sc.upload(in);
+    a.ldIn = n;
+    a.addIn = sc.upload(residual);
+    a.xNext = residual.empty() ? nullptr : sc.alloc<float>((size_t)B * n);
+    a.normW = sc.upload(normW);
+    a.eps = eps;
+    a.out = sc.alloc<float>((size_t)B * outRows);
+    a.ldOut = outRows;
+    a.act = 1;
+    const size_t lds = hipk::gemvLdsBytes(n, B, true, hipk::gemvRowsPerPass(n, rows, B, true) * a.passes,
+                                          hipk::PRO_RESNORM);
+    DL_CHECK(B == 1 || lds <= 64 * 1024, "gemv LDS footprint too large for this batch");
+    hipk::launchGemv(a, B, hipk::PRO_RESNORM, ep, true, sc.s);
+    sc.sync();
+    if (xNext && a.xNext) *xNext = sc.download(a.xNext, (size_t)B * n);
+    return sc.download(a.out, (size_t)B * outRows);
+}
+
+std::vector<float> gemvQ40Q80In(const std::vector<uint8_t> &blocks, int rows, int n, const std::vector<float> &in,
+                                int B) {
+    DL_CHECK(B == 1 || B == 2 || B == 4, "gemv batch must be 1, 2 or 4");
+    DL_CHECK(in.size() == (size_t)B * n, "gemv input size");
+    Scratch sc;
+    const DevQ40 w = uploadQ40(sc, blocks, rows, n);
+    // host Q80 (the reference quantizer) -> int8 codes + (d, sum of codes) per block, as the
+    // attention / SwiGLU epilogues hand them to this kernel
+    const int nb = n / 32;
+    std::vector<BlockQ80> q((size_t)B * nb);
+    quantizeQ80(in.data(), q.data(), (u64)B * n);
+    std::vector<int8_t> codes((size_t)B * n);
+    std::vector<float> scales((size_t)B * nb * 2);
+    for (size_t i = 0; i < q.size(); i++) {
+        int s = 0;
+        for (int j = 0; j < 32; j++) {
+            codes[i * 32 + j] = q[i].qs[j];
+            s += q[i].qs[j];
+        }
+        scales[2 * i] = f16ToF32(q[i].d);
+        scales[2 * i + 1] = (float)s;
+    }
+    hipk::GemvArgs a;
+    a.qs = w.qs;
+    a.wd = w.d;
+    a.rows = rows;
+    a.n = n;
+    a.lanes = w.lanes;
+    a.passes = hipk::gemvDefaultPasses(n, rows, B, true, hipk::EPI_STORE);
+    a.aq = sc.upload(codes);
+    a.as = reinterpret_cast<const float2 *>(sc.upload(scales));
+    a.out = sc.alloc<float>((size_t)B * rows);
+    a.ldOut = rows;
+    hipk::launchGemv(a, B, hipk::PRO_GLOBAL, hipk::EPI_STORE, true, sc.s);
+    sc.sync();
+    return sc.download(a.out, (size_t)B * rows);
+}
+
+std::vector<float> gemmQ40(const std::vector<uint8_t> &blocks, int rows, int n, const std::vector<float> &in,
+                           const std::vector<float> &residual, const std::vector<float> &normW, float eps, int M) {
+    DL_CHECK(M >= 1 && M <= 32, "gemm tokens must be 1..32");
+    DL_CHECK(in.size() == (size_t)M * n, "gemm input size");
+    checkRows(residual, (size_t)M * n, "residual");
+    checkRows(normW, (size_t)n, "norm weights");
+    Scratch sc;
+    const DevQ40 w = uploadQ40(sc, blocks, rows, n);
+    hipk::GemvArgs nq;
+    nq.n = n;
+    nq.in = sc.upload(in);
+    nq.ldIn = n;
+    nq.addIn = sc.upload(residual);
+    nq.normW = sc.upload(normW);
+    nq.eps = eps;
+    _Float16 *xh = sc.alloc<_Float16>((size_t)((M + 15) / 16 * 16) * n);  // rows past M read as zeros
+    hipk::launchNormF16(nq, xh, M, sc.s);
+    hipk::GemmArgs g;
+    g.e.qs = w.qs;
+    g.e.wd = w.d;
+    g.e.rows = rows;
+    g.e.n = n;
+    g.e.lanes = w.lanes;
+    g.e.out = sc.alloc<float>((size_t)M * rows);
+    g.e.ldOut = rows;
+    g.x = xh;
+    g.M = M;
+    g.splits = hipk::gemmSplits(rows, n);
+    const size_t part = hipk::gemmPartFloats(rows, n, M);
+    g.part = part ? sc.alloc<float>(part) : nullptr;
+    g.counters = sc.alloc<int>((size_t)(rows + 63) / 64 + 1);
+    hipk::launchGemmQ40(g, hipk::EPI_STORE, sc.s);
+    sc.sync();
+    return sc.download(g.e.out, (size_t)M * rows);
+}
+
+std::vector<float> qkvRope(const std::vector<uint8_t> &blocks, int q0, int kv0, int hs, int n,
+                           const std::vector<float> &in, const std::vector<float> &normW, float eps,
+                           const std::vector<float> &rope, int seqLen, const std::vector<int> &pos, bool kvBf16,
+                           std::vector<float> *kOut, std::vector<float> *vOut) {
+    const int B = (int)pos.size(), rows = q0 + 2 * kv0;
+    DL_CHECK(B == 1 || B == 2 || B == 4, "qkv batch must be 1, 2 or 4");
+    DL_CHECK(hs % 2 == 0 && hs <= 128 && q0 % hs == 0 && kv0 % hs == 0, "qkv head layout");
+    DL_CHECK(in.size() == (size_t)B * n && rope.size() == (size_t)seqLen * hs, "qkv operand sizes");
+    checkRows(normW, (size_t)n, "norm weights");
+    for (int p : pos) DL_CHECK(p >= 0 && p < seqLen, "qkv position out of range");
+    Scratch sc;
+    const DevQ40 w = uploadQ40(sc, blocks, rows, n);
+    std::vector<int> slots(B);
+    for (int b = 0; b < B; b++) slots[b] = b;
+    const size_t cacheElems = (size_t)B * seqLen * kv0;
+    void *kc = kvBf16 ? (void *)sc.alloc<uint16_t>(cacheElems) : (void *)sc.alloc<float>(cacheElems);
+    void *vc = kvBf16 ? (void *)sc.alloc<uint16_t>(cacheElems) : (void *)sc.alloc<float>(cacheElems);
+    hipk::GemvArgs a;
+    a.qs = w.qs;
+    a.wd = w.d;
+    a.rows = rows;
+    a.n = n;
+    a.lanes = w.lanes;
+    a.passes = hipk::gemvDefaultPasses(n, rows, B, true, hipk::EPI_QKV);
+    a.in = sc.upload(in);
+    a.ldIn = n;
+    a.normW = sc.upload(normW);
+    a.eps = eps;
+    a.out = sc.alloc<float>((size_t)B * q0);
+    a.ldOut = q0;
+    a.q0 = q0;
+    a.kv0 = kv0;
+    a.hs = hs;
+    a.seqLen = seqLen;
+    a.rope = reinterpret_cast<const float2 *>(sc.upload(rope));
+    a.pos = sc.upload(pos);
+    a.slot = sc.upload(slots);
+    a.kcache = kc;
+    a.vcache = vc;
+    a.kvBf16 = kvBf16 ? 1 : 0;
+    hipk::launchGemv(a, B, hipk::PRO_RESNORM, hipk::EPI_QKV, true, sc.s);
+    sc.sync();
+    auto row = [&](void *cache, int b) {
+        std::vector<float> r(kv0);
+        const size_t off = ((size_t)b * seqLen + pos[b]) * kv0;
+        if (kvBf16) {
+            const std::vector<uint16_t> h = sc.download(static_cast<uint16_t *>(cache) + off, kv0);
+            for (int i = 0; i < kv0; i++) {
+                const uint32_t u = (uint32_t)h[i] << 16;
+                std::memcpy(&r[i], &u, 4);
+            }
+        } else {
+            r = sc.download(static_cast<float *>(cache) + off, kv0);
+        }
+        return r;
+    };
+    if (kOut) kOut->clear();
+    if (vOut) vOut->clear();
+    for (int b = 0; b < B; b++) {
+        if (kOut) {
+            const std::vector<float> r = row(kc, b);
+            kOut->insert(kOut->end(), r.begin(), r.end());
+        }
+        if (vOut) {
+            const std::vector<float> r = row(vc, b);
+            vOut->insert(vOut->end(), r.begin(), r.end());
+        }
+    }
+    return sc.download(a.out, (size_t)B * q0);
+}
+
+std::vector<float> attention(const std::vector<float> &q, const std::vector<float> &k, const std::vector<float> &v,
+                             int nSlots, int seqLen, int nHeads0, int kvMul, int hs, const std::vector<int> &pos,
+                             const std::vector<int> &slot, bool kvBf16) {
+    const int B = (int)pos.size();
+    DL_CHECK(B >= 1 && slot.size() == pos.size(), "attention rows");
+    DL_CHECK(kvMul >= 1 && nHeads0 % kvMul == 0 && (hs == 64 || hs == 128), "attention head layout");
+    const int q0 = nHeads0 * hs, kv0 = nHeads0 / kvMul * hs;
+    const size_t cacheElems = (size_t)nSlots * seqLen * kv0;
+    DL_CHECK(q.size() == (size_t)B * q0 && k.size() == cacheElems && v.size() == cacheElems, "attention sizes");
+    for (int b = 0; b < B; b++)
+        DL_CHECK(pos[b] >= 0 && pos[b] < seqLen && slot[b] >= 0 && slot[b] < nSlots, "attention row out of range");
+    Scratch sc;
+    auto cache = [&](const std::vector<float> &x) -> void * {
+        if (!kvBf16) return sc.upload(x);
+        std::vector<uint16_t> h(x.size());
+        for (size_t i = 0; i < x.size(); i++) {  // round to nearest even, as the QKV epilogue stores
+            uint32_t u;
+            std::memcpy(&u, &x[i], 4);
+            h[i] = (uint16_t)((u + 0x7FFF + ((u >> 16) & 1)) >> 16);
+        }
+        return sc.upload(h);
+    };
+    hipk::AttnArgs a;
+    a.q = sc.upload(q);
+    a.ldq = q0;
+    a.kcache = cache(k);
+    a.vcache = cache(v);
+    a.pos = sc.upload(pos);
+    a.slot = sc.upload(slot);
+    a.nHeads0 = nHeads0;
+    a.kvMul = kvMul;
+    a.hs = hs;
+    a.kv0 = kv0;
+    a.seqLen = seqLen;
+    a.splitGrid = hipk::attnSplitGrid(seqLen);
+    a.chunkMax = hipk::attnChunkMax(seqLen, a.splitGrid);
+    a.partO = sc.alloc<float>((size_t)B * nHeads0 * a.splitGrid * hs);
+    a.partML = sc.alloc<float>((size_t)B * nHeads0 * a.splitGrid * 2);
+    a.out = sc.alloc<float>((size_t)B * q0);
+    a.ldOut = q0;
+    a.kvBf16 = kvBf16 ? 1 : 0;
+    a.counters = sc.alloc<int>((size_t)B * nHeads0);
+    hipk::launchAttention(a, B, sc.s);
+    sc.sync();
+    return sc.download(a.out, (size_t)B * q0);
+}
+
+std::vector<int> argmax(const std::vector<float> &logits, int B, int vocab) {
+    DL_CHECK(B >= 1 && vocab >= 1 && logits.size() == (size_t)B * vocab, "argmax sizes");
+    Scratch sc;
+    hipk::ArgmaxArgs g;
+    g.logits = sc.upload(logits);
+    g.vocab = vocab;
+    g.ids = sc.alloc<int>(B);
+    g.partV = sc.alloc<float>((size_t)B * 64);
+    g.partI = sc.alloc<int>((size_t)B * 64);
+    g.counters = sc.alloc<int>(B);
+    hipk::launchArgmax(g, B, sc.s);
+    sc.sync();
+    return sc.download(g.ids, B);
+}
+
+std::vector<float> embedding(const std::vector<float> &table, int vocab, int dim, const std::vector<int> &tokens) {
+    const int B = (int)tokens.size();
+    DL_CHECK(dim % 4 == 0 && table.size() == (size_t)vocab * dim, "embedding sizes");
+    for (int t : tokens) DL_CHECK(t >= 0 && t < vocab, "embedding token out of range");
+    Scratch sc;
+    const float *tab = sc.upload(table);
+    const int *tok = sc.upload(tokens);
+    float *x = sc.alloc<float>((size_t)B * dim);
+    hipk::launchEmbedding(tab, tok, x, dim, B, sc.s);
+    sc.sync();
+    return sc.download(x, (size_t)B * dim);
+}
+
+}  // namespace ops
+}  // namespace dl

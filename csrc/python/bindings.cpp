@@ -10,6 +10,7 @@
 #include "../core/plan.h"
 #include "../core/quant.h"
 #include "../hip/engine.h"
+#include "../hip/ops.h"
 #include "../runtime/backend.h"
 #include "../runtime/weight_stream.h"
 #include "../text/tokenizer.h"
@@ -130,10 +131,126 @@ struct PyHipEngine {
     std::unique_ptr<HipEngine> engine;
 };
 
+
+template <typename T>
+std::vector<T> vec(const py::object &o) {  // None -> empty
+    if (o.is_none()) return {};
+    py::array_t<T, py::array::c_style | py::array::forcecast> a(o);
+    return std::vector<T>(a.data(), a.data() + a.size());
+}
+
+template <typename T>
+py::array_t<T> arr(const std::vector<T> &v, std::vector<py::ssize_t> shape) {
+    py::array_t<T> a(shape);
+    DL_CHECK((size_t)a.size() == v.size(), "result shape");
+    std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+    return a;
+}
+
+void bindOps(py::module_ &m) {
+    // every py::object is converted to a std::vector while the GIL is held; only the device work
+    // runs with it released
+    py::module_ o = m.def_submodule("ops", "single-kernel entry points (csrc/hip/ops.h) for numerics tests");
+    o.def("gemv_q40",
+          [](py::object blocks, int rows, int n, py::object x, py::object residual, py::object normW, float eps, int epi) {
+              const std::vector<uint8_t> w = vec<uint8_t>(blocks);
+              const std::vector<float> in = vec<float>(x), res = vec<float>(residual), nw = vec<float>(normW);
+              const int B = (int)(in.size() / n);
+              std::vector<float> out, xn;
+              {
+                  py::gil_scoped_release rel;
+                  out = ops::gemvQ40(w, rows, n, in, res, nw, eps, B, epi, &xn);
+              }
+              py::object xo = py::none();
+              if (!xn.empty()) xo = arr(xn, {B, n});
+              return py::make_tuple(arr(out, {B, (py::ssize_t)(out.size() / B)}), xo);
+          },
+          py::arg("blocks"), py::arg("rows"), py::arg("n"), py::arg("x"), py::arg("residual") = py::none(),
+          py::arg("norm_w") = py::none(), py::arg("eps") = 1e-5f, py::arg("epi") = 0);
+    o.def("gemv_q40_q80_in",
+          [](py::object blocks, int rows, int n, py::object x) {
+              const std::vector<uint8_t> w = vec<uint8_t>(blocks);
+              const std::vector<float> in = vec<float>(x);
+              const int B = (int)(in.size() / n);
+              std::vector<float> out;
+              {
+                  py::gil_scoped_release rel;
+                  out = ops::gemvQ40Q80In(w, rows, n, in, B);
+              }
+              return arr(out, {B, rows});
+          },
+          py::arg("blocks"), py::arg("rows"), py::arg("n"), py::arg("x"));
+    o.def("gemm_q40",
+          [](py::object blocks, int rows, int n, py::object x, py::object residual, py::object normW, float eps) {
+              const std::vector<uint8_t> w = vec<uint8_t>(blocks);
+              const std::vector<float> in = vec<float>(x), res = vec<float>(residual), nw = vec<float>(normW);
+              const int M = (int)(in.size() / n);
+              std::vector<float> out;
+              {
+                  py::gil_scoped_release rel;
+                  out = ops::gemmQ40(w, rows, n, in, res, nw, eps, M);
+              }
+              return arr(out, {M, rows});
+          },
+          py::arg("blocks"), py::arg("rows"), py::arg("n"), py::arg("x"), py::arg("residual") = py::none(),
+          py::arg("norm_w") = py::none(), py::arg("eps") = 1e-5f);
+    o.def("qkv_rope",
+          [](py::object blocks, int q0, int kv0, int hs, int n, py::object x, py::object normW, float eps, py::object rope,
+             int seqLen, std::vector<int> pos, bool kvBf16) {
+              const std::vector<uint8_t> w = vec<uint8_t>(blocks);
+              const std::vector<float> in = vec<float>(x), nw = vec<float>(normW), rp = vec<float>(rope);
+              std::vector<float> k, v, q;
+              {
+                  py::gil_scoped_release rel;
+                  q = ops::qkvRope(w, q0, kv0, hs, n, in, nw, eps, rp, seqLen, pos, kvBf16, &k, &v);
+              }
+              const py::ssize_t B = (py::ssize_t)pos.size();
+              return py::make_tuple(arr(q, {B, q0}), arr(k, {B, kv0}), arr(v, {B, kv0}));
+          },
+          py::arg("blocks"), py::arg("q0"), py::arg("kv0"), py::arg("head_size"), py::arg("n"), py::arg("x"),
+          py::arg("norm_w"), py::arg("eps"), py::arg("rope"), py::arg("seq_len"), py::arg("pos"), py::arg("kv_bf16") = true);
+    o.def("attention",
+          [](py::object q, py::object k, py::object v, int nSlots, int seqLen, int nHeads0, int kvMul, int hs,
+             std::vector<int> pos, std::vector<int> slot, bool kvBf16) {
+              const std::vector<float> qv = vec<float>(q), kv = vec<float>(k), vv = vec<float>(v);
+              std::vector<float> out;
+              {
+                  py::gil_scoped_release rel;
+                  out = ops::attention(qv, kv, vv, nSlots, seqLen, nHeads0, kvMul, hs, pos, slot, kvBf16);
+              }
+              return arr(out, {(py::ssize_t)pos.size(), (py::ssize_t)nHeads0 * hs});
+          },
+          py::arg("q"), py::arg("k"), py::arg("v"), py::arg("n_slots"), py::arg("seq_len"), py::arg("n_heads0"),
+          py::arg("kv_mul"), py::arg("head_size"), py::arg("pos"), py::arg("slot"), py::arg("kv_bf16") = true);
+    o.def("argmax",
+          [](py::object logits, int B) {
+              const std::vector<float> l = vec<float>(logits);
+              std::vector<int> ids;
+              {
+                  py::gil_scoped_release rel;
+                  ids = ops::argmax(l, B, (int)(l.size() / B));
+              }
+              return ids;
+          },
+          py::arg("logits"), py::arg("batch"));
+    o.def("embedding",
+          [](py::object table, int vocab, int dim, std::vector<int> tokens) {
+              const std::vector<float> t = vec<float>(table);
+              std::vector<float> out;
+              {
+                  py::gil_scoped_release rel;
+                  out = ops::embedding(t, vocab, dim, tokens);
+              }
+              return arr(out, {(py::ssize_t)tokens.size(), dim});
+          },
+          py::arg("table"), py::arg("vocab"), py::arg("dim"), py::arg("tokens"));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
     m.doc() = "MI355X-native distributed Llama engine (native core)";
+    bindOps(m);
     m.def("set_log_level", &setLogLevel);
     m.def("hip_device_count", &hipDeviceCount);
 
