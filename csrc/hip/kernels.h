@@ -43,6 +43,29 @@ Q40Tiling q40Tiling(int rows, int n, int L);
 // Host repack of row-major SoA blocks (qs [rows][nb][16], d [rows][nb] f16) into the tiled layout.
 void tileQ40(const uint8_t *qs, const uint16_t *d, int rows, int n, int L, uint8_t *qsOut, uint32_t *dOut);
 
+struct AttnArgs {
+    const float *q = nullptr;   // [B][ldq], rotated queries
+    int ldq = 0;
+    const void *kcache = nullptr, *vcache = nullptr;  // layer base [slot][seqLen][kv0]
+    const int *pos = nullptr, *slot = nullptr;
+    int nHeads0 = 0, kvMul = 1, hs = 0, kv0 = 0, seqLen = 0;
+    int splitGrid = 1;          // max sequence splits (grid.y)
+    int chunkMax = 256;         // LDS capacity in positions per split
+    float *partO = nullptr;     // [B][nHeads0][splitGrid][hs]
+    float *partML = nullptr;    // [B][nHeads0][splitGrid][2]
+    float *out = nullptr;       // [B][ldOut] f32 output (when outQ and outH are null)
+    _Float16 *outH = nullptr;   // [B][ldOut] f16 output (batched path)
+    int8_t *outQ = nullptr;     // [B][ldOut] Q80 output (+ outS [B][ldOut/32])
+    float2 *outS = nullptr;
+    int ldOut = 0;
+    int kvBf16 = 1;
+    int *counters = nullptr;    // [B][nHeads0/HG] arrival counters (zero-initialised, self-resetting)
+    // optional MALL warm-up run by extra workgroups of the same launch (weights of the next GEMVs)
+    const void *pf0 = nullptr, *pf1 = nullptr;
+    size_t pf0Bytes = 0, pf1Bytes = 0;
+    int pfBlocks = 0;
+};
+
 struct GemvArgs {
     // weights: Q40 tiled (see Q40Tiling; `lanes` must be the tiling's L) or F32 [rows][n]
     const uint8_t *qs = nullptr;
@@ -114,28 +137,6 @@ size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg, int pro);
 // resident at once (DL_GEMV_RESIDENT workgroups, default 512); ACT_Q80 -> whole Q80 blocks per WG.
 int gemvDefaultPasses(int n, int rows, int B, bool q40, int epi);
 
-struct AttnArgs {
-    const float *q = nullptr;   // [B][ldq], rotated queries
-    int ldq = 0;
-    const void *kcache = nullptr, *vcache = nullptr;  // layer base [slot][seqLen][kv0]
-    const int *pos = nullptr, *slot = nullptr;
-    int nHeads0 = 0, kvMul = 1, hs = 0, kv0 = 0, seqLen = 0;
-    int splitGrid = 1;          // max sequence splits (grid.y)
-    int chunkMax = 256;         // LDS capacity in positions per split
-    float *partO = nullptr;     // [B][nHeads0][splitGrid][hs]
-    float *partML = nullptr;    // [B][nHeads0][splitGrid][2]
-    float *out = nullptr;       // [B][ldOut] f32 output (when outQ and outH are null)
-    _Float16 *outH = nullptr;   // [B][ldOut] f16 output (batched path)
-    int8_t *outQ = nullptr;     // [B][ldOut] Q80 output (+ outS [B][ldOut/32])
-    float2 *outS = nullptr;
-    int ldOut = 0;
-    int kvBf16 = 1;
-    int *counters = nullptr;    // [B][nHeads0/HG] arrival counters (zero-initialised, self-resetting)
-    // optional MALL warm-up run by extra workgroups of the same launch (weights of the next GEMVs)
-    const void *pf0 = nullptr, *pf1 = nullptr;
-    size_t pf0Bytes = 0, pf1Bytes = 0;
-    int pfBlocks = 0;
-};
 void launchAttention(const AttnArgs &a, int B, hipStream_t s);
 int attnSplitGrid(int seqLen);
 int attnChunkMax(int seqLen, int splitGrid);

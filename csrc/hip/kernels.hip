@@ -17,6 +17,7 @@
 #include "device_common.h"
 #include "kernels.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -391,6 +392,16 @@ __device__ __forceinline__ void stageQ80(const GemvArgs &a, int8_t *sq, float2 *
         for (int i = threadIdx.x; i < nb; i += kThreads) ssc[b * nb + i] = a.as[(size_t)b * nb + i];
     }
     __syncthreads();
+}
+
+// Sequence split of a decode-attention row of length `len`: nSplit chunks of ch positions
+// (~256 per chunk, at most splitGrid chunks).
+__device__ __forceinline__ void attnSplit(int len, int splitGrid, int &nSplit, int &ch) {
+    int ns = (len + 255) / 256;
+    if (ns > splitGrid) ns = splitGrid;
+    if (ns < 1) ns = 1;
+    ch = (((len + ns - 1) / ns) + 15) & ~15;
+    nSplit = (len + ch - 1) / ch;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1170,13 +1181,6 @@ int attnChunkMax(int seqLen, int splitGrid) {
     return ((per + 15) / 16) * 16 + 16;
 }
 
-__device__ __forceinline__ void attnSplit(int len, int splitGrid, int &nSplit, int &ch) {
-    int ns = (len + 255) / 256;
-    if (ns > splitGrid) ns = splitGrid;
-    if (ns < 1) ns = 1;
-    ch = (((len + ns - 1) / ns) + 15) & ~15;
-    nSplit = (len + ch - 1) / ch;
-}
 
 template <int DPL, bool BF16>
 __device__ __forceinline__ void loadKv(const void *base, size_t off, float (&v)[DPL]) {
@@ -1255,14 +1259,14 @@ static constexpr int kAttnThreads = 512;  // 8 waves = 32 groups of 16 lanes, on
 // keeps 8 partial-output loads in flight per thread: a serial loop over the chunks costs one
 // cross-XCD round trip per chunk (~30 us at 32 chunks).
 template <int HG, int HS, int AT>
-__device__ __forceinline__ void attnFinish(const AttnArgs &a, int b, int head0, int c, int nSplit, float *redL,
+__device__ __forceinline__ bool attnFinish(const AttnArgs &a, int b, int hgIdx, int c, int nSplit, float *redL,
                                            float *mlL, int *flagL, float *scratch) {
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, head0 = hgIdx * HG;
     if (nSplit == 1) {
         for (int i = tid; i < HG * HS; i += AT) redL[i] = redL[i] / mlL[(i / HS) * 2 + 1];
         __syncthreads();
         attnWriteOut<HG, HS, AT>(a, b, head0, redL);
-        return;
+        return true;
     }
     const int G = a.splitGrid;
     const size_t pbase = ((size_t)b * a.nHeads0 + head0) * G;  // [HG][G] chunks of this head group
@@ -1276,7 +1280,7 @@ __device__ __forceinline__ void attnFinish(const AttnArgs &a, int b, int head0, 
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    int *cnt = a.counters + (size_t)b * (a.nHeads0 / HG) + blockIdx.x;
+    int *cnt = a.counters + (size_t)b * (a.nHeads0 / HG) + hgIdx;
     if (tid == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1284,7 +1288,7 @@ __device__ __forceinline__ void attnFinish(const AttnArgs &a, int b, int head0, 
         flagL[0] = old == nSplit - 1;
     }
     __syncthreads();
-    if (!flagL[0]) return;
+    if (!flagL[0]) return false;
     if (tid == 0) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1331,51 +1335,26 @@ __device__ __forceinline__ void attnFinish(const AttnArgs &a, int b, int head0, 
     }
     __syncthreads();
     attnWriteOut<HG, HS, AT>(a, b, head0, redL);
+    return true;
 }
 
-template <int HG, int HS, bool BF16>
-__global__ __launch_bounds__(kAttnThreads) void attnKernel(AttnArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int AT = kAttnThreads, NW = AT / 64, NG = AT / 16;
+// One attention task: query heads [hgIdx*HG, +HG) of row b over sequence chunk c, AT threads.
+// Returns true when this call wrote the head group's final output (single chunk, or the last
+// chunk to arrive combined all of them).
+template <int HG, int HS, bool BF16, int AT>
+__device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, int c, char *smem) {
+    constexpr int NW = AT / 64, NG = AT / 16;
     constexpr int DPL = HS / 16;           // dims per lane: 16 lanes cover one position's head vector
     constexpr int TU = BF16 ? 8 : 4;       // keys per group loaded before any is consumed
     constexpr int RW = BF16 ? DPL / 2 : DPL;  // 32-bit words per lane per key (packed bf16 pairs)
-    const int hgx = a.nHeads0 / HG;  // attention workgroups per (split, row) slice
-    if ((int)blockIdx.x >= hgx) {
-        // MALL warm-up role: every extra workgroup of every slice streams its share of the next
-        // GEMVs' weights with plain loads (allocating in the Infinity Cache) and discards them
-        const int pfx = gridDim.x - hgx;
-        const int id = (blockIdx.z * gridDim.y + blockIdx.y) * pfx + (blockIdx.x - hgx);
-        const int nPf = pfx * gridDim.y * gridDim.z;
-        typedef unsigned int u32x4l __attribute__((ext_vector_type(4)));
-        const size_t n0 = a.pf0Bytes / 16, n1 = a.pf1Bytes / 16, tot = n0 + n1;
-        const size_t per = (tot + nPf - 1) / nPf;
-        const size_t i0 = (size_t)id * per, i1 = min(i0 + per, tot);
-        const u32x4l *p0 = reinterpret_cast<const u32x4l *>(a.pf0), *p1 = reinterpret_cast<const u32x4l *>(a.pf1);
-        u32x4l acc = {0u, 0u, 0u, 0u};
-        for (size_t i = i0 + threadIdx.x; i < i1; i += 4 * kAttnThreads) {
-            u32x4l v[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const size_t j = min(i + (size_t)u * kAttnThreads, i1 - 1);
-                v[u] = j < n0 ? p0[j] : p1[j - n0];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) acc ^= v[u];
-        }
-        asm volatile("" ::"v"(acc.x), "v"(acc.y), "v"(acc.z), "v"(acc.w));
-        return;
-    }
-    const int b = blockIdx.z;
     const int pos = a.pos[b], sl = a.slot[b];
     const int len = pos + 1;
     int nSplit, ch;
     attnSplit(len, a.splitGrid, nSplit, ch);
-    const int c = blockIdx.y;
-    if (c >= nSplit) return;
+    if (c >= nSplit) return false;
     const int t0 = c * ch;
     const int t1 = min(t0 + ch, len);
-    const int head0 = blockIdx.x * HG;
+    const int head0 = hgIdx * HG;
     const int kvh = head0 / a.kvMul;
     const int tid = threadIdx.x, wave = tid / 64, lane = tid % 64;
     const int g16 = tid / 16, l16 = tid % 16;
@@ -1519,7 +1498,39 @@ __global__ __launch_bounds__(kAttnThreads) void attnKernel(AttnArgs a) {
     }
     __syncthreads();
 
-    attnFinish<HG, HS, AT>(a, b, head0, c, nSplit, redL, mlL, flagL, oW);
+    return attnFinish<HG, HS, AT>(a, b, hgIdx, c, nSplit, redL, mlL, flagL, oW);
+}
+
+template <int HG, int HS, bool BF16>
+__global__ __launch_bounds__(kAttnThreads) void attnKernel(AttnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int hgx = a.nHeads0 / HG;  // attention workgroups per (split, row) slice
+    if ((int)blockIdx.x >= hgx) {
+        // MALL warm-up role: every extra workgroup of every slice streams its share of the next
+        // GEMVs' weights with plain loads (allocating in the Infinity Cache) and discards them
+        const int pfx = gridDim.x - hgx;
+        const int id = (blockIdx.z * gridDim.y + blockIdx.y) * pfx + (blockIdx.x - hgx);
+        const int nPf = pfx * gridDim.y * gridDim.z;
+        typedef unsigned int u32x4l __attribute__((ext_vector_type(4)));
+        const size_t n0 = a.pf0Bytes / 16, n1 = a.pf1Bytes / 16, tot = n0 + n1;
+        const size_t per = (tot + nPf - 1) / nPf;
+        const size_t i0 = (size_t)id * per, i1 = min(i0 + per, tot);
+        const u32x4l *p0 = reinterpret_cast<const u32x4l *>(a.pf0), *p1 = reinterpret_cast<const u32x4l *>(a.pf1);
+        u32x4l acc = {0u, 0u, 0u, 0u};
+        for (size_t i = i0 + threadIdx.x; i < i1; i += 4 * kAttnThreads) {
+            u32x4l v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const size_t j = min(i + (size_t)u * kAttnThreads, i1 - 1);
+                v[u] = j < n0 ? p0[j] : p1[j - n0];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) acc ^= v[u];
+        }
+        asm volatile("" ::"v"(acc.x), "v"(acc.y), "v"(acc.z), "v"(acc.w));
+        return;
+    }
+    attnTask<HG, HS, BF16, kAttnThreads>(a, blockIdx.z, blockIdx.x, blockIdx.y, smem);
 }
 
 template <int HS, bool BF16>
