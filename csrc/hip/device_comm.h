@@ -23,6 +23,12 @@ class DeviceComm {
     virtual void allGather(const float *send, float *recv, size_t nPerRank, hipStream_t s) = 0;
     virtual void broadcastInts(int *buf, size_t n, int root, hipStream_t s) = 0;
     virtual std::string name() const = 0;
+    // Health reporting: device int set non-zero when a collective stopped waiting
+    // for a peer (null if the transport has none), and the transport's host-side error text.
+    virtual const int *deviceErrorFlag() const { return nullptr; }
+    virtual std::string asyncError() { return ""; }
+    // Release the communicator without waiting for peers (used after an error).
+    virtual void shutdownNow() {}
 };
 
 // 128-byte RCCL unique id (generated on rank 0, distributed over the control plane).

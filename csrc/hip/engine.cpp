@@ -106,7 +106,7 @@ class HipEngineImpl : public HipEngine {
             DL_HIP(hipMemcpyAsync(hLogits_, src, (size_t)n * h_.vocabSize * sizeof(float), hipMemcpyDeviceToHost,
                                   stream_));
         }
-        DL_HIP(hipStreamSynchronize(stream_));
+        syncAndCheckComm();
         if (root && logits) std::memcpy(logits, hLogits_, (size_t)n * h_.vocabSize * sizeof(float));
         stats_.computeMs = t.elapsedMs();
         stats_.syncMs = 0;
@@ -117,7 +117,7 @@ class HipEngineImpl : public HipEngine {
         setInputs(n, tokens, positions, slots);
         runGraph(n, GraphKind::ARGMAX);
         DL_HIP(hipMemcpyAsync(hIds_, dIds_, n * sizeof(int), hipMemcpyDeviceToHost, stream_));
-        DL_HIP(hipStreamSynchronize(stream_));
+        syncAndCheckComm();
         std::memcpy(out, hIds_, n * sizeof(int));
         stats_.computeMs = t.elapsedMs();
     }
@@ -144,6 +144,7 @@ class HipEngineImpl : public HipEngine {
         DL_HIP(hipEventElapsedTime(&ms, e0, e1));
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
+        syncAndCheckComm();
         if (outTokens) {
             std::vector<int> hist((size_t)cfg_.maxBatch * h_.seqLen);
             DL_HIP(hipMemcpy(hist.data(), dHist_, hist.size() * sizeof(int), hipMemcpyDeviceToHost));
@@ -179,6 +180,25 @@ class HipEngineImpl : public HipEngine {
   private:
     enum class GraphKind { LOGITS = 0, ARGMAX = 1, CHAIN = 2 };
 
+    // Wait for the stream, then turn a tensor-parallel transport failure into an exception (the
+    // worker loop re-serves, the root reports it) instead of returning results computed from a
+    // peer's stale data: the xGMI collectives flag a peer that did not arrive within 2 s, RCCL
+    // reports asynchronous errors (the communicator is then released without waiting).
+    void syncAndCheckComm() {
+        const int *flag = comm_ ? comm_->deviceErrorFlag() : nullptr;
+        if (flag) DL_HIP(hipMemcpyAsync(hErr_, flag, sizeof(int), hipMemcpyDeviceToHost, stream_));
+        DL_HIP(hipStreamSynchronize(stream_));
+        if (flag && *hErr_ != 0)
+            throw Error("tensor-parallel collective timed out: a peer rank did not arrive within 2 s (worker lost?)");
+        if (comm_) {
+            const std::string e = comm_->asyncError();
+            if (!e.empty()) {
+                comm_->shutdownNow();
+                throw Error("tensor-parallel transport failed: " + e);
+            }
+        }
+    }
+
     int rank() const { return comm_ ? comm_->rank() : 0; }
 
     template <typename T>
@@ -208,6 +228,8 @@ class HipEngineImpl : public HipEngine {
         dHist_ = dalloc<int>((size_t)MB * h_.seqLen);
         hIn_ = halloc<int>(3 * MB);
         hIds_ = halloc<int>(MB);
+        hErr_ = halloc<int>(1);
+        *hErr_ = 0;
         hLogits_ = halloc<float>((size_t)MB * h_.vocabSize);
         dX_[0] = dalloc<float>((size_t)MB * h_.dim);
         dX_[1] = dalloc<float>((size_t)MB * h_.dim);
@@ -800,7 +822,7 @@ class HipEngineImpl : public HipEngine {
     DevMat wcls_;
     float *emb_ = nullptr, *rmsFinal_ = nullptr;
     int *dTok_ = nullptr, *dPos_ = nullptr, *dSlot_ = nullptr, *dIds_ = nullptr, *dHist_ = nullptr;
-    int *hIn_ = nullptr, *hIds_ = nullptr;
+    int *hIn_ = nullptr, *hIds_ = nullptr, *hErr_ = nullptr;
     float *hLogits_ = nullptr;
     float *dX_[2] = {nullptr, nullptr};
     float *dY_ = nullptr, *dQ_ = nullptr, *dAtt_ = nullptr, *dH_ = nullptr, *dLogits_ = nullptr;

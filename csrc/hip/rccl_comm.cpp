@@ -33,6 +33,16 @@ class RcclComm : public DeviceComm {
     ~RcclComm() override {
         if (comm_) ncclCommDestroy(comm_);
     }
+    std::string asyncError() override {
+        if (!comm_) return "communicator released after an error";
+        ncclResult_t st = ncclSuccess;
+        if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) return "ncclCommGetAsyncError failed";
+        return st == ncclSuccess || st == ncclInProgress ? "" : std::string("RCCL async error: ") + ncclGetErrorString(st);
+    }
+    void shutdownNow() override {
+        if (comm_) (void)ncclCommAbort(comm_);
+        comm_ = nullptr;
+    }
     int rank() const override { return rank_; }
     int size() const override { return size_; }
     std::string name() const override { return "rccl"; }

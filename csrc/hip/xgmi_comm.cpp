@@ -189,6 +189,7 @@ class XgmiComm : public DeviceComm {
     void broadcastInts(int *, size_t, int, hipStream_t) override {
         throw Error("xgmi comm: broadcastInts is not used on the device data plane");
     }
+    const int *deviceErrorFlag() const override { return error_; }
     bool timedOut() {
         int v = 0;
         DL_HIP(hipMemcpy(&v, error_, sizeof(int), hipMemcpyDeviceToHost));
