@@ -80,6 +80,13 @@ static void inference(InferenceSession &sess, const AppArgs &args) {
     std::fflush(stdout);
 
     int token = input[nInput - 1];
+    if (args.profile) {
+        // eager replay of the next decode step with per-kernel-class device times (the KV row it
+        // writes is rewritten by the real step that follows)
+        const int slot = 0;
+        if (!sess.profileForward(1, &token, &pos, &slot))
+            std::printf("⏱️  --profile needs a single-process GPU run (--gpu-index, no --workers)\n");
+    }
     tok.resetDecoder();
     const int maxPos = (int)std::min<u32>(seqLen, (u32)args.steps);
     std::vector<float> logits;
@@ -178,6 +185,7 @@ static void usage() {
                  "  --chat-template {llama2|llama3|deepSeek3}\n"
                  "  --max-seq-len <n> --max-batch <n> --slots <n>\n"
                  "  --kv-dtype {bf16|f32} --graph {0|1} --log-level {0|1|2}\n"
+                 "  --metrics <file|->                  (JSON line per forward)  --profile 1  (GPU kernel table)\n"
                  "  --synthetic {llama3_2_1b|llama3_1_8b|llama3_3_70b|llama3_1_405b}  (random-init weights)\n"
                  "  --net-turbo {0|1} --gpu-segments <a:b>  (accepted for compatibility)\n");
 }

@@ -7,7 +7,8 @@
 //           {"id","object","created","model","choices":[...],"usage":{...}} fields;
 //           "stream": true -> server-sent events with chat.completion.chunk objects + [DONE]
 //   GET  /v1/models            {"object":"list","data":[{"id":<model file name>, ...}]}
-//   GET  /health               scheduler counters
+//   GET  /health               scheduler counters (JSON)
+//   GET  /v1/metrics           the same counters in Prometheus text format
 //   GET  /, /app.js, /style.css  the chat web UI (--web-ui <dir>, default ./web-ui when present)
 // Requests run concurrently (thread per connection); the scheduler batches them into shared forwards.
 #include <csignal>
@@ -172,6 +173,30 @@ struct Api {
         conn.writeJson(200, list.dump());
     }
 
+    // Prometheus text exposition of the scheduler counters (SURVEY §5.5 "GET /v1/metrics").
+    void metrics(const HttpRequest &, HttpConnection &conn, int connections) {
+        const SchedulerStats s = sched->stats();
+        std::string out;
+        auto metric = [&](const char *name, const char *type, const char *help, double v) {
+            char line[256];
+            std::snprintf(line, sizeof(line), "# HELP %s %s\n# TYPE %s %s\n%s %.17g\n", name, help, name, type, name, v);
+            out += line;
+        };
+        metric("dllama_forwards_total", "counter", "Batched forward passes run by the scheduler.", (double)s.forwards);
+        metric("dllama_rows_total", "counter", "Token rows processed (prefill + decode).", (double)s.rows);
+        metric("dllama_prefill_rows_total", "counter", "Prompt token rows prefilled.", (double)s.prefillRows);
+        metric("dllama_decode_rows_total", "counter", "Decode token rows.", (double)s.decodeRows);
+        metric("dllama_requests_completed_total", "counter", "Finished requests.", (double)s.completed);
+        metric("dllama_generated_tokens_total", "counter", "Tokens generated for finished requests.", (double)s.generatedTokens);
+        metric("dllama_busy_seconds_total", "counter", "Time spent in forward passes.", s.busyMs / 1000.0);
+        metric("dllama_active_requests", "gauge", "Requests holding a KV slot.", (double)s.active);
+        metric("dllama_queued_requests", "gauge", "Requests waiting for a KV slot.", (double)s.queued);
+        metric("dllama_kv_slots", "gauge", "KV-cache slots (max concurrent sequences).", (double)sess->nSlots());
+        metric("dllama_nodes", "gauge", "Tensor-parallel ranks.", (double)sess->nNodes());
+        metric("dllama_http_connections", "gauge", "Open HTTP connections.", (double)connections);
+        conn.writeResponse(200, "text/plain; version=0.0.4; charset=utf-8", out);
+    }
+
     void health(const HttpRequest &, HttpConnection &conn) {
         SchedulerStats s = sched->stats();
         Value v = Value::object();
@@ -226,7 +251,7 @@ void usage() {
                  "        [--nthreads <n>] [--gpu-index <i>]\n"
                  "        [--workers <ip:port> ...]\n"
                  "        [--temperature <temp>] [--topp <t>] [--seed <s>] [--chat-template <t>]\n"
-                 "        [--web-ui <dir>]\n");
+                 "        [--web-ui <dir>] [--metrics <file|->]\n");
 }
 
 }  // namespace
@@ -260,6 +285,8 @@ int main(int argc, char **argv) {
         server.route("POST", "/v1/chat/completions", [&](const HttpRequest &r, HttpConnection &c) { api.complete(r, c); });
         server.route("GET", "/v1/models", [&](const HttpRequest &r, HttpConnection &c) { api.models(r, c); });
         server.route("GET", "/health", [&](const HttpRequest &r, HttpConnection &c) { api.health(r, c); });
+        server.route("GET", "/v1/metrics",
+                     [&](const HttpRequest &r, HttpConnection &c) { api.metrics(r, c, server.activeConnections()); });
         std::string ui = args.webUi;
         std::string probe;
         if (ui.empty() && readFile("web-ui/index.html", probe)) ui = "web-ui";

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../core/quant.h"
+#include "../runtime/metrics.h"
 #include "kernels.h"
 
 namespace dl {
@@ -510,8 +511,9 @@ class HipEngineImpl : public HipEngine {
     struct ProfScope {
         HipEngineImpl *e;
         std::string name;
+        TraceRange trace;  // roctx range (DL_ROCTX=1): per kernel class in eager runs
         hipEvent_t a = nullptr, b = nullptr;
-        ProfScope(HipEngineImpl *e_, const char *n_) : e(e_), name(n_) {
+        ProfScope(HipEngineImpl *e_, const char *n_) : e(e_), name(n_), trace(n_) {
             if (e->profile_) {
                 (void)hipEventCreate(&a);
                 (void)hipEventCreate(&b);

@@ -23,6 +23,8 @@ Socket &Socket::operator=(Socket &&o) noexcept {
         fd_ = o.fd_;
         sent_ = o.sent_;
         recv_ = o.recv_;
+        totalSent_ = o.totalSent_;
+        totalRecv_ = o.totalRecv_;
         o.fd_ = -1;
     }
     return *this;
@@ -84,6 +86,7 @@ void Socket::sendAll(const void *data, u64 n) {
         p += s;
         n -= (u64)s;
         sent_ += (u64)s;
+        totalSent_ += (u64)s;
     }
 }
 
@@ -100,6 +103,7 @@ void Socket::recvAll(void *data, u64 n) {
         p += r;
         n -= (u64)r;
         recv_ += (u64)r;
+        totalRecv_ += (u64)r;
     }
 }
 

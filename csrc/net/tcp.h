@@ -27,7 +27,10 @@ class Socket {
     Socket() = default;
     explicit Socket(int fd) : fd_(fd) {}
     ~Socket();
-    Socket(Socket &&o) noexcept : fd_(o.fd_), sent_(o.sent_), recv_(o.recv_) { o.fd_ = -1; }
+    Socket(Socket &&o) noexcept
+        : fd_(o.fd_), sent_(o.sent_), recv_(o.recv_), totalSent_(o.totalSent_), totalRecv_(o.totalRecv_) {
+        o.fd_ = -1;
+    }
     Socket &operator=(Socket &&o) noexcept;
     Socket(const Socket &) = delete;
     Socket &operator=(const Socket &) = delete;
@@ -42,6 +45,9 @@ class Socket {
     u64 sentBytes() const { return sent_; }
     u64 recvBytes() const { return recv_; }
     void resetStats() { sent_ = recv_ = 0; }
+    // never reset (metrics deltas)
+    u64 totalSentBytes() const { return totalSent_; }
+    u64 totalRecvBytes() const { return totalRecv_; }
 
     template <typename T>
     void sendPod(const T &v) {
@@ -59,6 +65,7 @@ class Socket {
   private:
     int fd_ = -1;
     u64 sent_ = 0, recv_ = 0;
+    u64 totalSent_ = 0, totalRecv_ = 0;
 };
 
 class ServerSocket {

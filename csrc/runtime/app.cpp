@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include "../hip/engine.h"
+#include "metrics.h"
 #include "weight_stream.h"
 
 namespace dl {
@@ -72,6 +73,8 @@ AppArgs AppArgs::parse(int argc, char **argv, bool requireMode) {
         else if (name == "--web-ui") a.webUi = value;
         else if (name == "--stream-weights") a.streamWeights = std::atoi(value) != 0;
         else if (name == "--weights-cache") a.weightsCache = value;
+        else if (name == "--metrics") a.metricsPath = value;
+        else if (name == "--profile") a.profile = std::atoi(value) != 0;
         else throw Error("Unknown option: " + name);
     }
     setLogLevel(a.logLevel);
@@ -125,6 +128,7 @@ static std::unique_ptr<Backend> makeBackend(const EngineConfig &c, bool gpu, Hos
 }
 
 InferenceSession::InferenceSession(const AppArgs &args, int nSlots) : args_(args), nSlots_(nSlots) {
+    if (!args.metricsPath.empty()) MetricsSink::global().open(args.metricsPath);
     maxBatch_ = args.nBatches;
     gpu_ = args.gpuIndex >= 0 || !args.synthetic.empty();
     AppArgs a = args;
@@ -231,13 +235,46 @@ void InferenceSession::sendControl(Cmd cmd, int n, const int *tokens, const int 
 }
 
 void InferenceSession::forward(int n, const int *tokens, const int *positions, const int *slots, float *logits) {
+    TraceRange tr("dllama.forward");
+    Timer t;
     sendControl(Cmd::FORWARD, n, tokens, positions, slots);
     backend_->forward(n, tokens, positions, slots, logits);
+    recordMetrics("forward", n, t.elapsedMs());
 }
 
 void InferenceSession::forwardArgmax(int n, const int *tokens, const int *positions, const int *slots, int *out) {
+    TraceRange tr("dllama.forward_argmax");
+    Timer t;
     sendControl(Cmd::FORWARD_ARGMAX, n, tokens, positions, slots);
     backend_->forwardArgmax(n, tokens, positions, slots, out);
+    recordMetrics("forward_argmax", n, t.elapsedMs());
+}
+
+void InferenceSession::recordMetrics(const char *kind, int n, double ms) {
+    MetricsSink &m = MetricsSink::global();
+    if (!m.enabled()) return;
+    unsigned long long sent = 0, recv = 0;
+    for (auto &w : workers_) {
+        sent += w.totalSentBytes();
+        recv += w.totalRecvBytes();
+    }
+    const ForwardStats st = backend_->lastStats();
+    char buf[512];
+    std::snprintf(buf, sizeof(buf),
+                  "{\"ts_ms\":%.3f,\"event\":\"%s\",\"rows\":%d,\"ms\":%.4f,\"compute_ms\":%.4f,\"sync_ms\":%.4f,"
+                  "\"sent_bytes\":%llu,\"recv_bytes\":%llu,\"nodes\":%d,\"backend\":\"%s\"}",
+                  epochMs(), kind, n, ms, st.computeMs, st.syncMs, sent - mSent_, recv - mRecv_, nNodes(),
+                  gpu_ ? "hip" : "cpu");
+    mSent_ = sent;
+    mRecv_ = recv;
+    m.write(buf);
+}
+
+bool InferenceSession::profileForward(int n, const int *tokens, const int *positions, const int *slots) {
+    HipEngine *e = dynamic_cast<HipEngine *>(backend_.get());
+    if (!e || !workers_.empty()) return false;  // single-process GPU runs only
+    e->profileForward(n, tokens, positions, slots);
+    return true;
 }
 
 ForwardStats InferenceSession::lastStats() {

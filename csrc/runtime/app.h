@@ -2,7 +2,7 @@
 //
 // CLI parity with the reference (src/app.cpp:33-136; flag table SURVEY §5.6): every reference
 // flag is accepted with the same name and default; MI355X additions: --tp-gpus / --max-batch /
-// --slots / --kv-dtype / --graph / --log-level / --synthetic.
+// --slots / --kv-dtype / --graph / --log-level / --synthetic / --metrics / --profile.
 #pragma once
 
 #include <memory>
@@ -42,6 +42,8 @@ struct AppArgs {
     std::string webUi;                           // dllama-api: directory served at GET /
     bool streamWeights = false;                  // worker: always fetch slices from the root
     std::string weightsCache = "/tmp";           // worker: directory for streamed weight files
+    std::string metricsPath;                     // --metrics: JSON-lines sink ("-" = stderr)
+    bool profile = false;                        // --profile 1: per-kernel-class table (GPU, eager)
 
     static AppArgs parse(int argc, char **argv, bool requireMode);
 };
@@ -66,9 +68,12 @@ class InferenceSession {
     void forwardArgmax(int n, const int *tokens, const int *positions, const int *slots, int *out);
     ForwardStats lastStats();
     void finish();  // stop workers (they return to listening)
+    // GPU only: one eager forward of these rows with a per-kernel-class device-time table.
+    bool profileForward(int n, const int *tokens, const int *positions, const int *slots);
 
   private:
     void sendControl(Cmd cmd, int n, const int *tokens, const int *positions, const int *slots);
+    void recordMetrics(const char *kind, int n, double ms);
 
     AppArgs args_;
     int nSlots_, maxBatch_;
@@ -80,6 +85,7 @@ class InferenceSession {
     std::unique_ptr<Tokenizer> tokenizer_;
     std::unique_ptr<Sampler> sampler_;
     bool finished_ = false;
+    unsigned long long mSent_ = 0, mRecv_ = 0;  // control-plane bytes at the previous metrics record
 };
 
 // `dllama worker`: serve forever; a root disconnect returns to listening.

@@ -124,3 +124,17 @@ def test_launcher_writes_tp_script(tmp_path):
     assert script.count("build/dllama worker") == 3 and "--gpu-index 3" in script
     assert "--workers 127.0.0.1:9997 127.0.0.1:9996 127.0.0.1:9995" in script
     assert len(launch.MODELS["llama3_1_405b_instruct_q40"].urls) == 56
+
+
+def test_prometheus_metrics(server):
+    _chat(server, "metrics please", max_tokens=4)
+    text = urllib.request.urlopen(server + "/v1/metrics").read().decode()
+    vals = {}
+    for line in text.splitlines():
+        if line and not line.startswith("#"):
+            name, v = line.split()
+            vals[name] = float(v)
+    assert vals["dllama_requests_completed_total"] >= 1
+    assert vals["dllama_rows_total"] == vals["dllama_prefill_rows_total"] + vals["dllama_decode_rows_total"]
+    assert vals["dllama_generated_tokens_total"] >= 1 and vals["dllama_kv_slots"] == 4
+    assert "# TYPE dllama_forwards_total counter" in text

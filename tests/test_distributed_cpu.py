@@ -174,3 +174,19 @@ def test_too_many_nodes_rejected(assets):
     finally:
         for p in procs:
             p.kill()
+
+
+def test_metrics_jsonl_per_forward(kv4, tmp_path):
+    import json
+    procs, addrs = _workers(1)
+    path = tmp_path / "m.jsonl"
+    try:
+        rc, out = _inference(kv4, addrs, steps=10, extra=("--metrics", str(path)))
+    finally:
+        for p in procs:
+            p.kill()
+    assert rc == 0, out
+    recs = [json.loads(l) for l in path.read_text().splitlines()]
+    assert recs and all(r["event"] == "forward_argmax" and r["nodes"] == 2 and r["backend"] == "cpu" for r in recs)
+    assert sum(r["rows"] for r in recs) == 10  # one row per position 0..steps-1
+    assert all(r["sent_bytes"] > 0 and r["recv_bytes"] > 0 and r["ms"] >= r["sync_ms"] for r in recs)
