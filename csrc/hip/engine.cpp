@@ -304,11 +304,16 @@ class HipEngineImpl : public HipEngine {
     static void repackRowsQ40(const u8 *src, u32 cols, u32 r0, u32 nr, u32 c0, u32 nc, std::vector<u8> &qs,
                               std::vector<u16> &d) {
         const u32 nbAll = cols / kQBlock, nb0 = c0 / kQBlock, nb = nc / kQBlock;
-        for (u32 r = r0; r < r0 + nr; r++) {
-            const BlockQ40 *row = reinterpret_cast<const BlockQ40 *>(src) + (u64)r * nbAll + nb0;
+        const size_t q0 = qs.size(), d0 = d.size();
+        qs.resize(q0 + (size_t)nr * nb * 16);
+        d.resize(d0 + (size_t)nr * nb);
+        for (u32 r = 0; r < nr; r++) {
+            const BlockQ40 *row = reinterpret_cast<const BlockQ40 *>(src) + (u64)(r0 + r) * nbAll + nb0;
+            u8 *qo = qs.data() + q0 + (size_t)r * nb * 16;
+            u16 *dd = d.data() + d0 + (size_t)r * nb;
             for (u32 j = 0; j < nb; j++) {
-                qs.insert(qs.end(), row[j].qs, row[j].qs + 16);
-                d.push_back(row[j].d);
+                std::memcpy(qo + (size_t)j * 16, row[j].qs, 16);
+                dd[j] = row[j].d;
             }
         }
     }

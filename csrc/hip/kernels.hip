@@ -19,6 +19,9 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
 #include <type_traits>
 
 namespace dl {
@@ -112,10 +115,33 @@ Q40Tiling q40Tiling(int rows, int n, int L) {
     return t;
 }
 
+static void tileQ40Groups(const uint8_t *qs, const uint16_t *d, int rows, int nb, const Q40Tiling &t, int gBegin,
+                          int gEnd, uint8_t *qsOut, uint32_t *dOut);
+
 void tileQ40(const uint8_t *qs, const uint16_t *d, int rows, int n, int L, uint8_t *qsOut, uint32_t *dOut) {
     const Q40Tiling t = q40Tiling(rows, n, L);
     const int nb = n / 32;
-    for (int g = 0; g < t.groups; g++)
+    // pass groups are independent output ranges: split them over host threads (a 405B TP8 shard
+    // is ~28 GB of Q40 per rank, so the repack at load time must not be single-threaded)
+    const int hw = (int)std::thread::hardware_concurrency();
+    const int nThreads = std::max(1, std::min({hw > 0 ? hw : 1, 32, t.groups / 4}));
+    if (nThreads > 1) {
+        std::vector<std::thread> pool;
+        for (int ti = 0; ti < nThreads; ti++)
+            pool.emplace_back([&, ti] {
+                const int g0 = (int)((long)t.groups * ti / nThreads), g1 = (int)((long)t.groups * (ti + 1) / nThreads);
+                tileQ40Groups(qs, d, rows, nb, t, g0, g1, qsOut, dOut);
+            });
+        for (auto &th : pool) th.join();
+        return;
+    }
+    tileQ40Groups(qs, d, rows, nb, t, 0, t.groups, qsOut, dOut);
+}
+
+static void tileQ40Groups(const uint8_t *qs, const uint16_t *d, int rows, int nb, const Q40Tiling &t, int gBegin,
+                          int gEnd, uint8_t *qsOut, uint32_t *dOut) {
+    const int L = t.L;
+    for (int g = gBegin; g < gEnd; g++)
         for (int k = 0; k < t.K; k++) {
             const size_t c = (size_t)g * t.K + k;
             for (int tid = 0; tid < kThreads; tid++) {
@@ -127,10 +153,10 @@ void tileQ40(const uint8_t *qs, const uint16_t *d, int rows, int n, int L, uint8
                     const int row = row0 + r;
                     if (row < rows && j < nb) {
                         const size_t blk = (size_t)row * nb + j;
-                        for (int i = 0; i < 16; i++) dst[i] = qs[blk * 16 + i];
+                        std::memcpy(dst, qs + blk * 16, 16);
                         dd |= (uint32_t)d[blk] << (16 * r);
                     } else {
-                        for (int i = 0; i < 16; i++) dst[i] = 0;
+                        std::memset(dst, 0, 16);
                     }
                 }
                 dOut[c * kThreads + tid] = dd;
