@@ -49,5 +49,7 @@ std::unique_ptr<DeviceComm> makeXgmiComm(int rank, int world, size_t maxFloats);
 std::string xgmiHandle(DeviceComm *c);
 void xgmiConnect(DeviceComm *c, const std::vector<std::string> &handles);
 bool xgmiTimedOut(DeviceComm *c);
+void xgmiSetLowLatency(DeviceComm *c, bool on);  // LL push protocol for small all-reduces (default on)
+void xgmiResetError(DeviceComm *c);
 
 }  // namespace dl

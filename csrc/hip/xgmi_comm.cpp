@@ -12,6 +12,16 @@
 //   flags[W][kSlots]    flags[p][g] = last epoch rank p published for slot g (written remotely)
 //   epochs[kSlots]      local epoch per slot
 //   error               set when a wait timed out
+// Small all-reduces (<= kLLMax floats, i.e. every decode-time residual update) use a second,
+// lower-latency protocol instead ("LL", after the low-latency protocol of NCCL/RCCL): every rank
+// PUSHES its chunk straight into each peer's receive buffer as 8-byte words {float bits, epoch}
+// and each rank polls its OWN buffer until every word carries the current epoch, then sums the
+// ranks' values in rank order. Data and flag travel in the same atomic 8-byte store, so there is
+// no release fence, no separate flag store and no remote read: one one-way xGMI trip per call
+// (the pull protocol below needs a fence, a flag trip and a remote read round trip). Receive
+// buffers alternate by epoch parity per chunk; a rank can only write epoch e+2 into a peer's
+// buffer after finishing call e+1, which needed that peer's e+1 data, which the peer only sends
+// after it finished reading epoch e.
 // Elements are owned by fixed slots: chunk c (kChunk floats) belongs to slot c % kSlots, for
 // every message size, so a slot only ever races with the same slot on other ranks. Protocol per
 // call and slot (workgroup g): e = ++epochs[g]; write my chunks to pub[e&1]; release (system);
@@ -21,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -35,10 +46,13 @@ constexpr int kSlots = 64;          // workgroups per call (max)
 constexpr int kChunk = 1024;        // floats per chunk (256 threads x float4)
 constexpr int kMaxRanks = 16;
 constexpr int kThreads = 256;
+constexpr int kLLMax = 16384;       // largest LL all-reduce (floats per rank)
+constexpr int kLLSlots = kLLMax / kChunk;
 
 struct XgmiPeers {
     float *pub[kMaxRanks];          // each rank's pub base (pub[p] + parity * maxFloats)
     int *flags[kMaxRanks];          // each rank's flags base: [W][kSlots]
+    uint64_t *ll[kMaxRanks];        // each rank's LL receive buffer: [2 parities][kMaxRanks senders][kLLMax]
 };
 
 struct XgmiCall {
@@ -138,6 +152,72 @@ __global__ __launch_bounds__(kThreads) void xgmiKernel(XgmiCall a) {
     if (tid == 0) a.epochs[g] = e;
 }
 
+// LL all-reduce (see the header): grid = chunks of kChunk floats, thread = 4 consecutive floats.
+// W = world size as a template parameter so every peer loop unrolls with constant indices (peer
+// pointers stay in SGPRs, polled words in VGPRs; no scratch).
+template <int W>
+__global__ __launch_bounds__(kThreads) void xgmiLLKernel(XgmiCall a, unsigned *llEpochs) {
+    const int g = blockIdx.x, tid = threadIdx.x, me = a.rank;
+    __shared__ unsigned sEpoch;
+    if (tid == 0) sEpoch = llEpochs[g] + 1;
+    __syncthreads();
+    const unsigned e = sEpoch, q = e & 1;
+    const long long i0 = (long long)g * kChunk + tid * 4;
+    const int cnt = a.n - i0 >= 4 ? 4 : (a.n > i0 ? (int)(a.n - i0) : 0);
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] = k < cnt ? a.in[i0 + k] : 0.f;
+    // 1. push my values to every peer: {float bits, epoch} in one 8-byte store
+#pragma unroll
+    for (int p = 0; p < W; p++) {
+        if (p == me) continue;
+        uint64_t *dst = a.peers.ll[p] + ((size_t)q * kMaxRanks + me) * kLLMax + i0;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (k < cnt)
+                __hip_atomic_store(dst + k, (uint64_t)__float_as_uint(v[k]) | ((uint64_t)e << 32), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // 2. sum every rank's values in rank order (bitwise identical on all ranks); my own are in v.
+    //    All peers' words are loaded first (independent loads in flight together); only words that
+    //    had not arrived yet are polled again.
+    const uint64_t *mine = a.peers.ll[me] + (size_t)q * kMaxRanks * kLLMax + i0;
+    uint64_t w[W][4];
+#pragma unroll
+    for (int p = 0; p < W; p++)
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            w[p][k] = (p != me && k < cnt)
+                          ? __hip_atomic_load(mine + (size_t)p * kLLMax + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                          : ((uint64_t)e << 32);
+    const bool failed = __hip_atomic_load(a.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < W; p++) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            uint64_t x = w[p][k];
+            if ((unsigned)(x >> 32) != e && !failed) {
+                const long long t0 = rtClock();
+                while ((unsigned)(x >> 32) != e) {
+                    __builtin_amdgcn_s_sleep(1);
+                    x = __hip_atomic_load(mine + (size_t)p * kLLMax + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (rtClock() - t0 > a.timeoutTicks) {  // a peer never arrived: flag it, stop waiting
+                        __hip_atomic_store(a.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        break;
+                    }
+                }
+            }
+            acc[k] += p == me ? v[k] : __uint_as_float((unsigned)x);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (k < cnt) a.out[i0 + k] = acc[k];
+    __syncthreads();
+    if (tid == 0) llEpochs[g] = e;
+}
+
 class XgmiComm : public DeviceComm {
   public:
     XgmiComm(int rank, int world, size_t maxFloats) : rank_(rank), world_(world), maxFloats_(maxFloats) {
@@ -146,12 +226,15 @@ class XgmiComm : public DeviceComm {
         maxFloats_ = (maxFloats_ + kChunk - 1) / kChunk * kChunk;
         pubBytes_ = 2 * maxFloats_ * sizeof(float);
         flagsBytes_ = (size_t)kMaxRanks * kSlots * sizeof(int);
-        const size_t total = pubBytes_ + flagsBytes_ + kSlots * sizeof(int) + 64;
+        llOff_ = (pubBytes_ + flagsBytes_ + kSlots * sizeof(int) + 64 + 255) / 256 * 256;
+        const size_t llBytes = (size_t)2 * kMaxRanks * kLLMax * sizeof(uint64_t);
+        const size_t total = llOff_ + llBytes + kLLSlots * sizeof(unsigned);
         DL_HIP(hipMalloc(&base_, total));
         DL_HIP(hipMemset(base_, 0, total));
         DL_HIP(hipDeviceSynchronize());
         epochs_ = reinterpret_cast<int *>(static_cast<char *>(base_) + pubBytes_ + flagsBytes_);
         error_ = epochs_ + kSlots;
+        llEpochs_ = reinterpret_cast<unsigned *>(static_cast<char *>(base_) + llOff_ + llBytes);
         hipIpcMemHandle_t h;
         DL_HIP(hipIpcGetMemHandle(&h, base_));
         handle_.assign(reinterpret_cast<const char *>(&h), reinterpret_cast<const char *>(&h) + sizeof(h));
@@ -176,13 +259,19 @@ class XgmiComm : public DeviceComm {
             }
             peers_.pub[p] = static_cast<float *>(peerBase_[p]);
             peers_.flags[p] = reinterpret_cast<int *>(static_cast<char *>(peerBase_[p]) + pubBytes_);
+            peers_.ll[p] = reinterpret_cast<uint64_t *>(static_cast<char *>(peerBase_[p]) + llOff_);
         }
         connected_ = true;
     }
     int rank() const override { return rank_; }
     int size() const override { return world_; }
     std::string name() const override { return "xgmi"; }
-    void allReduceSum(float *buf, size_t n, hipStream_t s) override { launch(buf, buf, n, false, s); }
+    void allReduceSum(float *buf, size_t n, hipStream_t s) override {
+        if (ll_ && n <= (size_t)kLLMax && !pullOnly() && (world_ == 2 || world_ == 4 || world_ == 8))
+            launchLL(buf, n, s);
+        else
+            launch(buf, buf, n, false, s);
+    }
     void allGather(const float *send, float *recv, size_t nPerRank, hipStream_t s) override {
         launch(send, recv, nPerRank, true, s);
     }
@@ -190,6 +279,13 @@ class XgmiComm : public DeviceComm {
         throw Error("xgmi comm: broadcastInts is not used on the device data plane");
     }
     const int *deviceErrorFlag() const override { return error_; }
+    // The LL protocol can be switched off (e.g. when its pre-flight test fails on a platform);
+    // resetError clears a timed-out flag so the other protocol can be tested.
+    void setLowLatency(bool on) { ll_ = on; }
+    void resetError() {
+        DL_HIP(hipMemset(error_, 0, sizeof(int)));
+        DL_HIP(hipDeviceSynchronize());
+    }
     bool timedOut() {
         int v = 0;
         DL_HIP(hipMemcpy(&v, error_, sizeof(int), hipMemcpyDeviceToHost));
@@ -197,9 +293,14 @@ class XgmiComm : public DeviceComm {
     }
 
   private:
-    void launch(const float *in, float *out, size_t n, bool gather, hipStream_t s) {
-        DL_CHECK(connected_, "xgmi comm: connect() was not called");
-        DL_CHECK(n <= maxFloats_, "xgmi comm: message larger than the published buffer");
+    static bool pullOnly() {  // DL_XGMI_LL=0: always the pull protocol (comparison runs)
+        static const bool v = [] {
+            const char *e = std::getenv("DL_XGMI_LL");
+            return e && *e == '0';
+        }();
+        return v;
+    }
+    XgmiCall call(const float *in, float *out, size_t n, bool gather) const {
         XgmiCall c;
         c.peers = peers_;
         c.epochs = epochs_;
@@ -212,6 +313,24 @@ class XgmiComm : public DeviceComm {
         c.world = world_;
         c.gather = gather ? 1 : 0;
         c.timeoutTicks = 200LL * 1000 * 1000;  // 2 s at 100 MHz
+        return c;
+    }
+    void launchLL(float *buf, size_t n, hipStream_t s) {
+        DL_CHECK(connected_, "xgmi comm: connect() was not called");
+        const int grid = (int)((n + kChunk - 1) / kChunk);
+        if (grid == 0) return;
+        const XgmiCall c = call(buf, buf, n, false);
+        switch (world_) {
+            case 2: hipLaunchKernelGGL(xgmiLLKernel<2>, dim3(grid), dim3(kThreads), 0, s, c, llEpochs_); break;
+            case 4: hipLaunchKernelGGL(xgmiLLKernel<4>, dim3(grid), dim3(kThreads), 0, s, c, llEpochs_); break;
+            default: hipLaunchKernelGGL(xgmiLLKernel<8>, dim3(grid), dim3(kThreads), 0, s, c, llEpochs_); break;
+        }
+        DL_HIP(hipGetLastError());
+    }
+    void launch(const float *in, float *out, size_t n, bool gather, hipStream_t s) {
+        DL_CHECK(connected_, "xgmi comm: connect() was not called");
+        DL_CHECK(n <= maxFloats_, "xgmi comm: message larger than the published buffer");
+        const XgmiCall c = call(in, out, n, gather);
         const long long chunks = ((long long)n + kChunk - 1) / kChunk;
         const int grid = (int)(chunks < kSlots ? chunks : kSlots);
         if (grid == 0) return;
@@ -220,13 +339,15 @@ class XgmiComm : public DeviceComm {
     }
 
     int rank_, world_;
-    size_t maxFloats_, pubBytes_ = 0, flagsBytes_ = 0;
+    size_t maxFloats_, pubBytes_ = 0, flagsBytes_ = 0, llOff_ = 0;
+    unsigned *llEpochs_ = nullptr;
     void *base_ = nullptr;
     void *peerBase_[kMaxRanks] = {};
     XgmiPeers peers_{};
     int *epochs_ = nullptr, *error_ = nullptr;
     std::string handle_;
     bool connected_ = false;
+    bool ll_ = true;
 };
 
 }  // namespace
@@ -239,5 +360,7 @@ void xgmiConnect(DeviceComm *c, const std::vector<std::string> &handles) {
     static_cast<XgmiComm *>(c)->connect(handles);
 }
 bool xgmiTimedOut(DeviceComm *c) { return static_cast<XgmiComm *>(c)->timedOut(); }
+void xgmiSetLowLatency(DeviceComm *c, bool on) { static_cast<XgmiComm *>(c)->setLowLatency(on); }
+void xgmiResetError(DeviceComm *c) { static_cast<XgmiComm *>(c)->resetError(); }
 
 }  // namespace dl

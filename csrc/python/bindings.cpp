@@ -461,6 +461,8 @@ PYBIND11_MODULE(_C, m) {
                  xgmiConnect(c.comm.get(), hs);
              })
         .def("timed_out", [](PyComm &c) { return xgmiTimedOut(c.comm.get()); })
+        .def("set_low_latency", [](PyComm &c, bool on) { xgmiSetLowLatency(c.comm.get(), on); })
+        .def("reset_error", [](PyComm &c) { xgmiResetError(c.comm.get()); })
         // µs per in-graph all-reduce of n floats (iters back-to-back collectives in one hipGraph)
         .def("bench_all_reduce",
              [](PyComm &c, size_t n, int iters) {

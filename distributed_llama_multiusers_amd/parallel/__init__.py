@@ -110,9 +110,11 @@ def init_device_comm(C, dist, rank: int, world: int, max_floats: int, device: in
     """Set up the engine's device data plane for `world` torch.distributed ranks.
 
     kind "xgmi": every rank allocates its IPC-shared buffer, handles are all-gathered over `dist`,
-    each rank maps its peers, then ONE exact all-reduce runs across the real GPUs as a pre-flight
-    self-test. The decision is agreed by all ranks (MIN all-reduce of a success flag): if any
-    rank failed, every rank falls back to RCCL, so no rank waits on a peer using the other plane.
+    each rank maps its peers, then exact all-reduces run across the real GPUs as a pre-flight
+    self-test (the low-latency push protocol, then both protocols). Every decision is agreed by all
+    ranks (MIN all-reduce of a success flag): if the push protocol fails anywhere it is switched
+    off on every rank; if the rest fails anywhere, every rank falls back to RCCL, so no rank ever
+    waits on a peer that uses another data plane.
     kind "rccl" (or fallback): rank 0's ncclUniqueId is broadcast.
     Returns (comm or None, rccl uid or None, kind actually used)."""
     import numpy as np
@@ -146,17 +148,29 @@ def init_device_comm(C, dist, rank: int, world: int, max_floats: int, device: in
             except Exception as e:  # noqa: BLE001
                 ok = failed("peer mapping", e)
             ok = agreed(ok)
-        if ok:
-            # pre-flight: one exact all-reduce across the real GPUs before trusting the path (a
-            # device-side collective, so it only runs once every rank has mapped its peers)
+
+        def self_test(n, stage):
             try:
-                got = comm.all_reduce(np.full(4096, rank + 1, np.float32))
+                got = comm.all_reduce(np.full(n, rank + 1, np.float32))
                 want = world * (world + 1) / 2
                 if comm.timed_out() or not np.all(got == want):
                     raise RuntimeError(f"got {got[:4]}, want {want}")
+                return True
             except Exception as e:  # noqa: BLE001
-                ok = failed("self-test", e)
-            ok = agreed(ok)
+                return failed(stage, e)
+
+        if ok:
+            # pre-flight: exact all-reduces across the real GPUs before trusting the path (device-
+            # side collectives, so they only run once every rank has mapped its peers). First the
+            # low-latency push protocol used for decode-size messages; if it fails anywhere, every
+            # rank switches it off and the pull protocol is tested on its own.
+            if not agreed(self_test(4096, "low-latency self-test")):
+                comm.set_low_latency(False)
+                comm.reset_error()
+                dist.barrier()
+            small = self_test(4096, "self-test")
+            large = self_test(min(1 << 17, max_floats), "large self-test")  # the pull protocol
+            ok = agreed(small and large)
         if not ok:
             comm, kind = None, "rccl"
         dist.barrier()

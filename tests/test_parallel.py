@@ -75,6 +75,12 @@ class _FakeComm:
     def timed_out(self):
         return False
 
+    def set_low_latency(self, on):
+        pass
+
+    def reset_error(self):
+        pass
+
 
 class _FakeC:
     XgmiComm = _FakeComm
