@@ -599,7 +599,7 @@ class HipEngineImpl : public HipEngine {
     // tests can compare both paths in one process)
     static int gemmMinTokens() {
         const char *e = std::getenv("DL_GEMM_MIN");
-        return e && *e ? std::atoi(e) : 2;
+        return e && *e ? std::atoi(e) : 5;  // GEMV up to 4 rows: 1.78 vs 3.44 ms/step at 2, 2.77 vs 3.47 at 4 (8B)
     }
 
     bool batchedPath(int n) const { return q40_ && n >= gemmMinTokens(); }

@@ -60,9 +60,10 @@ def test_engine_batched_prefill_gemv_chunks(C, assets, graphs, monkeypatch):
 
 @pytest.mark.parametrize("graphs", [True, False])
 @pytest.mark.parametrize("n", [2, 7, 16, 23, 40])
-def test_engine_batched_prefill_mfma(C, assets, graphs, n):
+def test_engine_batched_prefill_mfma(C, assets, graphs, n, monkeypatch):
     """MFMA GEMM batch path (f16 dequantized Q40 x Q80, split-K, fused epilogues; 40 rows = two
     chunks) vs sequential int8 GEMV decodes and vs the CPU reference backend."""
+    monkeypatch.setenv("DL_GEMM_MIN", "2")
     rng = np.random.default_rng(n)
     tokens = [int(t) for t in rng.integers(0, 512, n)]
     a = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=64, use_graphs=graphs)
