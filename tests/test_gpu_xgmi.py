@@ -155,3 +155,49 @@ def test_cli_root_workers_over_xgmi(tmp_path, n_workers):
         for p in procs:
             p.kill()
             p.wait()
+
+
+def test_stalled_worker_gives_clean_root_error(tmp_path):
+    """Fault injection: a GPU worker frozen mid-decode (SIGSTOP, sockets stay open)
+    must make the root fail cleanly - its xGMI collectives stop waiting after 2 s, raise the error
+    flag, and the engine turns it into an exception - instead of hanging or printing tokens computed
+    without the peer's partial sums."""
+    import signal
+    import subprocess
+    import time
+    from conftest import REPO
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    dllama = os.path.join(REPO, "build", "dllama")
+    m, t, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=4096, seed=7, dim=512, n_heads=8,
+                               n_kv_heads=4, hidden_dim=1024)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", DL_TP_COMM="xgmi")
+    port = _port()
+    worker = subprocess.Popen([dllama, "worker", "--port", str(port), "--gpu-index", "0"], stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, env=env)
+    root = None
+    try:
+        time.sleep(0.5)
+        root = subprocess.Popen([dllama, "inference", "--model", m, "--tokenizer", t, "--buffer-float-type", "q80",
+                                 "--prompt", "hello world the", "--steps", "4000", "--temperature", "0", "--gpu-index",
+                                 "0", "--workers", f"127.0.0.1:{port}"], stdout=subprocess.PIPE,
+                                stderr=subprocess.STDOUT, env=env)
+        buf, deadline = b"", time.time() + 60
+        while time.time() < deadline and buf.count(b"Pred") < 20:
+            chunk = root.stdout.read1(4096)
+            if not chunk:
+                break
+            buf += chunk
+        assert buf.count(b"Pred") >= 20, buf.decode(errors="replace")[-2000:]
+        worker.send_signal(signal.SIGSTOP)
+        t0 = time.time()
+        out = buf + root.communicate(timeout=90)[0]
+        text = out.decode(errors="replace")
+        assert root.returncode != 0, text[-2000:]
+        assert "Critical error" in text and "timed out" in text, text[-2000:]
+        assert time.time() - t0 < 60
+    finally:
+        if root is not None and root.poll() is None:
+            root.kill()
+        worker.send_signal(signal.SIGKILL)
+        worker.wait()
