@@ -25,8 +25,12 @@ endif
 
 HOSTFLAGS  := -std=c++17 $(OPT) -fPIC -march=x86-64-v3 -Wall -Wno-unused-function -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include $(SAN)
 HIPFLAGS   := -std=c++17 $(OPT) -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Wno-unused-result -munsafe-fp-atomics
+# Sanitizer builds instrument the g++-compiled host code (runtime, scheduler, API, TCP, CPU
+# backend, tokenizer); the hipcc translation units stay uninstrumented so that one sanitizer
+# runtime (gcc's) is linked. Device code is never sanitized on this pool.
+LIBLINK    := $(HIPCC) -shared --offload-arch=$(ARCH)
 ifneq ($(SAN),)
-  HIPFLAGS += -Xarch_host $(firstword $(SAN)) -fno-omit-frame-pointer
+  LIBLINK  := $(CXX) -shared
 endif
 LDROCM     := -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lrccl
 
@@ -58,7 +62,7 @@ $(BUILD)/obj/hip/%.cpp.o: csrc/hip/%.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(LIB): $(HOST_OBJS) $(HIP_OBJS)
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ $(LDROCM) -lpthread $(SAN) -Wl,-soname,libdllama.so
+	$(LIBLINK) -o $@ $^ $(LDROCM) -lpthread $(SAN) -Wl,-soname,libdllama.so
 
 $(BUILD)/obj/python/bindings.o: csrc/python/bindings.cpp $(HDRS)
 	@mkdir -p $(dir $@)
