@@ -1,11 +1,19 @@
 // CPU reference backend.
 //
+// Matmuls are AVX2/FMA (x86-64-v3) and batched: every weight row is read once per forward for all
+// of its activation rows (the reference reaches the same reuse with vendored tinyBLAS for
+// batch > 1, nn-cpu-ops.cpp:1000-1016 / sgemm.cpp; here one kernel serves decode and prefill).
+// Q40 x Q80 blocks are int8 dot products (maddubs on |w| and sign-transferred x, exact int32 per
+// block) scaled by d_w * d_x in f32, like matmul_Q80_Q40_F32 (nn-cpu-ops.cpp:222-440).
 // Semantics follow the reference's CPU ops (src/nn/nn-cpu-ops.cpp): invRms/rmsNorm (105-166),
 // Q80xQ40 and F32 matmul (182-440), SiLU/GELU (445-491), RoPE over adjacent pairs (1090-1120),
 // KV append at `pos` (1253-1275) and multi-head attention with GQA (749-784). It is the test
 // oracle for the HIP engine and the `--nthreads` CPU path (BASELINE config #1). Differences
 // from the reference, all deliberate: partial sums are exchanged in f32 (the reference quantizes
 // them to Q80, llm.cpp:150); every row carries its own KV slot; GELU is honoured (Q6).
+#include <immintrin.h>
+
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -140,44 +148,75 @@ class CpuBackend : public Backend {
         }
     }
 
-    // y[r] = W[r,:] . x  for r in [0, rows)
-    void matmul(const Mat &W, const Act &x, float *y) {
+    // ys[t][r] = W[r,:] . xs[t]  for r in [0, rows), t in [0, B): each weight row is loaded once
+    // for all B activation rows (groups of kGroup keep the accumulators in registers)
+    static constexpr int kGroup = 8;
+
+    static float hsum(__m256 v) {
+        __m128 s = _mm_add_ps(_mm256_castps256_ps128(v), _mm256_extractf128_ps(v, 1));
+        s = _mm_add_ps(s, _mm_movehl_ps(s, s));
+        s = _mm_add_ss(s, _mm_movehdup_ps(s));
+        return _mm_cvtss_f32(s);
+    }
+
+    void matmul(const Mat &W, const Act *const *xs, int B, float *const *ys) {
         if (W.type == FloatType::F32) {
             const float *w = (const float *)W.data;
-            const float *xv = x.f.data();
             const u32 n = W.cols;
+            DL_CHECK(n % 8 == 0, "f32 matmul: columns must be a multiple of 8");
             pool_.parallelFor(W.rows, [&](long s, long e) {
                 for (long r = s; r < e; r++) {
                     const float *wr = w + (u64)r * n;
-                    float acc = 0.f;
-                    for (u32 i = 0; i < n; i++) acc += wr[i] * xv[i];
-                    y[r] = acc;
-                }
-            });
-        } else {
-            DL_CHECK(W.type == FloatType::Q40 && q80_, "Q40 matmul needs Q80 activations");
-            const BlockQ40 *w = (const BlockQ40 *)W.data;
-            const BlockQ80 *xq = x.q.data();
-            const u32 nb = W.cols / kQBlock;
-            std::vector<float> xd(nb);
-            for (u32 b = 0; b < nb; b++) xd[b] = f16ToF32(xq[b].d);
-            pool_.parallelFor(W.rows, [&](long s, long e) {
-                for (long r = s; r < e; r++) {
-                    const BlockQ40 *wr = w + (u64)r * nb;
-                    float acc = 0.f;
-                    for (u32 b = 0; b < nb; b++) {
-                        int isum = 0;
-                        for (int j = 0; j < 16; j++) {
-                            const int lo = (wr[b].qs[j] & 0x0F) - 8;
-                            const int hi = (wr[b].qs[j] >> 4) - 8;
-                            isum += lo * xq[b].qs[j] + hi * xq[b].qs[j + 16];
+                    for (int t0 = 0; t0 < B; t0 += kGroup) {
+                        const int g = std::min(kGroup, B - t0);
+                        __m256 acc[kGroup];
+                        for (int t = 0; t < g; t++) acc[t] = _mm256_setzero_ps();
+                        for (u32 i = 0; i < n; i += 8) {
+                            const __m256 wv = _mm256_loadu_ps(wr + i);
+                            for (int t = 0; t < g; t++)
+                                acc[t] = _mm256_fmadd_ps(wv, _mm256_loadu_ps(xs[t0 + t]->f.data() + i), acc[t]);
                         }
-                        acc += (float)isum * f16ToF32(wr[b].d) * xd[b];
+                        for (int t = 0; t < g; t++) ys[t0 + t][r] = hsum(acc[t]);
                     }
-                    y[r] = acc;
                 }
             });
+            return;
         }
+        DL_CHECK(W.type == FloatType::Q40 && q80_, "Q40 matmul needs Q80 activations");
+        const BlockQ40 *w = (const BlockQ40 *)W.data;
+        const u32 nb = W.cols / kQBlock;
+        // activation scales as f32, once per forward row
+        std::vector<float> xd((size_t)B * nb);
+        for (int t = 0; t < B; t++)
+            for (u32 b = 0; b < nb; b++) xd[(size_t)t * nb + b] = f16ToF32(xs[t]->q[b].d);
+        pool_.parallelFor(W.rows, [&](long s, long e) {
+            const __m256i low4 = _mm256_set1_epi8(0x0F), eight = _mm256_set1_epi8(8);
+            const __m256i ones = _mm256_set1_epi16(1);
+            for (long r = s; r < e; r++) {
+                const BlockQ40 *wr = w + (u64)r * nb;
+                for (int t0 = 0; t0 < B; t0 += kGroup) {
+                    const int g = std::min(kGroup, B - t0);
+                    __m256 acc[kGroup];
+                    for (int t = 0; t < g; t++) acc[t] = _mm256_setzero_ps();
+                    for (u32 b = 0; b < nb; b++) {
+                        // 32 weights in Q80 element order: [lo nibbles 0..15 | hi nibbles 0..15] - 8
+                        const __m128i raw = _mm_loadu_si128(reinterpret_cast<const __m128i *>(wr[b].qs));
+                        const __m256i nib = _mm256_set_m128i(_mm_srli_epi16(raw, 4), raw);
+                        const __m256i wq = _mm256_sub_epi8(_mm256_and_si256(nib, low4), eight);
+                        const __m256i aw = _mm256_sign_epi8(wq, wq);
+                        const float dw = f16ToF32(wr[b].d);
+                        for (int t = 0; t < g; t++) {
+                            const __m256i xq = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(xs[t0 + t]->q[b].qs));
+                            const __m256i p16 = _mm256_maddubs_epi16(aw, _mm256_sign_epi8(xq, wq));
+                            const __m256i p32 = _mm256_madd_epi16(p16, ones);
+                            const __m256 sc = _mm256_set1_ps(dw * xd[(size_t)(t0 + t) * nb + b]);
+                            acc[t] = _mm256_fmadd_ps(_mm256_cvtepi32_ps(p32), sc, acc[t]);
+                        }
+                    }
+                    for (int t = 0; t < g; t++) ys[t0 + t][r] = hsum(acc[t]);
+                }
+            }
+        });
     }
 
     static float invRms(const float *x, u32 n, float eps) {
@@ -223,25 +262,37 @@ class CpuBackend : public Backend {
             DL_CHECK(slots[b] >= 0 && (u32)slots[b] < cfg_.nSlots, "slot out of range");
             DL_CHECK(tokens[b] >= 0 && (u32)tokens[b] < h_.vocabSize, "token out of range");
         }
-        std::vector<float> x((u64)n * dim), xn(dim), q((u64)n * p.q0), k(p.kv0), v(p.kv0);
-        std::vector<float> att((u64)n * p.q0), y((u64)n * dim), hbuf(p.hidden0), gbuf(p.hidden0);
-        std::vector<float> scores(h_.seqLen);
-        Act a;
+        std::vector<float> x((u64)n * dim), xn(dim), q((u64)n * p.q0), k((u64)n * p.kv0), v((u64)n * p.kv0);
+        std::vector<float> att((u64)n * p.q0), y((u64)n * dim), hbuf((u64)n * p.hidden0), gbuf((u64)n * p.hidden0);
+        std::vector<Act> acts(n);
+        std::vector<const Act *> ap(n);
+        for (int b = 0; b < n; b++) ap[b] = &acts[b];
+        // row pointers of an [n][width] buffer
+        auto rows = [n](std::vector<float> &buf, u32 width) {
+            std::vector<float *> r(n);
+            for (int b = 0; b < n; b++) r[b] = &buf[(u64)b * width];
+            return r;
+        };
+        const std::vector<float *> qR = rows(q, p.q0), kR = rows(k, p.kv0), vR = rows(v, p.kv0), yR = rows(y, dim),
+                                   hR = rows(hbuf, p.hidden0), gR = rows(gbuf, p.hidden0);
         for (int b = 0; b < n; b++) std::memcpy(&x[(u64)b * dim], emb_ + (u64)tokens[b] * dim, dim * sizeof(float));
 
         for (u32 l = 0; l < h_.nLayers; l++) {
             Layer &L = layers_[l];
-            // attention block: norm -> q,k,v -> rope -> kv append (all rows first, then attention)
+            // attention block: norm -> q,k,v (one pass over each weight for all rows) -> rope ->
+            // kv append (all rows first, then attention)
             for (int b = 0; b < n; b++) {
                 rmsNorm(&x[(u64)b * dim], L.rmsAtt, xn.data());
-                setAct(a, xn.data(), dim);
-                matmul(L.wq, a, &q[(u64)b * p.q0]);
-                matmul(L.wk, a, k.data());
-                matmul(L.wv, a, v.data());
-                rope(&q[(u64)b * p.q0], p.q0, positions[b]);
-                rope(k.data(), p.kv0, positions[b]);
-                std::memcpy(kc(l, slots[b], positions[b]), k.data(), p.kv0 * sizeof(float));
-                std::memcpy(vc(l, slots[b], positions[b]), v.data(), p.kv0 * sizeof(float));
+                setAct(acts[b], xn.data(), dim);
+            }
+            matmul(L.wq, ap.data(), n, qR.data());
+            matmul(L.wk, ap.data(), n, kR.data());
+            matmul(L.wv, ap.data(), n, vR.data());
+            for (int b = 0; b < n; b++) {
+                rope(qR[b], p.q0, positions[b]);
+                rope(kR[b], p.kv0, positions[b]);
+                std::memcpy(kc(l, slots[b], positions[b]), kR[b], p.kv0 * sizeof(float));
+                std::memcpy(vc(l, slots[b], positions[b]), vR[b], p.kv0 * sizeof(float));
             }
             const float scale = 1.0f / std::sqrt((float)hs);
             for (int b = 0; b < n; b++) {
@@ -275,10 +326,8 @@ class CpuBackend : public Backend {
                     }
                 });
             }
-            for (int b = 0; b < n; b++) {
-                setAct(a, &att[(u64)b * p.q0], p.q0);
-                matmul(L.wo, a, &y[(u64)b * dim]);
-            }
+            for (int b = 0; b < n; b++) setAct(acts[b], &att[(u64)b * p.q0], p.q0);
+            matmul(L.wo, ap.data(), n, yR.data());
             Timer st;
             comm_->allReduceSum(y.data(), (u64)n * dim);
             syncMs += st.elapsedMs();
@@ -287,21 +336,25 @@ class CpuBackend : public Backend {
             // feed-forward block
             for (int b = 0; b < n; b++) {
                 rmsNorm(&x[(u64)b * dim], L.rmsFfn, xn.data());
-                setAct(a, xn.data(), dim);
-                matmul(L.w1, a, hbuf.data());
-                matmul(L.w3, a, gbuf.data());
+                setAct(acts[b], xn.data(), dim);
+            }
+            matmul(L.w1, ap.data(), n, hR.data());
+            matmul(L.w3, ap.data(), n, gR.data());
+            for (int b = 0; b < n; b++) {
+                float *hb = hR[b];
+                const float *gb = gR[b];
                 for (u32 i = 0; i < p.hidden0; i++) {
-                    const float z = hbuf[i];
+                    const float z = hb[i];
                     float act;
                     if (h_.hiddenAct == HiddenAct::GELU)
                         act = 0.5f * z * (1.0f + std::tanh(0.79788456080286535588f * z * (1.0f + 0.044715f * z * z)));
                     else
                         act = z / (1.0f + std::exp(-z));
-                    hbuf[i] = act * gbuf[i];
+                    hb[i] = act * gb[i];
                 }
-                setAct(a, hbuf.data(), p.hidden0);
-                matmul(L.w2, a, &y[(u64)b * dim]);
+                setAct(acts[b], hb, p.hidden0);
             }
+            matmul(L.w2, ap.data(), n, yR.data());
             st.reset();
             comm_->allReduceSum(y.data(), (u64)n * dim);
             syncMs += st.elapsedMs();
@@ -310,11 +363,12 @@ class CpuBackend : public Backend {
 
         // final norm + vocab-sharded classifier, gathered to the root
         std::vector<float> lg((u64)n * p.vocab0);
+        const std::vector<float *> lR = rows(lg, p.vocab0);
         for (int b = 0; b < n; b++) {
             rmsNorm(&x[(u64)b * dim], rmsFinal_, xn.data());
-            setAct(a, xn.data(), dim);
-            matmul(wcls_, a, &lg[(u64)b * p.vocab0]);
+            setAct(acts[b], xn.data(), dim);
         }
+        matmul(wcls_, ap.data(), n, lR.data());
         Timer st;
         if (comm_->size() == 1) {
             if (logitsOut) std::memcpy(logitsOut, lg.data(), lg.size() * sizeof(float));
