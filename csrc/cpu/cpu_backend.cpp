@@ -9,8 +9,9 @@
 // Q80xQ40 and F32 matmul (182-440), SiLU/GELU (445-491), RoPE over adjacent pairs (1090-1120),
 // KV append at `pos` (1253-1275) and multi-head attention with GQA (749-784). It is the test
 // oracle for the HIP engine and the `--nthreads` CPU path (BASELINE config #1). Differences
-// from the reference, all deliberate: partial sums are exchanged in f32 (the reference quantizes
-// them to Q80, llm.cpp:150); every row carries its own KV slot; GELU is honoured (Q6).
+// from the reference, all deliberate: partial sums are exchanged in f32 by default, which keeps
+// TP=N bit-compatible with TP=1 (`--sync-type q80` selects the reference's Q80 exchange,
+// llm.cpp:150); every row carries its own KV slot; GELU is honoured (Q6).
 #include <immintrin.h>
 
 #include <algorithm>
@@ -56,6 +57,8 @@ class CpuBackend : public Backend {
         h_ = file_->header();
         plan_ = ShardPlan::make(h_, comm_->size(), comm_->rank());
         q80_ = cfg.bufferType == FloatType::Q80;
+        DL_CHECK(cfg.syncType == FloatType::F32 || cfg.syncType == FloatType::Q80, "sync type must be f32 or q80");
+        syncQ80_ = cfg.syncType == FloatType::Q80;
         if (h_.weightType == FloatType::Q40 && !q80_)
             throw Error("This version supports only Q40 weights with Q80 sync type");
         if (h_.weightType == FloatType::F32 && q80_)
@@ -219,6 +222,13 @@ class CpuBackend : public Backend {
         });
     }
 
+    void allReduce(float *y, u64 n) {
+        if (syncQ80_)
+            comm_->allReduceSumQ80(y, n);
+        else
+            comm_->allReduceSum(y, n);
+    }
+
     static float invRms(const float *x, u32 n, float eps) {
         float s = 0.f;
         for (u32 i = 0; i < n; i++) s += x[i] * x[i];
@@ -329,7 +339,7 @@ class CpuBackend : public Backend {
             for (int b = 0; b < n; b++) setAct(acts[b], &att[(u64)b * p.q0], p.q0);
             matmul(L.wo, ap.data(), n, yR.data());
             Timer st;
-            comm_->allReduceSum(y.data(), (u64)n * dim);
+            allReduce(y.data(), (u64)n * dim);
             syncMs += st.elapsedMs();
             for (u64 i = 0; i < (u64)n * dim; i++) x[i] += y[i];
 
@@ -356,7 +366,7 @@ class CpuBackend : public Backend {
             }
             matmul(L.w2, ap.data(), n, yR.data());
             st.reset();
-            comm_->allReduceSum(y.data(), (u64)n * dim);
+            allReduce(y.data(), (u64)n * dim);
             syncMs += st.elapsedMs();
             for (u64 i = 0; i < (u64)n * dim; i++) x[i] += y[i];
         }
@@ -395,7 +405,7 @@ class CpuBackend : public Backend {
     std::unique_ptr<ModelFile> file_;
     ModelHeader h_;
     ShardPlan plan_;
-    bool q80_ = false;
+    bool q80_ = false, syncQ80_ = false;
     std::vector<Layer> layers_;
     const float *emb_ = nullptr, *rmsFinal_ = nullptr;
     Mat wcls_;

@@ -1,5 +1,7 @@
 #include "tcp.h"
 
+#include "../core/quant.h"
+
 #include <arpa/inet.h>
 #include <netdb.h>
 #include <netinet/in.h>
@@ -7,6 +9,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <chrono>
 #include <cstring>
@@ -184,6 +187,7 @@ std::string encodeWorkerConfig(const WorkerConfig &c) {
     o << "magic=" << kProtoMagic << "\nversion=" << kProtoVersion << "\nrank=" << c.rank << "\nworld=" << c.world
       << "\ngpu=" << (c.gpu ? 1 : 0) << "\nmodel=" << e.modelPath << "\nmax_seq_len=" << e.maxSeqLen
       << "\nmax_batch=" << e.maxBatch << "\nn_slots=" << e.nSlots << "\nbuffer=" << (int)e.bufferType
+      << "\nsync=" << (int)e.syncType
       << "\ngraphs=" << (e.useGraphs ? 1 : 0) << "\nkv_bf16=" << (e.kvBf16 ? 1 : 0)
       << "\nsynthetic=" << (e.synthetic ? 1 : 0) << "\nseed=" << e.seed << "\nh_dim=" << h.dim
       << "\nh_hidden=" << h.hiddenDim << "\nh_layers=" << h.nLayers << "\nh_heads=" << h.nHeads
@@ -216,6 +220,7 @@ WorkerConfig decodeWorkerConfig(const std::string &s) {
         else if (k == "max_batch") e.maxBatch = std::stoul(v);
         else if (k == "n_slots") e.nSlots = std::stoul(v);
         else if (k == "buffer") e.bufferType = (FloatType)std::stoi(v);
+        else if (k == "sync") e.syncType = (FloatType)std::stoi(v);
         else if (k == "graphs") e.useGraphs = v == "1";
         else if (k == "kv_bf16") e.kvBf16 = v == "1";
         else if (k == "synthetic") e.synthetic = v == "1";
@@ -256,6 +261,28 @@ void TcpHostComm::allReduceSum(float *data, u64 n) {
     } else {
         peers_[0]->sendAll(data, n * sizeof(float));
         peers_[0]->recvAll(data, n * sizeof(float));
+    }
+}
+
+void TcpHostComm::allReduceSumQ80(float *data, u64 n) {
+    if (size_ == 1) return;
+    DL_CHECK(n % kQBlock == 0, "Q80 sync needs 32-aligned vectors");
+    const u64 part = n / kQBlock * sizeof(BlockQ80);
+    q80_.resize(part * size_);
+    // my quantized partial goes to slot [rank]; the root relays all slots (star topology)
+    quantizeQ80(data, reinterpret_cast<BlockQ80 *>(q80_.data() + part * rank_), n);
+    if (rank_ == 0) {
+        for (size_t i = 0; i < peers_.size(); i++) peers_[i]->recvAll(q80_.data() + part * (i + 1), part);
+        for (Socket *s : peers_) s->sendAll(q80_.data(), part * size_);
+    } else {
+        peers_[0]->sendAll(q80_.data() + part * rank_, part);
+        peers_[0]->recvAll(q80_.data(), part * size_);
+    }
+    tmp_.resize(n);
+    std::fill(data, data + n, 0.f);
+    for (int r = 0; r < size_; r++) {
+        dequantizeQ80(reinterpret_cast<const BlockQ80 *>(q80_.data() + part * r), tmp_.data(), n);
+        for (u64 i = 0; i < n; i++) data[i] += tmp_[i];
     }
 }
 

@@ -112,6 +112,7 @@ class TcpHostComm : public HostComm {
     int rank() const override { return rank_; }
     int size() const override { return size_; }
     void allReduceSum(float *data, u64 n) override;
+    void allReduceSumQ80(float *data, u64 n) override;
     void gatherToRoot(const float *local, u64 nLocal, float *out) override;
     void stats(u64 &sent, u64 &recv) const override;
 
@@ -119,6 +120,7 @@ class TcpHostComm : public HostComm {
     int rank_, size_;
     std::vector<Socket *> peers_;
     std::vector<float> tmp_;
+    std::vector<u8> q80_;
 };
 
 }  // namespace dl

@@ -74,6 +74,7 @@ AppArgs AppArgs::parse(int argc, char **argv, bool requireMode) {
         else if (name == "--stream-weights") a.streamWeights = std::atoi(value) != 0;
         else if (name == "--weights-cache") a.weightsCache = value;
         else if (name == "--metrics") a.metricsPath = value;
+        else if (name == "--sync-type") a.syncType = parseFloatType(value);
         else if (name == "--profile") a.profile = std::atoi(value) != 0;
         else throw Error("Unknown option: " + name);
     }
@@ -110,6 +111,7 @@ static EngineConfig engineConfigFrom(const AppArgs &a, int nSlots) {
     c.maxBatch = (u32)a.nBatches;
     c.nSlots = (u32)nSlots;
     c.bufferType = a.bufferType;
+    c.syncType = a.syncType;
     c.nThreads = a.nThreads;
     c.gpuIndex = a.gpuIndex;
     c.useGraphs = a.graphs;

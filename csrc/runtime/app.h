@@ -20,6 +20,7 @@ struct AppArgs {
     std::string mode;
     std::string modelPath, tokenizerPath, prompt;
     FloatType bufferType = FloatType::F32;
+    FloatType syncType = FloatType::F32;  // --sync-type: CPU TP wire format (f32 exact | q80 reference)
     std::vector<std::string> workerHosts;
     std::vector<int> workerPorts;
     int port = 9990;

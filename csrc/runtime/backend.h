@@ -21,6 +21,9 @@ struct EngineConfig {
     u32 maxBatch = 32;              // max rows per forward (reference nBatches, app.cpp:37)
     u32 nSlots = 1;                 // independent KV-cache slots (concurrent sequences)
     FloatType bufferType = FloatType::F32;  // activation quantization: Q80 or F32
+    FloatType syncType = FloatType::F32;    // CPU tensor-parallel wire format of partial sums:
+                                            // F32 (exact, TP=N == TP=1) or Q80 (the reference's
+                                            // quantized all-gather, llm.cpp:150, 3.8x fewer bytes)
     int nThreads = 1;               // CPU backend threads
     int gpuIndex = -1;              // HIP device ordinal (-1 = CPU backend)
     bool useGraphs = true;          // capture per-batch-size hipGraphs
@@ -60,6 +63,10 @@ class HostComm {
     virtual int rank() const = 0;
     virtual int size() const = 0;
     virtual void allReduceSum(float *data, u64 n) = 0;
+    // Reference semantics of SYNC_NODE_SLICES with Q80 buffers (nn-network.cpp:537-569,
+    // llm.cpp:212-217): every rank's partial is quantized to Q80 once, every rank receives all
+    // ranks' quantized partials and sums them dequantized in rank order (identical on all ranks).
+    virtual void allReduceSumQ80(float *data, u64 n) { allReduceSum(data, n); }
     // every rank contributes nLocal floats; root receives size()*nLocal floats in rank order
     virtual void gatherToRoot(const float *local, u64 nLocal, float *out) = 0;
     virtual void stats(u64 &sent, u64 &recv) const {

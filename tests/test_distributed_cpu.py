@@ -190,3 +190,29 @@ def test_metrics_jsonl_per_forward(kv4, tmp_path):
     assert recs and all(r["event"] == "forward_argmax" and r["nodes"] == 2 and r["backend"] == "cpu" for r in recs)
     assert sum(r["rows"] for r in recs) == 10  # one row per position 0..steps-1
     assert all(r["sent_bytes"] > 0 and r["recv_bytes"] > 0 and r["ms"] >= r["sync_ms"] for r in recs)
+
+
+def _sync_kb(out):
+    """(sent, recv) kB of the root per predicted token, from the '🔶 Pred' lines."""
+    rows = [re.search(r"Sent\s+(\d+) kB Recv\s+(\d+) kB", l) for l in out.splitlines() if l.startswith("🔶 Pred")]
+    return [(int(m.group(1)), int(m.group(2))) for m in rows if m]
+
+
+def test_q80_sync_type_reference_wire_format(kv4):
+    """--sync-type q80: partial sums cross the wire as Q80 blocks (the reference's SYNC_NODE_SLICES
+    format, 34 B per 32 values instead of 128 B) and every rank merges the same quantized parts, so
+    the greedy continuation stays (almost) that of the exact f32 exchange."""
+    procs, addrs = _workers(1)
+    try:
+        rc, f32 = _inference(kv4, addrs, steps=24)
+        assert rc == 0, f32
+        rc, q80 = _inference(kv4, addrs, steps=24, extra=("--sync-type", "q80"))
+        assert rc == 0, q80
+    finally:
+        for p in procs:
+            p.kill()
+    a, b = _preds(f32), _preds(q80)
+    assert len(a) == len(b) and sum(x == y for x, y in zip(a, b)) >= 0.75 * len(a)
+    sf, sq = _sync_kb(f32), _sync_kb(q80)
+    # per token the root receives the worker's partials (2 per layer) + its logits slice
+    assert sum(r for _, r in sq) < sum(r for _, r in sf)
