@@ -216,3 +216,16 @@ def test_q80_sync_type_reference_wire_format(kv4):
     sf, sq = _sync_kb(f32), _sync_kb(q80)
     # per token the root receives the worker's partials (2 per layer) + its logits slice
     assert sum(r for _, r in sq) < sum(r for _, r in sf)
+
+
+def test_chat_mode_multi_turn(assets):
+    """`dllama chat` (dllama.cpp:130-214): system prompt + user turn read from stdin through the chat
+    template. A random-init model never samples an end-of-turn token, so the first assistant turn
+    runs to the end of the context window and the session ends cleanly there."""
+    cmd = [DLLAMA, "chat", "--model", assets["q40"], "--tokenizer", assets["tok"], "--buffer-float-type", "q80",
+           "--nthreads", "2", "--temperature", "0", "--chat-template", "llama3"]
+    r = subprocess.run(cmd, input=b"be brief\nhello world\nand again\n", capture_output=True, timeout=120)
+    out = r.stdout.decode("utf-8", errors="replace")
+    assert r.returncode == 0, out
+    assert out.count("🤖 Assistant") == 1 and out.count("👱 User") == 1
+    assert out.rstrip().endswith("(end of context)")
