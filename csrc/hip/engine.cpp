@@ -849,7 +849,8 @@ class HipEngineImpl : public HipEngine {
 
 }  // namespace
 
-double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int passes, int copies, int iters) {
+double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int passes, int copies, int iters,
+                    std::vector<unsigned long long> *trace) {
     hipStream_t s;
     DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     std::vector<void *> mem;
@@ -919,9 +920,12 @@ double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int pas
         a.kcache = alloc((size_t)a.kv0 * 2);
         a.vcache = alloc((size_t)a.kv0 * 2);
     }
+    const int grid = (rows + (256 / L) * 2 * a.passes - 1) / ((256 / L) * 2 * a.passes);
+    unsigned long long *tbuf = trace ? (unsigned long long *)alloc((size_t)iters * grid * 8 * 8) : nullptr;
     auto launch = [&](int c) {
         a.qs = qs[c % copies];
         a.wd = d[c % copies];
+        a.trace = tbuf ? tbuf + (size_t)c * grid * 8 : nullptr;
         hipk::launchGemv(a, B, pro, epi, true, s);
     };
     launch(0);
@@ -943,6 +947,10 @@ double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int pas
     DL_HIP(hipEventSynchronize(e1));
     float ms = 0;
     DL_HIP(hipEventElapsedTime(&ms, e0, e1));
+    if (trace) {
+        trace->resize((size_t)iters * grid * 8);
+        DL_HIP(hipMemcpy(trace->data(), tbuf, trace->size() * 8, hipMemcpyDeviceToHost));
+    }
     (void)hipGraphExecDestroy(ge);
     (void)hipGraphDestroy(g);
     (void)hipEventDestroy(e0);

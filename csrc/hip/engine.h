@@ -32,7 +32,9 @@ int hipDeviceCount();
 
 // Micro-benchmark of one Q40 GEMV configuration: `copies` weight matrices (to defeat the 256 MB
 // infinity cache) are cycled through a graph of `iters` launches. Returns microseconds per launch.
-double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int passes, int copies, int iters);
+// trace: per launch x workgroup 8 u64 (GemvArgs::trace layout; s_memrealtime, 100 MHz)
+double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int passes, int copies, int iters,
+                    std::vector<unsigned long long> *trace = nullptr);
 // Micro-benchmark of the decode attention kernel (bf16 KV, Q80 output): `copies` KV caches cycled
 // through a graph of `iters` launches, every row at position `pos`. Returns microseconds per launch.
 double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B, int copies, int iters);

@@ -98,6 +98,10 @@ struct GemvArgs {
     void *kcache = nullptr;       // layer base: [slot][seqLen][kv0]
     void *vcache = nullptr;
     int kvBf16 = 1;
+    // diagnostics (gemvQ40Kernel): when set, workgroup g writes 8 u64 at trace[8g..]: s_memrealtime
+    // at entry, prologue done, exit, (HW_ID << 32 | XCC_ID), prologue loads landed (early path),
+    // first ring slot consumed (thread 0's view)
+    unsigned long long *trace = nullptr;
 };
 
 // Batched Q40 matmul on MFMA (2..32 tokens per launch): GemvArgs `e` carries the weights (tiled,

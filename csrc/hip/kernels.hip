@@ -442,6 +442,10 @@ __device__ __forceinline__ void attnSplit(int len, int splitGrid, int &nSplit, i
 //   of upstream Q80), row-pair epilogues (SwiGLU, RoPE + KV append) run in registers.
 // ------------------------------------------------------------------------------------------------
 static constexpr int kRing = 8;
+#ifndef DL_GEMV_KE
+#define DL_GEMV_KE 2
+#endif
+static constexpr int kEarlySlots = DL_GEMV_KE;  // ring slots issued before the early prologue's wait
 
 template <int L, int B, int PRO, int EPI>
 __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
@@ -456,6 +460,9 @@ __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
     float2 *ssc = reinterpret_cast<float2 *>(smem + lay.sc);
     const int tid = threadIdx.x, gi = tid / L, li = tid % L;
     const int rowBase = blockIdx.x * R;
+    // timestamps stay in SGPRs until the end: a store here would join the ring's vmcnt accounting
+    const unsigned long long tEntry = a.trace ? wall_clock64() : 0ull;
+    unsigned long long tReady = 0ull, tLoaded = 0ull, tFirst = 0ull;
 
     // slot = 2 rows x 16 B of nibbles + the pair's two f16 scales in one 32-bit word
     u32x4 w[D][RG];
@@ -485,20 +492,9 @@ __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
         asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(ws[1]) : "v"(p0 + kThreads));
         asm volatile("global_load_dword %0, %1, off" : "=v"(ds) : "v"(pd));
     };
-    // The same step as compiler-visible loads (first round of the early-prologue path): the
-    // waitcnt pass then counts them, so the prologue's own (older) loads are waited for with
-    // vmcnt(3 * kRing) while the ring's first round is still in flight.
-    auto issueVisible = [&](u32x4(&ws)[RG], uint32_t &ds) {
-        const u32x4 *p0;
-        const uint32_t *pd;
-        stepPtrs(p0, pd);
-        ws[0] = __builtin_nontemporal_load(p0);
-        ws[1] = __builtin_nontemporal_load(p0 + kThreads);
-        ds = *pd;
-    };
-    // The prologue's loads were issued after the ring's (late path), or the ring's first round is
-    // compiler-visible (early path); either way this explicit wait pins every slot register before
-    // the loop, so no copy of an in-flight register can be made.
+    // Late path: the prologue's compiler-visible loads were issued after the ring's, so waiting
+    // for them waits for the whole first round anyway; this explicit wait also pins every slot
+    // register before the loop, so no copy of an in-flight register can be made.
     auto waitAll = [&]() {
 #pragma unroll
         for (int s = 0; s < D; s++) asm volatile("s_waitcnt vmcnt(0)" : "+v"(w[s][0]), "+v"(w[s][1]), "+v"(dh[s]));
@@ -519,40 +515,76 @@ __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
     auto earlyPath = [&](auto pkTag) {
         constexpr int PK = decltype(pkTag)::value, PS = (PK + 1) / 2;
         const int nChunks = n >> 3, n16 = n >> 4;
-        float4 ex[PK][2], ey[PK][2], ew[PK][2];
+        f32x4 ex[PK][2], ey[PK][2], ew[PK][2];
         u32x4 eq[PK];
         u32x2 es[PS];
-        // unconditional, clamped loads in one basic block: a branch here would let the compiler
-        // pull the arithmetic up to the loads and wait for them before the ring is issued
-        float2 ropeV = make_float2(0.f, 0.f);
-        if constexpr (EPI == EPI_QKV) ropeV = a.rope[(size_t)posB[0] * (a.hs >> 1) + min(tid, (a.hs >> 1) - 1)];
+        // Every load of this path is inline asm with explicit waits: the compiler's waitcnt pass
+        // does not see them, so nothing flushes vmcnt(0) before the loop and each ring slot is
+        // waited for on its own inside it (the first slot's dot products start while the rest of
+        // the first round is still in flight). Loads are unconditional and clamped.
+        auto ld4a = [](f32x4 &r, const float *p) { asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p)); };
+        u32x2 ropeV = {0u, 0u};
+        if constexpr (EPI == EPI_QKV) {
+            const float2 *rp = a.rope + (size_t)posB[0] * (a.hs >> 1) + min(tid, (a.hs >> 1) - 1);
+            asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(ropeV) : "v"(rp));
+        }
         if constexpr (PRO == PRO_RESNORM) {
             const float *yp = a.addIn ? a.addIn : a.in;
             const float *wp = a.normW ? a.normW : a.in;
 #pragma unroll
             for (int k = 0; k < PK; k++) {
                 const int c = min(tid + k * kThreads, nChunks - 1);
-                ex[k][0] = ld4(a.in + c * 8);
-                ex[k][1] = ld4(a.in + c * 8 + 4);
-                ey[k][0] = ld4(yp + c * 8);
-                ey[k][1] = ld4(yp + c * 8 + 4);
-                ew[k][0] = ld4(wp + c * 8);
-                ew[k][1] = ld4(wp + c * 8 + 4);
+                ld4a(ex[k][0], a.in + c * 8);
+                ld4a(ex[k][1], a.in + c * 8 + 4);
+                ld4a(ey[k][0], yp + c * 8);
+                ld4a(ey[k][1], yp + c * 8 + 4);
+                ld4a(ew[k][0], wp + c * 8);
+                ld4a(ew[k][1], wp + c * 8 + 4);
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < PK; k++) eq[k] = reinterpret_cast<const u32x4 *>(a.aq)[min(tid + k * kThreads, n16 - 1)];
+            for (int k = 0; k < PK; k++) {
+                const u32x4 *src = reinterpret_cast<const u32x4 *>(a.aq) + min(tid + k * kThreads, n16 - 1);
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(eq[k]) : "v"(src));
+            }
 #pragma unroll
-            for (int k = 0; k < PS; k++) es[k] = reinterpret_cast<const u32x2 *>(a.as)[min(tid + k * kThreads, nb - 1)];
+            for (int k = 0; k < PS; k++) {
+                const u32x2 *src = reinterpret_cast<const u32x2 *>(a.as) + min(tid + k * kThreads, nb - 1);
+                asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(es[k]) : "v"(src));
+            }
         }
+        // A CU returns vector loads in issue order across its waves: without this barrier a wave's
+        // prologue loads queue behind the other waves' ring rounds (~3 us at the CU's share of
+        // HBM bandwidth, measured with GemvArgs::trace). s_barrier alone, no fence: it does not
+        // wait for the loads, only orders every wave's prologue issue before any ring issue.
         __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        // KE slots go out before the prologue's wait, the rest of the ring once the prologue's
+        // loads have landed (a full first round floods the memory queues and delays them)
+        constexpr int KE = kEarlySlots < D ? kEarlySlots : D;
 #pragma unroll
-        for (int s = 0; s < D; s++) {
-            issueVisible(w[s], dh[s]);
+        for (int s = 0; s < KE; s++) {
+            issue(w[s], dh[s]);
             __builtin_amdgcn_sched_barrier(0);
         }
+        // the prologue's loads are older than the ring's 3 * KE: wait for them only
+        if constexpr (EPI == EPI_QKV) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(ropeV) : "i"(3 * KE));
+        if constexpr (PRO == PRO_RESNORM) {
+#pragma unroll
+            for (int k = 0; k < PK; k++)
+                asm volatile("s_waitcnt vmcnt(%6)"
+                             : "+v"(ex[k][0]), "+v"(ex[k][1]), "+v"(ey[k][0]), "+v"(ey[k][1]), "+v"(ew[k][0]), "+v"(ew[k][1])
+                             : "i"(3 * KE));
+        } else {
+#pragma unroll
+            for (int k = 0; k < PK; k++) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(eq[k]) : "i"(3 * KE));
+#pragma unroll
+            for (int k = 0; k < PS; k++) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(es[k]) : "i"(3 * KE));
+        }
+        if (a.trace) tLoaded = wall_clock64();
         if constexpr (EPI == EPI_QKV)
-            if (tid < (a.hs >> 1)) sRope[tid] = ropeV;
+            if (tid < (a.hs >> 1)) sRope[tid] = make_float2(__uint_as_float(ropeV.x), __uint_as_float(ropeV.y));
         if constexpr (PRO == PRO_RESNORM) {
             float *xo = (blockIdx.x == 0 && a.xNext) ? a.xNext : nullptr;
             float v[PK][8];
@@ -560,14 +592,14 @@ __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
 #pragma unroll
             for (int k = 0; k < PK; k++) {
                 const int c = tid + k * kThreads;
-                float4 v0 = ex[k][0], v1 = ex[k][1];
+                f32x4 v0 = ex[k][0], v1 = ex[k][1];
                 if (a.addIn) {
-                    v0.x += ey[k][0].x; v0.y += ey[k][0].y; v0.z += ey[k][0].z; v0.w += ey[k][0].w;
-                    v1.x += ey[k][1].x; v1.y += ey[k][1].y; v1.z += ey[k][1].z; v1.w += ey[k][1].w;
+                    v0 += ey[k][0];
+                    v1 += ey[k][1];
                 }
                 if (xo && c < nChunks) {
-                    st4(xo + c * 8, v0);
-                    st4(xo + c * 8 + 4, v1);
+                    *reinterpret_cast<f32x4 *>(xo + c * 8) = v0;
+                    *reinterpret_cast<f32x4 *>(xo + c * 8 + 4) = v1;
                 }
                 v[k][0] = v0.x; v[k][1] = v0.y; v[k][2] = v0.z; v[k][3] = v0.w;
                 v[k][4] = v1.x; v[k][5] = v1.y; v[k][6] = v1.z; v[k][7] = v1.w;
@@ -603,17 +635,18 @@ __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
                 if (tid + k * kThreads < nb) reinterpret_cast<u32x2 *>(ssc)[tid + k * kThreads] = es[k];
         }
         __syncthreads();
-        waitAll();
+        if (a.trace) tReady = wall_clock64();
+        // The rest of the ring only now: a wave stalls at ISSUE once its CU's memory queue is full,
+        // so issuing it before the prologue's arithmetic made the norm wait for most of the
+        // matrix to stream in (trace: prologue loads landed at 0.6 us, prologue done at 2.8 us).
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = KE; s < D; s++) {
+            issue(w[s], dh[s]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
     };
-    const int unitsPerThread = PRO == PRO_RESNORM ? (n + 8 * kThreads - 1) / (8 * kThreads)
-                                                  : (n + 16 * kThreads - 1) / (16 * kThreads);
-    if (B == 1 && unitsPerThread <= 1) {
-        earlyPath(std::integral_constant<int, 1>{});
-    } else if (B == 1 && unitsPerThread <= 2) {
-        earlyPath(std::integral_constant<int, 2>{});
-    } else if (B == 1 && unitsPerThread <= 4) {
-        earlyPath(std::integral_constant<int, 4>{});
-    } else {
+    auto latePath = [&]() {
         // sched_barrier keeps issue order == slot order, so each step waits for exactly its own
         // slot (vmcnt = loads of the other kRing-1 slots) instead of the scheduler batching the ring.
 #pragma unroll
@@ -633,8 +666,12 @@ __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
         else
             stageQ80<B>(a, sq, ssc);
         waitAll();
-    }
+        if (a.trace) tReady = wall_clock64();
+    };
 
+    // The ring's consume loop. Each prologue path below inlines its own copy, so no ring register
+    // is live across a join of two paths (a join could copy a register whose load is in flight).
+    auto mainLoop = [&]() __attribute__((always_inline)) {
     float acc[RG][B];
 #pragma unroll
     for (int r = 0; r < RG; r++)
@@ -692,6 +729,7 @@ __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
         for (int s = 0; s < D; s++) {
             asm volatile("s_waitcnt vmcnt(%3)" : "+v"(w[s][0]), "+v"(w[s][1]), "+v"(dh[s]) : "i"(3 * (D - 1)));
             consume(w[s], dh[s], true);
+            if (a.trace && s == 0 && t0 == 0) tFirst = wall_clock64();
             issue(w[s], dh[s]);
             advance();
             __builtin_amdgcn_sched_barrier(0);
@@ -704,13 +742,46 @@ __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
         asm volatile("s_waitcnt vmcnt(%3)" : "+v"(w[s][0]), "+v"(w[s][1]), "+v"(dh[s]) : "i"(3 * (D - 1 - s)));
         if (t0 + s < T) {
             consume(w[s], dh[s], true);
+            if (a.trace && s == 0 && t0 == 0) tFirst = wall_clock64();
             advance();
         }
         __builtin_amdgcn_sched_barrier(0);
     }
+    };
+
+    const int unitsPerThread = PRO == PRO_RESNORM ? (n + 8 * kThreads - 1) / (8 * kThreads)
+                                                  : (n + 16 * kThreads - 1) / (16 * kThreads);
+    if (B == 1 && unitsPerThread <= 1) {
+        earlyPath(std::integral_constant<int, 1>{});
+        mainLoop();
+    } else if (B == 1 && unitsPerThread <= 2) {
+        earlyPath(std::integral_constant<int, 2>{});
+        mainLoop();
+    } else if (B == 1 && unitsPerThread <= 4) {
+        earlyPath(std::integral_constant<int, 4>{});
+        mainLoop();
+    } else {
+        latePath();
+        mainLoop();
+    }
     if constexpr (EPI == EPI_ACT_Q80) {
         __syncthreads();
         storeHiddenQ80<B>(a, hbuf, R >> 1, rowBase >> 1);
+    }
+    if (a.trace) {
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned long long tExit = wall_clock64();
+            const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+            const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+            unsigned long long *t = a.trace + 8 * (size_t)blockIdx.x;
+            t[0] = tEntry;
+            t[1] = tReady;
+            t[2] = tExit;
+            t[3] = ((unsigned long long)hw << 32) | xcc;
+            t[4] = tLoaded;
+            t[5] = tFirst;
+        }
     }
 }
 

@@ -404,9 +404,25 @@ PYBIND11_MODULE(_C, m) {
           py::arg("model"), py::arg("buffer_type") = "q80", py::arg("nthreads") = 1, py::arg("max_seq_len") = 0,
           py::arg("max_batch") = 32, py::arg("n_slots") = 1);
 
-    m.def("bench_gemv_q40", &benchGemvQ40, py::arg("rows"), py::arg("n"), py::arg("pro"), py::arg("epi"),
-          py::arg("batch") = 1, py::arg("lanes") = 0, py::arg("passes") = 1, py::arg("copies") = 8,
-          py::arg("iters") = 200, py::call_guard<py::gil_scoped_release>());
+    m.def("bench_gemv_q40",
+          [](int rows, int n, int pro, int epi, int B, int lanes, int passes, int copies, int iters) {
+              return benchGemvQ40(rows, n, pro, epi, B, lanes, passes, copies, iters);
+          },
+          py::arg("rows"), py::arg("n"), py::arg("pro"), py::arg("epi"), py::arg("batch") = 1, py::arg("lanes") = 0,
+          py::arg("passes") = 1, py::arg("copies") = 8, py::arg("iters") = 200, py::call_guard<py::gil_scoped_release>());
+    m.def("trace_gemv_q40",
+          [](int rows, int n, int pro, int epi, int B, int lanes, int passes, int copies, int iters) {
+              std::vector<unsigned long long> t;
+              double us;
+              {
+                  py::gil_scoped_release nogil;
+                  us = benchGemvQ40(rows, n, pro, epi, B, lanes, passes, copies, iters, &t);
+              }
+              return py::make_tuple(us, py::array_t<unsigned long long>(t.size(), t.data()));
+          },
+          py::arg("rows"), py::arg("n"), py::arg("pro"), py::arg("epi"), py::arg("batch") = 1, py::arg("lanes") = 0,
+          py::arg("passes") = 0, py::arg("copies") = 8, py::arg("iters") = 20,
+          "bench_gemv_q40 with per-workgroup s_memrealtime stamps: (us, u64[iters*grid*4])");
     m.def("bench_attention", &benchAttention, py::arg("n_heads0"), py::arg("kv_mul"), py::arg("head_size"),
           py::arg("seq_len"), py::arg("pos"), py::arg("batch") = 1, py::arg("copies") = 32, py::arg("iters") = 200,
           py::call_guard<py::gil_scoped_release>());

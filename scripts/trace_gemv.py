@@ -1,0 +1,65 @@
+"""Workgroup timeline of the Q40 GEMV inside a hipGraph of back-to-back launches.
+
+Every workgroup stamps s_memrealtime (100 MHz, one clock for the whole device) at entry, when the
+ring's first round of weight loads has landed (prologue done), and at exit (GemvArgs::trace).
+Per shape this prints, averaged over the launches after the first few:
+  span   first entry -> last exit of a launch
+  gap    last exit of launch i -> first entry of launch i+1 (the dependent-kernel boundary)
+  entry  spread of workgroup entry times (dispatch ramp)
+  loaded entry -> prologue loads landed (median; early path only)
+  ready  entry -> prologue done (median / p90; late path: first ring round landed too)
+  first  entry -> first ring slot consumed (median)
+  exit   spread of exit times relative to the launch's first entry (median / p90 / max)
+  python scripts/trace_gemv.py [shape ...]
+"""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import distributed_llama_multiusers_amd as dl
+
+C = dl.native()
+PRO_GLOBAL, PRO_RESNORM = 0, 1
+EPI_STORE, EPI_ACT, EPI_QKV, EPI_ACT_Q80 = 0, 1, 2, 3
+SHAPES = {
+    "qkv": (6144, 4096, PRO_RESNORM, EPI_QKV),
+    "wo": (4096, 4096, PRO_GLOBAL, EPI_STORE),
+    "w13": (28672, 4096, PRO_RESNORM, EPI_ACT_Q80),
+    "w2": (4096, 14336, PRO_GLOBAL, EPI_STORE),
+    "wcls": (128256, 4096, PRO_RESNORM, EPI_STORE),
+}
+TICK_US = 0.01  # s_memrealtime runs at 100 MHz
+
+
+def analyse(name, us, t, iters):
+    t = t.reshape(iters, -1, 8).astype(np.int64)
+    grid = t.shape[1]
+    rows = []
+    for i in range(4, iters):
+        e, r, x, ld, f = t[i, :, 0], t[i, :, 1], t[i, :, 2], t[i, :, 4], t[i, :, 5]
+        t0 = e.min()
+        rows.append(dict(loaded=np.median(ld - e) if ld.min() > 0 else np.nan, first=np.median(f - e),span=x.max() - t0, entry=e.max() - t0, ready_med=np.median(r - e), ready_p90=np.percentile(r - e, 90),
+                         exit_med=np.median(x - t0), exit_p90=np.percentile(x - t0, 90), exit_min=x.min() - t0,
+                         gap=(t[i + 1, :, 0].min() - x.max()) if i + 1 < iters else np.nan))
+    avg = {k: np.nanmean([r[k] for r in rows]) * TICK_US for k in rows[0]}
+    xcc = (t[-1, :, 3] & 0xF)
+    per_xcc = np.bincount(xcc, minlength=8)
+    print(f"{name:5s} grid {grid:4d} | {us:6.2f} us/launch | span {avg['span']:5.2f} gap {avg['gap']:4.2f} | "
+          f"entry spread {avg['entry']:4.2f} | loaded {avg['loaded']:4.2f} | first {avg['first']:4.2f} | ready med {avg['ready_med']:4.2f} p90 {avg['ready_p90']:4.2f} | "
+          f"exit min {avg['exit_min']:5.2f} med {avg['exit_med']:5.2f} p90 {avg['exit_p90']:5.2f} | WGs/XCC {per_xcc.tolist()}",
+          flush=True)
+
+
+def main():
+    names = sys.argv[1:] or list(SHAPES)
+    iters = int(os.environ.get("ITERS", "24"))
+    for name in names:
+        rows, n, pro, epi = SHAPES[name]
+        us, t = C.trace_gemv_q40(rows, n, pro, epi, 1, 0, 0, 8, iters)
+        analyse(name, us, t, iters)
+
+
+if __name__ == "__main__":
+    main()
