@@ -956,10 +956,30 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 static constexpr int kGemmRows = 64;
 static constexpr int kGemmCh = 8;  // Q40 blocks per pipeline stage (~25 KB at 32 tokens)
 
+// Split-K degree: grow S until the grid reaches the workgroup target (DL_GEMM_WG, read once) or
+// a split would get fewer than kGemmCh blocks. The target is sized so every CU holds its 3
+// resident workgroups: with one chunk in flight per workgroup, bytes in flight per CU (and so
+// HBM bandwidth) scale with resident workgroups, not with tiles.
+static int gemmWgTarget() {
+    static const int v = [] {
+        const char *e = std::getenv("DL_GEMM_WG");
+        return e ? std::max(1, std::atoi(e)) : 256;
+    }();
+    return v;
+}
+static int gemmMaxSplits() {
+    static const int v = [] {
+        const char *e = std::getenv("DL_GEMM_MAXS");
+        return e ? std::max(1, std::atoi(e)) : 8;
+    }();
+    return v;
+}
+
 int gemmSplits(int rows, int n) {
     const int tiles = (rows + kGemmRows - 1) / kGemmRows, nb = n / 32;
+    const int target = gemmWgTarget(), maxS = gemmMaxSplits();
     int S = 1;
-    while (S < 8 && tiles * S < 256 && nb % (2 * S) == 0 && nb / (2 * S) >= kGemmCh) S *= 2;
+    while (2 * S <= maxS && tiles * S < target && nb % (2 * S) == 0 && nb / (2 * S) >= kGemmCh) S *= 2;
     return S;
 }
 
@@ -1135,10 +1155,22 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
             __hip_atomic_store(ga.counters + tileIdx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
-        for (int i = tid; i < MP * kGemmRows; i += kThreads) {
-            float v = 0.f;
-            for (int s2 = 0; s2 < S; s2++) v += ga.part[((size_t)s2 * tiles + tileIdx) * MP * kGemmRows + i];
-            tile[i] = v;
+        // combine in split order (deterministic), 16-B loads with all of a thread's splits in
+        // flight at once: this tail runs on one workgroup per tile after the others finished
+        const f32x4 *P = reinterpret_cast<const f32x4 *>(ga.part) + (size_t)tileIdx * MP * kGemmRows / 4;
+        const size_t st4 = (size_t)tiles * MP * kGemmRows / 4;
+        f32x4 *tile4 = reinterpret_cast<f32x4 *>(tile);
+        for (int i = tid; i < MP * kGemmRows / 4; i += kThreads) {
+            f32x4 v[8];
+#pragma unroll
+            for (int s2 = 0; s2 < 8; s2++)
+                if (s2 < S) v[s2] = P[s2 * st4 + i];
+            f32x4 r = v[0];
+#pragma unroll
+            for (int s2 = 1; s2 < 8; s2++)
+                if (s2 < S) r += v[s2];
+            for (int s2 = 8; s2 < S; s2++) r += P[s2 * st4 + i];
+            tile4[i] = r;
         }
     }
     __syncthreads();
