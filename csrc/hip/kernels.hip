@@ -992,7 +992,10 @@ size_t gemmPartFloats(int rows, int n, int maxTokens) {
 // stage layout (bytes): weights [64 rows][8 units] x 16 B | scales [32 pairs][8] u32 | x [MP][32 units] x 16 B
 static constexpr int kStW = kGemmRows * kGemmCh * 16, kStD = (kGemmRows / 2) * kGemmCh * 4;
 __host__ __device__ static constexpr int gemmStageBytes(int MT) { return kStW + kStD + MT * 16 * kGemmCh * 64; }
-static constexpr int kGemmStages = 2;  // stage buffers (kGemmStages-1 chunks in flight); 2 -> 3 WGs/CU
+#ifndef DL_GEMM_STAGES
+#define DL_GEMM_STAGES 2  // 3 stages (2 WGs/CU) measured slower: batch-32 8.1k vs 8.8k tok/s
+#endif
+static constexpr int kGemmStages = DL_GEMM_STAGES;  // stage buffers (kGemmStages-1 chunks in flight)
 static size_t gemmLds(int MT) { return kGemmStages * (size_t)gemmStageBytes(MT) + 16; }
 
 // 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d via the 0x6400 | q magic (1024 + q)
@@ -1212,6 +1215,8 @@ void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
     const size_t lds = gemmLds(MT);
 #define DL_GEMM_CASE(M_, E)                                                                   \
     if (MT == M_ && epi == E) {                                                               \
+        static const bool ldsOk = (allowLds((const void *)gemmQ40Kernel<M_, E>, lds), true); \
+        (void)ldsOk;                                                                          \
         hipLaunchKernelGGL((gemmQ40Kernel<M_, E>), grid, dim3(kThreads), lds, s, ga);         \
         return;                                                                               \
     }
