@@ -615,7 +615,7 @@ class HipEngineImpl : public HipEngine {
         return (size_t)(e && *e ? std::atoi(e) : 24) << 20;
     }
 
-    // Batched path (>= gemmMinTokens rows, Q40): per chunk of <= 32 tokens, a norm kernel (f32 ->
+    // Batched path (>= gemmMinTokens rows, Q40): per chunk of <= 64 tokens, a norm kernel (f32 ->
     // f16, RESNORM) or the producer's f16 rows (xh) feed the MFMA GEMM with the fused epilogue.
     void gemmBatched(const DevMat &m, int n, int epi, const float *in, int ldIn, const float *add, float *xNext,
                      const float *normW, const _Float16 *xh, float *out, int ldOut, _Float16 *outH,
@@ -809,7 +809,7 @@ class HipEngineImpl : public HipEngine {
         DL_HIP(hipGetLastError());
     }
 
-    static constexpr int kGemmMaxTokens = 32;
+    static constexpr int kGemmMaxTokens = 64;  // tokens per MFMA GEMM launch (one weight pass)
     _Float16 *dXh_ = nullptr, *dAttH_ = nullptr, *dHh_ = nullptr;
     float *dPart_ = nullptr;
     int *dGemmCnt_ = nullptr;

@@ -120,6 +120,8 @@ struct GemmArgs {
 void launchGemmQ40(const GemmArgs &a, int epi, hipStream_t s);
 int gemmSplits(int rows, int n);
 size_t gemmPartFloats(int rows, int n, int maxTokens);
+// token rows one GEMM launch of M (1..64) tokens reads from its f16 activation operand (16/32/64)
+int gemmTokenPad(int M);
 // Residual add + RMS norm (normW may be null: no norm) of M rows -> f16:
 // in/addIn/xNext [M][ldIn] f32 -> out [M][n] f16 (xNext = in + addIn when set).
 void launchNormF16(const GemvArgs &a, _Float16 *out, int M, hipStream_t s);

@@ -983,9 +983,11 @@ int gemmSplits(int rows, int n) {
     return S;
 }
 
+int gemmTokenPad(int M) { return M <= 16 ? 16 : M <= 32 ? 32 : 64; }
+
 size_t gemmPartFloats(int rows, int n, int maxTokens) {
     const int tiles = (rows + kGemmRows - 1) / kGemmRows, S = gemmSplits(rows, n);
-    const int mp = (maxTokens + 15) / 16 * 16;
+    const int mp = gemmTokenPad(maxTokens);
     return S > 1 ? (size_t)S * tiles * mp * kGemmRows : 0;
 }
 
@@ -1210,7 +1212,7 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
 
 void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
     const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
-    const int MT = ga.M <= 16 ? 1 : 2;
+    const int MT = gemmTokenPad(ga.M) / 16;
     const dim3 grid(tiles, ga.splits);
     const size_t lds = gemmLds(MT);
 #define DL_GEMM_CASE(M_, E)                                                                   \
@@ -1224,6 +1226,8 @@ void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
     DL_GEMM_CASE(1, EPI_ACT_F16)
     DL_GEMM_CASE(2, EPI_STORE) DL_GEMM_CASE(2, EPI_ACT) DL_GEMM_CASE(2, EPI_ACT_Q80) DL_GEMM_CASE(2, EPI_QKV)
     DL_GEMM_CASE(2, EPI_ACT_F16)
+    DL_GEMM_CASE(4, EPI_STORE) DL_GEMM_CASE(4, EPI_ACT) DL_GEMM_CASE(4, EPI_ACT_Q80) DL_GEMM_CASE(4, EPI_QKV)
+    DL_GEMM_CASE(4, EPI_ACT_F16)
 #undef DL_GEMM_CASE
 }
 

@@ -168,7 +168,7 @@ std::vector<float> gemvQ40Q80In(const std::vector<uint8_t> &blocks, int rows, in
 
 std::vector<float> gemmQ40(const std::vector<uint8_t> &blocks, int rows, int n, const std::vector<float> &in,
                            const std::vector<float> &residual, const std::vector<float> &normW, float eps, int M) {
-    DL_CHECK(M >= 1 && M <= 32, "gemm tokens must be 1..32");
+    DL_CHECK(M >= 1 && M <= 64, "gemm tokens must be 1..64");
     DL_CHECK(in.size() == (size_t)M * n, "gemm input size");
     checkRows(residual, (size_t)M * n, "residual");
     checkRows(normW, (size_t)n, "norm weights");
@@ -181,7 +181,7 @@ std::vector<float> gemmQ40(const std::vector<uint8_t> &blocks, int rows, int n, 
     nq.addIn = sc.upload(residual);
     nq.normW = sc.upload(normW);
     nq.eps = eps;
-    _Float16 *xh = sc.alloc<_Float16>((size_t)((M + 15) / 16 * 16) * n);  // rows past M read as zeros
+    _Float16 *xh = sc.alloc<_Float16>((size_t)hipk::gemmTokenPad(M) * n);  // rows past M read as zeros
     hipk::launchNormF16(nq, xh, M, sc.s);
     hipk::GemmArgs g;
     g.e.qs = w.qs;
