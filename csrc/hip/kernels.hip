@@ -998,7 +998,7 @@ __host__ __device__ static constexpr int gemmStageBytes(int MT) { return kStW + 
 #define DL_GEMM_STAGES 2  // 3 stages (2 WGs/CU) measured slower: batch-32 8.1k vs 8.8k tok/s
 #endif
 static constexpr int kGemmStages = DL_GEMM_STAGES;  // stage buffers (kGemmStages-1 chunks in flight)
-static size_t gemmLds(int MT) { return kGemmStages * (size_t)gemmStageBytes(MT) + 16; }
+static size_t gemmLds(int MT, int stages) { return stages * (size_t)gemmStageBytes(MT) + 16; }
 
 // 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d via the 0x6400 | q magic (1024 + q)
 __device__ __forceinline__ half8 dequantQ40x8(u32x2 wv, int nibHi, uint32_t d16) {
@@ -1033,7 +1033,9 @@ __device__ __forceinline__ void glds4(const void *g, void *lds) {
                                          reinterpret_cast<uintptr_t>(lds)), 4, 0, 0);
 }
 
-template <int MT, int EPI>
+// STG = stage buffers: 2 double-buffers the chunk stream inside a workgroup; 1 (the 64-token
+// tile) drops that to fit 3 workgroups per CU, which then overlap each other's loads.
+template <int MT, int EPI, int STG>
 __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     const GemvArgs &a = ga.e;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1041,7 +1043,7 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     constexpr int SB = gemmStageBytes(MT);
     constexpr int NW = kGemmRows * kGemmCh / kThreads, NX = MT * 16 * kGemmCh * 4 / kThreads;
     constexpr int NLD = NW + 1 + NX;  // glds instructions per thread per stage
-    int *flag = reinterpret_cast<int *>(smem + kGemmStages * SB);
+    int *flag = reinterpret_cast<int *>(smem + STG * SB);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int col = lane & 15, h = lane >> 4;
     const int n = a.n, nb = n >> 5, L = a.lanes, NG = kThreads / L, KS = (nb + L - 1) / L;
@@ -1099,10 +1101,10 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     const int rl = wave * 16 + col;  // this lane's weight row (local)
     const int byteHalf = h & 1, nibHi = h >> 1;
 
-    constexpr int PF = kGemmStages - 1;  // chunks in flight ahead of the one consumed
+    constexpr int PF = STG - 1;  // chunks in flight ahead of the one consumed
     for (int c = 0; c < PF && c < nch; c++) issue(c, c);
     for (int c = 0; c < nch; c++) {
-        if (c + PF < nch) issue(c + PF, (c + PF) % kGemmStages);
+        if (c + PF < nch) issue(c + PF, (c + PF) % STG);
         // wait until chunk c landed (this thread): the chunks issued after it may stay in flight
         const int after = min(nch - 1, c + PF) - c;
         if (after >= 2)
@@ -1112,7 +1114,7 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // ... and for every thread
-        const char *st = smem + (c % kGemmStages) * SB;
+        const char *st = smem + (c % STG) * SB;
         const int cn = min(kGemmCh, bps - c * kGemmCh);
 #pragma unroll
         for (int jj = 0; jj < kGemmCh; jj++) {
@@ -1129,7 +1131,7 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // stage c % kGemmStages is refilled at iteration c + 1
+        __builtin_amdgcn_s_barrier();  // stage c % STG is refilled at iteration c + 1
     }
 
     float *tile = reinterpret_cast<float *>(smem);  // [MP][64], stages are free now
@@ -1210,24 +1212,32 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     }
 }
 
+static int gemmStages4() {  // stage buffers of the 64-token tile (DL_GEMM_STG4, read once)
+    static const int v = [] {
+        const char *e = std::getenv("DL_GEMM_STG4");
+        return e && std::atoi(e) == 2 ? 2 : 1;
+    }();
+    return v;
+}
+
 void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
     const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
     const int MT = gemmTokenPad(ga.M) / 16;
+    const int stg = MT == 4 ? gemmStages4() : kGemmStages;
     const dim3 grid(tiles, ga.splits);
-    const size_t lds = gemmLds(MT);
-#define DL_GEMM_CASE(M_, E)                                                                   \
-    if (MT == M_ && epi == E) {                                                               \
-        static const bool ldsOk = (allowLds((const void *)gemmQ40Kernel<M_, E>, lds), true); \
-        (void)ldsOk;                                                                          \
-        hipLaunchKernelGGL((gemmQ40Kernel<M_, E>), grid, dim3(kThreads), lds, s, ga);         \
-        return;                                                                               \
+    const size_t lds = gemmLds(MT, stg);
+#define DL_GEMM_CASE(M_, E, G)                                                                    \
+    if (MT == M_ && epi == E && stg == G) {                                                       \
+        static const bool ldsOk = (allowLds((const void *)gemmQ40Kernel<M_, E, G>, lds), true);  \
+        (void)ldsOk;                                                                              \
+        hipLaunchKernelGGL((gemmQ40Kernel<M_, E, G>), grid, dim3(kThreads), lds, s, ga);         \
+        return;                                                                                   \
     }
-    DL_GEMM_CASE(1, EPI_STORE) DL_GEMM_CASE(1, EPI_ACT) DL_GEMM_CASE(1, EPI_ACT_Q80) DL_GEMM_CASE(1, EPI_QKV)
-    DL_GEMM_CASE(1, EPI_ACT_F16)
-    DL_GEMM_CASE(2, EPI_STORE) DL_GEMM_CASE(2, EPI_ACT) DL_GEMM_CASE(2, EPI_ACT_Q80) DL_GEMM_CASE(2, EPI_QKV)
-    DL_GEMM_CASE(2, EPI_ACT_F16)
-    DL_GEMM_CASE(4, EPI_STORE) DL_GEMM_CASE(4, EPI_ACT) DL_GEMM_CASE(4, EPI_ACT_Q80) DL_GEMM_CASE(4, EPI_QKV)
-    DL_GEMM_CASE(4, EPI_ACT_F16)
+#define DL_GEMM_CASES(M_, G)                                                                      \
+    DL_GEMM_CASE(M_, EPI_STORE, G) DL_GEMM_CASE(M_, EPI_ACT, G) DL_GEMM_CASE(M_, EPI_ACT_Q80, G)  \
+    DL_GEMM_CASE(M_, EPI_QKV, G) DL_GEMM_CASE(M_, EPI_ACT_F16, G)
+    DL_GEMM_CASES(1, kGemmStages) DL_GEMM_CASES(2, kGemmStages) DL_GEMM_CASES(4, 1) DL_GEMM_CASES(4, 2)
+#undef DL_GEMM_CASES
 #undef DL_GEMM_CASE
 }
 
