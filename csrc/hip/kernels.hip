@@ -1228,10 +1228,19 @@ static int gemmStages2() {  // stage buffers of the 32-token tile (DL_GEMM_STG2,
     return v;
 }
 
+static int gemmStages1() {  // stage buffers of the 16-token tile (DL_GEMM_STG1 = 2..4, read once)
+    static const int v = [] {
+        const char *e = std::getenv("DL_GEMM_STG1");
+        const int k = e ? std::atoi(e) : kGemmStages;
+        return k >= 2 && k <= 4 ? k : kGemmStages;
+    }();
+    return v;
+}
+
 void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
     const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
     const int MT = gemmTokenPad(ga.M) / 16;
-    const int stg = MT == 4 ? gemmStages4() : MT == 2 ? gemmStages2() : kGemmStages;
+    const int stg = MT == 4 ? gemmStages4() : MT == 2 ? gemmStages2() : gemmStages1();
     const dim3 grid(tiles, ga.splits);
     const size_t lds = gemmLds(MT, stg);
 #define DL_GEMM_CASE(M_, E, G)                                                                    \
@@ -1244,7 +1253,7 @@ void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
 #define DL_GEMM_CASES(M_, G)                                                                      \
     DL_GEMM_CASE(M_, EPI_STORE, G) DL_GEMM_CASE(M_, EPI_ACT, G) DL_GEMM_CASE(M_, EPI_ACT_Q80, G)  \
     DL_GEMM_CASE(M_, EPI_QKV, G) DL_GEMM_CASE(M_, EPI_ACT_F16, G)
-    DL_GEMM_CASES(1, kGemmStages) DL_GEMM_CASES(2, kGemmStages) DL_GEMM_CASES(2, 1) DL_GEMM_CASES(4, 1) DL_GEMM_CASES(4, 2)
+    DL_GEMM_CASES(1, kGemmStages) DL_GEMM_CASES(1, 3) DL_GEMM_CASES(1, 4) DL_GEMM_CASES(2, kGemmStages) DL_GEMM_CASES(2, 1) DL_GEMM_CASES(4, 1) DL_GEMM_CASES(4, 2)
 #undef DL_GEMM_CASES
 #undef DL_GEMM_CASE
 }
