@@ -90,6 +90,11 @@ struct Api {
         }
         const int promptTokens = (int)prompt.size();
         auto r = sched->submit(std::move(prompt), p);
+        // if this handler unwinds early (client gone: a write throws), stop generating for it
+        struct CancelOnExit {
+            GenRequest *r;
+            ~CancelOnExit() { r->cancel(); }
+        } cancelGuard{r.get()};
         const std::string id = "chatcmpl-" + std::to_string(r->id);
         const long created = (long)std::time(nullptr);
         if (stream) {
@@ -188,6 +193,8 @@ struct Api {
         metric("dllama_decode_rows_total", "counter", "Decode token rows.", (double)s.decodeRows);
         metric("dllama_requests_completed_total", "counter", "Finished requests.", (double)s.completed);
         metric("dllama_generated_tokens_total", "counter", "Tokens generated for finished requests.", (double)s.generatedTokens);
+        metric("dllama_requests_cancelled_total", "counter", "Requests dropped after their client disconnected.",
+               (double)s.cancelled);
         metric("dllama_busy_seconds_total", "counter", "Time spent in forward passes.", s.busyMs / 1000.0);
         metric("dllama_active_requests", "gauge", "Requests holding a KV slot.", (double)s.active);
         metric("dllama_queued_requests", "gauge", "Requests waiting for a KV slot.", (double)s.queued);
@@ -212,6 +219,7 @@ struct Api {
         v.set("prefill_rows", (double)s.prefillRows);
         v.set("decode_rows", (double)s.decodeRows);
         v.set("completed", (double)s.completed);
+        v.set("cancelled", (double)s.cancelled);
         v.set("generated_tokens", (double)s.generatedTokens);
         v.set("busy_ms", s.busyMs);
         conn.writeJson(200, v.dump());

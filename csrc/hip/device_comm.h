@@ -14,6 +14,10 @@
 
 namespace dl {
 
+namespace hipk {
+struct TpXchg;
+}
+
 class DeviceComm {
   public:
     virtual ~DeviceComm() = default;
@@ -29,6 +33,14 @@ class DeviceComm {
     virtual std::string asyncError() { return ""; }
     // Release the communicator without waiting for peers (used after an error).
     virtual void shutdownNow() {}
+    // Targets of the exchange fused into producer kernels (hipk::TpXchg): region 0 = residual
+    // partial sums (elements b * dim + row, up to 65536), region 1 = argmax winners (2 words per
+    // row). False when the transport has none (RCCL): the engine launches separate collectives.
+    virtual bool fusedXchg(int region, hipk::TpXchg *x) const {
+        (void)region;
+        (void)x;
+        return false;
+    }
 };
 
 // 128-byte RCCL unique id (generated on rank 0, distributed over the control plane).

@@ -74,6 +74,14 @@ class HipEngineImpl : public HipEngine {
         DL_CHECK(h_.headSize() == 64 || h_.headSize() == 128, "GPU kernels support head size 64 or 128");
         DL_CHECK(cfg.maxBatch >= 1 && cfg.nSlots >= 1, "maxBatch/nSlots");
         kvBf16_ = cfg.kvBf16;
+        syncQ80_ = cfg.syncType == FloatType::Q80;
+        if (comm_ && plan_.nRanks > 1) {
+            const char *e = std::getenv("DL_TP_FUSED");  // 0: separate all-reduce kernels (comparison)
+            tpFused_ = !(e && *e == '0') && comm_->fusedXchg(0, &tpVec_) && comm_->fusedXchg(1, &tpArg_) &&
+                       (size_t)std::min<u32>(cfg.maxBatch, 4) * h_.dim <= (size_t)tpVec_.stride &&
+                       (size_t)2 * cfg.maxBatch <= (size_t)tpArg_.stride;
+            tpVec_.q80 = syncQ80_ ? 1 : 0;
+        }
         allocBuffers();
         if (cfg.synthetic)
             loadSynthetic();
@@ -548,10 +556,12 @@ class HipEngineImpl : public HipEngine {
         return hipk::gemvDefaultPasses(m.n, m.rows, B, q40_, epi);
     }
 
-    // Launch a GEMV over all n rows, in batch chunks of <= 4.
+    // Launch a GEMV over all n rows, in batch chunks of <= 4. tp: all-reduce the EPI_STORE output
+    // over the tensor-parallel ranks in the kernel tail (fused exchange).
     void gemv(const DevMat &m, int n, int pro, int epi, const float *in, int ldIn, const float *add, float *xNext,
               const float *normW, float *out, int ldOut, const DevLayer *L, const int8_t *aq = nullptr,
-              const float2 *as = nullptr, int8_t *oq = nullptr, float2 *os = nullptr) {
+              const float2 *as = nullptr, int8_t *oq = nullptr, float2 *os = nullptr, bool tp = false) {
+        if (tp) epi = hipk::EPI_STORE_TP;
         const int bcMax = batchChunk(m, pro, epi);
         for (int c0 = 0; c0 < n;) {
             int bc = n - c0;
@@ -565,6 +575,11 @@ class HipEngineImpl : public HipEngine {
             a.n = m.n;
             a.passes = passesFor(m, epi, bc);
             a.lanes = m.lanes;
+            if (tp) {
+                a.tp = tpVec_;
+                if (tpVec_.q80)  // whole Q80 blocks of 32 rows per workgroup
+                    while ((256 / m.lanes * 2 * a.passes) % 32) a.passes++;
+            }
             a.in = in ? in + (size_t)c0 * ldIn : nullptr;
             a.aq = aq ? aq + (size_t)c0 * m.n : nullptr;
             a.as = as ? as + (size_t)c0 * (m.n / 32) : nullptr;
@@ -667,12 +682,17 @@ class HipEngineImpl : public HipEngine {
         }
     }
 
+    // Separate all-reduce of partial sums (batched path, RCCL, f32 weights). Q80 sync: every rank's
+    // partial is first rounded through Q80 blocks, as the reference's ZQ cast (llm.cpp:308-314).
     void allReduce(float *buf, size_t count) {
         if (plan_.nRanks > 1) {
             ProfScope ps(this, "allreduce");
+            if (syncQ80_) hipk::launchQ80Roundtrip(buf, count, stream_);
             comm_->allReduceSum(buf, count, stream_);
         }
     }
+    // Decode rows (GEMV path, Q40) exchange their wo / w2 partials inside the GEMV tail.
+    bool fusedTp(bool bat) const { return tpFused_ && !bat && q40_; }
 
     void enqueueForward(int n, GraphKind kind) {
         const ShardPlan &p = plan_;
@@ -742,9 +762,9 @@ class HipEngineImpl : public HipEngine {
                                 nullptr, nullptr);
                 else
                     gemv(L.wo, n, hipk::PRO_GLOBAL, hipk::EPI_STORE, q40_ ? nullptr : dAtt_, p.q0, nullptr, nullptr,
-                         nullptr, dY_, dim, nullptr, dAttQ_, dAttS_);
+                         nullptr, dY_, dim, nullptr, dAttQ_, dAttS_, nullptr, nullptr, fusedTp(bat));
             }
-            allReduce(dY_, (size_t)n * dim);
+            if (!fusedTp(bat)) allReduce(dY_, (size_t)n * dim);
             // Q80 hand-off of h needs one workgroup per 32 hidden units; for skinny TP shards the
             // w13 epilogue emits f32 and w2 quantizes in its prologue instead.
             const bool hQ80 = q40_ && p.hidden0 / 32 >= 192;
@@ -765,12 +785,12 @@ class HipEngineImpl : public HipEngine {
                                 nullptr, nullptr);
                 else if (hQ80 || !q40_)
                     gemv(L.w2, n, hipk::PRO_GLOBAL, hipk::EPI_STORE, q40_ ? nullptr : dH_, p.hidden0, nullptr,
-                         nullptr, nullptr, dY_, dim, nullptr, dHQ_, dHS_);
+                         nullptr, nullptr, dY_, dim, nullptr, dHQ_, dHS_, nullptr, nullptr, fusedTp(bat));
                 else
                     gemv(L.w2, n, hipk::PRO_RESNORM, hipk::EPI_STORE, dH_, p.hidden0, nullptr, nullptr, nullptr, dY_,
-                         dim, nullptr);
+                         dim, nullptr, nullptr, nullptr, nullptr, nullptr, fusedTp(bat));
             }
-            allReduce(dY_, (size_t)n * dim);
+            if (!fusedTp(bat)) allReduce(dY_, (size_t)n * dim);
         }
         {
             ProfScope ps(this, "gemv_logits");
@@ -782,7 +802,11 @@ class HipEngineImpl : public HipEngine {
                      p.vocab0, nullptr);
         }
         const float *full = dLogits_;
-        if (p.nRanks > 1) {
+        // greedy rows on a fused TP data plane: each rank reduces its own vocab slice and only the
+        // (value, index) winners cross the links (reference: logits gathered to the root,
+        // llm.cpp:432); the full logits are gathered only when the host samples them
+        const bool distArgmax = tpFused_ && kind != GraphKind::LOGITS;
+        if (p.nRanks > 1 && !distArgmax) {
             ProfScope ps(this, "allgather");
             comm_->allGather(dLogits_, dLogitsAll_, (size_t)n * p.vocab0, stream_);
             hipk::launchUnshardLogits(dLogitsAll_, dLogitsFull_, p.nRanks, n, p.vocab0, stream_);
@@ -793,6 +817,11 @@ class HipEngineImpl : public HipEngine {
             hipk::ArgmaxArgs g;
             g.logits = full;
             g.vocab = h_.vocabSize;
+            if (distArgmax) {
+                g.vocab = p.vocab0;
+                g.vocabStart = p.vocabStart();
+                g.tp = tpArg_;
+            }
             g.ids = dIds_;
             g.partV = dArgV_;
             g.partI = dArgI_;
@@ -822,7 +851,8 @@ class HipEngineImpl : public HipEngine {
     std::unique_ptr<ModelFile> file_;
     ModelHeader h_;
     ShardPlan plan_;
-    bool q40_ = true, kvBf16_ = true;
+    bool q40_ = true, kvBf16_ = true, syncQ80_ = false, tpFused_ = false;
+    hipk::TpXchg tpVec_, tpArg_;
     std::vector<void *> allocs_, hostAllocs_;
     size_t deviceBytes_ = 0;
     std::vector<DevLayer> layers_;

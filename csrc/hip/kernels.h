@@ -26,7 +26,8 @@ namespace hipk {
 //             (normW == null: no norm, plain quantization of `in`).
 enum Prologue : int { PRO_GLOBAL = 0, PRO_RESNORM = 1 };
 // EPI_ACT_Q80: act(w1 x) * (w3 x), quantized to Q80 blocks for the next GEMV (32 hidden units/block).
-enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2, EPI_ACT_Q80 = 3, EPI_ACT_F16 = 4 };
+// EPI_STORE_TP: EPI_STORE whose rows are first all-reduced over the tensor-parallel ranks (GemvArgs::tp).
+enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2, EPI_ACT_Q80 = 3, EPI_ACT_F16 = 4, EPI_STORE_TP = 5 };
 
 // Q40 weights live on the device TILED in the ring GEMV's consumption order, for a lanes-per-row
 // count L fixed per matrix (NG = 256/L row pairs per workgroup pass, K = ceil(nb/L) steps):
@@ -66,6 +67,28 @@ struct AttnArgs {
     int pfBlocks = 0;
 };
 
+// Tensor-parallel partial-sum exchange fused into the tail of the kernel that produces the partial
+// (wo / w2 GEMV, argmax), replacing a separate all-reduce kernel per residual update (reference:
+// cast to the ZQ pipe + SYNC_NODE_SLICES + merge-add, llm.cpp:308-314, nn-network.cpp:537-569).
+// Every rank pushes its values straight into each peer's receive region as 8-byte words
+// {payload u32, epoch u32} (one atomic store carries data and flag: no fence, no flag word, no
+// remote read), then polls its own region until every peer's word carries the current epoch and
+// sums all ranks' values in rank order, so every rank gets bitwise the same result. The regions
+// live in uncached device memory (xgmi_comm.cpp), so a poll always reads HBM, never a stale line.
+// Receive layout: recv[p] + (parity * world + sender) * stride + word; parity = epoch & 1.
+// Epochs are per exchange element (per 32-element block in Q80 mode), counted on each rank in
+// local memory: every rank runs the same exchange sequence, so the epochs agree.
+constexpr int kTpMaxRanks = 16;
+struct TpXchg {
+    uint64_t *recv[kTpMaxRanks] = {};  // each rank's receive region (peer-mapped)
+    unsigned *epochs = nullptr;         // local per-element (per-block) epoch counters, zeroed
+    int *error = nullptr;               // local timeout flag (set when a peer never arrived)
+    long long stride = 0;               // words per (parity, sender)
+    long long timeoutTicks = 0;         // s_memrealtime ticks (100 MHz)
+    int rank = 0, world = 1;
+    int q80 = 0;                        // exchange Q80 blocks (the reference's ZQ wire format)
+};
+
 struct GemvArgs {
     // weights: Q40 tiled (see Q40Tiling; `lanes` must be the tiling's L) or F32 [rows][n]
     const uint8_t *qs = nullptr;
@@ -98,6 +121,9 @@ struct GemvArgs {
     void *kcache = nullptr;       // layer base: [slot][seqLen][kv0]
     void *vcache = nullptr;
     int kvBf16 = 1;
+    // EPI_STORE_TP (Q40 GEMV): the partial rows are all-reduced over the tensor-parallel ranks in
+    // the kernel tail before `out` is written (exchange element = b * ldOut + row)
+    TpXchg tp;
     // diagnostics (gemvQ40Kernel): when set, workgroup g writes 8 u64 at trace[8g..]: s_memrealtime
     // at entry, prologue done, exit, (HW_ID << 32 | XCC_ID), prologue loads landed (early path),
     // first ring slot consumed (thread 0's view)
@@ -159,7 +185,14 @@ struct ArgmaxArgs {
     int *counters = nullptr;
     int *tokens = nullptr, *pos = nullptr, *hist = nullptr;
     int seqLen = 0;
+    // tensor parallel: `logits` is this rank's vocab slice starting at vocabStart; the per-row
+    // (value, index) winners are exchanged (tp.world > 1) and every rank picks the same global one
+    TpXchg tp;
+    int vocabStart = 0;
 };
+// Round-trip f32 partial sums through Q80 blocks in place (the reference's ZQ cast before the
+// exchange) - used ahead of a plain all-reduce when the fused exchange is not available.
+void launchQ80Roundtrip(float *x, size_t n, hipStream_t s);
 void launchArgmax(const ArgmaxArgs &a, int B, hipStream_t s);
 // logits gathered rank-major [nRanks][B][vocab0] -> row-major [B][vocab]
 void launchUnshardLogits(const float *in, float *out, int nRanks, int B, int vocab0, hipStream_t s);

@@ -420,6 +420,148 @@ __device__ __forceinline__ void stageQ80(const GemvArgs &a, int8_t *sq, float2 *
     __syncthreads();
 }
 
+// ------------------------------------------------------------------------------------------------
+// Fused tensor-parallel exchange (TpXchg, kernels.h). Peer words are 8-byte {payload, epoch}
+// granules in uncached memory: one relaxed system-scope store publishes data and flag together,
+// a relaxed system-scope load polls them (cdna_hip_programming.md Guideline 16 "R2": the data is
+// the flag, no fence needed); a wait gives up after tp.timeoutTicks and raises tp.error.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t tpLoad(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool tpFailed(const TpXchg &x) {
+    return __hip_atomic_load(x.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+}
+
+// Push `payload` as exchange word `w` (epoch e) to every peer, then collect word `w` of every rank
+// into vals[p] (this rank's own payload included). Peer loads are all issued before any wait.
+__device__ __forceinline__ void tpPushCollect(const TpXchg &x, long long w, unsigned e, unsigned payload,
+                                              unsigned (&vals)[kTpMaxRanks], bool failed) {
+    const int me = x.rank, W = x.world;
+    const long long par = e & 1;
+    const uint64_t word = (uint64_t)payload | ((uint64_t)e << 32);
+#pragma unroll
+    for (int p = 0; p < kTpMaxRanks; p++)
+        if (p < W && p != me)
+            __hip_atomic_store(x.recv[p] + (par * W + me) * x.stride + w, word, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t *mine = x.recv[me] + par * W * x.stride + w;
+    uint64_t got[kTpMaxRanks];
+#pragma unroll
+    for (int p = 0; p < kTpMaxRanks; p++) got[p] = (p < W && p != me) ? tpLoad(mine + p * x.stride) : word;
+#pragma unroll
+    for (int p = 0; p < kTpMaxRanks; p++) {
+        if (p < W) {
+            uint64_t v = got[p];
+            if ((unsigned)(v >> 32) != e && !failed) {
+                const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+                while ((unsigned)(v >> 32) != e) {
+                    __builtin_amdgcn_s_sleep(1);
+                    v = tpLoad(mine + p * x.stride);
+                    if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > x.timeoutTicks) {
+                        __hip_atomic_store(x.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        break;
+                    }
+                }
+            }
+            vals[p] = (unsigned)v;
+        }
+    }
+}
+
+// LDS bytes of the Q80 exchange staging for nEl elements over W ranks.
+__host__ __device__ static inline size_t tpQ80Lds(int nEl, int W) {
+    return alignUp((size_t)nEl, 16) + alignUp((size_t)nEl / 32 * 4, 16) + (size_t)W * (nEl / 32) * 9 * 4;
+}
+
+// f32 exchange of a workgroup's partial rows res[B][R] (rows rowBase..) -> a.out summed over ranks.
+template <int B>
+__device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *res, int R, int rowBase) {
+    const TpXchg &x = a.tp;
+    const bool failed = tpFailed(x);
+    for (int i = threadIdx.x; i < B * R; i += kThreads) {
+        const int b = i / R, row = rowBase + i % R;
+        if (row >= a.rows) continue;
+        const long long el = (long long)b * a.ldOut + row;
+        const unsigned e = x.epochs[el] + 1;
+        unsigned v[kTpMaxRanks];
+        tpPushCollect(x, el, e, __float_as_uint(res[i]), v, failed);
+        float s = 0.f;
+#pragma unroll
+        for (int p = 0; p < kTpMaxRanks; p++)
+            if (p < x.world) s += __uint_as_float(v[p]);
+        a.out[el] = s;
+        x.epochs[el] = e;
+    }
+}
+
+// Q80 exchange (the reference's ZQ pipe: every rank's partial quantized once to Q80 blocks of 32
+// rows, all ranks' blocks dequantized and summed in rank order, own included). R and rowBase are
+// multiples of 32. A block travels as 9 words: 8 x 4 int8 + the f16 scale. `lds` = free staging.
+template <int B>
+__device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *res, int R, int rowBase, char *lds) {
+    const TpXchg &x = a.tp;
+    const int nEl = B * R, nBlk = nEl >> 5, W = x.world;
+    int8_t *q8 = reinterpret_cast<int8_t *>(lds);
+    uint32_t *dq = reinterpret_cast<uint32_t *>(lds + alignUp((size_t)nEl, 16));
+    uint32_t *rv = reinterpret_cast<uint32_t *>(lds + alignUp((size_t)nEl, 16) + alignUp((size_t)nBlk * 4, 16));
+    const bool failed = tpFailed(x);
+    // 1. quantize this rank's partial (whole 32-lane groups per block: the loop is uniform)
+    for (int base = 0; base < nEl; base += kThreads) {
+        const int i = base + threadIdx.x;
+        const float v = i < nEl ? res[i] : 0.f;
+        const float amax = groupMax<32>(fabsf(v));
+        const float d = amax / 127.0f;
+        const float id = d != 0.f ? 1.0f / d : 0.f;
+        int q = (int)rintf(v * id);
+        q = q > 127 ? 127 : (q < -127 ? -127 : q);
+        if (i < nEl) {
+            q8[i] = (int8_t)q;
+            if ((i & 31) == 0) dq[i >> 5] = __half_as_ushort(__float2half(d));
+        }
+    }
+    __syncthreads();
+    auto blockId = [&](int blk, bool &live) -> long long {  // global block id in the exchange space
+        const int b = (blk * 32) / R, row = rowBase + (blk * 32) % R;
+        live = row < a.rows;
+        return ((long long)b * a.ldOut + row) >> 5;
+    };
+    // 2. push / collect the 9 words of every block
+    for (int j = threadIdx.x; j < nBlk * 9; j += kThreads) {
+        const int blk = j / 9, w = j % 9;
+        bool live;
+        const long long gb = blockId(blk, live);
+        if (!live) continue;
+        const unsigned e = x.epochs[gb] + 1;
+        const unsigned payload = w < 8 ? reinterpret_cast<const uint32_t *>(q8)[blk * 8 + w] : dq[blk];
+        unsigned v[kTpMaxRanks];
+        tpPushCollect(x, gb * 9 + w, e, payload, v, failed);
+#pragma unroll
+        for (int p = 0; p < kTpMaxRanks; p++)
+            if (p < W) rv[(p * nBlk + blk) * 9 + w] = v[p];
+    }
+    __syncthreads();
+    // 3. dequantize and sum in rank order
+    for (int i = threadIdx.x; i < nEl; i += kThreads) {
+        const int b = i / R, row = rowBase + i % R, blk = i >> 5;
+        if (row >= a.rows) continue;
+        float s = 0.f;
+        for (int p = 0; p < W; p++) {
+            const uint32_t *bw = rv + (p * nBlk + blk) * 9;
+            const float d = __half2float(__ushort_as_half((uint16_t)(bw[8] & 0xFFFFu)));
+            const int q = (int)(int8_t)(bw[(i & 31) >> 2] >> (8 * (i & 3)));
+            s += (float)q * d;
+        }
+        a.out[(size_t)b * a.ldOut + row] = s;
+    }
+    // 4. advance the block epochs (every word of step 2 has read them)
+    for (int blk = threadIdx.x; blk < nBlk; blk += kThreads) {
+        bool live;
+        const long long gb = blockId(blk, live);
+        if (live) x.epochs[gb] += 1;
+    }
+}
+
 // Sequence split of a decode-attention row of length `len`: nSplit chunks of ch positions
 // (~256 per chunk, at most splitGrid chunks).
 __device__ __forceinline__ void attnSplit(int len, int splitGrid, int &nSplit, int &ch) {
@@ -458,6 +600,8 @@ __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
     float *hbuf = reinterpret_cast<float *>(smem + lay.hbuf);
     int8_t *sq = reinterpret_cast<int8_t *>(smem + lay.act);
     float2 *ssc = reinterpret_cast<float2 *>(smem + lay.sc);
+    float *res = reinterpret_cast<float *>(smem + lay.res);  // partial rows held for the TP exchange
+    constexpr bool tpx = EPI == EPI_STORE_TP;
     const int tid = threadIdx.x, gi = tid / L, li = tid % L;
     const int rowBase = blockIdx.x * R;
     // timestamps stay in SGPRs until the end: a store here would join the ring's vmcnt accounting
@@ -700,7 +844,10 @@ __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
 #pragma unroll
             for (int b = 0; b < B; b++) {
                 const float v0 = acc[0][b], v1 = acc[1][b];
-                if constexpr (EPI == EPI_STORE) {
+                if constexpr (EPI == EPI_STORE_TP) {
+                    res[b * R + (r0 - rowBase)] = v0;
+                    res[b * R + (r0 - rowBase) + 1] = v1;
+                } else if constexpr (EPI == EPI_STORE) {
                     float *o = a.out + (size_t)b * a.ldOut + r0;
                     o[0] = v0;
                     if (r0 + 1 < a.rows) o[1] = v1;
@@ -767,6 +914,11 @@ __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
     if constexpr (EPI == EPI_ACT_Q80) {
         __syncthreads();
         storeHiddenQ80<B>(a, hbuf, R >> 1, rowBase >> 1);
+    }
+    if constexpr (tpx) {  // all-reduce the partial rows over the TP ranks, then store (sq is free now)
+        __syncthreads();
+        if (a.tp.q80) tpExchangeQ80<B>(a, res, R, rowBase, reinterpret_cast<char *>(sq));
+        else tpExchangeF32<B>(a, res, R, rowBase);
     }
     if (a.trace) {
         __syncthreads();
@@ -905,6 +1057,8 @@ static void gemvDispatchPE(const GemvArgs &a, int pro, int epi, size_t lds, int 
     DL_GEMV_CASE(PRO_RESNORM, EPI_ACT)
     if constexpr (Q40) {
         DL_GEMV_CASE(PRO_RESNORM, EPI_ACT_Q80)
+        DL_GEMV_CASE(PRO_GLOBAL, EPI_STORE_TP)
+        DL_GEMV_CASE(PRO_RESNORM, EPI_STORE_TP)
     }
 #undef DL_GEMV_CASE
 }
@@ -923,7 +1077,11 @@ void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_
     const int L = a.lanes > 0 ? a.lanes : gemvLanesPerRow(a.n, a.rows, B, q40);
     const int R = (kThreads / L) * gemvRowGroup(B, q40) * a.passes;
     const int grid = (a.rows + R - 1) / R;
-    const size_t lds = gemvLdsBytes(a.n, B, q40, R, pro);
+    size_t lds = gemvLdsBytes(a.n, B, q40, R, pro);
+    if (q40 && epi == EPI_STORE_TP && a.tp.q80) {  // Q80 exchange staging reuses `act`
+        const GemvLds lay = gemvLayout(a.n, B, true, R, PRO_RESNORM);
+        lds = std::max(lds, lay.act + tpQ80Lds(B * R, a.tp.world));
+    }
     if (q40) {
         switch (L) {
             case 16: gemvDispatchB<16, true>(a, B, pro, epi, lds, grid, s); break;
@@ -1107,7 +1265,9 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
         if (c + PF < nch) issue(c + PF, (c + PF) % STG);
         // wait until chunk c landed (this thread): the chunks issued after it may stay in flight
         const int after = min(nch - 1, c + PF) - c;
-        if (after >= 2)
+        if (after >= 3)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * NLD) : "memory");
+        else if (after == 2)
             asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * NLD) : "memory");
         else if (after == 1)
             asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NLD) : "memory");
@@ -1245,8 +1405,7 @@ void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
     const size_t lds = gemmLds(MT, stg);
 #define DL_GEMM_CASE(M_, E, G)                                                                    \
     if (MT == M_ && epi == E && stg == G) {                                                       \
-        static const bool ldsOk = (allowLds((const void *)gemmQ40Kernel<M_, E, G>, lds), true);  \
-        (void)ldsOk;                                                                              \
+        if (lds > 65536) allowLds((const void *)gemmQ40Kernel<M_, E, G>, lds); /* per device */  \
         hipLaunchKernelGGL((gemmQ40Kernel<M_, E, G>), grid, dim3(kThreads), lds, s, ga);         \
         return;                                                                                   \
     }
@@ -1805,6 +1964,20 @@ __global__ __launch_bounds__(256) void argmaxKernel(ArgmaxArgs a) {
     for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x)
         argBetter(bv, bi, a.partV[b * kArgmaxBlocks + i], a.partI[b * kArgmaxBlocks + i]);
     blockArgmax(bv, bi, sv, si);
+    if (threadIdx.x == 0 && a.tp.world > 1) {
+        // tensor parallel: every rank offers its slice's winner (value, global index); all ranks
+        // pick the same one in rank order (ties -> lowest index, like a full-vocabulary argmax)
+        const TpXchg &x = a.tp;
+        const bool failed = tpFailed(x);
+        const unsigned e = x.epochs[b] + 1;
+        unsigned vv[kTpMaxRanks], vi[kTpMaxRanks];
+        tpPushCollect(x, 2LL * b, e, __float_as_uint(bv), vv, failed);
+        tpPushCollect(x, 2LL * b + 1, e, (unsigned)(bi + a.vocabStart), vi, failed);
+        bv = -INFINITY;
+        bi = 0x7fffffff;
+        for (int p = 0; p < x.world; p++) argBetter(bv, bi, __uint_as_float(vv[p]), (int)vi[p]);
+        x.epochs[b] = e;
+    }
     if (threadIdx.x == 0) {
         a.ids[b] = bi;
         if (a.tokens) {
@@ -1818,6 +1991,23 @@ __global__ __launch_bounds__(256) void argmaxKernel(ArgmaxArgs a) {
 
 void launchArgmax(const ArgmaxArgs &a, int B, hipStream_t s) {
     hipLaunchKernelGGL(argmaxKernel, dim3(kArgmaxBlocks, B), dim3(256), 0, s, a);
+}
+
+// In-place Q80 round trip of f32 values (32-element blocks, rintf like every Q80 producer here).
+__global__ void q80RoundtripKernel(float *x, size_t n) {
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;  // n % 32 == 0: whole groups
+    const float v = i < n ? x[i] : 0.f;
+    const float amax = groupMax<32>(fabsf(v));
+    const float d = amax / 127.0f;
+    const float id = d != 0.f ? 1.0f / d : 0.f;
+    int q = (int)rintf(v * id);
+    q = q > 127 ? 127 : (q < -127 ? -127 : q);
+    if (i < n) x[i] = (float)q * __half2float(__float2half(d));
+}
+
+void launchQ80Roundtrip(float *x, size_t n, hipStream_t s) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(q80RoundtripKernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, n);
 }
 
 __global__ void unshardKernel(const float *in, float *out, int nRanks, int B, int vocab0) {

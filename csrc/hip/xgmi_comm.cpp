@@ -22,6 +22,14 @@
 // buffers alternate by epoch parity per chunk; a rank can only write epoch e+2 into a peer's
 // buffer after finishing call e+1, which needed that peer's e+1 data, which the peer only sends
 // after it finished reading epoch e.
+// Memory: the whole shared region is allocated UNCACHED (hipDeviceMallocUncached): every flag poll,
+// LL word poll and remote read goes to HBM instead of a cache line that a peer's xGMI write does
+// not invalidate (a plain coarse-grained hipMalloc would let a local L2 line go stale while the
+// peer writes the HBM copy). Writers use system-scope atomic stores, readers system-scope atomic
+// loads, so neither side depends on cache maintenance; DL_XGMI_CACHED=1 selects plain hipMalloc
+// for comparison runs only.
+// Fused-exchange regions (TpXchg in kernels.h): producer kernels (wo / w2 GEMV tails, argmax)
+// push their partials straight into these, so TP decode needs no separate all-reduce kernel.
 // Elements are owned by fixed slots: chunk c (kChunk floats) belongs to slot c % kSlots, for
 // every message size, so a slot only ever races with the same slot on other ranks. Protocol per
 // call and slot (workgroup g): e = ++epochs[g]; write my chunks to pub[e&1]; release (system);
@@ -37,6 +45,7 @@
 
 #include "../core/common.h"
 #include "device_comm.h"
+#include "kernels.h"
 
 namespace dl {
 
@@ -48,6 +57,9 @@ constexpr int kMaxRanks = 16;
 constexpr int kThreads = 256;
 constexpr int kLLMax = 16384;       // largest LL all-reduce (floats per rank)
 constexpr int kLLSlots = kLLMax / kChunk;
+constexpr long long kFusedVec = 1 << 16;   // fused residual exchange: words per (parity, sender)
+constexpr long long kFusedArg = 2048;      // fused argmax exchange: 2 words per batch row
+constexpr long long kTimeoutTicks = 200LL * 1000 * 1000;  // 2 s at 100 MHz
 
 struct XgmiPeers {
     float *pub[kMaxRanks];          // each rank's pub base (pub[p] + parity * maxFloats)
@@ -228,9 +240,17 @@ class XgmiComm : public DeviceComm {
         flagsBytes_ = (size_t)kMaxRanks * kSlots * sizeof(int);
         llOff_ = (pubBytes_ + flagsBytes_ + kSlots * sizeof(int) + 64 + 255) / 256 * 256;
         const size_t llBytes = (size_t)2 * kMaxRanks * kLLMax * sizeof(uint64_t);
-        const size_t total = llOff_ + llBytes + kLLSlots * sizeof(unsigned);
-        DL_HIP(hipMalloc(&base_, total));
+        fvOff_ = (llOff_ + llBytes + kLLSlots * sizeof(unsigned) + 255) / 256 * 256;
+        faOff_ = fvOff_ + (size_t)2 * world * kFusedVec * sizeof(uint64_t);
+        const size_t total = faOff_ + (size_t)2 * world * kFusedArg * sizeof(uint64_t);
+        const char *cached = std::getenv("DL_XGMI_CACHED");
+        if (cached && *cached == '1')
+            DL_HIP(hipMalloc(&base_, total));
+        else
+            DL_HIP(hipExtMallocWithFlags(&base_, total, hipDeviceMallocUncached));
         DL_HIP(hipMemset(base_, 0, total));
+        DL_HIP(hipMalloc(&fusedEpochs_, (kFusedVec + kFusedArg) * sizeof(unsigned)));
+        DL_HIP(hipMemset(fusedEpochs_, 0, (kFusedVec + kFusedArg) * sizeof(unsigned)));
         DL_HIP(hipDeviceSynchronize());
         epochs_ = reinterpret_cast<int *>(static_cast<char *>(base_) + pubBytes_ + flagsBytes_);
         error_ = epochs_ + kSlots;
@@ -243,6 +263,7 @@ class XgmiComm : public DeviceComm {
         for (int p = 0; p < world_; p++)
             if (p != rank_ && peerBase_[p]) (void)hipIpcCloseMemHandle(peerBase_[p]);
         if (base_) (void)hipFree(base_);
+        if (fusedEpochs_) (void)hipFree(fusedEpochs_);
     }
     const std::string &handle() const { return handle_; }
     // handles[p] = rank p's handle() bytes; call on every rank after all ranks were created.
@@ -260,6 +281,8 @@ class XgmiComm : public DeviceComm {
             peers_.pub[p] = static_cast<float *>(peerBase_[p]);
             peers_.flags[p] = reinterpret_cast<int *>(static_cast<char *>(peerBase_[p]) + pubBytes_);
             peers_.ll[p] = reinterpret_cast<uint64_t *>(static_cast<char *>(peerBase_[p]) + llOff_);
+            fusedVec_[p] = reinterpret_cast<uint64_t *>(static_cast<char *>(peerBase_[p]) + fvOff_);
+            fusedArg_[p] = reinterpret_cast<uint64_t *>(static_cast<char *>(peerBase_[p]) + faOff_);
         }
         connected_ = true;
     }
@@ -279,6 +302,18 @@ class XgmiComm : public DeviceComm {
         throw Error("xgmi comm: broadcastInts is not used on the device data plane");
     }
     const int *deviceErrorFlag() const override { return error_; }
+    bool fusedXchg(int region, hipk::TpXchg *x) const override {
+        if (!connected_ || world_ < 2) return false;
+        *x = hipk::TpXchg{};
+        for (int p = 0; p < world_; p++) x->recv[p] = region == 0 ? fusedVec_[p] : fusedArg_[p];
+        x->epochs = region == 0 ? fusedEpochs_ : fusedEpochs_ + kFusedVec;
+        x->error = error_;
+        x->stride = region == 0 ? kFusedVec : kFusedArg;
+        x->timeoutTicks = kTimeoutTicks;
+        x->rank = rank_;
+        x->world = world_;
+        return true;
+    }
     // The LL protocol can be switched off (e.g. when its pre-flight test fails on a platform);
     // resetError clears a timed-out flag so the other protocol can be tested.
     void setLowLatency(bool on) { ll_ = on; }
@@ -312,7 +347,7 @@ class XgmiComm : public DeviceComm {
         c.rank = rank_;
         c.world = world_;
         c.gather = gather ? 1 : 0;
-        c.timeoutTicks = 200LL * 1000 * 1000;  // 2 s at 100 MHz
+        c.timeoutTicks = kTimeoutTicks;
         return c;
     }
     void launchLL(float *buf, size_t n, hipStream_t s) {
@@ -339,7 +374,9 @@ class XgmiComm : public DeviceComm {
     }
 
     int rank_, world_;
-    size_t maxFloats_, pubBytes_ = 0, flagsBytes_ = 0, llOff_ = 0;
+    size_t maxFloats_, pubBytes_ = 0, flagsBytes_ = 0, llOff_ = 0, fvOff_ = 0, faOff_ = 0;
+    uint64_t *fusedVec_[kMaxRanks] = {}, *fusedArg_[kMaxRanks] = {};
+    unsigned *fusedEpochs_ = nullptr;
     unsigned *llEpochs_ = nullptr;
     void *base_ = nullptr;
     void *peerBase_[kMaxRanks] = {};

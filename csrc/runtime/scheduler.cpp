@@ -113,6 +113,11 @@ bool Scheduler::step() {
         while (!queue_.empty() && !freeSlots_.empty()) {
             auto r = queue_.front();
             queue_.pop_front();
+            if (r->isCancelled()) {
+                r->finish("cancelled");
+                stats_.cancelled++;
+                continue;
+            }
             if (r->prompt.empty() || r->prompt.size() >= seqLen) {
                 r->error = r->prompt.empty() ? "empty prompt" : "prompt longer than the context";
                 r->finish("error");
@@ -136,6 +141,16 @@ bool Scheduler::step() {
             r->eos.reset(new EosDetector(eosIds, stops, (int)maxLen, (int)maxLen));
             active_.push_back(r);
         }
+        // requests whose client disconnected give their slot back before the batch is built
+        for (auto &r : active_)
+            if (r->isCancelled()) {
+                r->finish("cancelled");
+                freeSlots_.push_back(r->slot);
+                stats_.cancelled++;
+            }
+        active_.erase(std::remove_if(active_.begin(), active_.end(),
+                                     [](const std::shared_ptr<GenRequest> &x) { return x->isCancelled(); }),
+                      active_.end());
         stats_.active = (int)active_.size();
     }
     if (active_.empty()) return false;

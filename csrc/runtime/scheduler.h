@@ -7,6 +7,7 @@
 // the loop has a lifecycle (stop()) and the API front end is concurrent.
 #pragma once
 
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -44,6 +45,11 @@ class GenRequest {
     bool done = false;
     int completionTokens = 0;
 
+    // The client went away (e.g. a streaming connection dropped): the scheduler finishes the
+    // request at its next step and frees its KV slot instead of generating to max_tokens.
+    void cancel() { cancelled.store(true); }
+    bool isCancelled() const { return cancelled.load(); }
+
     // Blocks until finished; returns the full text.
     std::string wait();
     // Pops the next delta (blocking); returns false once the request is done and drained.
@@ -51,6 +57,7 @@ class GenRequest {
 
   private:
     friend class Scheduler;
+    std::atomic<bool> cancelled{false};
     int slot = -1;
     size_t prefilled = 0;
     std::vector<int> generated;
@@ -62,7 +69,7 @@ class GenRequest {
 };
 
 struct SchedulerStats {
-    u64 forwards = 0, rows = 0, prefillRows = 0, decodeRows = 0, completed = 0, generatedTokens = 0;
+    u64 forwards = 0, rows = 0, prefillRows = 0, decodeRows = 0, completed = 0, generatedTokens = 0, cancelled = 0;
     double busyMs = 0;
     int active = 0, queued = 0;
 };

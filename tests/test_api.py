@@ -138,3 +138,26 @@ def test_prometheus_metrics(server):
     assert vals["dllama_rows_total"] == vals["dllama_prefill_rows_total"] + vals["dllama_decode_rows_total"]
     assert vals["dllama_generated_tokens_total"] >= 1 and vals["dllama_kv_slots"] == 4
     assert "# TYPE dllama_forwards_total counter" in text
+
+
+def test_stream_client_disconnect_frees_slot(server):
+    """A streaming client that hangs up mid-generation: the handler's write fails, the request is
+    cancelled and its KV slot returns to the pool instead of generating to the end of the context."""
+    h0 = json.loads(urllib.request.urlopen(server + "/health").read())
+    host, port = server.split("//")[1].split(":")
+    body = json.dumps({"messages": [{"role": "user", "content": "tell me a long story"}], "max_tokens": 0,
+                       "temperature": 0, "stream": True}).encode()
+    sock = socket.create_connection((host, int(port)), timeout=30)
+    sock.sendall(b"POST /v1/chat/completions HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
+                 b"Content-Length: " + str(len(body)).encode() + b"\r\n\r\n" + body)
+    assert b"200" in sock.recv(64)  # response started: generation is under way
+    sock.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, b"\x01\x00\x00\x00\x00\x00\x00\x00")  # RST
+    sock.close()
+    for _ in range(400):
+        h = json.loads(urllib.request.urlopen(server + "/health").read())
+        if h["cancelled"] > h0["cancelled"] and h["active"] == 0:
+            break
+        time.sleep(0.05)
+    assert h["cancelled"] == h0["cancelled"] + 1, h
+    assert h["active"] == 0 and h["completed"] == h0["completed"], h
+    assert _chat(server, "still serving", max_tokens=3)["choices"][0]["finish_reason"] in ("length", "stop")
