@@ -1,12 +1,19 @@
 #!/usr/bin/env python3
-"""Headline benchmark: Llama-3.1-8B Q40 weights / Q80 activations, single-stream decode
-(tokens/s = 1000 / ms-per-token), tensor-parallel over N MI355X GPUs (one process per GPU,
-RCCL over xGMI for the per-layer all-reduces).
+"""Headline benchmark: Llama-3.1-8B Q40 weights / Q80 activations, tensor-parallel over N MI355X
+GPUs (one process per GPU; per-layer partial sums exchanged over xGMI inside the producing GEMVs).
 
-Metric and config are the ones BASELINE.json names (reference: `dllama inference` Evaluation /
-Prediction summary lines, src/dllama.cpp:98-113). Weights are random-init on device with the real
-Llama-3.1-8B shapes (no network for checkpoints). One timed "step" = one full decode token:
-embedding -> 32 layers -> logits -> argmax, with the sampled token fed back on device.
+Metric and config are the ones BASELINE.json names: "avg eval+pred ms/token" (reference:
+`dllama inference` Evaluation / Prediction summary lines, src/dllama.cpp:98-113). Weights are
+random-init on device with the real Llama-3.1-8B shapes (no network for checkpoints).
+* eval = prompt evaluation, chunks of 32 rows per forward (the reference's nBatches), timed
+  between barrier + device syncs;
+* pred = single-stream decode; one timed "step" = one full decode token (embedding -> 32 layers ->
+  logits -> argmax, the token fed back on device), K steps between barrier + device syncs;
+* value = B * 1000 / ((eval_ms_per_token + pred_ms_per_token) / 2), the named metric; the decode-only
+  rate is reported as config.pred_tokens_per_s.
+Extra points in `config`: decode at position >= 4096 (long_ctx_pred_ms_per_token) and, on one GPU,
+the product path through `build/dllama inference --synthetic llama3_1_8b` (cli_*: per-token host
+round trips included).
 
     python bench.py --gpus 1 --steps 128 --warmup 16
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
@@ -33,6 +40,37 @@ LLAMA31_8B = dict(dim=4096, hidden_dim=14336, n_layers=32, n_heads=32, n_kv_head
                   weight_type=2, hidden_act=1)
 
 
+def _cli_point(local: int, prompt_tokens: int, steps: int) -> dict:
+    """Product path on one GPU: `dllama inference --synthetic llama3_1_8b` with greedy sampling
+    (per forward: H2D inputs, graph replay, D2H token, host sync), parsed from the reference's
+    Evaluation / Prediction summary lines (src/dllama.cpp:98-113)."""
+    import re
+    import subprocess
+    import tempfile
+    from distributed_llama_multiusers_amd.models.synthetic import make_tokenizer
+    exe = os.path.join(REPO, "build", "dllama")
+    if not os.path.exists(exe):
+        return {"cli_error": "build/dllama missing"}
+    with tempfile.TemporaryDirectory() as d:
+        tok = os.path.join(d, "llama3_synth.t")
+        make_tokenizer(tok, 128256)
+        # ~1 token per character of the synthetic tokenizer's byte fallback
+        prompt = ("The quick brown fox jumps over the lazy dog " * 8)[:prompt_tokens]
+        cmd = [exe, "inference", "--synthetic", "llama3_1_8b", "--tokenizer", tok, "--prompt", prompt, "--steps",
+               str(prompt_tokens + steps), "--temperature", "0", "--gpu-index", str(local), "--max-seq-len",
+               str(prompt_tokens + steps + 8), "--buffer-float-type", "q80", "--log-level", "0"]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        except subprocess.TimeoutExpired:
+            return {"cli_error": "timeout"}
+    out = r.stdout
+    m = re.findall(r"tokens/s:\s*([\d.]+)\s*\(([\d.]+) ms/tok\)", out)
+    if r.returncode != 0 or len(m) < 2:
+        return {"cli_error": (out + r.stderr)[-300:]}
+    return {"cli_eval_ms_per_token": float(m[0][1]), "cli_pred_ms_per_token": float(m[1][1]),
+            "cli_avg_tokens_per_s": round(1000.0 / ((float(m[0][1]) + float(m[1][1])) / 2), 2)}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -43,6 +81,10 @@ def main() -> int:
     ap.add_argument("--model", default="", help="optional .m file instead of synthetic 8B weights")
     ap.add_argument("--shape", default="llama3_1_8b",
                     help="synthetic shape (models/synthetic.py LLAMA_SHAPES); the headline metric is llama3_1_8b")
+    ap.add_argument("--sync-type", default=os.environ.get("DL_SYNC_TYPE", "f32"), choices=["f32", "q80"],
+                    help="TP partial-sum exchange: f32 (exact, measured faster) or q80 (the reference ZQ wire format)")
+    ap.add_argument("--long-ctx", type=int, default=4096, help="position of the long-context decode point (0: off)")
+    ap.add_argument("--no-cli", action="store_true", help="skip the dllama CLI product-path point (1 GPU)")
     ap.add_argument("--no-graphs", action="store_true")
     args = ap.parse_args()
 
@@ -63,6 +105,9 @@ def main() -> int:
     max_batch = max(32, args.batch)
     comm_kind = os.environ.get("DL_TP_COMM", "xgmi")
     torch.cuda.set_device(local)
+    hdr = C.load_header(args.model) if args.model else dict(
+        LLAMA31_8B, **__import__("distributed_llama_multiusers_amd.models.synthetic",
+                                 fromlist=["LLAMA_SHAPES"]).LLAMA_SHAPES[args.shape])
     if world > 1:
         import torch.distributed as tdist
         dist = tdist
@@ -70,23 +115,26 @@ def main() -> int:
         # is the engine's own device communicator
         dist.init_process_group("gloo")
         from distributed_llama_multiusers_amd.parallel import init_device_comm
-        hdr = C.load_header(args.model) if args.model else dict(
-            LLAMA31_8B, **__import__("distributed_llama_multiusers_amd.models.synthetic",
-                                     fromlist=["LLAMA_SHAPES"]).LLAMA_SHAPES[args.shape])
         vocab0 = -(-hdr["vocab_size"] // world)
         comm, uid, comm_kind = init_device_comm(C, dist, rank, world, max_batch * max(hdr["dim"], vocab0), local,
                                                 comm_kind)
 
+    long_pos = args.long_ctx if args.long_ctx > 0 else 0
     seq_len = args.prompt + args.warmup + args.steps + 8
     shape = LLAMA31_8B
     if args.shape != "llama3_1_8b":
         from distributed_llama_multiusers_amd.models.synthetic import LLAMA_SHAPES
         shape = dict(LLAMA31_8B, **LLAMA_SHAPES[args.shape])
-    synthetic = None if args.model else dict(shape, seq_len=seq_len)
+
+    def make_engine(max_seq=seq_len):
+        # the context length is sized to the run (attention split grids follow it)
+        synthetic = None if args.model else dict(shape, seq_len=max_seq)
+        return C.HipEngine(args.model, "q80", max_seq_len=max_seq, max_batch=max_batch, n_slots=args.batch,
+                           gpu_index=local, use_graphs=not args.no_graphs, synthetic=synthetic, seed=1234, rank=rank,
+                           world=world, uid=uid, comm=comm, sync_type=args.sync_type)
+
     t0 = time.time()
-    eng = C.HipEngine(args.model, "q80", max_seq_len=seq_len, max_batch=max_batch, n_slots=args.batch,
-                      gpu_index=local, use_graphs=not args.no_graphs, synthetic=synthetic, seed=1234, rank=rank,
-                      world=world, uid=uid, comm=comm)
+    eng = make_engine()
     load_s = time.time() - t0
     B = args.batch
 
@@ -94,9 +142,37 @@ def main() -> int:
         if dist is not None:
             dist.barrier()
 
+    prompt = [(i * 7919 + 13) % 128000 for i in range(args.prompt)]
+    if world > 1:
+        # pre-flight of the exact timed path (captured graphs, fused exchange, distributed argmax):
+        # every rank must decode the same tokens without a timed-out peer wait; otherwise every rank
+        # agrees to rebuild on RCCL (no rank ever waits on a peer using another data plane)
+        import numpy as np
+        ok = True
+        try:
+            eng.forward_argmax(prompt[:8], list(range(8)), [0] * 8)
+            _, toks = eng.decode_greedy(4, [prompt[7]], [8], [0])
+            if comm is not None and comm.timed_out():
+                raise RuntimeError("a peer wait timed out")
+        except Exception as e:  # noqa: BLE001 - reported, then the agreed fallback
+            print(f"rank {rank}: pre-flight failed: {e}", file=sys.stderr)
+            ok, toks = False, [-1] * 4
+        got = [None] * world
+        dist.all_gather_object(got, list(toks))
+        flag = torch.tensor([1 if ok and all(g == got[0] for g in got) else 0], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if not int(flag[0]):
+            if rank == 0:
+                print(f"pre-flight over {comm_kind} failed ({got}); rebuilding on rccl", file=sys.stderr)
+            del eng
+            comm, comm_kind = None, "rccl"
+            obj = [C.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            uid = obj[0]
+            eng = make_engine()
+
     # eval: prefill the prompt (chunks of 32 rows per forward, like the reference nBatches=32);
     # one untimed chunk first so the batch-32 graph is captured outside the timed region
-    prompt = [(i * 7919 + 13) % 128000 for i in range(args.prompt)]
     if len(prompt) >= 32:
         for b in range(B):
             eng.forward_argmax(prompt[:32], list(range(32)), [b] * 32)
@@ -108,7 +184,7 @@ def main() -> int:
         for b in range(B):
             eng.forward_argmax(chunk, list(range(s, s + len(chunk))), [b] * len(chunk))
     torch.cuda.synchronize()
-    eval_ms = (time.perf_counter() - te) * 1000.0
+    eval_s = time.perf_counter() - te
     barrier()
 
     pos0 = len(prompt)
@@ -124,16 +200,37 @@ def main() -> int:
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     barrier()
+
+    long_ms = None
+    if long_pos:  # decode at a long context, own engine sized for it (KV rows it never wrote are
+        del eng   # zeros: same work, same time)
+        eng = make_engine(long_pos + 24)
+        eng.decode_greedy(4, tokens, [long_pos] * B, list(range(B)))
+        barrier()
+        torch.cuda.synchronize()
+        tl = time.perf_counter()
+        eng.decode_greedy(16, tokens, [long_pos + 4] * B, list(range(B)))
+        torch.cuda.synchronize()
+        long_ms = (time.perf_counter() - tl) * 1000.0 / 16
+        barrier()
+
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64)
+        t = torch.tensor([elapsed, eval_s, long_ms or 0.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t[0])
+        elapsed, eval_s, long_ms = float(t[0]), float(t[1]), (float(t[2]) if long_ms is not None else None)
 
     ms_per_step = elapsed * 1000.0 / args.steps
-    tok_s = B * 1000.0 / ms_per_step
+    pred_ms_tok = ms_per_step / B
+    eval_ms_tok = eval_s * 1000.0 / max(1, len(prompt)) / B
+    avg_ms_tok = (eval_ms_tok + pred_ms_tok) / 2 if prompt else pred_ms_tok
+    tok_s = 1000.0 / avg_ms_tok
     # the published baselines are per model family: 7B/8B at 1/2/4/8 devices, 70B at 8 devices
     base = (BASELINE_MS.get(world) if args.shape == "llama3_1_8b" and not args.model
             else BASELINE_MS_70B.get(world) if args.shape == "llama3_3_70b" and not args.model else None)
+    cli = {}
+    if world == 1 and not args.no_cli and args.shape == "llama3_1_8b" and not args.model:
+        del eng
+        cli = _cli_point(local, min(args.prompt, 64), min(args.steps, 64))
     result = {
         "metric": METRIC,
         "value": round(tok_s, 3),
@@ -156,11 +253,18 @@ def main() -> int:
             "prompt_tokens": args.prompt,
             "parallelism": f"tp{world}",
             "kv_cache": "bf16",
-            "eval_ms_per_token": round(eval_ms / max(1, len(prompt)) / B, 4),
+            "value_formula": "B*1000/((eval_ms_per_token+pred_ms_per_token)/2)",
+            "eval_ms_per_token": round(eval_ms_tok, 4),
+            "pred_ms_per_token": round(pred_ms_tok, 4),
+            "pred_tokens_per_s": round(1000.0 * B / ms_per_step, 2),
             "device_ms_per_step": round(dev_ms / args.steps, 4),
+            "long_ctx_pos": long_pos or None,
+            "long_ctx_pred_ms_per_token": round(long_ms / B, 4) if long_ms is not None else None,
             "load_s": round(load_s, 2),
             "hip_graphs": not args.no_graphs,
             "tp_comm": comm_kind if world > 1 else None,
+            "tp_sync": args.sync_type if world > 1 else None,
+            **cli,
         },
     }
     if rank == 0:

@@ -116,6 +116,7 @@ class HipEngineImpl : public HipEngine {
                                   stream_));
         }
         syncAndCheckComm();
+        inputsInFlight_ = false;
         if (root && logits) std::memcpy(logits, hLogits_, (size_t)n * h_.vocabSize * sizeof(float));
         stats_.computeMs = t.elapsedMs();
         stats_.syncMs = 0;
@@ -127,6 +128,7 @@ class HipEngineImpl : public HipEngine {
         runGraph(n, GraphKind::ARGMAX);
         DL_HIP(hipMemcpyAsync(hIds_, dIds_, n * sizeof(int), hipMemcpyDeviceToHost, stream_));
         syncAndCheckComm();
+        inputsInFlight_ = false;
         std::memcpy(out, hIds_, n * sizeof(int));
         stats_.computeMs = t.elapsedMs();
     }
@@ -154,6 +156,7 @@ class HipEngineImpl : public HipEngine {
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
         syncAndCheckComm();
+        inputsInFlight_ = false;
         if (outTokens) {
             std::vector<int> hist((size_t)cfg_.maxBatch * h_.seqLen);
             DL_HIP(hipMemcpy(hist.data(), dHist_, hist.size() * sizeof(int), hipMemcpyDeviceToHost));
@@ -169,6 +172,7 @@ class HipEngineImpl : public HipEngine {
         profTimes_.clear();
         enqueueForward(n, GraphKind::LOGITS);
         DL_HIP(hipStreamSynchronize(stream_));
+        inputsInFlight_ = false;
         profile_ = false;
         std::map<std::string, double> agg;
         for (auto &p : profTimes_) {
@@ -230,9 +234,9 @@ class HipEngineImpl : public HipEngine {
     void allocBuffers() {
         const u32 MB = cfg_.maxBatch;
         const ShardPlan &p = plan_;
-        dTok_ = dalloc<int>(MB);
-        dPos_ = dalloc<int>(MB);
-        dSlot_ = dalloc<int>(MB);
+        dTok_ = dalloc<int>(3 * (size_t)MB);  // [tokens | positions | slots]: one H2D copy per forward
+        dPos_ = dTok_ + MB;
+        dSlot_ = dTok_ + 2 * MB;
         dIds_ = dalloc<int>(MB);
         dHist_ = dalloc<int>((size_t)MB * h_.seqLen);
         hIn_ = halloc<int>(3 * MB);
@@ -463,14 +467,15 @@ class HipEngineImpl : public HipEngine {
             DL_CHECK(slots[b] >= 0 && (u32)slots[b] < cfg_.nSlots, "slot out of range");
         }
         const u32 MB = cfg_.maxBatch;
-        // keep the pinned staging buffer stable while a previous copy may still read it
-        DL_HIP(hipStreamSynchronize(stream_));
+        // keep the pinned staging buffer stable while a previous copy may still read it (every
+        // public entry point ends with a stream sync, so this only waits after an async path)
+        if (inputsInFlight_) DL_HIP(hipStreamSynchronize(stream_));
         std::memcpy(hIn_, tokens, n * sizeof(int));
         std::memcpy(hIn_ + MB, positions, n * sizeof(int));
         std::memcpy(hIn_ + 2 * MB, slots, n * sizeof(int));
-        DL_HIP(hipMemcpyAsync(dTok_, hIn_, n * sizeof(int), hipMemcpyHostToDevice, stream_));
-        DL_HIP(hipMemcpyAsync(dPos_, hIn_ + MB, n * sizeof(int), hipMemcpyHostToDevice, stream_));
-        DL_HIP(hipMemcpyAsync(dSlot_, hIn_ + 2 * MB, n * sizeof(int), hipMemcpyHostToDevice, stream_));
+        // one copy of the three row arrays (the unused tail of each is never read)
+        DL_HIP(hipMemcpyAsync(dTok_, hIn_, (2 * (size_t)MB + n) * sizeof(int), hipMemcpyHostToDevice, stream_));
+        inputsInFlight_ = true;
     }
 
     void runGraph(int n, GraphKind kind) {
@@ -874,6 +879,7 @@ class HipEngineImpl : public HipEngine {
     std::map<int, hipGraphExec_t> graphs_;
     bool profile_ = false;
     bool graphsBroken_ = false;
+    bool inputsInFlight_ = false;  // an H2D copy from hIn_ may still be pending
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> profTimes_;
 };
 
