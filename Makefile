@@ -35,7 +35,7 @@ endif
 LDROCM     := -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lrccl
 
 HOST_SRCS  := csrc/core/quant.cpp csrc/core/model_file.cpp csrc/core/plan.cpp csrc/text/tokenizer.cpp \
-              csrc/cpu/thread_pool.cpp csrc/cpu/cpu_backend.cpp $(wildcard csrc/net/*.cpp) $(wildcard csrc/runtime/*.cpp)
+              csrc/cpu/thread_pool.cpp csrc/cpu/cpu_ops.cpp csrc/cpu/cpu_backend.cpp $(wildcard csrc/net/*.cpp) $(wildcard csrc/runtime/*.cpp)
 HIP_SRCS   := csrc/hip/kernels.hip csrc/hip/engine.cpp csrc/hip/rccl_comm.cpp csrc/hip/sim_comm.cpp csrc/hip/xgmi_comm.cpp csrc/hip/ops.cpp
 HOST_OBJS  := $(patsubst csrc/%.cpp,$(BUILD)/obj/%.o,$(HOST_SRCS))
 HIP_OBJS   := $(patsubst csrc/%,$(BUILD)/obj/%.o,$(HIP_SRCS))
@@ -45,7 +45,7 @@ LIB        := $(PKG)/libdllama.so
 EXT        := $(PKG)/_C$(PYEXT)
 APPS       := $(BUILD)/dllama $(BUILD)/dllama-api
 
-all: $(LIB) $(EXT) $(APPS)
+all: $(LIB) $(EXT) $(APPS) $(BUILD)/unit_tests
 
 lib: $(LIB) $(EXT)
 
@@ -81,7 +81,15 @@ $(BUILD)/dllama: $(BUILD)/obj/apps/dllama.o $(LIB)
 $(BUILD)/dllama-api: $(BUILD)/obj/apps/dllama_api.o $(LIB)
 	$(CXX) -o $@ $< -L$(PKG) -ldllama -Wl,-rpath,'$$ORIGIN/../$(PKG)' $(LDROCM) -lpthread $(SAN)
 
+# native unit tests (host code only): build/unit_tests
+$(BUILD)/unit_tests: tests/cpp/unit_tests.cpp $(LIB) $(HDRS)
+	@mkdir -p $(BUILD)
+	$(CXX) $(HOSTFLAGS) -o $@ $< -L$(PKG) -ldllama -Wl,-rpath,'$$ORIGIN/../$(PKG)' $(LDROCM) -lpthread $(SAN)
+
+test-cpp: $(BUILD)/unit_tests
+	$(BUILD)/unit_tests
+
 clean:
 	rm -rf $(BUILD) $(LIB) $(EXT)
 
-.PHONY: all lib clean
+.PHONY: all lib clean test-cpp

@@ -21,6 +21,7 @@
 
 #include "../core/quant.h"
 #include "../runtime/backend.h"
+#include "cpu_ops.h"
 #include "thread_pool.h"
 
 namespace dl {
@@ -151,75 +152,17 @@ class CpuBackend : public Backend {
         }
     }
 
-    // ys[t][r] = W[r,:] . xs[t]  for r in [0, rows), t in [0, B): each weight row is loaded once
-    // for all B activation rows (groups of kGroup keep the accumulators in registers)
-    static constexpr int kGroup = 8;
-
-    static float hsum(__m256 v) {
-        __m128 s = _mm_add_ps(_mm256_castps256_ps128(v), _mm256_extractf128_ps(v, 1));
-        s = _mm_add_ps(s, _mm_movehl_ps(s, s));
-        s = _mm_add_ss(s, _mm_movehdup_ps(s));
-        return _mm_cvtss_f32(s);
-    }
-
     void matmul(const Mat &W, const Act *const *xs, int B, float *const *ys) {
         if (W.type == FloatType::F32) {
-            const float *w = (const float *)W.data;
-            const u32 n = W.cols;
-            DL_CHECK(n % 8 == 0, "f32 matmul: columns must be a multiple of 8");
-            pool_.parallelFor(W.rows, [&](long s, long e) {
-                for (long r = s; r < e; r++) {
-                    const float *wr = w + (u64)r * n;
-                    for (int t0 = 0; t0 < B; t0 += kGroup) {
-                        const int g = std::min(kGroup, B - t0);
-                        __m256 acc[kGroup];
-                        for (int t = 0; t < g; t++) acc[t] = _mm256_setzero_ps();
-                        for (u32 i = 0; i < n; i += 8) {
-                            const __m256 wv = _mm256_loadu_ps(wr + i);
-                            for (int t = 0; t < g; t++)
-                                acc[t] = _mm256_fmadd_ps(wv, _mm256_loadu_ps(xs[t0 + t]->f.data() + i), acc[t]);
-                        }
-                        for (int t = 0; t < g; t++) ys[t0 + t][r] = hsum(acc[t]);
-                    }
-                }
-            });
+            std::vector<const float *> xf(B);
+            for (int t = 0; t < B; t++) xf[t] = xs[t]->f.data();
+            cpu::matmulF32((const float *)W.data, W.rows, W.cols, xf.data(), B, ys, pool_);
             return;
         }
         DL_CHECK(W.type == FloatType::Q40 && q80_, "Q40 matmul needs Q80 activations");
-        const BlockQ40 *w = (const BlockQ40 *)W.data;
-        const u32 nb = W.cols / kQBlock;
-        // activation scales as f32, once per forward row
-        std::vector<float> xd((size_t)B * nb);
-        for (int t = 0; t < B; t++)
-            for (u32 b = 0; b < nb; b++) xd[(size_t)t * nb + b] = f16ToF32(xs[t]->q[b].d);
-        pool_.parallelFor(W.rows, [&](long s, long e) {
-            const __m256i low4 = _mm256_set1_epi8(0x0F), eight = _mm256_set1_epi8(8);
-            const __m256i ones = _mm256_set1_epi16(1);
-            for (long r = s; r < e; r++) {
-                const BlockQ40 *wr = w + (u64)r * nb;
-                for (int t0 = 0; t0 < B; t0 += kGroup) {
-                    const int g = std::min(kGroup, B - t0);
-                    __m256 acc[kGroup];
-                    for (int t = 0; t < g; t++) acc[t] = _mm256_setzero_ps();
-                    for (u32 b = 0; b < nb; b++) {
-                        // 32 weights in Q80 element order: [lo nibbles 0..15 | hi nibbles 0..15] - 8
-                        const __m128i raw = _mm_loadu_si128(reinterpret_cast<const __m128i *>(wr[b].qs));
-                        const __m256i nib = _mm256_set_m128i(_mm_srli_epi16(raw, 4), raw);
-                        const __m256i wq = _mm256_sub_epi8(_mm256_and_si256(nib, low4), eight);
-                        const __m256i aw = _mm256_sign_epi8(wq, wq);
-                        const float dw = f16ToF32(wr[b].d);
-                        for (int t = 0; t < g; t++) {
-                            const __m256i xq = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(xs[t0 + t]->q[b].qs));
-                            const __m256i p16 = _mm256_maddubs_epi16(aw, _mm256_sign_epi8(xq, wq));
-                            const __m256i p32 = _mm256_madd_epi16(p16, ones);
-                            const __m256 sc = _mm256_set1_ps(dw * xd[(size_t)(t0 + t) * nb + b]);
-                            acc[t] = _mm256_fmadd_ps(_mm256_cvtepi32_ps(p32), sc, acc[t]);
-                        }
-                    }
-                    for (int t = 0; t < g; t++) ys[t0 + t][r] = hsum(acc[t]);
-                }
-            }
-        });
+        std::vector<const BlockQ80 *> xq(B);
+        for (int t = 0; t < B; t++) xq[t] = xs[t]->q.data();
+        cpu::matmulQ40Q80((const BlockQ40 *)W.data, W.rows, W.cols, xq.data(), B, ys, pool_);
     }
 
     void allReduce(float *y, u64 n) {
@@ -229,31 +172,12 @@ class CpuBackend : public Backend {
             comm_->allReduceSum(y, n);
     }
 
-    static float invRms(const float *x, u32 n, float eps) {
-        float s = 0.f;
-        for (u32 i = 0; i < n; i++) s += x[i] * x[i];
-        s /= (float)n;
-        s += eps;
-        return 1.0f / std::sqrt(s);
-    }
-
     void rmsNorm(const float *x, const float *w, float *out) {
-        const float inv = invRms(x, h_.dim, h_.normEpsilon);
+        const float inv = cpu::invRms(x, h_.dim, h_.normEpsilon);
         for (u32 i = 0; i < h_.dim; i++) out[i] = w[i] * (inv * x[i]);
     }
 
-    // rotate pairs (i, i+1) of a vector whose element i sits at within-head index i % headSize
-    void rope(float *v, u32 len, u32 pos) {
-        const u32 hs = plan_.headSize, half = hs / 2;
-        const float *t = &rope_[(u64)pos * half * 2];
-        for (u32 i = 0; i < len; i += 2) {
-            const u32 fi = (i % hs) / 2;
-            const float c = t[fi * 2], s = t[fi * 2 + 1];
-            const float v0 = v[i], v1 = v[i + 1];
-            v[i] = v0 * c - v1 * s;
-            v[i + 1] = v0 * s + v1 * c;
-        }
-    }
+    void rope(float *v, u32 len, u32 pos) { cpu::ropeApply(v, len, pos, plan_.headSize, rope_.data()); }
 
     float *kc(u32 layer, int slot, u32 pos) {
         return &kcache_[(((u64)layer * cfg_.nSlots + slot) * h_.seqLen + pos) * plan_.kv0];
@@ -355,11 +279,7 @@ class CpuBackend : public Backend {
                 const float *gb = gR[b];
                 for (u32 i = 0; i < p.hidden0; i++) {
                     const float z = hb[i];
-                    float act;
-                    if (h_.hiddenAct == HiddenAct::GELU)
-                        act = 0.5f * z * (1.0f + std::tanh(0.79788456080286535588f * z * (1.0f + 0.044715f * z * z)));
-                    else
-                        act = z / (1.0f + std::exp(-z));
+                    const float act = h_.hiddenAct == HiddenAct::GELU ? cpu::gelu(z) : cpu::silu(z);
                     hb[i] = act * gb[i];
                 }
                 setAct(acts[b], hb, p.hidden0);

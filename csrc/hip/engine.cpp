@@ -622,7 +622,10 @@ class HipEngineImpl : public HipEngine {
         return e && *e ? std::atoi(e) : 5;  // GEMV up to 4 rows: 1.78 vs 3.44 ms/step at 2, 2.77 vs 3.47 at 4 (8B)
     }
 
-    bool batchedPath(int n) const { return q40_ && n >= gemmMinTokens(); }
+    bool batchedPath(int n) const {
+        return q40_ && n >= gemmMinTokens() && hipk::gemmSupported(h_.dim) && hipk::gemmSupported(plan_.q0) &&
+               hipk::gemmSupported(plan_.hidden0);
+    }
 
     // MALL warm-up of wo + the head of w13 beside attention (DL_MALL_PREFETCH=1 enables;
     // DL_MALL_PREFETCH_MB sets the w13 head size)
@@ -680,7 +683,7 @@ class HipEngineImpl : public HipEngine {
                 a.kvBf16 = kvBf16_ ? 1 : 0;
             }
             g.M = bc;
-            g.splits = hipk::gemmSplits(m.rows, m.n);
+            g.splits = hipk::gemmSplits(m.rows, m.n, bc);
             g.part = dPart_;
             g.counters = dGemmCnt_;
             hipk::launchGemmQ40(g, epi, stream_);
@@ -843,7 +846,7 @@ class HipEngineImpl : public HipEngine {
         DL_HIP(hipGetLastError());
     }
 
-    static constexpr int kGemmMaxTokens = 64;  // tokens per MFMA GEMM launch (one weight pass)
+    static constexpr int kGemmMaxTokens = hipk::kGemmMaxTokens;  // tokens per MFMA GEMM launch (one weight pass)
     _Float16 *dXh_ = nullptr, *dAttH_ = nullptr, *dHh_ = nullptr;
     float *dPart_ = nullptr;
     int *dGemmCnt_ = nullptr;
@@ -989,6 +992,76 @@ double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int pas
     }
     (void)hipGraphExecDestroy(ge);
     (void)hipGraphDestroy(g);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    for (void *p : mem) (void)hipFree(p);
+    (void)hipStreamDestroy(s);
+    return ms * 1000.0 / iters;
+}
+
+double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters) {
+    DL_CHECK(M >= 1 && M <= hipk::kGemmMaxTokens && hipk::gemmSupported(n) && rows % 64 == 0, "bad gemm bench shape");
+    hipStream_t s;
+    DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<void *> mem;
+    auto alloc = [&](size_t bytes) {
+        void *p;
+        DL_HIP(hipMalloc(&p, bytes));
+        DL_HIP(hipMemsetAsync(p, 0, bytes, s));
+        mem.push_back(p);
+        return p;
+    };
+    const int L = hipk::gemvLanesPerRow(n, rows, 1, true);
+    const hipk::Q40Tiling t = hipk::q40Tiling(rows, n, L);
+    std::vector<uint8_t *> qs(copies);
+    std::vector<uint16_t *> d(copies);
+    for (int c = 0; c < copies; c++) {
+        qs[c] = (uint8_t *)alloc(t.qsBytes);
+        d[c] = (uint16_t *)alloc(t.dBytes);
+        hipk::launchFillQ40(qs[c], d[c], t.qsBytes / 16, 0.01f, 77 + c, s);
+    }
+    const int MP = hipk::gemmTokenPad(M);
+    _Float16 *x = (_Float16 *)alloc((size_t)MP * n * 2);
+    hipk::launchFillF32Uniform((float *)x, (size_t)MP * n / 2, 1e-3f, 3, s);  // small finite f16 pairs
+    const size_t part = hipk::gemmPartFloats(rows, n, M);
+    hipk::GemmArgs g;
+    g.e.rows = rows;
+    g.e.n = n;
+    g.e.lanes = L;
+    g.e.out = (float *)alloc((size_t)M * rows * 4);
+    g.e.ldOut = epi == hipk::EPI_STORE ? rows : rows / 2;
+    g.outH = (_Float16 *)alloc((size_t)M * rows * 2);
+    g.x = x;
+    g.M = M;
+    g.splits = hipk::gemmSplits(rows, n, M);
+    g.part = part ? (float *)alloc(part * 4) : nullptr;
+    g.counters = (int *)alloc((size_t)(rows / 64 + 1) * 4);
+    auto launch = [&](int c) {
+        g.e.qs = qs[c % copies];
+        g.e.wd = d[c % copies];
+        hipk::launchGemmQ40(g, epi, s);
+    };
+    launch(0);
+    DL_HIP(hipGetLastError());
+    hipGraph_t gr;
+    hipGraphExec_t ge;
+    DL_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < iters; i++) launch(i);
+    DL_HIP(hipStreamEndCapture(s, &gr));
+    DL_HIP(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+    DL_HIP(hipGraphLaunch(ge, s));
+    DL_HIP(hipStreamSynchronize(s));
+    hipEvent_t e0, e1;
+    DL_HIP(hipEventCreate(&e0));
+    DL_HIP(hipEventCreate(&e1));
+    DL_HIP(hipEventRecord(e0, s));
+    DL_HIP(hipGraphLaunch(ge, s));
+    DL_HIP(hipEventRecord(e1, s));
+    DL_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    DL_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipGraphExecDestroy(ge);
+    (void)hipGraphDestroy(gr);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     for (void *p : mem) (void)hipFree(p);

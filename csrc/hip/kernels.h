@@ -130,7 +130,7 @@ struct GemvArgs {
     unsigned long long *trace = nullptr;
 };
 
-// Batched Q40 matmul on MFMA (2..32 tokens per launch): GemvArgs `e` carries the weights (tiled,
+// Batched Q40 matmul on MFMA (1..32 tokens per launch): GemvArgs `e` carries the weights (tiled,
 // `lanes` = tiling L) and the epilogue fields; activations are f16 [>= roundup(M,16)][n] (`x`,
 // rows past M are read but their outputs dropped); split-K partials + per-tile counters
 // (zero-initialised, reset by the kernel) when splits > 1. EPI_ACT_F16 writes SwiGLU as f16 to outH.
@@ -144,9 +144,17 @@ struct GemmArgs {
     int *counters = nullptr;
 };
 void launchGemmQ40(const GemmArgs &a, int epi, hipStream_t s);
-int gemmSplits(int rows, int n);
+// Tile / split-K plan of one matrix (rt = 16-row tiles per wave: 64 * rt rows per workgroup).
+struct GemmPlan {
+    int rt = 1, tiles = 0, splits = 1;
+};
+constexpr int kGemmMaxTokens = 32;  // tokens per GEMM launch (16 or 32 padded)
+GemmPlan gemmPlan(int rows, int n, int M);
+bool gemmSupported(int n);  // input width a multiple of 128 (whole 4-block steps) that fits LDS
+int gemmSplits(int rows, int n, int M);
+// split-K partial floats for any launch of up to maxTokens tokens on this matrix
 size_t gemmPartFloats(int rows, int n, int maxTokens);
-// token rows one GEMM launch of M (1..64) tokens reads from its f16 activation operand (16/32/64)
+// token rows one GEMM launch of M (1..32) tokens reads from its f16 activation operand (16/32)
 int gemmTokenPad(int M);
 // Residual add + RMS norm (normW may be null: no norm) of M rows -> f16:
 // in/addIn/xNext [M][ldIn] f32 -> out [M][n] f16 (xNext = in + addIn when set).

@@ -14,6 +14,7 @@
 //   forward pass is captured once per batch size in a hipGraph and replayed.
 // * Cross-workgroup hand-offs (attention split combine, argmax) follow the agent-scope
 //   release/acquire counter recipe (cdna_hip_programming.md §5 "In-launch split-K reduction").
+#include "../core/common.h"
 #include "device_common.h"
 #include "kernels.h"
 
@@ -1098,26 +1099,38 @@ void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_
 }
 
 // ------------------------------------------------------------------------------------------------
-// Batched Q40 matmul on MFMA (prefill / multi-user decode, 2..32 tokens per launch).
+// Batched Q40 matmul on MFMA (prefill / multi-user decode, up to 32 tokens per launch).
 //   out[t][row] = sum_k W[row][k] * x[t][k], W Q40 (the GEMV's tiled layout), x f16.
-// Each workgroup owns 64 weight rows (4 waves x 16) and one K split, streamed in chunks of 16
-// Q40 blocks. Both operands are copied HBM/L2 -> LDS with global_load_lds_dwordx4 (no VGPR
-// staging; one 16-B unit per lane, contiguous 256-B+ runs per wave instruction), multi-buffered
-// with counted vmcnt waits and raw barriers (kGemmStages buffers), into XOR-swizzled images so the fragment reads are
-// bank-conflict free. Per block a lane dequantizes 8 nibbles of its row ((1024+q) - 1032 exact in
-// f16, times d) into the B fragment of v_mfma_f32_16x16x32_f16; A fragments are read as is.
-// Split-K partials are combined in split order by the last-arriving workgroup (agent-scope
-// release/acquire counter: deterministic), which runs the fused epilogues (store / SwiGLU /
-// SwiGLU -> f16 / SwiGLU -> Q80 / RoPE + KV append).
+// Workgroup = 4 waves; a wave owns RT row tiles of 16 rows (the workgroup 64 * RT rows) and all
+// MT token tiles of 16 tokens, over one K split of KW = n / splits columns:
+// * the workgroup's activations (MP tokens x KW, f16, <= 128 KB) are copied L2 -> LDS ONCE with
+//   global_load_lds (XOR-swizzled 16-B units: conflict-free ds_read_b128) and stay resident, so
+//   the K loop has no barrier and no LDS refill;
+// * weights go HBM -> VGPRs directly through a ring of D steps in flight (like the GEMV): a step is
+//   4 Q40 blocks (128 k); lane (col, h) loads block j + h of its row (16 B) and the row pair's
+//   scale word per row tile. vmcnt counts only weight loads inside the loop, so the ring depth is
+//   real (a ring shared with activation refills is limited by the refills' in-order retirement);
+// * one MFMA k-step (v_mfma_f32_16x16x32_f16) covers 8 k of each of the 4 blocks of the step:
+//   lane (col, h) feeds block j+h elements [8s, 8s+8) as B (its row) and A (its token) alike (a
+//   permutation of k, identical on both operands). A lane dequantizes 8 nibbles per k-step
+//   ((1024 + q) - 1032 exact in f16, times d); each A fragment feeds RT row tiles, each dequantized
+//   B fragment feeds MT token tiles.
+// Split-K partials are combined in split order by the last-arriving workgroup of a tile (agent-scope
+// release/acquire counter: deterministic), which runs the fused epilogue on the tile in LDS
+// (store / SwiGLU / SwiGLU -> f16 / SwiGLU -> Q80 / RoPE + KV append).
+// History: v1 staged weights through LDS and waited on every LDS read (1.1 TB/s on w13 at 64
+// tokens); v2 streamed weights to VGPRs but refilled activations through a 4-deep LDS ring on the
+// same vmcnt counter, which capped the weight stream at 3 steps in flight (0.2-1.9 TB/s).
 // ------------------------------------------------------------------------------------------------
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-static constexpr int kGemmRows = 64;
-static constexpr int kGemmCh = 8;  // Q40 blocks per pipeline stage (~25 KB at 32 tokens)
+static constexpr int kGemmMaxLdsAct = 128 * 1024;  // resident activation bytes per workgroup
 
-// Split-K degree: grow S until the grid reaches the workgroup target (DL_GEMM_WG, read once) or
-// a split would get fewer than kGemmCh blocks. The target is sized so every CU holds its 3
-// resident workgroups: with one chunk in flight per workgroup, bytes in flight per CU (and so
-// HBM bandwidth) scale with resident workgroups, not with tiles.
+// ring depth (steps in flight) per row-tile count: (D - 1) * 2 * RT loads <= 63 outstanding
+__host__ __device__ constexpr int gemmRing(int RT) { return RT >= 4 ? 8 : RT == 2 ? 12 : 16; }
+
+// Split-K / tile plan of one matrix for MT token tiles: row tiles of 64 * rt rows (rt = row tiles
+// of 16 per wave), the largest rt that still gives >= 64 tiles; splits so the resident activations
+// fit (MP x KW x 2 B <= 128 KB) and the grid reaches ~DL_GEMM_WG (256) workgroups.
 static int gemmWgTarget() {
     static const int v = [] {
         const char *e = std::getenv("DL_GEMM_WG");
@@ -1125,38 +1138,40 @@ static int gemmWgTarget() {
     }();
     return v;
 }
-static int gemmMaxSplits() {
-    static const int v = [] {
-        const char *e = std::getenv("DL_GEMM_MAXS");
-        return e ? std::max(1, std::atoi(e)) : 8;
-    }();
-    return v;
+
+GemmPlan gemmPlan(int rows, int n, int M) {
+    GemmPlan p;
+    const int steps = n / 128;  // 4-block steps
+    const int MP = gemmTokenPad(M);
+    p.rt = 4;
+    while (p.rt > 1 && (rows + 64 * p.rt - 1) / (64 * p.rt) < 64) p.rt >>= 1;
+    p.tiles = (rows + 64 * p.rt - 1) / (64 * p.rt);
+    p.splits = 1;
+    while ((size_t)MP * (n / p.splits) * 2 > (size_t)kGemmMaxLdsAct && steps % (2 * p.splits) == 0) p.splits *= 2;
+    while (p.tiles * p.splits < gemmWgTarget() && steps % (2 * p.splits) == 0 && steps / (2 * p.splits) >= 2)
+        p.splits *= 2;
+    return p;
 }
 
-int gemmSplits(int rows, int n) {
-    const int tiles = (rows + kGemmRows - 1) / kGemmRows, nb = n / 32;
-    const int target = gemmWgTarget(), maxS = gemmMaxSplits();
-    int S = 1;
-    while (2 * S <= maxS && tiles * S < target && nb % (2 * S) == 0 && nb / (2 * S) >= kGemmCh) S *= 2;
-    return S;
-}
+int gemmSplits(int rows, int n, int M) { return gemmPlan(rows, n, M).splits; }
 
-int gemmTokenPad(int M) { return M <= 16 ? 16 : M <= 32 ? 32 : 64; }
+int gemmTokenPad(int M) { return M <= 16 ? 16 : 32; }
 
 size_t gemmPartFloats(int rows, int n, int maxTokens) {
-    const int tiles = (rows + kGemmRows - 1) / kGemmRows, S = gemmSplits(rows, n);
-    const int mp = gemmTokenPad(maxTokens);
-    return S > 1 ? (size_t)S * tiles * mp * kGemmRows : 0;
+    size_t f = 0;
+    for (int M = 1; M <= std::min(maxTokens, kGemmMaxTokens); M += 16) {  // every token padding in use
+        const GemmPlan p = gemmPlan(rows, n, M);
+        if (p.splits > 1) f = std::max(f, (size_t)p.splits * p.tiles * gemmTokenPad(M) * 64 * p.rt);
+    }
+    return f;
 }
 
-// stage layout (bytes): weights [64 rows][8 units] x 16 B | scales [32 pairs][8] u32 | x [MP][32 units] x 16 B
-static constexpr int kStW = kGemmRows * kGemmCh * 16, kStD = (kGemmRows / 2) * kGemmCh * 4;
-__host__ __device__ static constexpr int gemmStageBytes(int MT) { return kStW + kStD + MT * 16 * kGemmCh * 64; }
-#ifndef DL_GEMM_STAGES
-#define DL_GEMM_STAGES 2  // 3 stages (2 WGs/CU) measured slower: batch-32 8.1k vs 8.8k tok/s
-#endif
-static constexpr int kGemmStages = DL_GEMM_STAGES;  // stage buffers (kGemmStages-1 chunks in flight)
-static size_t gemmLds(int MT, int stages) { return stages * (size_t)gemmStageBytes(MT) + 16; }
+bool gemmSupported(int n) {
+    // whole 4-block steps, and the resident activations of the largest split fit
+    if (n % 128) return false;
+    const GemmPlan p = gemmPlan(64, n, kGemmMaxTokens);
+    return (size_t)32 * (n / p.splits) * 2 <= (size_t)kGemmMaxLdsAct;
+}
 
 // 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d via the 0x6400 | q magic (1024 + q)
 __device__ __forceinline__ half8 dequantQ40x8(u32x2 wv, int nibHi, uint32_t d16) {
@@ -1186,128 +1201,153 @@ __device__ __forceinline__ void glds16(const void *g, void *lds) {
     __builtin_amdgcn_global_load_lds(const_cast<void *>(g), reinterpret_cast<__attribute__((address_space(3))) void *>(
                                          reinterpret_cast<uintptr_t>(lds)), 16, 0, 0);
 }
-__device__ __forceinline__ void glds4(const void *g, void *lds) {
-    __builtin_amdgcn_global_load_lds(const_cast<void *>(g), reinterpret_cast<__attribute__((address_space(3))) void *>(
-                                         reinterpret_cast<uintptr_t>(lds)), 4, 0, 0);
+
+template <int MT, int RT>
+__host__ __device__ constexpr size_t gemmTileBytes() { return (size_t)MT * 16 * 64 * RT * sizeof(float); }
+// dynamic LDS of a launch: resident activations (KW columns) or the output tile, + the arrival flag
+template <int MT, int RT>
+__host__ __device__ inline size_t gemmLdsBytes(int KW) {
+    const size_t act = (size_t)MT * 16 * KW * 2;
+    return (act > gemmTileBytes<MT, RT>() ? act : gemmTileBytes<MT, RT>()) + 16;
 }
 
-// STG = stage buffers: 2 double-buffers the chunk stream inside a workgroup; 1 (the 64-token
-// tile) drops that to fit 3 workgroups per CU, which then overlap each other's loads.
-template <int MT, int EPI, int STG>
+template <int MT, int RT, int EPI>
 __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     const GemvArgs &a = ga.e;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int MP = MT * 16;
-    constexpr int SB = gemmStageBytes(MT);
-    constexpr int NW = kGemmRows * kGemmCh / kThreads, NX = MT * 16 * kGemmCh * 4 / kThreads;
-    constexpr int NLD = NW + 1 + NX;  // glds instructions per thread per stage
-    int *flag = reinterpret_cast<int *>(smem + STG * SB);
+    constexpr int MP = MT * 16, WR = RT * 16, TR = 4 * WR;
+    constexpr int D = gemmRing(RT), NLD = 2 * RT;  // ring steps, weight loads per step
+    static_assert((D - 1) * NLD <= 63, "vmcnt range");
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int col = lane & 15, h = lane >> 4;
     const int n = a.n, nb = n >> 5, L = a.lanes, NG = kThreads / L, KS = (nb + L - 1) / L;
     const int lgL = 31 - __builtin_clz(L);
     const int tileIdx = blockIdx.x, sp = blockIdx.y, S = ga.splits;
-    const int R0 = tileIdx * kGemmRows;
-    const int bps = nb / S, j0 = sp * bps, j1 = j0 + bps;
-    const int nch = (bps + kGemmCh - 1) / kGemmCh;
-    const uint8_t *qs = a.qs;
-    const uint32_t *wd2 = reinterpret_cast<const uint32_t *>(a.wd);
-    auto unitOf = [&](int row, int j) -> size_t {  // tiled 16-B unit of (row, block j), clamped
-        row = min(row, a.rows - 1);
-        j = min(j, j1 - 1);
-        const int g = row / (2 * NG), rem = row % (2 * NG), gi = rem >> 1, rpar = rem & 1;
-        const int k = j >> lgL, li = j & (L - 1);
-        return (((size_t)g * KS + k) * 2 + rpar) * kThreads + gi * L + li;
-    };
-    auto scaleIdx = [&](int pairRow, int j) -> size_t {  // tiled u32 pair scale of (row pair, block j)
-        const int row = min(pairRow, a.rows - 1);
-        j = min(j, j1 - 1);
+    const int R0 = tileIdx * TR;
+    const int bps = nb / S, j0 = sp * bps, T = bps >> 2;
+    const int KW = bps * 32, UPT = KW >> 3;  // resident columns, 16-B units per token row
+    int *flag = reinterpret_cast<int *>(smem + gemmLdsBytes<MT, RT>(KW) - 16);
+
+    // this lane's rows (one per row tile) in the GEMV tiling: unit(row, j) =
+    // ((g*KS + j/L)*2 + rpar)*256 + gi*L + j%L, scale word (g*KS + j/L)*256 + gi*L + j%L
+    size_t uBase[RT], dBase[RT];
+    int rpar[RT];
+#pragma unroll
+    for (int t = 0; t < RT; t++) {
+        const int row = min(R0 + wave * WR + t * 16 + col, a.rows - 1);
         const int g = row / (2 * NG), rem = row % (2 * NG), gi = rem >> 1;
+        rpar[t] = rem & 1;
+        uBase[t] = ((size_t)g * KS * 2 + rpar[t]) * kThreads + gi * L;
+        dBase[t] = (size_t)g * KS * kThreads + gi * L;
+    }
+    const u32x4 *qs = reinterpret_cast<const u32x4 *>(a.qs);
+    const uint32_t *wd2 = reinterpret_cast<const uint32_t *>(a.wd);
+
+    u32x4 wq[D][RT];
+    uint32_t wsc[D][RT];
+    int it = 0;  // issue cursor (steps); past the last step it re-reads the last (L2 hits)
+    auto issue = [&](u32x4(&q)[RT], uint32_t(&d)[RT]) {
+        const int ii = min(it, T - 1);
+        ++it;
+        const int j = j0 + 4 * ii + h;
         const int k = j >> lgL, li = j & (L - 1);
-        return ((size_t)g * KS + k) * kThreads + gi * L + li;
-    };
-    // issue the copies of chunk c into stage buffer b
-    auto issue = [&](int c, int b) {
-        char *st = smem + b * SB;
-        const int c0 = j0 + c * kGemmCh;
-        // weights: unit u = s*256 + tid -> (row_l = u/8, position p = u%8) holds block p ^ (row_l&7)
 #pragma unroll
-        for (int s = 0; s < NW; s++) {
-            const int u = s * kThreads + tid, rl = u / kGemmCh, pp = u % kGemmCh;
-            const size_t unit = unitOf(R0 + rl, c0 + (pp ^ (rl & (kGemmCh - 1))));
-            glds16(qs + unit * 16, st + (size_t)(s * kThreads + wave * 64) * 16);
-        }
-        // pair scales: u = tid -> (pair_l = u/8, block u%8), 4 B each
-        {
-            const int pl = tid / kGemmCh, jj = tid % kGemmCh;
-            glds4(wd2 + scaleIdx(R0 + 2 * pl, c0 + jj), st + kStW + (size_t)(wave * 64) * 4);
-        }
-        // activations: token row t = 4*kGemmCh units of 8 f16; position p holds unit p ^ (t&15)
-#pragma unroll
-        for (int s = 0; s < NX; s++) {
-            const int u = s * kThreads + tid, t = u / (4 * kGemmCh), pp = u % (4 * kGemmCh);
-            const int uu = pp ^ (t & 15);
-            const int cb = min(c0 + (uu >> 2), j1 - 1);  // block of this unit (clamped)
-            const _Float16 *src = ga.x + (size_t)t * n + (size_t)cb * 32 + (uu & 3) * 8;
-            glds16(src, st + kStW + kStD + (size_t)(s * kThreads + wave * 64) * 16);
+        for (int t = 0; t < RT; t++) {
+            const u32x4 *p = qs + uBase[t] + (size_t)k * 2 * kThreads + li;
+            const uint32_t *pd = wd2 + dBase[t] + (size_t)k * kThreads + li;
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(q[t]) : "v"(p));
+            asm volatile("global_load_dword %0, %1, off" : "=v"(d[t]) : "v"(pd));
         }
     };
 
-    f32x4 acc[MT];
+    // prologue: the weight ring first (HBM latency), then the resident activations
 #pragma unroll
-    for (int t = 0; t < MT; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int rl = wave * 16 + col;  // this lane's weight row (local)
-    const int byteHalf = h & 1, nibHi = h >> 1;
+    for (int s = 0; s < D; s++) {
+        issue(wq[s], wsc[s]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    {
+        const int units = MP * UPT;
+        const _Float16 *xb = ga.x + (size_t)j0 * 32;
+        for (int q0 = 0; q0 < units; q0 += kThreads) {  // uniform: units is a multiple of 256
+            const int q = q0 + tid, tk = q / UPT, p = q - tk * UPT, uu = p ^ (tk & 15);
+            glds16(xb + (size_t)tk * n + (size_t)uu * 8, smem + (size_t)(q0 + wave * 64) * 16);
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < D; s++)
+#pragma unroll
+        for (int t = 0; t < RT; t++) asm volatile("s_waitcnt vmcnt(0)" : "+v"(wq[s][t]), "+v"(wsc[s][t]));
+    __syncthreads();
 
-    constexpr int PF = STG - 1;  // chunks in flight ahead of the one consumed
-    for (int c = 0; c < PF && c < nch; c++) issue(c, c);
-    for (int c = 0; c < nch; c++) {
-        if (c + PF < nch) issue(c + PF, (c + PF) % STG);
-        // wait until chunk c landed (this thread): the chunks issued after it may stay in flight
-        const int after = min(nch - 1, c + PF) - c;
-        if (after >= 3)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * NLD) : "memory");
-        else if (after == 2)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * NLD) : "memory");
-        else if (after == 1)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NLD) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // ... and for every thread
-        const char *st = smem + (c % STG) * SB;
-        const int cn = min(kGemmCh, bps - c * kGemmCh);
+    f32x4 acc[RT][MT];
 #pragma unroll
-        for (int jj = 0; jj < kGemmCh; jj++) {
-            const int pp = jj ^ (rl & (kGemmCh - 1));
-            const u32x2 wv = *reinterpret_cast<const u32x2 *>(st + (size_t)(rl * kGemmCh + pp) * 16 + byteHalf * 8);
-            const uint32_t dw = *reinterpret_cast<const uint32_t *>(st + kStW + (size_t)((rl >> 1) * kGemmCh + jj) * 4);
-            const uint32_t d16 = jj < cn ? ((rl & 1) ? dw >> 16 : dw & 0xFFFFu) : 0u;
-            const half8 b = dequantQ40x8(wv, nibHi, d16);
+    for (int t = 0; t < RT; t++)
 #pragma unroll
-            for (int t = 0; t < MT; t++) {
-                const int tok = t * 16 + col, up = (jj * 4 + h) ^ (tok & 15);
-                const half8 av = *reinterpret_cast<const half8 *>(st + kStW + kStD + (size_t)(tok * 4 * kGemmCh + up) * 16);
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b, acc[t], 0, 0, 0);
+        for (int m = 0; m < MT; m++) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto compute = [&](int i, const u32x4(&q)[RT], const uint32_t(&d)[RT]) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ks++) {
+            const int u = (4 * i + h) * 4 + ks;  // block 4i+h of the split, unit ks
+            half8 av[MT];
+#pragma unroll
+            for (int m = 0; m < MT; m++) {  // token m*16 + col (swizzle: low 4 unit bits ^ token)
+                const int tk = m * 16 + col;
+                av[m] = *reinterpret_cast<const half8 *>(smem + ((size_t)tk * UPT + (u ^ col)) * 16);
+            }
+#pragma unroll
+            for (int t = 0; t < RT; t++) {
+                const u32x2 wv = (ks & 1) ? u32x2{q[t].z, q[t].w} : u32x2{q[t].x, q[t].y};
+                const uint32_t d16 = rpar[t] ? d[t] >> 16 : d[t] & 0xFFFFu;
+                const half8 b = dequantQ40x8(wv, ks >> 1, d16);
+#pragma unroll
+                for (int m = 0; m < MT; m++) acc[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[m], b, acc[t][m], 0, 0, 0);
             }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();  // stage c % STG is refilled at iteration c + 1
+    };
+    // full rounds: consume slot s (step t0 + s), refill it with step t0 + s + D
+    int t0 = 0;
+    for (; t0 + D < T; t0 += D) {
+#pragma unroll
+        for (int s = 0; s < D; s++) {
+#pragma unroll
+            for (int t = 0; t < RT; t++)
+                asm volatile("s_waitcnt vmcnt(%2)" : "+v"(wq[s][t]), "+v"(wsc[s][t]) : "i"((D - 1) * NLD));
+            compute(t0 + s, wq[s], wsc[s]);
+            issue(wq[s], wsc[s]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
+    // last round: no refills; slot s waits for itself only (the younger slots stay in flight)
+#pragma unroll
+    for (int s = 0; s < D; s++) {
+#pragma unroll
+        for (int t = 0; t < RT; t++)
+            asm volatile("s_waitcnt vmcnt(%2)" : "+v"(wq[s][t]), "+v"(wsc[s][t]) : "i"((D - 1 - s) * NLD));
+        if (t0 + s < T) compute(t0 + s, wq[s], wsc[s]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();  // every wave is done reading the activations: the LDS becomes the tile
 
-    float *tile = reinterpret_cast<float *>(smem);  // [MP][64], stages are free now
-    // C layout: weight row (local) wave*16 + col, token t*16 + h*4 + i
+    float *tile = reinterpret_cast<float *>(smem);  // [MP][TR]
+    // C layout: weight row (local) wave*WR + t*16 + col, token m*16 + h*4 + i
     if (S == 1) {
 #pragma unroll
-        for (int t = 0; t < MT; t++)
+        for (int t = 0; t < RT; t++)
 #pragma unroll
-            for (int i = 0; i < 4; i++) tile[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
+            for (int m = 0; m < MT; m++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) tile[(m * 16 + h * 4 + i) * TR + wave * WR + t * 16 + col] = acc[t][m][i];
     } else {
         const int tiles = gridDim.x;
-        float *part = ga.part + ((size_t)sp * tiles + tileIdx) * MP * kGemmRows;
+        float *part = ga.part + ((size_t)sp * tiles + tileIdx) * MP * TR;
 #pragma unroll
-        for (int t = 0; t < MT; t++)
+        for (int t = 0; t < RT; t++)
 #pragma unroll
-            for (int i = 0; i < 4; i++) part[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
+            for (int m = 0; m < MT; m++)
+#pragma unroll
+                for (int i = 0; i < 4; i++) part[(m * 16 + h * 4 + i) * TR + wave * WR + t * 16 + col] = acc[t][m][i];
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
@@ -1322,12 +1362,12 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
             __hip_atomic_store(ga.counters + tileIdx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
-        // combine in split order (deterministic), 16-B loads with all of a thread's splits in
-        // flight at once: this tail runs on one workgroup per tile after the others finished
-        const f32x4 *P = reinterpret_cast<const f32x4 *>(ga.part) + (size_t)tileIdx * MP * kGemmRows / 4;
-        const size_t st4 = (size_t)tiles * MP * kGemmRows / 4;
+        // combine in split order (deterministic), only the M real tokens, all of a thread's
+        // splits in flight at once
+        const f32x4 *P = reinterpret_cast<const f32x4 *>(ga.part) + (size_t)tileIdx * MP * TR / 4;
+        const size_t st4 = (size_t)tiles * MP * TR / 4;
         f32x4 *tile4 = reinterpret_cast<f32x4 *>(tile);
-        for (int i = tid; i < MP * kGemmRows / 4; i += kThreads) {
+        for (int i = tid; i < ga.M * TR / 4; i += kThreads) {
             f32x4 v[8];
 #pragma unroll
             for (int s2 = 0; s2 < 8; s2++)
@@ -1341,10 +1381,11 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
         }
     }
     __syncthreads();
-    // fused epilogues on row pairs (2k, 2k+1) of the tile, 32 pairs per token
-    for (int i = tid; i < ga.M * 32; i += kThreads) {
-        const int t = i >> 5, k = i & 31, r0 = R0 + 2 * k;
-        const float v0 = tile[t * kGemmRows + 2 * k], v1 = tile[t * kGemmRows + 2 * k + 1];
+    // fused epilogues on row pairs (2k, 2k+1) of the tile, TR/2 pairs per token
+    constexpr int HP = TR / 2;
+    for (int i = tid; i < ga.M * HP; i += kThreads) {
+        const int t = i / HP, k = i % HP, r0 = R0 + 2 * k;
+        const float v0 = tile[t * TR + 2 * k], v1 = tile[t * TR + 2 * k + 1];
         if constexpr (EPI == EPI_STORE) {
             if (r0 < a.rows) a.out[(size_t)t * a.ldOut + r0] = v0;
             if (r0 + 1 < a.rows) a.out[(size_t)t * a.ldOut + r0 + 1] = v1;
@@ -1353,17 +1394,21 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
         } else if constexpr (EPI == EPI_ACT_F16) {
             if (r0 < a.rows) ga.outH[(size_t)t * a.ldOut + (r0 >> 1)] = (_Float16)(gateAct(a, v0) * v1);
         } else if constexpr (EPI == EPI_ACT_Q80) {
-            const int hBase = R0 >> 1;
-            if (hBase >= (a.rows >> 1)) continue;  // whole 32-unit block: uniform per lane group
-            const float hv = gateAct(a, v0) * v1;
+            // 32 consecutive hidden units (lanes k..k+31 of one token) form one Q80 block; HP is a
+            // multiple of 32 and the hidden row count a multiple of 32: whole groups per block
+            const int hu = (R0 >> 1) + k;
+            const bool live = hu < (a.rows >> 1);
+            const float hv = live ? gateAct(a, v0) * v1 : 0.f;
             const float amax = groupMax<32>(fabsf(hv));
             const float d = amax / 127.0f;
             const float id = d != 0.f ? 1.0f / d : 0.f;
             int q = (int)rintf(hv * id);
             q = q > 127 ? 127 : (q < -127 ? -127 : q);
-            a.oq[(size_t)t * a.ldOut + hBase + k] = (int8_t)q;
             const float qsum = groupSum<32>((float)q);
-            if (k == 0) a.os[(size_t)t * (a.ldOut >> 5) + (hBase >> 5)] = make_float2(roundF16(d), qsum);
+            if (live) {
+                a.oq[(size_t)t * a.ldOut + hu] = (int8_t)q;
+                if ((hu & 31) == 0) a.os[(size_t)t * (a.ldOut >> 5) + (hu >> 5)] = make_float2(roundF16(d), qsum);
+            }
         } else {
             if (r0 < a.rows)
                 qkvPairStore(a, r0, v0, v1, a.rope + (size_t)a.pos[t] * (a.hs >> 1), a.pos[t], a.slot[t],
@@ -1372,49 +1417,39 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     }
 }
 
-static int gemmStages4() {  // stage buffers of the 64-token tile (DL_GEMM_STG4, read once)
-    static const int v = [] {
-        const char *e = std::getenv("DL_GEMM_STG4");
-        return e && std::atoi(e) == 2 ? 2 : 1;
-    }();
-    return v;
+template <int MT, int RT>
+static void gemmLaunchE(const GemmArgs &ga, int epi, dim3 grid, hipStream_t s) {
+    const int KW = ga.e.n / ga.splits;
+    const size_t lds = gemmLdsBytes<MT, RT>(KW);
+#define DL_GEMM_CASE(E)                                                                           \
+    if (epi == E) {                                                                               \
+        if (lds > 65536) allowLds((const void *)gemmQ40Kernel<MT, RT, E>, lds); /* per device */  \
+        hipLaunchKernelGGL((gemmQ40Kernel<MT, RT, E>), grid, dim3(kThreads), lds, s, ga);         \
+        return;                                                                                   \
+    }
+    DL_GEMM_CASE(EPI_STORE) DL_GEMM_CASE(EPI_ACT) DL_GEMM_CASE(EPI_ACT_Q80) DL_GEMM_CASE(EPI_QKV)
+    DL_GEMM_CASE(EPI_ACT_F16)
+#undef DL_GEMM_CASE
 }
 
-static int gemmStages2() {  // stage buffers of the 32-token tile (DL_GEMM_STG2, read once)
-    static const int v = [] {
-        const char *e = std::getenv("DL_GEMM_STG2");
-        return e && std::atoi(e) == 1 ? 1 : kGemmStages;
-    }();
-    return v;
-}
-
-static int gemmStages1() {  // stage buffers of the 16-token tile (DL_GEMM_STG1 = 2..4, read once)
-    static const int v = [] {
-        const char *e = std::getenv("DL_GEMM_STG1");
-        const int k = e ? std::atoi(e) : kGemmStages;
-        return k >= 2 && k <= 4 ? k : kGemmStages;
-    }();
-    return v;
+template <int MT>
+static void gemmLaunchR(const GemmArgs &ga, int epi, int rt, dim3 grid, hipStream_t s) {
+    switch (rt) {
+        case 4: gemmLaunchE<MT, 4>(ga, epi, grid, s); break;
+        case 2: gemmLaunchE<MT, 2>(ga, epi, grid, s); break;
+        default: gemmLaunchE<MT, 1>(ga, epi, grid, s); break;
+    }
 }
 
 void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
-    const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
-    const int MT = gemmTokenPad(ga.M) / 16;
-    const int stg = MT == 4 ? gemmStages4() : MT == 2 ? gemmStages2() : gemmStages1();
-    const dim3 grid(tiles, ga.splits);
-    const size_t lds = gemmLds(MT, stg);
-#define DL_GEMM_CASE(M_, E, G)                                                                    \
-    if (MT == M_ && epi == E && stg == G) {                                                       \
-        if (lds > 65536) allowLds((const void *)gemmQ40Kernel<M_, E, G>, lds); /* per device */  \
-        hipLaunchKernelGGL((gemmQ40Kernel<M_, E, G>), grid, dim3(kThreads), lds, s, ga);         \
-        return;                                                                                   \
-    }
-#define DL_GEMM_CASES(M_, G)                                                                      \
-    DL_GEMM_CASE(M_, EPI_STORE, G) DL_GEMM_CASE(M_, EPI_ACT, G) DL_GEMM_CASE(M_, EPI_ACT_Q80, G)  \
-    DL_GEMM_CASE(M_, EPI_QKV, G) DL_GEMM_CASE(M_, EPI_ACT_F16, G)
-    DL_GEMM_CASES(1, kGemmStages) DL_GEMM_CASES(1, 3) DL_GEMM_CASES(1, 4) DL_GEMM_CASES(2, kGemmStages) DL_GEMM_CASES(2, 1) DL_GEMM_CASES(4, 1) DL_GEMM_CASES(4, 2)
-#undef DL_GEMM_CASES
-#undef DL_GEMM_CASE
+    const GemmPlan p = gemmPlan(ga.e.rows, ga.e.n, ga.M);
+    if (!gemmSupported(ga.e.n) || ga.M < 1 || ga.M > kGemmMaxTokens || ga.splits != p.splits)
+        throw Error("launchGemmQ40: unsupported shape (n % 128, 1..32 tokens, splits from gemmPlan)");
+    const dim3 grid(p.tiles, p.splits);
+    if (gemmTokenPad(ga.M) == 16)
+        gemmLaunchR<1>(ga, epi, p.rt, grid, s);
+    else
+        gemmLaunchR<2>(ga, epi, p.rt, grid, s);
 }
 
 // Residual add + RMS norm (optional) of M rows -> f16 (one workgroup per row): the batched

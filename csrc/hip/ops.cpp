@@ -170,6 +170,7 @@ std::vector<float> gemmQ40(const std::vector<uint8_t> &blocks, int rows, int n, 
                            const std::vector<float> &residual, const std::vector<float> &normW, float eps, int M) {
     DL_CHECK(M >= 1 && M <= 64, "gemm tokens must be 1..64");
     DL_CHECK(in.size() == (size_t)M * n, "gemm input size");
+    DL_CHECK(hipk::gemmSupported(n), "gemm input width must be a multiple of 128");
     checkRows(residual, (size_t)M * n, "residual");
     checkRows(normW, (size_t)n, "norm weights");
     Scratch sc;
@@ -181,25 +182,34 @@ std::vector<float> gemmQ40(const std::vector<uint8_t> &blocks, int rows, int n, 
     nq.addIn = sc.upload(residual);
     nq.normW = sc.upload(normW);
     nq.eps = eps;
-    _Float16 *xh = sc.alloc<_Float16>((size_t)hipk::gemmTokenPad(M) * n);  // rows past M read as zeros
+    // rows past M are read by the last launch (padded to 16/32) and their outputs dropped
+    const int rowsPad = (M + hipk::kGemmMaxTokens - 1) / hipk::kGemmMaxTokens * hipk::kGemmMaxTokens;
+    _Float16 *xh = sc.alloc<_Float16>((size_t)rowsPad * n);
     hipk::launchNormF16(nq, xh, M, sc.s);
-    hipk::GemmArgs g;
-    g.e.qs = w.qs;
-    g.e.wd = w.d;
-    g.e.rows = rows;
-    g.e.n = n;
-    g.e.lanes = w.lanes;
-    g.e.out = sc.alloc<float>((size_t)M * rows);
-    g.e.ldOut = rows;
-    g.x = xh;
-    g.M = M;
-    g.splits = hipk::gemmSplits(rows, n);
+    float *out = sc.alloc<float>((size_t)M * rows);
     const size_t part = hipk::gemmPartFloats(rows, n, M);
-    g.part = part ? sc.alloc<float>(part) : nullptr;
-    g.counters = sc.alloc<int>((size_t)(rows + 63) / 64 + 1);
-    hipk::launchGemmQ40(g, hipk::EPI_STORE, sc.s);
+    float *partBuf = part ? sc.alloc<float>(part) : nullptr;
+    int *counters = sc.alloc<int>((size_t)(rows + 63) / 64 + 1);
+    // one launch per <= 32 tokens (the engine's chunking)
+    for (int c0 = 0; c0 < M; c0 += hipk::kGemmMaxTokens) {
+        const int bc = std::min(hipk::kGemmMaxTokens, M - c0);
+        hipk::GemmArgs g;
+        g.e.qs = w.qs;
+        g.e.wd = w.d;
+        g.e.rows = rows;
+        g.e.n = n;
+        g.e.lanes = w.lanes;
+        g.e.out = out + (size_t)c0 * rows;
+        g.e.ldOut = rows;
+        g.x = xh + (size_t)c0 * n;
+        g.M = bc;
+        g.splits = hipk::gemmSplits(rows, n, bc);
+        g.part = partBuf;
+        g.counters = counters;
+        hipk::launchGemmQ40(g, hipk::EPI_STORE, sc.s);
+    }
     sc.sync();
-    return sc.download(g.e.out, (size_t)M * rows);
+    return sc.download(out, (size_t)M * rows);
 }
 
 std::vector<float> qkvRope(const std::vector<uint8_t> &blocks, int q0, int kv0, int hs, int n,

@@ -6,6 +6,7 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -110,6 +111,59 @@ void Socket::recvAll(void *data, u64 n) {
     }
 }
 
+void exchangeAll(const std::vector<Socket *> &peers, const void *send, u64 n, const std::vector<void *> &recv) {
+    const size_t P = peers.size();
+    std::vector<u64> sent(P, 0), got(P, 0);
+    std::vector<pollfd> fds;
+    std::vector<size_t> idx;
+    for (;;) {
+        fds.clear();
+        idx.clear();
+        for (size_t i = 0; i < P; i++) {
+            if (!peers[i]) continue;
+            short ev = 0;
+            if (sent[i] < n) ev |= POLLOUT;
+            if (got[i] < n) ev |= POLLIN;
+            if (!ev) continue;
+            fds.push_back(pollfd{peers[i]->fd(), ev, 0});
+            idx.push_back(i);
+        }
+        if (fds.empty()) return;
+        const int r = ::poll(fds.data(), fds.size(), 60000);
+        if (r < 0) {
+            if (errno == EINTR) continue;
+            throw NetError(std::string("poll: ") + std::strerror(errno));
+        }
+        if (r == 0) throw NetError("Socket exchange timeout");
+        for (size_t k = 0; k < fds.size(); k++) {
+            const size_t i = idx[k];
+            if (fds[k].revents & (POLLERR | POLLHUP | POLLNVAL) && !(fds[k].revents & POLLIN))
+                throw NetError("Socket closed during exchange");
+            if ((fds[k].revents & POLLOUT) && sent[i] < n) {
+                const u64 left = n - sent[i];
+                const ssize_t w = ::send(fds[k].fd, (const char *)send + sent[i], left > (1u << 20) ? (1u << 20) : left,
+                                         MSG_NOSIGNAL | MSG_DONTWAIT);
+                if (w < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)
+                    throw NetError(std::string("Error writing to socket: ") + std::strerror(errno));
+                if (w > 0) {
+                    sent[i] += (u64)w;
+                    peers[i]->addStats((u64)w, 0);
+                }
+            }
+            if ((fds[k].revents & POLLIN) && got[i] < n) {
+                const ssize_t g = ::recv(fds[k].fd, (char *)recv[i] + got[i], n - got[i], MSG_DONTWAIT);
+                if (g == 0) throw NetError("Socket closed");
+                if (g < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)
+                    throw NetError(std::string("Error reading from socket: ") + std::strerror(errno));
+                if (g > 0) {
+                    got[i] += (u64)g;
+                    peers[i]->addStats(0, (u64)g);
+                }
+            }
+        }
+    }
+}
+
 void Socket::setRecvTimeout(int ms) {
     timeval tv;
     tv.tv_sec = ms / 1000;
@@ -196,6 +250,7 @@ std::string encodeWorkerConfig(const WorkerConfig &c) {
       << "\nh_rsf=" << h.ropeScalingFactor << "\nh_rlo=" << h.ropeScalingLowFreqFactor
       << "\nh_rhi=" << h.ropeScalingHighFreqFactor << "\nh_rorig=" << h.ropeScalingOrigMaxSeqLen
       << "\nuid=" << hexOf(c.rcclUid) << "\ndev_comm=" << c.devComm << "\nxgmi_max=" << c.xgmiMaxFloats << "\n";
+    for (size_t i = 0; i < c.peerHosts.size(); i++) o << "peer=" << c.peerHosts[i] << ":" << c.peerPorts[i] << "\n";
     return o.str();
 }
 
@@ -242,6 +297,12 @@ WorkerConfig decodeWorkerConfig(const std::string &s) {
         else if (k == "uid") c.rcclUid = unhex(v);
         else if (k == "dev_comm") c.devComm = v;
         else if (k == "xgmi_max") c.xgmiMaxFloats = std::stoull(v);
+        else if (k == "peer") {
+            const size_t colon = v.rfind(':');
+            if (colon == std::string::npos) throw NetError("bad peer address in config");
+            c.peerHosts.push_back(v.substr(0, colon));
+            c.peerPorts.push_back(std::stoi(v.substr(colon + 1)));
+        }
     }
     if (!magicOk) throw NetError("bad control-plane magic");
     h.origSeqLen = h.seqLen;
@@ -251,16 +312,16 @@ WorkerConfig decodeWorkerConfig(const std::string &s) {
 // ---- CPU data plane ----------------------------------------------------------------------------
 void TcpHostComm::allReduceSum(float *data, u64 n) {
     if (size_ == 1) return;
-    if (rank_ == 0) {
-        tmp_.resize(n);
-        for (Socket *s : peers_) {
-            s->recvAll(tmp_.data(), n * sizeof(float));
-            for (u64 i = 0; i < n; i++) data[i] += tmp_[i];
-        }
-        for (Socket *s : peers_) s->sendAll(data, n * sizeof(float));
-    } else {
-        peers_[0]->sendAll(data, n * sizeof(float));
-        peers_[0]->recvAll(data, n * sizeof(float));
+    tmp_.resize(n * size_);
+    std::vector<void *> recv(size_);
+    for (int r = 0; r < size_; r++) recv[r] = tmp_.data() + (u64)r * n;
+    exchangeAll(peers_, data, n * sizeof(float), recv);
+    std::memcpy(tmp_.data() + (u64)rank_ * n, data, n * sizeof(float));
+    // every rank sums the same partials in the same (rank) order: bitwise identical results
+    std::memcpy(data, tmp_.data(), n * sizeof(float));
+    for (int r = 1; r < size_; r++) {
+        const float *src = tmp_.data() + (u64)r * n;
+        for (u64 i = 0; i < n; i++) data[i] += src[i];
     }
 }
 
@@ -269,15 +330,11 @@ void TcpHostComm::allReduceSumQ80(float *data, u64 n) {
     DL_CHECK(n % kQBlock == 0, "Q80 sync needs 32-aligned vectors");
     const u64 part = n / kQBlock * sizeof(BlockQ80);
     q80_.resize(part * size_);
-    // my quantized partial goes to slot [rank]; the root relays all slots (star topology)
+    // my quantized partial goes to slot [rank] and to every peer; theirs land in their slots
     quantizeQ80(data, reinterpret_cast<BlockQ80 *>(q80_.data() + part * rank_), n);
-    if (rank_ == 0) {
-        for (size_t i = 0; i < peers_.size(); i++) peers_[i]->recvAll(q80_.data() + part * (i + 1), part);
-        for (Socket *s : peers_) s->sendAll(q80_.data(), part * size_);
-    } else {
-        peers_[0]->sendAll(q80_.data() + part * rank_, part);
-        peers_[0]->recvAll(q80_.data(), part * size_);
-    }
+    std::vector<void *> recv(size_);
+    for (int r = 0; r < size_; r++) recv[r] = q80_.data() + part * r;
+    exchangeAll(peers_, q80_.data() + part * rank_, part, recv);
     tmp_.resize(n);
     std::fill(data, data + n, 0.f);
     for (int r = 0; r < size_; r++) {
@@ -289,13 +346,13 @@ void TcpHostComm::allReduceSumQ80(float *data, u64 n) {
 void TcpHostComm::gatherToRoot(const float *local, u64 nLocal, float *out) {
     if (rank_ == 0) {
         if (out) std::memcpy(out, local, nLocal * sizeof(float));
-        for (size_t i = 0; i < peers_.size(); i++) {
-            float *dst = out ? out + (i + 1) * nLocal : nullptr;
+        for (int r = 1; r < size_; r++) {
+            float *dst = out ? out + (u64)r * nLocal : nullptr;
             if (dst) {
-                peers_[i]->recvAll(dst, nLocal * sizeof(float));
+                peers_[r]->recvAll(dst, nLocal * sizeof(float));
             } else {
                 tmp_.resize(nLocal);
-                peers_[i]->recvAll(tmp_.data(), nLocal * sizeof(float));
+                peers_[r]->recvAll(tmp_.data(), nLocal * sizeof(float));
             }
         }
     } else {
@@ -306,6 +363,7 @@ void TcpHostComm::gatherToRoot(const float *local, u64 nLocal, float *out) {
 void TcpHostComm::stats(u64 &sent, u64 &recv) const {
     sent = recv = 0;
     for (Socket *s : peers_) {
+        if (!s) continue;
         sent += s->sentBytes();
         recv += s->recvBytes();
     }

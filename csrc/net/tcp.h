@@ -45,6 +45,12 @@ class Socket {
     u64 sentBytes() const { return sent_; }
     u64 recvBytes() const { return recv_; }
     void resetStats() { sent_ = recv_ = 0; }
+    void addStats(u64 sent, u64 recv) {
+        sent_ += sent;
+        recv_ += recv;
+        totalSent_ += sent;
+        totalRecv_ += recv;
+    }
     // never reset (metrics deltas)
     u64 totalSentBytes() const { return totalSent_; }
     u64 totalRecvBytes() const { return totalRecv_; }
@@ -80,8 +86,14 @@ class ServerSocket {
     int port_;
 };
 
+// Send `n` bytes to every non-null peer and receive `n` bytes from each into recv[i], multiplexed
+// with poll() so no pair of ranks can deadlock on full socket buffers (the reference's
+// non-blocking round-robin writeMany/readMany, nn-network.cpp:419-491).
+void exchangeAll(const std::vector<Socket *> &peers, const void *send, u64 n, const std::vector<void *> &recv);
+
 // ---- control protocol ------------------------------------------------------------------------
 constexpr u32 kProtoMagic = 0xD11A3355;  // "dllama MI355"
+constexpr u32 kMeshMagic = 0xD11A3356;   // worker -> worker data-plane connection
 constexpr u32 kProtoVersion = 1;
 constexpr u32 kAck = 23571114;           // same ACK value as the reference (nn-network.cpp:23)
 
@@ -100,15 +112,23 @@ struct WorkerConfig {
     std::vector<unsigned char> rcclUid;
     std::string devComm = "xgmi";  // GPU data plane: "xgmi" (IPC one-shot) or "rccl"
     u64 xgmiMaxFloats = 0;          // largest single message per rank (xgmi)
+    // CPU data plane: every worker's address by rank (index rank - 1), for the worker-to-worker mesh
+    std::vector<std::string> peerHosts;
+    std::vector<int> peerPorts;
 };
 std::string encodeWorkerConfig(const WorkerConfig &c);
 WorkerConfig decodeWorkerConfig(const std::string &s);
 
-// CPU-backend data plane over the root<->worker sockets (star topology through the root).
+// CPU-backend data plane over a full mesh of sockets (reference: every node holds N-1 sockets and
+// writes its slice to all peers, nn-network.cpp:264-348, 537-569): every rank sends its partial to
+// every other rank and sums all partials in rank order, so all ranks get bitwise the same result
+// and no rank relays another's traffic.
 class TcpHostComm : public HostComm {
   public:
-    // root: one socket per worker (rank i+1 at index i); worker: single socket to the root
-    TcpHostComm(int rank, int size, std::vector<Socket *> peers) : rank_(rank), size_(size), peers_(std::move(peers)) {}
+    // peers[r] = socket to rank r (nullptr at r == rank); rank 0 is the root
+    TcpHostComm(int rank, int size, std::vector<Socket *> peers) : rank_(rank), size_(size), peers_(std::move(peers)) {
+        DL_CHECK((int)peers_.size() == size_, "TcpHostComm: one socket slot per rank");
+    }
     int rank() const override { return rank_; }
     int size() const override { return size_; }
     void allReduceSum(float *data, u64 n) override;

@@ -9,6 +9,7 @@
 #include "../core/model_file.h"
 #include "../core/plan.h"
 #include "../core/quant.h"
+#include "../cpu/cpu_ops.h"
 #include "../hip/engine.h"
 #include "../hip/ops.h"
 #include "../runtime/backend.h"
@@ -281,6 +282,64 @@ PYBIND11_MODULE(_C, m) {
         return out;
     });
 
+    // CPU reference primitives (csrc/cpu/cpu_ops.h) for the reference-golden tests
+    py::module_ co = m.def_submodule("cpu_ops", "CPU reference primitives (csrc/cpu/cpu_ops.h)");
+    co.def("inv_rms", [](py::array_t<float, py::array::c_style | py::array::forcecast> x, float eps) {
+        return cpu::invRms(x.data(), (u32)x.size(), eps);
+    });
+    auto elementwise = [](float (*f)(float)) {
+        return [f](py::array_t<float, py::array::c_style | py::array::forcecast> x) {
+            py::array_t<float> out(x.size());
+            for (py::ssize_t i = 0; i < x.size(); i++) out.mutable_data()[i] = f(x.data()[i]);
+            return out;
+        };
+    };
+    co.def("silu", elementwise(&cpu::silu));
+    co.def("gelu", elementwise(&cpu::gelu));
+    co.def("softmax", [](py::array_t<float, py::array::c_style | py::array::forcecast> x) {
+        py::array_t<float> out(x.size());
+        std::memcpy(out.mutable_data(), x.data(), x.size() * sizeof(float));
+        softmaxInPlace(out.mutable_data(), (u64)x.size());
+        return out;
+    });
+    // the engines' RoPE table ([seqLen][headSize/2] (cos, sin), Llama-3.1 scaling when the header
+    // has rope_scaling_factor != 1) for a header dict
+    co.def("rope_table", [](py::dict header) {
+        const ModelHeader h = dictToHeader(header);
+        std::vector<float> t = buildRopeTable(h);
+        py::array_t<float> out({(py::ssize_t)h.seqLen, (py::ssize_t)(h.headSize() / 2), (py::ssize_t)2});
+        std::memcpy(out.mutable_data(), t.data(), t.size() * sizeof(float));
+        return out;
+    });
+    co.def("rope_apply", [](py::array_t<float, py::array::c_style | py::array::forcecast> x, int pos, int headSize,
+                            py::array_t<float, py::array::c_style | py::array::forcecast> table) {
+        py::array_t<float> out(x.size());
+        std::memcpy(out.mutable_data(), x.data(), x.size() * sizeof(float));
+        cpu::ropeApply(out.mutable_data(), (u32)x.size(), (u32)pos, (u32)headSize, table.data());
+        return out;
+    });
+    // y[B][rows] = W . x[b] with W Q40 blocks [rows][cols/32] and x quantized to Q80 (the
+    // reference's matmul_Q80_Q40_F32)
+    co.def("matmul_q40_q80", [](py::array_t<uint8_t, py::array::c_style> blocks, int rows, int cols,
+                                py::array_t<float, py::array::c_style | py::array::forcecast> x, int nThreads) {
+        DL_CHECK(cols % kQBlock == 0 && (size_t)blocks.size() == (size_t)rows * cols / kQBlock * kQ40BlockBytes &&
+                     x.size() % cols == 0, "matmul_q40_q80 shapes");
+        const int B = (int)(x.size() / cols);
+        std::vector<BlockQ80> xq((size_t)B * cols / kQBlock);
+        quantizeQ80(x.data(), xq.data(), (u64)B * cols);
+        std::vector<const BlockQ80 *> xs(B);
+        py::array_t<float> out({(py::ssize_t)B, (py::ssize_t)rows});
+        std::vector<float *> ys(B);
+        for (int b = 0; b < B; b++) {
+            xs[b] = xq.data() + (size_t)b * cols / kQBlock;
+            ys[b] = out.mutable_data() + (size_t)b * rows;
+        }
+        ThreadPool pool(nThreads);
+        py::gil_scoped_release rel;
+        cpu::matmulQ40Q80(reinterpret_cast<const BlockQ40 *>(blocks.data()), rows, cols, xs.data(), B, ys.data(), pool);
+        return out;
+    }, py::arg("blocks"), py::arg("rows"), py::arg("cols"), py::arg("x"), py::arg("nthreads") = 4);
+
     m.def("load_header", [](const std::string &path, u32 maxSeqLen) { return headerToDict(loadModelHeader(path, maxSeqLen)); },
           py::arg("path"), py::arg("max_seq_len") = 0);
     m.def("tensor_table", [](const std::string &path) {
@@ -423,6 +482,8 @@ PYBIND11_MODULE(_C, m) {
           py::arg("rows"), py::arg("n"), py::arg("pro"), py::arg("epi"), py::arg("batch") = 1, py::arg("lanes") = 0,
           py::arg("passes") = 0, py::arg("copies") = 8, py::arg("iters") = 20,
           "bench_gemv_q40 with per-workgroup s_memrealtime stamps: (us, u64[iters*grid*4])");
+    m.def("bench_gemm_q40", &benchGemmQ40, py::arg("rows"), py::arg("n"), py::arg("tokens"), py::arg("epi") = 0,
+          py::arg("copies") = 8, py::arg("iters") = 100, py::call_guard<py::gil_scoped_release>());
     m.def("bench_attention", &benchAttention, py::arg("n_heads0"), py::arg("kv_mul"), py::arg("head_size"),
           py::arg("seq_len"), py::arg("pos"), py::arg("batch") = 1, py::arg("copies") = 32, py::arg("iters") = 200,
           py::call_guard<py::gil_scoped_release>());

@@ -165,6 +165,9 @@ InferenceSession::InferenceSession(const AppArgs &args, int nSlots) : args_(args
                 std::printf("⭕ Connecting to worker %s:%d\n", args.workerHosts[i].c_str(), args.workerPorts[i]);
             workers_.push_back(Socket::connectTo(args.workerHosts[i], args.workerPorts[i]));
         }
+        // every worker learns every other worker's address (the CPU data plane is a full mesh)
+        wc.peerHosts = args.workerHosts;
+        wc.peerPorts = args.workerPorts;
         for (size_t i = 0; i < workers_.size(); i++) {
             wc.rank = (u32)(i + 1);
             workers_[i].sendPod<u32>(kProtoMagic);
@@ -180,7 +183,7 @@ InferenceSession::InferenceSession(const AppArgs &args, int nSlots) : args_(args
                 throw NetError("worker failed before loading weights");
             }
         }
-        std::vector<Socket *> peers;
+        std::vector<Socket *> peers{nullptr};  // by rank: the root's data sockets are its control sockets
         for (auto &s : workers_) peers.push_back(&s);
         if (gpu_) {
             DL_HIP(hipSetDevice(a.gpuIndex));
@@ -338,6 +341,7 @@ void runWorker(const AppArgs &args) {
             ec.nThreads = args.nThreads;
             ec.gpuIndex = args.gpuIndex >= 0 ? args.gpuIndex : (wc.gpu ? (int)wc.rank : -1);
             ec.useGraphs = ec.useGraphs && args.graphs;
+            std::vector<Socket> mesh;  // CPU data plane sockets to the other workers
             std::unique_ptr<HostComm> hc;
             std::unique_ptr<DeviceComm> dc;
             std::unique_ptr<Backend> backend;
@@ -355,7 +359,28 @@ void runWorker(const AppArgs &args) {
                         dc = makeRcclComm(wc.rcclUid, (int)wc.rank, (int)wc.world);
                     }
                 } else {
-                    hc.reset(new TcpHostComm((int)wc.rank, (int)wc.world, {&root}));
+                    // full mesh: connect to the higher ranks (their listen backlog takes the
+                    // connection before they accept), then accept the lower ones
+                    mesh.reserve(wc.world);
+                    std::vector<Socket *> byRank(wc.world, nullptr);
+                    byRank[0] = &root;
+                    for (u32 r = wc.rank + 1; r < wc.world; r++) {
+                        DL_CHECK(r - 1 < wc.peerHosts.size(), "config lacks peer addresses");
+                        mesh.push_back(Socket::connectTo(wc.peerHosts[r - 1], wc.peerPorts[r - 1]));
+                        mesh.back().sendPod<u32>(kMeshMagic);
+                        mesh.back().sendPod<u32>(wc.rank);
+                        byRank[r] = &mesh.back();
+                    }
+                    for (u32 k = 1; k < wc.rank; k++) {
+                        mesh.push_back(server.accept());
+                        if (mesh.back().recvPod<u32>() != kMeshMagic) throw NetError("bad magic from a peer worker");
+                        const u32 r = mesh.back().recvPod<u32>();
+                        if (r == 0 || r >= wc.rank || byRank[r]) throw NetError("unexpected peer rank");
+                        byRank[r] = &mesh.back();
+                    }
+                    if (logLevel() >= 1)
+                        std::printf("⭕ Data-plane mesh: %u peer sockets\n", wc.world - 1);
+                    hc.reset(new TcpHostComm((int)wc.rank, (int)wc.world, byRank));
                 }
                 backend = makeBackend(ec, wc.gpu, hc.get(), dc.get());
             } catch (const std::exception &e) {

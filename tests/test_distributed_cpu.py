@@ -90,6 +90,9 @@ def test_tensor_parallel_matches_single(kv4, n_workers):
         logs = [p.communicate()[0].decode(errors="replace") for p in procs]
     for l in logs:
         assert "Stop signal" in l and l.count("Listening on port") >= 2
+        # full-mesh data plane: every worker holds a socket to every other rank (reference
+        # nn-network.cpp:264-348), not just to the root
+        assert f"Data-plane mesh: {n_workers} peer sockets" in l, l
 
 
 def test_workers_without_model_file_get_streamed_slices(kv4, tmp_path):
@@ -102,6 +105,11 @@ def test_workers_without_model_file_get_streamed_slices(kv4, tmp_path):
         rc, out = _inference(kv4, addrs)
         assert rc == 0, out
         assert _preds(out) == _preds(ref)
+        # the workers process the stop signal asynchronously: let them end the session
+        for _ in range(100):
+            if not list(tmp_path.glob("dllama_r*")):
+                break
+            time.sleep(0.05)
     finally:
         for p in procs:
             p.kill()

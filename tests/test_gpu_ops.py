@@ -93,7 +93,13 @@ def test_qkv_rope_kv_append(ops, kv_bf16):
     pos = [5, 63]
     x = torch.randn(len(pos), n, generator=g)
     nw = torch.rand(n, generator=g) + 0.5
-    rope = ops.ref_rope_table(seq, hs, 500000.0)
+    # the engines' Llama-3.1-scaled table (pinned to the reference's goldens in test_goldens.py)
+    import distributed_llama_multiusers_amd as dl
+    rope = torch.from_numpy(dl.native().cpu_ops.rope_table(dict(
+        dim=32 * hs, hidden_dim=1, n_layers=1, n_heads=32, n_kv_heads=8, vocab_size=32, seq_len=seq,
+        rope_theta=500000.0, rope_scaling_factor=8.0, rope_scaling_low_freq_factor=1.0,
+        rope_scaling_high_freq_factor=4.0, rope_scaling_orig_max_seq_len=8192, rope_type=2)))
+    assert not torch.allclose(rope, ops.ref_rope_table(seq, hs, 500000.0), atol=1e-3)  # scaling is active
     q, k, v = ops.qkv_rope(blocks, q0, kv0, hs, n, x, nw, 1e-5, rope, seq, pos, kv_bf16)
     y = ops.dequantize_q80(ops.ref_rmsnorm(x, nw)) @ wd.T
     tol = 8e-3 if kv_bf16 else 2e-4  # bf16 cache rows
@@ -137,3 +143,20 @@ def test_embedding_gather(ops):
     table = torch.randn(1000, 256, generator=torch.Generator().manual_seed(13))
     tokens = [0, 999, 5, 5]
     assert torch.equal(ops.embedding(table, tokens), table[tokens])
+
+
+def test_gemv_matmul_q80_q40_golden(ops):
+    """The reference's 4096 x 4096 Q80 x Q40 matmul check (src/nn/nn-vulkan-test.cpp:533-587:
+    x = i * 1e-5, W = i * 1e-6, every output within 3.5 % of the f32 sum) on the decode GEMV, and
+    the GEMV equal to the CPU backend's matmul on the same quantized operands."""
+    import numpy as np
+    import distributed_llama_multiusers_amd as dl
+    n = d = 4096
+    x = (torch.arange(4 * n, dtype=torch.float64) * 0.00001).float().reshape(4, n)
+    w = (torch.arange(n * d, dtype=torch.float64) * 0.000001).float().reshape(d, n)
+    blocks = ops.quantize_q40(w)
+    out = ops.gemv_q40_q80_in(blocks, d, n, x)
+    ref = x.double() @ w.double().T
+    assert bool(((out.double() - ref).abs() <= ref.abs() * 0.035).all())
+    cpu = torch.from_numpy(dl.native().cpu_ops.matmul_q40_q80(np.asarray(blocks), d, n, x.numpy()))
+    assert rel(out, cpu) < 1e-5
