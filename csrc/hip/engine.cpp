@@ -74,6 +74,11 @@ class HipEngineImpl : public HipEngine {
         DL_CHECK(h_.headSize() == 64 || h_.headSize() == 128, "GPU kernels support head size 64 or 128");
         DL_CHECK(cfg.maxBatch >= 1 && cfg.nSlots >= 1, "maxBatch/nSlots");
         kvBf16_ = cfg.kvBf16;
+        if (kvBf16_) {  // the bf16 (MFMA) attention reads 4-position runs of the transposed V rows
+            h_.seqLen = (h_.seqLen + 7) / 8 * 8;
+            DL_CHECK(hipk::attnMfmaSupported((int)plan_.kvMul, (int)h_.headSize(), (int)h_.seqLen),
+                     "bf16 KV cache: attention shape not supported (use --kv-dtype f32)");
+        }
         syncQ80_ = cfg.syncType == FloatType::Q80;
         if (comm_ && plan_.nRanks > 1) {
             const char *e = std::getenv("DL_TP_FUSED");  // 0: separate all-reduce kernels (comparison)
@@ -999,7 +1004,7 @@ double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int pas
     return ms * 1000.0 / iters;
 }
 
-double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters) {
+double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters, int probe) {
     DL_CHECK(M >= 1 && M <= hipk::kGemmMaxTokens && hipk::gemmSupported(n) && rows % 64 == 0, "bad gemm bench shape");
     hipStream_t s;
     DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -1036,6 +1041,12 @@ double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters) {
     g.splits = hipk::gemmSplits(rows, n, M);
     g.part = part ? (float *)alloc(part * 4) : nullptr;
     g.counters = (int *)alloc((size_t)(rows / 64 + 1) * 4);
+    if (probe) {  // the contiguous probe addresses cover exactly tiles x tile rows x nb blocks
+        const hipk::GemmPlan gp = hipk::gemmPlan(rows, n, M);
+        DL_CHECK(rows % (rows / gp.tiles) == 0 && (size_t)gp.tiles * (rows / gp.tiles) == (size_t)rows,
+                 "gemm probe needs whole tiles");
+    }
+    g.probe = probe;
     auto launch = [&](int c) {
         g.e.qs = qs[c % copies];
         g.e.wd = d[c % copies];

@@ -142,6 +142,7 @@ struct GemmArgs {
     int splits = 1;
     float *part = nullptr;
     int *counters = nullptr;
+    int probe = 0;  // microbenchmark only: 1 = contiguous weight addresses (timing, wrong results)
 };
 void launchGemmQ40(const GemmArgs &a, int epi, hipStream_t s);
 // Tile / split-K plan of one matrix (rt = 16-row tiles per wave: 64 * rt rows per workgroup).
@@ -177,7 +178,10 @@ size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg, int pro);
 // resident at once (DL_GEMV_RESIDENT workgroups, default 512); ACT_Q80 -> whole Q80 blocks per WG.
 int gemvDefaultPasses(int n, int rows, int B, bool q40, int epi);
 
+// bf16 KV caches run the MFMA kernel and store V transposed ([slot][kv0][seqLen]); f32 caches run
+// the VALU kernel with row-major V ([slot][seqLen][kv0]). K is row-major in both.
 void launchAttention(const AttnArgs &a, int B, hipStream_t s);
+bool attnMfmaSupported(int kvMul, int hs, int seqLen);
 int attnSplitGrid(int seqLen);
 int attnChunkMax(int seqLen, int splitGrid);
 

@@ -31,6 +31,7 @@ namespace hipk {
 using namespace dl::dev;
 
 static constexpr int kThreads = 256;
+static constexpr int kAttnMChunkKeys = 128;  // keys per workgroup chunk of the MFMA attention
 static constexpr int kMaxHeadSize = 128;  // RoPE rows staged in LDS by the QKV epilogue
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -379,11 +380,13 @@ __device__ __forceinline__ void qkvPairStore(const GemvArgs &a, int r0, float v0
             }
         }
     } else {
-        const size_t off = ((size_t)sl * a.seqLen + p) * a.kv0 + (r0 - a.q0 - a.kv0);
-        if (a.kvBf16) {
-            const uint32_t pk = (uint32_t)f32ToBf16(v0) | ((uint32_t)f32ToBf16(v1) << 16);
-            *reinterpret_cast<uint32_t *>(reinterpret_cast<uint16_t *>(a.vcache) + off) = pk;
+        const int e = r0 - a.q0 - a.kv0;
+        if (a.kvBf16) {  // bf16 V is stored transposed, [slot][kv0][seqLen] (MFMA attention operand)
+            uint16_t *vt = reinterpret_cast<uint16_t *>(a.vcache) + ((size_t)sl * a.kv0 + e) * a.seqLen + p;
+            vt[0] = f32ToBf16(v0);
+            vt[a.seqLen] = f32ToBf16(v1);
         } else {
+            const size_t off = ((size_t)sl * a.seqLen + p) * a.kv0 + e;
             *reinterpret_cast<float2 *>(reinterpret_cast<float *>(a.vcache) + off) = make_float2(v0, v1);
         }
     }
@@ -1101,8 +1104,9 @@ void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_
 // ------------------------------------------------------------------------------------------------
 // Batched Q40 matmul on MFMA (prefill / multi-user decode, up to 32 tokens per launch).
 //   out[t][row] = sum_k W[row][k] * x[t][k], W Q40 (the GEMV's tiled layout), x f16.
-// Workgroup = 4 waves; a wave owns RT row tiles of 16 rows (the workgroup 64 * RT rows) and all
-// MT token tiles of 16 tokens, over one K split of KW = n / splits columns:
+// Workgroup = 8 waves (two per SIMD: a lone wave issues VALU at half rate and the Q40 dequant is
+// VALU work); a wave owns RT row tiles of 16 rows (the workgroup 128 * RT rows) and all MT token
+// tiles of 16 tokens, over one K split of KW = n / splits columns:
 // * the workgroup's activations (MP tokens x KW, f16, <= 128 KB) are copied L2 -> LDS ONCE with
 //   global_load_lds (XOR-swizzled 16-B units: conflict-free ds_read_b128) and stay resident, so
 //   the K loop has no barrier and no LDS refill;
@@ -1125,10 +1129,12 @@ void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 static constexpr int kGemmMaxLdsAct = 128 * 1024;  // resident activation bytes per workgroup
 
-// ring depth (steps in flight) per row-tile count: (D - 1) * 2 * RT loads <= 63 outstanding
-__host__ __device__ constexpr int gemmRing(int RT) { return RT >= 4 ? 8 : RT == 2 ? 12 : 16; }
+static constexpr int kGemmWaves = 8, kGemmThreads = kGemmWaves * 64;
+// ring depth (steps in flight) per row-tile count: (D - 1) * 2 * RT loads <= 63 outstanding, and
+// <= 256 VGPRs per wave (two waves per SIMD)
+__host__ __device__ constexpr int gemmRing(int RT) { return RT >= 2 ? 10 : 16; }
 
-// Split-K / tile plan of one matrix for MT token tiles: row tiles of 64 * rt rows (rt = row tiles
+// Split-K / tile plan of one matrix for MT token tiles: row tiles of 128 * rt rows (rt = row tiles
 // of 16 per wave), the largest rt that still gives >= 64 tiles; splits so the resident activations
 // fit (MP x KW x 2 B <= 128 KB) and the grid reaches ~DL_GEMM_WG (256) workgroups.
 static int gemmWgTarget() {
@@ -1143,9 +1149,10 @@ GemmPlan gemmPlan(int rows, int n, int M) {
     GemmPlan p;
     const int steps = n / 128;  // 4-block steps
     const int MP = gemmTokenPad(M);
-    p.rt = 4;
-    while (p.rt > 1 && (rows + 64 * p.rt - 1) / (64 * p.rt) < 64) p.rt >>= 1;
-    p.tiles = (rows + 64 * p.rt - 1) / (64 * p.rt);
+    const int wr = 16 * kGemmWaves;  // rows per workgroup per row tile
+    p.rt = 2;
+    while (p.rt > 1 && (rows + wr * p.rt - 1) / (wr * p.rt) < 64) p.rt >>= 1;
+    p.tiles = (rows + wr * p.rt - 1) / (wr * p.rt);
     p.splits = 1;
     while ((size_t)MP * (n / p.splits) * 2 > (size_t)kGemmMaxLdsAct && steps % (2 * p.splits) == 0) p.splits *= 2;
     while (p.tiles * p.splits < gemmWgTarget() && steps % (2 * p.splits) == 0 && steps / (2 * p.splits) >= 2)
@@ -1161,7 +1168,7 @@ size_t gemmPartFloats(int rows, int n, int maxTokens) {
     size_t f = 0;
     for (int M = 1; M <= std::min(maxTokens, kGemmMaxTokens); M += 16) {  // every token padding in use
         const GemmPlan p = gemmPlan(rows, n, M);
-        if (p.splits > 1) f = std::max(f, (size_t)p.splits * p.tiles * gemmTokenPad(M) * 64 * p.rt);
+        if (p.splits > 1) f = std::max(f, (size_t)p.splits * p.tiles * gemmTokenPad(M) * 16 * kGemmWaves * p.rt);
     }
     return f;
 }
@@ -1169,7 +1176,7 @@ size_t gemmPartFloats(int rows, int n, int maxTokens) {
 bool gemmSupported(int n) {
     // whole 4-block steps, and the resident activations of the largest split fit
     if (n % 128) return false;
-    const GemmPlan p = gemmPlan(64, n, kGemmMaxTokens);
+    const GemmPlan p = gemmPlan(16 * kGemmWaves, n, kGemmMaxTokens);
     return (size_t)32 * (n / p.splits) * 2 <= (size_t)kGemmMaxLdsAct;
 }
 
@@ -1203,7 +1210,7 @@ __device__ __forceinline__ void glds16(const void *g, void *lds) {
 }
 
 template <int MT, int RT>
-__host__ __device__ constexpr size_t gemmTileBytes() { return (size_t)MT * 16 * 64 * RT * sizeof(float); }
+__host__ __device__ constexpr size_t gemmTileBytes() { return (size_t)MT * 16 * 16 * kGemmWaves * RT * sizeof(float); }
 // dynamic LDS of a launch: resident activations (KW columns) or the output tile, + the arrival flag
 template <int MT, int RT>
 __host__ __device__ inline size_t gemmLdsBytes(int KW) {
@@ -1212,10 +1219,10 @@ __host__ __device__ inline size_t gemmLdsBytes(int KW) {
 }
 
 template <int MT, int RT, int EPI>
-__global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
+__global__ __launch_bounds__(kGemmThreads) void gemmQ40Kernel(GemmArgs ga) {
     const GemvArgs &a = ga.e;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int MP = MT * 16, WR = RT * 16, TR = 4 * WR;
+    constexpr int MP = MT * 16, WR = RT * 16, TR = kGemmWaves * WR;
     constexpr int D = gemmRing(RT), NLD = 2 * RT;  // ring steps, weight loads per step
     static_assert((D - 1) * NLD <= 63, "vmcnt range");
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1255,6 +1262,13 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
         for (int t = 0; t < RT; t++) {
             const u32x4 *p = qs + uBase[t] + (size_t)k * 2 * kThreads + li;
             const uint32_t *pd = wd2 + dBase[t] + (size_t)k * kThreads + li;
+            if (ga.probe) {  // timing probe: the same bytes per step, 1 KB contiguous per wave load
+                // (units: rows x nb 16-B blocks; scale words: rows x nb / 2 - both stay in bounds
+                // when rows is a multiple of the tile rows, which the probe caller checks)
+                const size_t w = (((size_t)tileIdx * S + sp) * kGemmWaves + wave) * RT + t;
+                p = qs + (w * T + ii) * 64 + lane;
+                pd = wd2 + ((w * T + ii) * 64 + lane) / 2;
+            }
             asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(q[t]) : "v"(p));
             asm volatile("global_load_dword %0, %1, off" : "=v"(d[t]) : "v"(pd));
         }
@@ -1269,7 +1283,7 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     {
         const int units = MP * UPT;
         const _Float16 *xb = ga.x + (size_t)j0 * 32;
-        for (int q0 = 0; q0 < units; q0 += kThreads) {  // uniform: units is a multiple of 256
+        for (int q0 = 0; q0 < units; q0 += kGemmThreads) {  // uniform: units is a multiple of 512
             const int q = q0 + tid, tk = q / UPT, p = q - tk * UPT, uu = p ^ (tk & 15);
             glds16(xb + (size_t)tk * n + (size_t)uu * 8, smem + (size_t)(q0 + wave * 64) * 16);
         }
@@ -1367,7 +1381,7 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
         const f32x4 *P = reinterpret_cast<const f32x4 *>(ga.part) + (size_t)tileIdx * MP * TR / 4;
         const size_t st4 = (size_t)tiles * MP * TR / 4;
         f32x4 *tile4 = reinterpret_cast<f32x4 *>(tile);
-        for (int i = tid; i < ga.M * TR / 4; i += kThreads) {
+        for (int i = tid; i < ga.M * TR / 4; i += kGemmThreads) {
             f32x4 v[8];
 #pragma unroll
             for (int s2 = 0; s2 < 8; s2++)
@@ -1383,7 +1397,7 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     __syncthreads();
     // fused epilogues on row pairs (2k, 2k+1) of the tile, TR/2 pairs per token
     constexpr int HP = TR / 2;
-    for (int i = tid; i < ga.M * HP; i += kThreads) {
+    for (int i = tid; i < ga.M * HP; i += kGemmThreads) {
         const int t = i / HP, k = i % HP, r0 = R0 + 2 * k;
         const float v0 = tile[t * TR + 2 * k], v1 = tile[t * TR + 2 * k + 1];
         if constexpr (EPI == EPI_STORE) {
@@ -1424,7 +1438,7 @@ static void gemmLaunchE(const GemmArgs &ga, int epi, dim3 grid, hipStream_t s) {
 #define DL_GEMM_CASE(E)                                                                           \
     if (epi == E) {                                                                               \
         if (lds > 65536) allowLds((const void *)gemmQ40Kernel<MT, RT, E>, lds); /* per device */  \
-        hipLaunchKernelGGL((gemmQ40Kernel<MT, RT, E>), grid, dim3(kThreads), lds, s, ga);         \
+        hipLaunchKernelGGL((gemmQ40Kernel<MT, RT, E>), grid, dim3(kGemmThreads), lds, s, ga);     \
         return;                                                                                   \
     }
     DL_GEMM_CASE(EPI_STORE) DL_GEMM_CASE(EPI_ACT) DL_GEMM_CASE(EPI_ACT_Q80) DL_GEMM_CASE(EPI_QKV)
@@ -1435,7 +1449,6 @@ static void gemmLaunchE(const GemmArgs &ga, int epi, dim3 grid, hipStream_t s) {
 template <int MT>
 static void gemmLaunchR(const GemmArgs &ga, int epi, int rt, dim3 grid, hipStream_t s) {
     switch (rt) {
-        case 4: gemmLaunchE<MT, 4>(ga, epi, grid, s); break;
         case 2: gemmLaunchE<MT, 2>(ga, epi, grid, s); break;
         default: gemmLaunchE<MT, 1>(ga, epi, grid, s); break;
     }
@@ -1530,7 +1543,7 @@ void launchNormF16(const GemvArgs &a, _Float16 *out, int M, hipStream_t s) {
 // each workgroup publishes its online-softmax partial and the last arriver combines them.
 // ------------------------------------------------------------------------------------------------
 int attnSplitGrid(int seqLen) {
-    int g = (seqLen + 255) / 256;
+    int g = (seqLen + kAttnMChunkKeys - 1) / kAttnMChunkKeys;  // the MFMA kernel's 128-key chunks
     return g < 1 ? 1 : (g > 128 ? 128 : g);
 }
 
@@ -1892,6 +1905,280 @@ __global__ __launch_bounds__(kAttnThreads) void attnKernel(AttnArgs a) {
     attnTask<HG, HS, BF16, kAttnThreads>(a, blockIdx.z, blockIdx.x, blockIdx.y, smem);
 }
 
+// ------------------------------------------------------------------------------------------------
+// MFMA attention over a bf16 KV cache (decode rows and prefill rows alike; every row attends to
+// positions [0, pos] of its own slot). Layouts: K row-major [slot][pos][kv0]; V TRANSPOSED
+// [slot][kv0][seqLen] (written so by the QKV epilogues), so every MFMA operand is a contiguous
+// load. Task = (kv head, sequence chunk, row); 4 waves split the chunk; a wave walks tiles of 32
+// keys for all kvMul query heads of the kv head at once (<= 16, padded to the 16 MFMA columns):
+//   S^T = K . Q^T      A = K rows (16 keys x 32 dims, 16-B loads), B = Q^T (registers, bf16)
+//   P^T = exp(S^T - m) C layout: lane (key 4h+i [+16], query l&15) - online softmax per query
+//   O^T += V^T . P^T   A = V^T (16 dims x 32 keys, two 8-B loads), B = P^T straight from the
+//                      C registers of S^T (k order permuted identically on both operands)
+// so every per-query statistic lives in the lanes of that query (l & 15) and no data moves
+// between lanes except the max / sum across the 4 lane groups. Waves merge through LDS; several
+// chunks merge through partO/partML and the last-arriving workgroup (the split combine of the
+// VALU kernel). Output: f32, f16 (batched path) or Q80 (decode path), per head.
+// ------------------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+static constexpr int kAttnMThreads = 256, kAttnMWaves = 4, kAttnMChunk = kAttnMChunkKeys;
+
+__device__ __forceinline__ bf16x8 f32x8ToBf16(const float (&v)[8]) {
+    bf16x8 r;
+#pragma unroll
+    for (int j = 0; j < 8; j++) r[j] = (__bf16)v[j];
+    return r;
+}
+
+// Final output of nq heads from LDS fin[nq][HS] -> f32 / f16 / Q80 (32-element blocks) in global.
+template <int HS>
+__device__ __forceinline__ void attnWriteOutN(const AttnArgs &a, int b, int head0, int nq, const float *fin) {
+    const int tid = threadIdx.x, total = nq * HS;  // a multiple of 32: whole lane groups per block
+    if (a.outQ) {
+        for (int base = 0; base < total; base += kAttnMThreads) {
+            const int i = base + tid;
+            const float v = i < total ? fin[i] : 0.f;
+            const float amax = groupMax<32>(fabsf(v));
+            const float d = amax / 127.0f;
+            const float id = d != 0.f ? 1.0f / d : 0.f;
+            int q = (int)rintf(v * id);
+            q = q > 127 ? 127 : (q < -127 ? -127 : q);
+            const float qs = groupSum<32>((float)q);
+            if (i < total) {
+                const int col = head0 * HS + i;
+                a.outQ[(size_t)b * a.ldOut + col] = (int8_t)q;
+                if ((i & 31) == 0) a.outS[(size_t)b * (a.ldOut >> 5) + (col >> 5)] = make_float2(roundF16(d), qs);
+            }
+        }
+    } else if (a.outH) {
+        for (int i = tid; i < total; i += kAttnMThreads) a.outH[(size_t)b * a.ldOut + head0 * HS + i] = (_Float16)fin[i];
+    } else {
+        for (int i = tid; i < total; i += kAttnMThreads) a.out[(size_t)b * a.ldOut + head0 * HS + i] = fin[i];
+    }
+}
+
+template <int HS>
+__global__ __launch_bounds__(kAttnMThreads) void attnMfmaKernel(AttnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int DS = HS / 32, NT = HS / 16;  // 32-dim k-steps of S, 16-dim tiles of O
+    const int g = blockIdx.x, c = blockIdx.y, b = blockIdx.z;
+    const int nq = a.kvMul, head0 = g * nq;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, col = lane & 15, h = lane >> 4;
+    const int pos = a.pos[b], sl = a.slot[b], len = pos + 1;
+    int nSplit = (len + kAttnMChunk - 1) / kAttnMChunk;
+    if (nSplit > a.splitGrid) nSplit = a.splitGrid;
+    const int ch = ((len + nSplit - 1) / nSplit + kAttnMChunk - 1) / kAttnMChunk * kAttnMChunk;
+    if (c >= nSplit) return;
+    const int wch = ch / kAttnMWaves;  // keys per wave (multiple of 32)
+    const int k0 = c * ch + wave * wch, k1 = min(min(c * ch + (wave + 1) * wch, len), c * ch + ch);
+
+    float *mW = reinterpret_cast<float *>(smem);       // [4][16]
+    float *lW = mW + kAttnMWaves * 16;                  // [4][16]
+    float *oW = lW + kAttnMWaves * 16;                  // [4][16][HS]
+    float *redL = oW + kAttnMWaves * 16 * HS;           // [16][HS]
+    float *mlL = redL + 16 * HS;                        // [16][2]
+    int *flagL = reinterpret_cast<int *>(mlL + 32);
+
+    // Q^T fragments (B operand): lane (query col, k-octet h) holds Q[col][32 s + 8 h .. + 7], scaled
+    const float scale = 1.0f / sqrtf((float)HS);
+    bf16x8 qf[DS];
+#pragma unroll
+    for (int s = 0; s < DS; s++) {
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (col < nq) {
+            const float *qp = a.q + (size_t)b * a.ldq + (size_t)(head0 + col) * HS + 32 * s + 8 * h;
+            const float4 x0 = ld4(qp), x1 = ld4(qp + 4);
+            v[0] = x0.x * scale; v[1] = x0.y * scale; v[2] = x0.z * scale; v[3] = x0.w * scale;
+            v[4] = x1.x * scale; v[5] = x1.y * scale; v[6] = x1.z * scale; v[7] = x1.w * scale;
+        }
+        qf[s] = f32x8ToBf16(v);
+    }
+    const __bf16 *kc = reinterpret_cast<const __bf16 *>(a.kcache);
+    const __bf16 *vc = reinterpret_cast<const __bf16 *>(a.vcache);
+    const size_t kBase = (size_t)sl * a.seqLen * a.kv0 + (size_t)g * HS;     // + pos * kv0 + dim
+    const size_t vBase = ((size_t)sl * a.kv0 + (size_t)g * HS) * a.seqLen;  // + dim * seqLen + pos
+    const int last = a.seqLen - 1;
+
+    f32x4 o[NT];
+#pragma unroll
+    for (int n = 0; n < NT; n++) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, lsum = 0.f;
+    for (int t0 = k0; t0 < k1; t0 += 32) {
+        bf16x8 kf[2][DS];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int key = min(t0 + 16 * u + col, last);
+#pragma unroll
+            for (int s = 0; s < DS; s++)
+                kf[u][s] = *reinterpret_cast<const bf16x8 *>(kc + kBase + (size_t)key * a.kv0 + 32 * s + 8 * h);
+        }
+        bf16x8 vf[NT];
+        const int p0 = min(t0 + 4 * h, last - 3), p1 = min(t0 + 16 + 4 * h, last - 3);
+#pragma unroll
+        for (int n = 0; n < NT; n++) {
+            const __bf16 *vr = vc + vBase + (size_t)(16 * n + col) * a.seqLen;
+            const bf16x4 lo = *reinterpret_cast<const bf16x4 *>(vr + p0);
+            const bf16x4 hi = *reinterpret_cast<const bf16x4 *>(vr + p1);
+            vf[n] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+        f32x4 st[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            st[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < DS; s++) st[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[u][s], qf[s], st[u], 0, 0, 0);
+        }
+        // mask keys past the row's length (and past this wave's range), then the online softmax
+        float mx = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int key = t0 + 16 * u + 4 * h + i;
+                if (key >= k1) st[u][i] = -INFINITY;
+                mx = fmaxf(mx, st[u][i]);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float mn = fmaxf(m, mx);
+        const float corr = m == -INFINITY ? 0.f : __expf(m - mn);
+        float p[2][4], ps = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                p[u][i] = st[u][i] == -INFINITY ? 0.f : __expf(st[u][i] - mn);
+                ps += p[u][i];
+            }
+        lsum = lsum * corr + ps;
+        m = mn;
+        const float pv[8] = {p[0][0], p[0][1], p[0][2], p[0][3], p[1][0], p[1][1], p[1][2], p[1][3]};
+        const bf16x8 pf = f32x8ToBf16(pv);
+#pragma unroll
+        for (int n = 0; n < NT; n++) {
+            o[n] *= corr;
+            o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[n], pf, o[n], 0, 0, 0);
+        }
+    }
+    lsum += __shfl_xor(lsum, 16);
+    lsum += __shfl_xor(lsum, 32);
+    // waves -> LDS: O^T C layout: lane holds O[query col][dim 16 n + 4 h + i]
+    if (h == 0) {
+        mW[wave * 16 + col] = m;
+        lW[wave * 16 + col] = lsum;
+    }
+#pragma unroll
+    for (int n = 0; n < NT; n++)
+#pragma unroll
+        for (int i = 0; i < 4; i++) oW[(wave * 16 + col) * HS + 16 * n + 4 * h + i] = o[n][i];
+    __syncthreads();
+    for (int i = tid; i < nq * HS; i += kAttnMThreads) {
+        const int q = i / HS, d = i % HS;
+        float M = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < kAttnMWaves; w++) M = fmaxf(M, mW[w * 16 + q]);
+        float acc = 0.f, Ls = 0.f;
+#pragma unroll
+        for (int w = 0; w < kAttnMWaves; w++) {
+            const float e = M == -INFINITY || mW[w * 16 + q] == -INFINITY ? 0.f : __expf(mW[w * 16 + q] - M);
+            acc += e * oW[(w * 16 + q) * HS + d];
+            Ls += e * lW[w * 16 + q];
+        }
+        redL[i] = acc;
+        if (d == 0) {
+            mlL[q * 2] = M;
+            mlL[q * 2 + 1] = Ls;
+        }
+    }
+    __syncthreads();
+    if (nSplit == 1) {
+        for (int i = tid; i < nq * HS; i += kAttnMThreads) redL[i] = redL[i] / mlL[(i / HS) * 2 + 1];
+        __syncthreads();
+        attnWriteOutN<HS>(a, b, head0, nq, redL);
+        return;
+    }
+    // several chunks: publish this chunk's partial, the last arriver combines (as attnFinish)
+    const int G = a.splitGrid;
+    const size_t pbase = ((size_t)b * a.nHeads0 + head0) * G;  // [nq][G] chunks of these heads
+    for (int i = tid; i < nq * HS; i += kAttnMThreads) {
+        const int q = i / HS, d = i % HS;
+        a.partO[((pbase + (size_t)q * G) + c) * HS + d] = redL[i];
+    }
+    if (tid < nq) {
+        a.partML[((pbase + (size_t)tid * G) + c) * 2] = mlL[tid * 2];
+        a.partML[((pbase + (size_t)tid * G) + c) * 2 + 1] = mlL[tid * 2 + 1];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int *cnt = a.counters + (size_t)b * (a.nHeads0 / nq) + g;
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flagL[0] = old == nSplit - 1;
+    }
+    __syncthreads();
+    if (!flagL[0]) return;
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    float *scratch = oW;  // >= 2 * 16 * G floats (G <= 128)
+    for (int i = tid; i < nq * nSplit; i += kAttnMThreads) {
+        const int q = i / nSplit, cc = i % nSplit;
+        const float2 ml = *reinterpret_cast<const float2 *>(a.partML + ((pbase + (size_t)q * G) + cc) * 2);
+        scratch[2 * (q * G + cc)] = ml.x;
+        scratch[2 * (q * G + cc) + 1] = ml.y;
+    }
+    __syncthreads();
+    if (tid < nq) {
+        float M = -INFINITY;
+        for (int cc = 0; cc < nSplit; cc++) M = fmaxf(M, scratch[2 * (tid * G + cc)]);
+        float Ls = 0.f;
+        for (int cc = 0; cc < nSplit; cc++) {
+            float *ml = scratch + 2 * (tid * G + cc);
+            const float w = M == -INFINITY || ml[0] == -INFINITY ? 0.f : __expf(ml[0] - M);
+            ml[0] = w;
+            Ls += w * ml[1];
+        }
+        mlL[tid * 2 + 1] = Ls;
+    }
+    __syncthreads();
+    constexpr int U = 8;
+    for (int i = tid; i < nq * HS; i += kAttnMThreads) {
+        const int q = i / HS, d = i % HS;
+        const float *po = a.partO + (pbase + (size_t)q * G) * HS + d;
+        const float *wv = scratch + 2 * q * G;
+        float acc = 0.f;
+        int cc = 0;
+        for (; cc + U <= nSplit; cc += U) {
+            float v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) v[u] = po[(size_t)(cc + u) * HS];
+#pragma unroll
+            for (int u = 0; u < U; u++) acc += wv[2 * (cc + u)] * v[u];
+        }
+        for (; cc < nSplit; cc++) acc += wv[2 * cc] * po[(size_t)cc * HS];
+        redL[i] = acc / mlL[q * 2 + 1];
+    }
+    __syncthreads();
+    attnWriteOutN<HS>(a, b, head0, nq, redL);
+}
+
+template <int HS>
+static void attnMfmaLaunch(const AttnArgs &a, int B, hipStream_t s) {
+    const size_t lds = sizeof(float) * (2 * kAttnMWaves * 16 + kAttnMWaves * 16 * HS + 16 * HS + 32) + 16;
+    const dim3 grid(a.nHeads0 / a.kvMul, a.splitGrid, B);
+    hipLaunchKernelGGL((attnMfmaKernel<HS>), grid, dim3(kAttnMThreads), lds, s, a);
+}
+
+bool attnMfmaSupported(int kvMul, int hs, int seqLen) {
+    return kvMul >= 1 && kvMul <= 16 && (hs == 64 || hs == 128) && seqLen % 8 == 0;
+}
+
 template <int HS, bool BF16>
 static void attnDispatchHG(const AttnArgs &a, int B, int HG, hipStream_t s) {
     constexpr int NW = kAttnThreads / 64;
@@ -1908,6 +2195,13 @@ static void attnDispatchHG(const AttnArgs &a, int B, int HG, hipStream_t s) {
 }
 
 void launchAttention(const AttnArgs &a, int B, hipStream_t s) {
+    if (a.kvBf16) {  // bf16 cache: MFMA kernel (V stored transposed); f32 cache: the VALU kernel
+        if (!attnMfmaSupported(a.kvMul, a.hs, a.seqLen))
+            throw Error("bf16 KV attention needs kvMul <= 16, head size 64/128 and seqLen % 8 == 0");
+        if (a.hs == 128) attnMfmaLaunch<128>(a, B, s);
+        else attnMfmaLaunch<64>(a, B, s);
+        return;
+    }
     static const int hgOverride = [] {  // experiments: DL_ATTN_HG forces query heads per workgroup
         const char *e = getenv("DL_ATTN_HG");
         return e ? atoi(e) : 0;

@@ -254,17 +254,24 @@ std::vector<float> qkvRope(const std::vector<uint8_t> &blocks, int q0, int kv0, 
     a.kvBf16 = kvBf16 ? 1 : 0;
     hipk::launchGemv(a, B, hipk::PRO_RESNORM, hipk::EPI_QKV, true, sc.s);
     sc.sync();
-    auto row = [&](void *cache, int b) {
+    // row `pos[b]` of slot b; bf16 V is stored transposed ([slot][kv0][seqLen], see launchAttention)
+    auto row = [&](void *cache, int b, bool transposed) {
         std::vector<float> r(kv0);
-        const size_t off = ((size_t)b * seqLen + pos[b]) * kv0;
         if (kvBf16) {
-            const std::vector<uint16_t> h = sc.download(static_cast<uint16_t *>(cache) + off, kv0);
+            std::vector<uint16_t> h(kv0);
+            if (transposed) {
+                const std::vector<uint16_t> all =
+                    sc.download(static_cast<uint16_t *>(cache) + (size_t)b * kv0 * seqLen, (size_t)kv0 * seqLen);
+                for (int i = 0; i < kv0; i++) h[i] = all[(size_t)i * seqLen + pos[b]];
+            } else {
+                h = sc.download(static_cast<uint16_t *>(cache) + ((size_t)b * seqLen + pos[b]) * kv0, kv0);
+            }
             for (int i = 0; i < kv0; i++) {
                 const uint32_t u = (uint32_t)h[i] << 16;
                 std::memcpy(&r[i], &u, 4);
             }
         } else {
-            r = sc.download(static_cast<float *>(cache) + off, kv0);
+            r = sc.download(static_cast<float *>(cache) + ((size_t)b * seqLen + pos[b]) * kv0, kv0);
         }
         return r;
     };
@@ -272,11 +279,11 @@ std::vector<float> qkvRope(const std::vector<uint8_t> &blocks, int q0, int kv0, 
     if (vOut) vOut->clear();
     for (int b = 0; b < B; b++) {
         if (kOut) {
-            const std::vector<float> r = row(kc, b);
+            const std::vector<float> r = row(kc, b, false);
             kOut->insert(kOut->end(), r.begin(), r.end());
         }
         if (vOut) {
-            const std::vector<float> r = row(vc, b);
+            const std::vector<float> r = row(vc, b, true);
             vOut->insert(vOut->end(), r.begin(), r.end());
         }
     }
@@ -295,21 +302,28 @@ std::vector<float> attention(const std::vector<float> &q, const std::vector<floa
     for (int b = 0; b < B; b++)
         DL_CHECK(pos[b] >= 0 && pos[b] < seqLen && slot[b] >= 0 && slot[b] < nSlots, "attention row out of range");
     Scratch sc;
-    auto cache = [&](const std::vector<float> &x) -> void * {
+    // caches come in [slot][seqLen][kv0]; bf16 V goes to the device transposed ([slot][kv0][seqLen])
+    auto cache = [&](const std::vector<float> &x, bool transpose) -> void * {
         if (!kvBf16) return sc.upload(x);
         std::vector<uint16_t> h(x.size());
         for (size_t i = 0; i < x.size(); i++) {  // round to nearest even, as the QKV epilogue stores
             uint32_t u;
             std::memcpy(&u, &x[i], 4);
-            h[i] = (uint16_t)((u + 0x7FFF + ((u >> 16) & 1)) >> 16);
+            const uint16_t hv = (uint16_t)((u + 0x7FFF + ((u >> 16) & 1)) >> 16);
+            if (!transpose) {
+                h[i] = hv;
+            } else {
+                const size_t e = i % kv0, p = (i / kv0) % seqLen, sl = i / ((size_t)kv0 * seqLen);
+                h[(sl * kv0 + e) * seqLen + p] = hv;
+            }
         }
         return sc.upload(h);
     };
     hipk::AttnArgs a;
     a.q = sc.upload(q);
     a.ldq = q0;
-    a.kcache = cache(k);
-    a.vcache = cache(v);
+    a.kcache = cache(k, false);
+    a.vcache = cache(v, true);
     a.pos = sc.upload(pos);
     a.slot = sc.upload(slot);
     a.nHeads0 = nHeads0;

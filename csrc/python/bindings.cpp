@@ -483,7 +483,7 @@ PYBIND11_MODULE(_C, m) {
           py::arg("passes") = 0, py::arg("copies") = 8, py::arg("iters") = 20,
           "bench_gemv_q40 with per-workgroup s_memrealtime stamps: (us, u64[iters*grid*4])");
     m.def("bench_gemm_q40", &benchGemmQ40, py::arg("rows"), py::arg("n"), py::arg("tokens"), py::arg("epi") = 0,
-          py::arg("copies") = 8, py::arg("iters") = 100, py::call_guard<py::gil_scoped_release>());
+          py::arg("copies") = 8, py::arg("iters") = 100, py::arg("probe") = 0, py::call_guard<py::gil_scoped_release>());
     m.def("bench_attention", &benchAttention, py::arg("n_heads0"), py::arg("kv_mul"), py::arg("head_size"),
           py::arg("seq_len"), py::arg("pos"), py::arg("batch") = 1, py::arg("copies") = 32, py::arg("iters") = 200,
           py::call_guard<py::gil_scoped_release>());

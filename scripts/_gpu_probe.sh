@@ -1,0 +1,6 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export DL_SKIP_BUILD=1
+PROBE=1 timeout -k 10 200 python -u scripts/bench_gemm.py 8 32 > gpurun_out/r2_bench_gemm_probe.log 2>&1 && \
+timeout -k 10 200 python -u scripts/bench_attn.py > gpurun_out/r2_bench_attn.log 2>&1

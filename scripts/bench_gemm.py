@@ -25,6 +25,6 @@ for name, rows, n, epi in shapes:
     mb = rows * n * 0.5625 / 1e6
     line = f"{name} {rows:6d}x{n:5d} {mb:7.1f} MB |"
     for m in tokens:
-        us = C.bench_gemm_q40(rows, n, m, epi, 8 if mb < 100 else 2, 50)
+        us = C.bench_gemm_q40(rows, n, m, epi, 8 if mb < 100 else 2, 50, int(os.environ.get("PROBE", "0")))
         line += f" M={m}: {us:7.2f} us {mb / us:5.2f} TB/s |"
     print(line, flush=True)

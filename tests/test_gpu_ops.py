@@ -128,7 +128,32 @@ def test_attention_decode(ops, kv_bf16, n_heads0, kv_mul, hs, seq, pos):
         k, v = k.bfloat16().float(), v.bfloat16().float()
     out = ops.attention(q, k, v, n_heads0, kv_mul, hs, pos, slots, kv_bf16)
     want = ops.ref_attention(q, k, v, n_heads0, kv_mul, hs, pos, slots)
-    assert rel(out, want) < 1e-4
+    if not kv_bf16:
+        assert rel(out, want) < 1e-4  # f32 cache: the VALU kernel, f32 throughout
+        return
+    # bf16 cache: the MFMA kernel multiplies bf16 Q (scaled) x K and bf16 P x V with f32 accumulation
+    assert rel(out, want) < 6e-3
+    qb = (q.view(B, n_heads0, hs) / hs ** 0.5).bfloat16().float().reshape(B, -1) * hs ** 0.5
+    assert rel(out, ops.ref_attention(qb, k, v, n_heads0, kv_mul, hs, pos, slots)) < 4e-3
+
+
+@pytest.mark.parametrize("n_heads0,kv_mul,hs,seq,pos", [
+    (4, 4, 128, 8192, [8100, 3, 511, 512, 513]),  # long context, chunk edges, several rows
+    (16, 16, 128, 1024, [1000]),                 # 405B-like GQA group of 16 heads
+    (8, 2, 64, 2048, [1900, 64]),
+])
+def test_attention_mfma_edges(ops, n_heads0, kv_mul, hs, seq, pos):
+    """MFMA attention: query padding (kvMul < 16), 32-key tile tails, chunk and split edges."""
+    kv0 = n_heads0 // kv_mul * hs
+    g = torch.Generator().manual_seed(13)
+    B = len(pos)
+    slots = list(range(B))
+    k = torch.randn(B, seq, kv0, generator=g).bfloat16().float()
+    v = torch.randn(B, seq, kv0, generator=g).bfloat16().float()
+    q = torch.randn(B, n_heads0 * hs, generator=g) * 2
+    out = ops.attention(q, k, v, n_heads0, kv_mul, hs, pos, slots, True)
+    want = ops.ref_attention(q, k, v, n_heads0, kv_mul, hs, pos, slots)
+    assert rel(out, want) < 6e-3
 
 
 def test_argmax_ties_lowest_index(ops):
