@@ -30,10 +30,14 @@ static int sampleOne(InferenceSession &sess, int token, int pos, std::vector<flo
     if (sess.sampler().temperature() == 0.0f) {
         sess.forwardArgmax(1, &token, &pos, &slot, &next);
     } else {
-        logits.resize(sess.header().vocabSize);
-        sess.forward(1, &token, &pos, &slot, logits.data());
-        next = sess.sampler().sample(logits.data());
+        // the draw runs on the backend with the coin the seeded sampler yields (same sequence)
+        SampleSpec sp;
+        sp.temperature = sess.sampler().temperature();
+        sp.topp = sess.sampler().topp();
+        sp.coin = sess.sampler().drawCoin();
+        sess.forwardSample(1, &token, &pos, &slot, &sp, &next);
     }
+    (void)logits;
     ms = t.elapsedMs();
     return next;
 }

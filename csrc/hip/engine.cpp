@@ -74,11 +74,6 @@ class HipEngineImpl : public HipEngine {
         DL_CHECK(h_.headSize() == 64 || h_.headSize() == 128, "GPU kernels support head size 64 or 128");
         DL_CHECK(cfg.maxBatch >= 1 && cfg.nSlots >= 1, "maxBatch/nSlots");
         kvBf16_ = cfg.kvBf16;
-        if (kvBf16_) {  // the bf16 (MFMA) attention reads 4-position runs of the transposed V rows
-            h_.seqLen = (h_.seqLen + 7) / 8 * 8;
-            DL_CHECK(hipk::attnMfmaSupported((int)plan_.kvMul, (int)h_.headSize(), (int)h_.seqLen),
-                     "bf16 KV cache: attention shape not supported (use --kv-dtype f32)");
-        }
         syncQ80_ = cfg.syncType == FloatType::Q80;
         if (comm_ && plan_.nRanks > 1) {
             const char *e = std::getenv("DL_TP_FUSED");  // 0: separate all-reduce kernels (comparison)
@@ -131,6 +126,18 @@ class HipEngineImpl : public HipEngine {
         Timer t;
         setInputs(n, tokens, positions, slots);
         runGraph(n, GraphKind::ARGMAX);
+        DL_HIP(hipMemcpyAsync(hIds_, dIds_, n * sizeof(int), hipMemcpyDeviceToHost, stream_));
+        syncAndCheckComm();
+        inputsInFlight_ = false;
+        std::memcpy(out, hIds_, n * sizeof(int));
+        stats_.computeMs = t.elapsedMs();
+    }
+
+    void forwardSample(int n, const int *tokens, const int *positions, const int *slots, const SampleSpec *specs,
+                       int *out) override {
+        Timer t;
+        setInputs(n, tokens, positions, slots, specs);
+        runGraph(n, GraphKind::SAMPLE);
         DL_HIP(hipMemcpyAsync(hIds_, dIds_, n * sizeof(int), hipMemcpyDeviceToHost, stream_));
         syncAndCheckComm();
         inputsInFlight_ = false;
@@ -196,7 +203,7 @@ class HipEngineImpl : public HipEngine {
     }
 
   private:
-    enum class GraphKind { LOGITS = 0, ARGMAX = 1, CHAIN = 2 };
+    enum class GraphKind { LOGITS = 0, ARGMAX = 1, CHAIN = 2, SAMPLE = 3 };
 
     // Wait for the stream, then turn a tensor-parallel transport failure into an exception (the
     // worker loop re-serves, the root reports it) instead of returning results computed from a
@@ -239,12 +246,14 @@ class HipEngineImpl : public HipEngine {
     void allocBuffers() {
         const u32 MB = cfg_.maxBatch;
         const ShardPlan &p = plan_;
-        dTok_ = dalloc<int>(3 * (size_t)MB);  // [tokens | positions | slots]: one H2D copy per forward
+        // [tokens | positions | slots | sample specs (4 floats per row)]: one H2D copy per forward
+        dTok_ = dalloc<int>(7 * (size_t)MB);
         dPos_ = dTok_ + MB;
         dSlot_ = dTok_ + 2 * MB;
+        dSpec_ = reinterpret_cast<float4 *>(dTok_ + 3 * MB);
         dIds_ = dalloc<int>(MB);
         dHist_ = dalloc<int>((size_t)MB * h_.seqLen);
-        hIn_ = halloc<int>(3 * MB);
+        hIn_ = halloc<int>(7 * MB);
         hIds_ = halloc<int>(MB);
         hErr_ = halloc<int>(1);
         *hErr_ = 0;
@@ -464,7 +473,7 @@ class HipEngineImpl : public HipEngine {
     }
 
     // ---------------------------------------------------------------- forward schedule
-    void setInputs(int n, const int *tokens, const int *positions, const int *slots) {
+    void setInputs(int n, const int *tokens, const int *positions, const int *slots, const SampleSpec *specs = nullptr) {
         DL_CHECK(n >= 1 && (u32)n <= cfg_.maxBatch, "batch size out of range");
         for (int b = 0; b < n; b++) {
             DL_CHECK(tokens[b] >= 0 && (u32)tokens[b] < h_.vocabSize, "token out of range");
@@ -478,8 +487,14 @@ class HipEngineImpl : public HipEngine {
         std::memcpy(hIn_, tokens, n * sizeof(int));
         std::memcpy(hIn_ + MB, positions, n * sizeof(int));
         std::memcpy(hIn_ + 2 * MB, slots, n * sizeof(int));
-        // one copy of the three row arrays (the unused tail of each is never read)
-        DL_HIP(hipMemcpyAsync(dTok_, hIn_, (2 * (size_t)MB + n) * sizeof(int), hipMemcpyHostToDevice, stream_));
+        size_t words = 2 * (size_t)MB + n;
+        if (specs) {
+            static_assert(sizeof(SampleSpec) == 4 * sizeof(float), "spec layout");
+            std::memcpy(hIn_ + 3 * MB, specs, n * sizeof(SampleSpec));
+            words = 3 * (size_t)MB + 4 * (size_t)n;
+        }
+        // one copy of the row arrays (the unused tail of each is never read)
+        DL_HIP(hipMemcpyAsync(dTok_, hIn_, words * sizeof(int), hipMemcpyHostToDevice, stream_));
         inputsInFlight_ = true;
     }
 
@@ -818,14 +833,22 @@ class HipEngineImpl : public HipEngine {
         // greedy rows on a fused TP data plane: each rank reduces its own vocab slice and only the
         // (value, index) winners cross the links (reference: logits gathered to the root,
         // llm.cpp:432); the full logits are gathered only when the host samples them
-        const bool distArgmax = tpFused_ && kind != GraphKind::LOGITS;
+        const bool distArgmax = tpFused_ && (kind == GraphKind::ARGMAX || kind == GraphKind::CHAIN);
         if (p.nRanks > 1 && !distArgmax) {
             ProfScope ps(this, "allgather");
             comm_->allGather(dLogits_, dLogitsAll_, (size_t)n * p.vocab0, stream_);
             hipk::launchUnshardLogits(dLogitsAll_, dLogitsFull_, p.nRanks, n, p.vocab0, stream_);
             full = dLogitsFull_;
         }
-        if (kind != GraphKind::LOGITS) {
+        if (kind == GraphKind::SAMPLE) {
+            ProfScope ps(this, "sample");
+            hipk::SampleArgs g;
+            g.logits = full;
+            g.vocab = h_.vocabSize;
+            g.spec = dSpec_;
+            g.ids = dIds_;
+            hipk::launchSample(g, n, stream_);
+        } else if (kind != GraphKind::LOGITS) {
             ProfScope ps(this, "argmax");
             hipk::ArgmaxArgs g;
             g.logits = full;
@@ -872,6 +895,7 @@ class HipEngineImpl : public HipEngine {
     DevMat wcls_;
     float *emb_ = nullptr, *rmsFinal_ = nullptr;
     int *dTok_ = nullptr, *dPos_ = nullptr, *dSlot_ = nullptr, *dIds_ = nullptr, *dHist_ = nullptr;
+    float4 *dSpec_ = nullptr;
     int *hIn_ = nullptr, *hIds_ = nullptr, *hErr_ = nullptr;
     float *hLogits_ = nullptr;
     float *dX_[2] = {nullptr, nullptr};
@@ -1004,7 +1028,7 @@ double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int pas
     return ms * 1000.0 / iters;
 }
 
-double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters, int probe) {
+double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters) {
     DL_CHECK(M >= 1 && M <= hipk::kGemmMaxTokens && hipk::gemmSupported(n) && rows % 64 == 0, "bad gemm bench shape");
     hipStream_t s;
     DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -1041,12 +1065,6 @@ double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters, int 
     g.splits = hipk::gemmSplits(rows, n, M);
     g.part = part ? (float *)alloc(part * 4) : nullptr;
     g.counters = (int *)alloc((size_t)(rows / 64 + 1) * 4);
-    if (probe) {  // the contiguous probe addresses cover exactly tiles x tile rows x nb blocks
-        const hipk::GemmPlan gp = hipk::gemmPlan(rows, n, M);
-        DL_CHECK(rows % (rows / gp.tiles) == 0 && (size_t)gp.tiles * (rows / gp.tiles) == (size_t)rows,
-                 "gemm probe needs whole tiles");
-    }
-    g.probe = probe;
     auto launch = [&](int c) {
         g.e.qs = qs[c % copies];
         g.e.wd = d[c % copies];

@@ -130,7 +130,7 @@ struct GemvArgs {
     unsigned long long *trace = nullptr;
 };
 
-// Batched Q40 matmul on MFMA (1..32 tokens per launch): GemvArgs `e` carries the weights (tiled,
+// Batched Q40 matmul on MFMA (1..64 tokens per launch): GemvArgs `e` carries the weights (tiled,
 // `lanes` = tiling L) and the epilogue fields; activations are f16 [>= roundup(M,16)][n] (`x`,
 // rows past M are read but their outputs dropped); split-K partials + per-tile counters
 // (zero-initialised, reset by the kernel) when splits > 1. EPI_ACT_F16 writes SwiGLU as f16 to outH.
@@ -142,20 +142,19 @@ struct GemmArgs {
     int splits = 1;
     float *part = nullptr;
     int *counters = nullptr;
-    int probe = 0;  // microbenchmark only: 1 = contiguous weight addresses (timing, wrong results)
 };
 void launchGemmQ40(const GemmArgs &a, int epi, hipStream_t s);
 // Tile / split-K plan of one matrix (rt = 16-row tiles per wave: 64 * rt rows per workgroup).
 struct GemmPlan {
     int rt = 1, tiles = 0, splits = 1;
 };
-constexpr int kGemmMaxTokens = 32;  // tokens per GEMM launch (16 or 32 padded)
+constexpr int kGemmMaxTokens = 64;  // tokens per GEMM launch (16, 32 or 64 padded)
 GemmPlan gemmPlan(int rows, int n, int M);
-bool gemmSupported(int n);  // input width a multiple of 128 (whole 4-block steps) that fits LDS
+bool gemmSupported(int n);  // input width a multiple of 32 (whole Q40 blocks)
 int gemmSplits(int rows, int n, int M);
 // split-K partial floats for any launch of up to maxTokens tokens on this matrix
 size_t gemmPartFloats(int rows, int n, int maxTokens);
-// token rows one GEMM launch of M (1..32) tokens reads from its f16 activation operand (16/32)
+// token rows one GEMM launch of M (1..64) tokens reads from its f16 activation operand (16/32/64)
 int gemmTokenPad(int M);
 // Residual add + RMS norm (normW may be null: no norm) of M rows -> f16:
 // in/addIn/xNext [M][ldIn] f32 -> out [M][n] f16 (xNext = in + addIn when set).
@@ -178,10 +177,7 @@ size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg, int pro);
 // resident at once (DL_GEMV_RESIDENT workgroups, default 512); ACT_Q80 -> whole Q80 blocks per WG.
 int gemvDefaultPasses(int n, int rows, int B, bool q40, int epi);
 
-// bf16 KV caches run the MFMA kernel and store V transposed ([slot][kv0][seqLen]); f32 caches run
-// the VALU kernel with row-major V ([slot][seqLen][kv0]). K is row-major in both.
 void launchAttention(const AttnArgs &a, int B, hipStream_t s);
-bool attnMfmaSupported(int kvMul, int hs, int seqLen);
 int attnSplitGrid(int seqLen);
 int attnChunkMax(int seqLen, int splitGrid);
 
@@ -202,6 +198,20 @@ struct ArgmaxArgs {
     TpXchg tp;
     int vocabStart = 0;
 };
+// Device sampling of B rows of full-vocabulary logits (the reference's Sampler::sample:
+// logits / temperature -> softmax -> coin -> multinomial in index order, or top-p: candidates
+// >= (1 - p) / (V - 1), descending by probability, cut where the cumulative mass first exceeds p,
+// draw r = coin * nucleus mass). spec[b] = (temperature, topp, coin, -): temperature 0 -> argmax,
+// < 0 -> no draw (ids[b] = -1). One 1024-thread workgroup per row; the top-p cut and the draw are
+// found by 8-bit radix searches over the order-preserving key of logit / temperature.
+struct SampleArgs {
+    const float *logits = nullptr;
+    int vocab = 0;
+    const float4 *spec = nullptr;
+    int *ids = nullptr;
+};
+void launchSample(const SampleArgs &a, int B, hipStream_t s);
+
 // Round-trip f32 partial sums through Q80 blocks in place (the reference's ZQ cast before the
 // exchange) - used ahead of a plain all-reduce when the fused exchange is not available.
 void launchQ80Roundtrip(float *x, size_t n, hipStream_t s);

@@ -31,7 +31,6 @@ namespace hipk {
 using namespace dl::dev;
 
 static constexpr int kThreads = 256;
-static constexpr int kAttnMChunkKeys = 128;  // keys per workgroup chunk of the MFMA attention
 static constexpr int kMaxHeadSize = 128;  // RoPE rows staged in LDS by the QKV epilogue
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
@@ -380,13 +379,11 @@ __device__ __forceinline__ void qkvPairStore(const GemvArgs &a, int r0, float v0
             }
         }
     } else {
-        const int e = r0 - a.q0 - a.kv0;
-        if (a.kvBf16) {  // bf16 V is stored transposed, [slot][kv0][seqLen] (MFMA attention operand)
-            uint16_t *vt = reinterpret_cast<uint16_t *>(a.vcache) + ((size_t)sl * a.kv0 + e) * a.seqLen + p;
-            vt[0] = f32ToBf16(v0);
-            vt[a.seqLen] = f32ToBf16(v1);
+        const size_t off = ((size_t)sl * a.seqLen + p) * a.kv0 + (r0 - a.q0 - a.kv0);
+        if (a.kvBf16) {
+            const uint32_t pk = (uint32_t)f32ToBf16(v0) | ((uint32_t)f32ToBf16(v1) << 16);
+            *reinterpret_cast<uint32_t *>(reinterpret_cast<uint16_t *>(a.vcache) + off) = pk;
         } else {
-            const size_t off = ((size_t)sl * a.seqLen + p) * a.kv0 + e;
             *reinterpret_cast<float2 *>(reinterpret_cast<float *>(a.vcache) + off) = make_float2(v0, v1);
         }
     }
@@ -1102,41 +1099,31 @@ void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_
 }
 
 // ------------------------------------------------------------------------------------------------
-// Batched Q40 matmul on MFMA (prefill / multi-user decode, up to 32 tokens per launch).
+// Batched GEMM design notes (measured, profiles/r2_gemm_designs.md): two alternatives were built
+// and measured slower than this kernel on every shape - (v2) weights HBM -> VGPR ring with the
+// activations refilled through a 4-deep LDS ring (shared vmcnt capped the weight stream at 3 steps
+// in flight), (v3) activations resident in LDS with a deep weight ring and 4 or 8 waves (1.4-1.7
+// TB/s on w13, issue-stall bound per PMC: SQ_WAIT_INST_ANY 46 % of wave cycles). This v1 stays.
+// Batched Q40 matmul on MFMA (prefill / multi-user decode, 2..32 tokens per launch).
 //   out[t][row] = sum_k W[row][k] * x[t][k], W Q40 (the GEMV's tiled layout), x f16.
-// Workgroup = 8 waves (two per SIMD: a lone wave issues VALU at half rate and the Q40 dequant is
-// VALU work); a wave owns RT row tiles of 16 rows (the workgroup 128 * RT rows) and all MT token
-// tiles of 16 tokens, over one K split of KW = n / splits columns:
-// * the workgroup's activations (MP tokens x KW, f16, <= 128 KB) are copied L2 -> LDS ONCE with
-//   global_load_lds (XOR-swizzled 16-B units: conflict-free ds_read_b128) and stay resident, so
-//   the K loop has no barrier and no LDS refill;
-// * weights go HBM -> VGPRs directly through a ring of D steps in flight (like the GEMV): a step is
-//   4 Q40 blocks (128 k); lane (col, h) loads block j + h of its row (16 B) and the row pair's
-//   scale word per row tile. vmcnt counts only weight loads inside the loop, so the ring depth is
-//   real (a ring shared with activation refills is limited by the refills' in-order retirement);
-// * one MFMA k-step (v_mfma_f32_16x16x32_f16) covers 8 k of each of the 4 blocks of the step:
-//   lane (col, h) feeds block j+h elements [8s, 8s+8) as B (its row) and A (its token) alike (a
-//   permutation of k, identical on both operands). A lane dequantizes 8 nibbles per k-step
-//   ((1024 + q) - 1032 exact in f16, times d); each A fragment feeds RT row tiles, each dequantized
-//   B fragment feeds MT token tiles.
-// Split-K partials are combined in split order by the last-arriving workgroup of a tile (agent-scope
-// release/acquire counter: deterministic), which runs the fused epilogue on the tile in LDS
-// (store / SwiGLU / SwiGLU -> f16 / SwiGLU -> Q80 / RoPE + KV append).
-// History: v1 staged weights through LDS and waited on every LDS read (1.1 TB/s on w13 at 64
-// tokens); v2 streamed weights to VGPRs but refilled activations through a 4-deep LDS ring on the
-// same vmcnt counter, which capped the weight stream at 3 steps in flight (0.2-1.9 TB/s).
+// Each workgroup owns 64 weight rows (4 waves x 16) and one K split, streamed in chunks of 16
+// Q40 blocks. Both operands are copied HBM/L2 -> LDS with global_load_lds_dwordx4 (no VGPR
+// staging; one 16-B unit per lane, contiguous 256-B+ runs per wave instruction), multi-buffered
+// with counted vmcnt waits and raw barriers (kGemmStages buffers), into XOR-swizzled images so the fragment reads are
+// bank-conflict free. Per block a lane dequantizes 8 nibbles of its row ((1024+q) - 1032 exact in
+// f16, times d) into the B fragment of v_mfma_f32_16x16x32_f16; A fragments are read as is.
+// Split-K partials are combined in split order by the last-arriving workgroup (agent-scope
+// release/acquire counter: deterministic), which runs the fused epilogues (store / SwiGLU /
+// SwiGLU -> f16 / SwiGLU -> Q80 / RoPE + KV append).
 // ------------------------------------------------------------------------------------------------
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-static constexpr int kGemmMaxLdsAct = 128 * 1024;  // resident activation bytes per workgroup
+static constexpr int kGemmRows = 64;
+static constexpr int kGemmCh = 8;  // Q40 blocks per pipeline stage (~25 KB at 32 tokens)
 
-static constexpr int kGemmWaves = 8, kGemmThreads = kGemmWaves * 64;
-// ring depth (steps in flight) per row-tile count: (D - 1) * 2 * RT loads <= 63 outstanding, and
-// <= 256 VGPRs per wave (two waves per SIMD)
-__host__ __device__ constexpr int gemmRing(int RT) { return RT >= 2 ? 10 : 16; }
-
-// Split-K / tile plan of one matrix for MT token tiles: row tiles of 128 * rt rows (rt = row tiles
-// of 16 per wave), the largest rt that still gives >= 64 tiles; splits so the resident activations
-// fit (MP x KW x 2 B <= 128 KB) and the grid reaches ~DL_GEMM_WG (256) workgroups.
+// Split-K degree: grow S until the grid reaches the workgroup target (DL_GEMM_WG, read once) or
+// a split would get fewer than kGemmCh blocks. The target is sized so every CU holds its 3
+// resident workgroups: with one chunk in flight per workgroup, bytes in flight per CU (and so
+// HBM bandwidth) scale with resident workgroups, not with tiles.
 static int gemmWgTarget() {
     static const int v = [] {
         const char *e = std::getenv("DL_GEMM_WG");
@@ -1144,41 +1131,49 @@ static int gemmWgTarget() {
     }();
     return v;
 }
+static int gemmMaxSplits() {
+    static const int v = [] {
+        const char *e = std::getenv("DL_GEMM_MAXS");
+        return e ? std::max(1, std::atoi(e)) : 8;
+    }();
+    return v;
+}
 
 GemmPlan gemmPlan(int rows, int n, int M) {
     GemmPlan p;
-    const int steps = n / 128;  // 4-block steps
-    const int MP = gemmTokenPad(M);
-    const int wr = 16 * kGemmWaves;  // rows per workgroup per row tile
-    p.rt = 2;
-    while (p.rt > 1 && (rows + wr * p.rt - 1) / (wr * p.rt) < 64) p.rt >>= 1;
-    p.tiles = (rows + wr * p.rt - 1) / (wr * p.rt);
-    p.splits = 1;
-    while ((size_t)MP * (n / p.splits) * 2 > (size_t)kGemmMaxLdsAct && steps % (2 * p.splits) == 0) p.splits *= 2;
-    while (p.tiles * p.splits < gemmWgTarget() && steps % (2 * p.splits) == 0 && steps / (2 * p.splits) >= 2)
-        p.splits *= 2;
+    p.rt = 1;
+    p.tiles = (rows + kGemmRows - 1) / kGemmRows;
+    p.splits = gemmSplits(rows, n, M);
     return p;
 }
 
-int gemmSplits(int rows, int n, int M) { return gemmPlan(rows, n, M).splits; }
+bool gemmSupported(int n) { return n % 32 == 0; }
 
-int gemmTokenPad(int M) { return M <= 16 ? 16 : 32; }
+int gemmSplits(int rows, int n, int M) {
+    (void)M;
+    const int tiles = (rows + kGemmRows - 1) / kGemmRows, nb = n / 32;
+    const int target = gemmWgTarget(), maxS = gemmMaxSplits();
+    int S = 1;
+    while (2 * S <= maxS && tiles * S < target && nb % (2 * S) == 0 && nb / (2 * S) >= kGemmCh) S *= 2;
+    return S;
+}
+
+int gemmTokenPad(int M) { return M <= 16 ? 16 : M <= 32 ? 32 : 64; }
 
 size_t gemmPartFloats(int rows, int n, int maxTokens) {
-    size_t f = 0;
-    for (int M = 1; M <= std::min(maxTokens, kGemmMaxTokens); M += 16) {  // every token padding in use
-        const GemmPlan p = gemmPlan(rows, n, M);
-        if (p.splits > 1) f = std::max(f, (size_t)p.splits * p.tiles * gemmTokenPad(M) * 16 * kGemmWaves * p.rt);
-    }
-    return f;
+    const int tiles = (rows + kGemmRows - 1) / kGemmRows, S = gemmSplits(rows, n, maxTokens);
+    const int mp = gemmTokenPad(maxTokens);
+    return S > 1 ? (size_t)S * tiles * mp * kGemmRows : 0;
 }
 
-bool gemmSupported(int n) {
-    // whole 4-block steps, and the resident activations of the largest split fit
-    if (n % 128) return false;
-    const GemmPlan p = gemmPlan(16 * kGemmWaves, n, kGemmMaxTokens);
-    return (size_t)32 * (n / p.splits) * 2 <= (size_t)kGemmMaxLdsAct;
-}
+// stage layout (bytes): weights [64 rows][8 units] x 16 B | scales [32 pairs][8] u32 | x [MP][32 units] x 16 B
+static constexpr int kStW = kGemmRows * kGemmCh * 16, kStD = (kGemmRows / 2) * kGemmCh * 4;
+__host__ __device__ static constexpr int gemmStageBytes(int MT) { return kStW + kStD + MT * 16 * kGemmCh * 64; }
+#ifndef DL_GEMM_STAGES
+#define DL_GEMM_STAGES 2  // 3 stages (2 WGs/CU) measured slower: batch-32 8.1k vs 8.8k tok/s
+#endif
+static constexpr int kGemmStages = DL_GEMM_STAGES;  // stage buffers (kGemmStages-1 chunks in flight)
+static size_t gemmLds(int MT, int stages) { return stages * (size_t)gemmStageBytes(MT) + 16; }
 
 // 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d via the 0x6400 | q magic (1024 + q)
 __device__ __forceinline__ half8 dequantQ40x8(u32x2 wv, int nibHi, uint32_t d16) {
@@ -1208,160 +1203,128 @@ __device__ __forceinline__ void glds16(const void *g, void *lds) {
     __builtin_amdgcn_global_load_lds(const_cast<void *>(g), reinterpret_cast<__attribute__((address_space(3))) void *>(
                                          reinterpret_cast<uintptr_t>(lds)), 16, 0, 0);
 }
-
-template <int MT, int RT>
-__host__ __device__ constexpr size_t gemmTileBytes() { return (size_t)MT * 16 * 16 * kGemmWaves * RT * sizeof(float); }
-// dynamic LDS of a launch: resident activations (KW columns) or the output tile, + the arrival flag
-template <int MT, int RT>
-__host__ __device__ inline size_t gemmLdsBytes(int KW) {
-    const size_t act = (size_t)MT * 16 * KW * 2;
-    return (act > gemmTileBytes<MT, RT>() ? act : gemmTileBytes<MT, RT>()) + 16;
+__device__ __forceinline__ void glds4(const void *g, void *lds) {
+    __builtin_amdgcn_global_load_lds(const_cast<void *>(g), reinterpret_cast<__attribute__((address_space(3))) void *>(
+                                         reinterpret_cast<uintptr_t>(lds)), 4, 0, 0);
 }
 
-template <int MT, int RT, int EPI>
-__global__ __launch_bounds__(kGemmThreads) void gemmQ40Kernel(GemmArgs ga) {
+// STG = stage buffers: 2 double-buffers the chunk stream inside a workgroup; 1 (the 64-token
+// tile) drops that to fit 3 workgroups per CU, which then overlap each other's loads.
+template <int MT, int EPI, int STG>
+__global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     const GemvArgs &a = ga.e;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int MP = MT * 16, WR = RT * 16, TR = kGemmWaves * WR;
-    constexpr int D = gemmRing(RT), NLD = 2 * RT;  // ring steps, weight loads per step
-    static_assert((D - 1) * NLD <= 63, "vmcnt range");
+    constexpr int MP = MT * 16;
+    constexpr int SB = gemmStageBytes(MT);
+    constexpr int NW = kGemmRows * kGemmCh / kThreads, NX = MT * 16 * kGemmCh * 4 / kThreads;
+    constexpr int NLD = NW + 1 + NX;  // glds instructions per thread per stage
+    int *flag = reinterpret_cast<int *>(smem + STG * SB);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int col = lane & 15, h = lane >> 4;
     const int n = a.n, nb = n >> 5, L = a.lanes, NG = kThreads / L, KS = (nb + L - 1) / L;
     const int lgL = 31 - __builtin_clz(L);
     const int tileIdx = blockIdx.x, sp = blockIdx.y, S = ga.splits;
-    const int R0 = tileIdx * TR;
-    const int bps = nb / S, j0 = sp * bps, T = bps >> 2;
-    const int KW = bps * 32, UPT = KW >> 3;  // resident columns, 16-B units per token row
-    int *flag = reinterpret_cast<int *>(smem + gemmLdsBytes<MT, RT>(KW) - 16);
-
-    // this lane's rows (one per row tile) in the GEMV tiling: unit(row, j) =
-    // ((g*KS + j/L)*2 + rpar)*256 + gi*L + j%L, scale word (g*KS + j/L)*256 + gi*L + j%L
-    size_t uBase[RT], dBase[RT];
-    int rpar[RT];
-#pragma unroll
-    for (int t = 0; t < RT; t++) {
-        const int row = min(R0 + wave * WR + t * 16 + col, a.rows - 1);
-        const int g = row / (2 * NG), rem = row % (2 * NG), gi = rem >> 1;
-        rpar[t] = rem & 1;
-        uBase[t] = ((size_t)g * KS * 2 + rpar[t]) * kThreads + gi * L;
-        dBase[t] = (size_t)g * KS * kThreads + gi * L;
-    }
-    const u32x4 *qs = reinterpret_cast<const u32x4 *>(a.qs);
+    const int R0 = tileIdx * kGemmRows;
+    const int bps = nb / S, j0 = sp * bps, j1 = j0 + bps;
+    const int nch = (bps + kGemmCh - 1) / kGemmCh;
+    const uint8_t *qs = a.qs;
     const uint32_t *wd2 = reinterpret_cast<const uint32_t *>(a.wd);
-
-    u32x4 wq[D][RT];
-    uint32_t wsc[D][RT];
-    int it = 0;  // issue cursor (steps); past the last step it re-reads the last (L2 hits)
-    auto issue = [&](u32x4(&q)[RT], uint32_t(&d)[RT]) {
-        const int ii = min(it, T - 1);
-        ++it;
-        const int j = j0 + 4 * ii + h;
+    auto unitOf = [&](int row, int j) -> size_t {  // tiled 16-B unit of (row, block j), clamped
+        row = min(row, a.rows - 1);
+        j = min(j, j1 - 1);
+        const int g = row / (2 * NG), rem = row % (2 * NG), gi = rem >> 1, rpar = rem & 1;
         const int k = j >> lgL, li = j & (L - 1);
+        return (((size_t)g * KS + k) * 2 + rpar) * kThreads + gi * L + li;
+    };
+    auto scaleIdx = [&](int pairRow, int j) -> size_t {  // tiled u32 pair scale of (row pair, block j)
+        const int row = min(pairRow, a.rows - 1);
+        j = min(j, j1 - 1);
+        const int g = row / (2 * NG), rem = row % (2 * NG), gi = rem >> 1;
+        const int k = j >> lgL, li = j & (L - 1);
+        return ((size_t)g * KS + k) * kThreads + gi * L + li;
+    };
+    // issue the copies of chunk c into stage buffer b
+    auto issue = [&](int c, int b) {
+        char *st = smem + b * SB;
+        const int c0 = j0 + c * kGemmCh;
+        // weights: unit u = s*256 + tid -> (row_l = u/8, position p = u%8) holds block p ^ (row_l&7)
 #pragma unroll
-        for (int t = 0; t < RT; t++) {
-            const u32x4 *p = qs + uBase[t] + (size_t)k * 2 * kThreads + li;
-            const uint32_t *pd = wd2 + dBase[t] + (size_t)k * kThreads + li;
-            if (ga.probe) {  // timing probe: the same bytes per step, 1 KB contiguous per wave load
-                // (units: rows x nb 16-B blocks; scale words: rows x nb / 2 - both stay in bounds
-                // when rows is a multiple of the tile rows, which the probe caller checks)
-                const size_t w = (((size_t)tileIdx * S + sp) * kGemmWaves + wave) * RT + t;
-                p = qs + (w * T + ii) * 64 + lane;
-                pd = wd2 + ((w * T + ii) * 64 + lane) / 2;
-            }
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(q[t]) : "v"(p));
-            asm volatile("global_load_dword %0, %1, off" : "=v"(d[t]) : "v"(pd));
+        for (int s = 0; s < NW; s++) {
+            const int u = s * kThreads + tid, rl = u / kGemmCh, pp = u % kGemmCh;
+            const size_t unit = unitOf(R0 + rl, c0 + (pp ^ (rl & (kGemmCh - 1))));
+            glds16(qs + unit * 16, st + (size_t)(s * kThreads + wave * 64) * 16);
+        }
+        // pair scales: u = tid -> (pair_l = u/8, block u%8), 4 B each
+        {
+            const int pl = tid / kGemmCh, jj = tid % kGemmCh;
+            glds4(wd2 + scaleIdx(R0 + 2 * pl, c0 + jj), st + kStW + (size_t)(wave * 64) * 4);
+        }
+        // activations: token row t = 4*kGemmCh units of 8 f16; position p holds unit p ^ (t&15)
+#pragma unroll
+        for (int s = 0; s < NX; s++) {
+            const int u = s * kThreads + tid, t = u / (4 * kGemmCh), pp = u % (4 * kGemmCh);
+            const int uu = pp ^ (t & 15);
+            const int cb = min(c0 + (uu >> 2), j1 - 1);  // block of this unit (clamped)
+            const _Float16 *src = ga.x + (size_t)t * n + (size_t)cb * 32 + (uu & 3) * 8;
+            glds16(src, st + kStW + kStD + (size_t)(s * kThreads + wave * 64) * 16);
         }
     };
 
-    // prologue: the weight ring first (HBM latency), then the resident activations
+    f32x4 acc[MT];
 #pragma unroll
-    for (int s = 0; s < D; s++) {
-        issue(wq[s], wsc[s]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    {
-        const int units = MP * UPT;
-        const _Float16 *xb = ga.x + (size_t)j0 * 32;
-        for (int q0 = 0; q0 < units; q0 += kGemmThreads) {  // uniform: units is a multiple of 512
-            const int q = q0 + tid, tk = q / UPT, p = q - tk * UPT, uu = p ^ (tk & 15);
-            glds16(xb + (size_t)tk * n + (size_t)uu * 8, smem + (size_t)(q0 + wave * 64) * 16);
-        }
-    }
-#pragma unroll
-    for (int s = 0; s < D; s++)
-#pragma unroll
-        for (int t = 0; t < RT; t++) asm volatile("s_waitcnt vmcnt(0)" : "+v"(wq[s][t]), "+v"(wsc[s][t]));
-    __syncthreads();
+    for (int t = 0; t < MT; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int rl = wave * 16 + col;  // this lane's weight row (local)
+    const int byteHalf = h & 1, nibHi = h >> 1;
 
-    f32x4 acc[RT][MT];
+    constexpr int PF = STG - 1;  // chunks in flight ahead of the one consumed
+    for (int c = 0; c < PF && c < nch; c++) issue(c, c);
+    for (int c = 0; c < nch; c++) {
+        if (c + PF < nch) issue(c + PF, (c + PF) % STG);
+        // wait until chunk c landed (this thread): the chunks issued after it may stay in flight
+        const int after = min(nch - 1, c + PF) - c;
+        if (after >= 3)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * NLD) : "memory");
+        else if (after == 2)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * NLD) : "memory");
+        else if (after == 1)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NLD) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // ... and for every thread
+        const char *st = smem + (c % STG) * SB;
+        const int cn = min(kGemmCh, bps - c * kGemmCh);
 #pragma unroll
-    for (int t = 0; t < RT; t++)
+        for (int jj = 0; jj < kGemmCh; jj++) {
+            const int pp = jj ^ (rl & (kGemmCh - 1));
+            const u32x2 wv = *reinterpret_cast<const u32x2 *>(st + (size_t)(rl * kGemmCh + pp) * 16 + byteHalf * 8);
+            const uint32_t dw = *reinterpret_cast<const uint32_t *>(st + kStW + (size_t)((rl >> 1) * kGemmCh + jj) * 4);
+            const uint32_t d16 = jj < cn ? ((rl & 1) ? dw >> 16 : dw & 0xFFFFu) : 0u;
+            const half8 b = dequantQ40x8(wv, nibHi, d16);
 #pragma unroll
-        for (int m = 0; m < MT; m++) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    auto compute = [&](int i, const u32x4(&q)[RT], const uint32_t(&d)[RT]) {
-#pragma unroll
-        for (int ks = 0; ks < 4; ks++) {
-            const int u = (4 * i + h) * 4 + ks;  // block 4i+h of the split, unit ks
-            half8 av[MT];
-#pragma unroll
-            for (int m = 0; m < MT; m++) {  // token m*16 + col (swizzle: low 4 unit bits ^ token)
-                const int tk = m * 16 + col;
-                av[m] = *reinterpret_cast<const half8 *>(smem + ((size_t)tk * UPT + (u ^ col)) * 16);
-            }
-#pragma unroll
-            for (int t = 0; t < RT; t++) {
-                const u32x2 wv = (ks & 1) ? u32x2{q[t].z, q[t].w} : u32x2{q[t].x, q[t].y};
-                const uint32_t d16 = rpar[t] ? d[t] >> 16 : d[t] & 0xFFFFu;
-                const half8 b = dequantQ40x8(wv, ks >> 1, d16);
-#pragma unroll
-                for (int m = 0; m < MT; m++) acc[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av[m], b, acc[t][m], 0, 0, 0);
+            for (int t = 0; t < MT; t++) {
+                const int tok = t * 16 + col, up = (jj * 4 + h) ^ (tok & 15);
+                const half8 av = *reinterpret_cast<const half8 *>(st + kStW + kStD + (size_t)(tok * 4 * kGemmCh + up) * 16);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b, acc[t], 0, 0, 0);
             }
         }
-    };
-    // full rounds: consume slot s (step t0 + s), refill it with step t0 + s + D
-    int t0 = 0;
-    for (; t0 + D < T; t0 += D) {
-#pragma unroll
-        for (int s = 0; s < D; s++) {
-#pragma unroll
-            for (int t = 0; t < RT; t++)
-                asm volatile("s_waitcnt vmcnt(%2)" : "+v"(wq[s][t]), "+v"(wsc[s][t]) : "i"((D - 1) * NLD));
-            compute(t0 + s, wq[s], wsc[s]);
-            issue(wq[s], wsc[s]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // stage c % STG is refilled at iteration c + 1
     }
-    // last round: no refills; slot s waits for itself only (the younger slots stay in flight)
-#pragma unroll
-    for (int s = 0; s < D; s++) {
-#pragma unroll
-        for (int t = 0; t < RT; t++)
-            asm volatile("s_waitcnt vmcnt(%2)" : "+v"(wq[s][t]), "+v"(wsc[s][t]) : "i"((D - 1 - s) * NLD));
-        if (t0 + s < T) compute(t0 + s, wq[s], wsc[s]);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    __syncthreads();  // every wave is done reading the activations: the LDS becomes the tile
 
-    float *tile = reinterpret_cast<float *>(smem);  // [MP][TR]
-    // C layout: weight row (local) wave*WR + t*16 + col, token m*16 + h*4 + i
+    float *tile = reinterpret_cast<float *>(smem);  // [MP][64], stages are free now
+    // C layout: weight row (local) wave*16 + col, token t*16 + h*4 + i
     if (S == 1) {
 #pragma unroll
-        for (int t = 0; t < RT; t++)
+        for (int t = 0; t < MT; t++)
 #pragma unroll
-            for (int m = 0; m < MT; m++)
-#pragma unroll
-                for (int i = 0; i < 4; i++) tile[(m * 16 + h * 4 + i) * TR + wave * WR + t * 16 + col] = acc[t][m][i];
+            for (int i = 0; i < 4; i++) tile[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
     } else {
         const int tiles = gridDim.x;
-        float *part = ga.part + ((size_t)sp * tiles + tileIdx) * MP * TR;
+        float *part = ga.part + ((size_t)sp * tiles + tileIdx) * MP * kGemmRows;
 #pragma unroll
-        for (int t = 0; t < RT; t++)
+        for (int t = 0; t < MT; t++)
 #pragma unroll
-            for (int m = 0; m < MT; m++)
-#pragma unroll
-                for (int i = 0; i < 4; i++) part[(m * 16 + h * 4 + i) * TR + wave * WR + t * 16 + col] = acc[t][m][i];
+            for (int i = 0; i < 4; i++) part[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
@@ -1376,12 +1339,12 @@ __global__ __launch_bounds__(kGemmThreads) void gemmQ40Kernel(GemmArgs ga) {
             __hip_atomic_store(ga.counters + tileIdx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
-        // combine in split order (deterministic), only the M real tokens, all of a thread's
-        // splits in flight at once
-        const f32x4 *P = reinterpret_cast<const f32x4 *>(ga.part) + (size_t)tileIdx * MP * TR / 4;
-        const size_t st4 = (size_t)tiles * MP * TR / 4;
+        // combine in split order (deterministic), 16-B loads with all of a thread's splits in
+        // flight at once: this tail runs on one workgroup per tile after the others finished
+        const f32x4 *P = reinterpret_cast<const f32x4 *>(ga.part) + (size_t)tileIdx * MP * kGemmRows / 4;
+        const size_t st4 = (size_t)tiles * MP * kGemmRows / 4;
         f32x4 *tile4 = reinterpret_cast<f32x4 *>(tile);
-        for (int i = tid; i < ga.M * TR / 4; i += kGemmThreads) {
+        for (int i = tid; i < MP * kGemmRows / 4; i += kThreads) {
             f32x4 v[8];
 #pragma unroll
             for (int s2 = 0; s2 < 8; s2++)
@@ -1395,11 +1358,10 @@ __global__ __launch_bounds__(kGemmThreads) void gemmQ40Kernel(GemmArgs ga) {
         }
     }
     __syncthreads();
-    // fused epilogues on row pairs (2k, 2k+1) of the tile, TR/2 pairs per token
-    constexpr int HP = TR / 2;
-    for (int i = tid; i < ga.M * HP; i += kGemmThreads) {
-        const int t = i / HP, k = i % HP, r0 = R0 + 2 * k;
-        const float v0 = tile[t * TR + 2 * k], v1 = tile[t * TR + 2 * k + 1];
+    // fused epilogues on row pairs (2k, 2k+1) of the tile, 32 pairs per token
+    for (int i = tid; i < ga.M * 32; i += kThreads) {
+        const int t = i >> 5, k = i & 31, r0 = R0 + 2 * k;
+        const float v0 = tile[t * kGemmRows + 2 * k], v1 = tile[t * kGemmRows + 2 * k + 1];
         if constexpr (EPI == EPI_STORE) {
             if (r0 < a.rows) a.out[(size_t)t * a.ldOut + r0] = v0;
             if (r0 + 1 < a.rows) a.out[(size_t)t * a.ldOut + r0 + 1] = v1;
@@ -1408,21 +1370,17 @@ __global__ __launch_bounds__(kGemmThreads) void gemmQ40Kernel(GemmArgs ga) {
         } else if constexpr (EPI == EPI_ACT_F16) {
             if (r0 < a.rows) ga.outH[(size_t)t * a.ldOut + (r0 >> 1)] = (_Float16)(gateAct(a, v0) * v1);
         } else if constexpr (EPI == EPI_ACT_Q80) {
-            // 32 consecutive hidden units (lanes k..k+31 of one token) form one Q80 block; HP is a
-            // multiple of 32 and the hidden row count a multiple of 32: whole groups per block
-            const int hu = (R0 >> 1) + k;
-            const bool live = hu < (a.rows >> 1);
-            const float hv = live ? gateAct(a, v0) * v1 : 0.f;
+            const int hBase = R0 >> 1;
+            if (hBase >= (a.rows >> 1)) continue;  // whole 32-unit block: uniform per lane group
+            const float hv = gateAct(a, v0) * v1;
             const float amax = groupMax<32>(fabsf(hv));
             const float d = amax / 127.0f;
             const float id = d != 0.f ? 1.0f / d : 0.f;
             int q = (int)rintf(hv * id);
             q = q > 127 ? 127 : (q < -127 ? -127 : q);
+            a.oq[(size_t)t * a.ldOut + hBase + k] = (int8_t)q;
             const float qsum = groupSum<32>((float)q);
-            if (live) {
-                a.oq[(size_t)t * a.ldOut + hu] = (int8_t)q;
-                if ((hu & 31) == 0) a.os[(size_t)t * (a.ldOut >> 5) + (hu >> 5)] = make_float2(roundF16(d), qsum);
-            }
+            if (k == 0) a.os[(size_t)t * (a.ldOut >> 5) + (hBase >> 5)] = make_float2(roundF16(d), qsum);
         } else {
             if (r0 < a.rows)
                 qkvPairStore(a, r0, v0, v1, a.rope + (size_t)a.pos[t] * (a.hs >> 1), a.pos[t], a.slot[t],
@@ -1431,38 +1389,49 @@ __global__ __launch_bounds__(kGemmThreads) void gemmQ40Kernel(GemmArgs ga) {
     }
 }
 
-template <int MT, int RT>
-static void gemmLaunchE(const GemmArgs &ga, int epi, dim3 grid, hipStream_t s) {
-    const int KW = ga.e.n / ga.splits;
-    const size_t lds = gemmLdsBytes<MT, RT>(KW);
-#define DL_GEMM_CASE(E)                                                                           \
-    if (epi == E) {                                                                               \
-        if (lds > 65536) allowLds((const void *)gemmQ40Kernel<MT, RT, E>, lds); /* per device */  \
-        hipLaunchKernelGGL((gemmQ40Kernel<MT, RT, E>), grid, dim3(kGemmThreads), lds, s, ga);     \
-        return;                                                                                   \
-    }
-    DL_GEMM_CASE(EPI_STORE) DL_GEMM_CASE(EPI_ACT) DL_GEMM_CASE(EPI_ACT_Q80) DL_GEMM_CASE(EPI_QKV)
-    DL_GEMM_CASE(EPI_ACT_F16)
-#undef DL_GEMM_CASE
+static int gemmStages4() {  // stage buffers of the 64-token tile (DL_GEMM_STG4, read once)
+    static const int v = [] {
+        const char *e = std::getenv("DL_GEMM_STG4");
+        return e && std::atoi(e) == 2 ? 2 : 1;
+    }();
+    return v;
 }
 
-template <int MT>
-static void gemmLaunchR(const GemmArgs &ga, int epi, int rt, dim3 grid, hipStream_t s) {
-    switch (rt) {
-        case 2: gemmLaunchE<MT, 2>(ga, epi, grid, s); break;
-        default: gemmLaunchE<MT, 1>(ga, epi, grid, s); break;
-    }
+static int gemmStages2() {  // stage buffers of the 32-token tile (DL_GEMM_STG2, read once)
+    static const int v = [] {
+        const char *e = std::getenv("DL_GEMM_STG2");
+        return e && std::atoi(e) == 1 ? 1 : kGemmStages;
+    }();
+    return v;
+}
+
+static int gemmStages1() {  // stage buffers of the 16-token tile (DL_GEMM_STG1 = 2..4, read once)
+    static const int v = [] {
+        const char *e = std::getenv("DL_GEMM_STG1");
+        const int k = e ? std::atoi(e) : kGemmStages;
+        return k >= 2 && k <= 4 ? k : kGemmStages;
+    }();
+    return v;
 }
 
 void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
-    const GemmPlan p = gemmPlan(ga.e.rows, ga.e.n, ga.M);
-    if (!gemmSupported(ga.e.n) || ga.M < 1 || ga.M > kGemmMaxTokens || ga.splits != p.splits)
-        throw Error("launchGemmQ40: unsupported shape (n % 128, 1..32 tokens, splits from gemmPlan)");
-    const dim3 grid(p.tiles, p.splits);
-    if (gemmTokenPad(ga.M) == 16)
-        gemmLaunchR<1>(ga, epi, p.rt, grid, s);
-    else
-        gemmLaunchR<2>(ga, epi, p.rt, grid, s);
+    const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
+    const int MT = gemmTokenPad(ga.M) / 16;
+    const int stg = MT == 4 ? gemmStages4() : MT == 2 ? gemmStages2() : gemmStages1();
+    const dim3 grid(tiles, ga.splits);
+    const size_t lds = gemmLds(MT, stg);
+#define DL_GEMM_CASE(M_, E, G)                                                                    \
+    if (MT == M_ && epi == E && stg == G) {                                                       \
+        if (lds > 65536) allowLds((const void *)gemmQ40Kernel<M_, E, G>, lds); /* per device */  \
+        hipLaunchKernelGGL((gemmQ40Kernel<M_, E, G>), grid, dim3(kThreads), lds, s, ga);         \
+        return;                                                                                   \
+    }
+#define DL_GEMM_CASES(M_, G)                                                                      \
+    DL_GEMM_CASE(M_, EPI_STORE, G) DL_GEMM_CASE(M_, EPI_ACT, G) DL_GEMM_CASE(M_, EPI_ACT_Q80, G)  \
+    DL_GEMM_CASE(M_, EPI_QKV, G) DL_GEMM_CASE(M_, EPI_ACT_F16, G)
+    DL_GEMM_CASES(1, kGemmStages) DL_GEMM_CASES(1, 3) DL_GEMM_CASES(1, 4) DL_GEMM_CASES(2, kGemmStages) DL_GEMM_CASES(2, 1) DL_GEMM_CASES(4, 1) DL_GEMM_CASES(4, 2)
+#undef DL_GEMM_CASES
+#undef DL_GEMM_CASE
 }
 
 // Residual add + RMS norm (optional) of M rows -> f16 (one workgroup per row): the batched
@@ -1543,7 +1512,7 @@ void launchNormF16(const GemvArgs &a, _Float16 *out, int M, hipStream_t s) {
 // each workgroup publishes its online-softmax partial and the last arriver combines them.
 // ------------------------------------------------------------------------------------------------
 int attnSplitGrid(int seqLen) {
-    int g = (seqLen + kAttnMChunkKeys - 1) / kAttnMChunkKeys;  // the MFMA kernel's 128-key chunks
+    int g = (seqLen + 255) / 256;
     return g < 1 ? 1 : (g > 128 ? 128 : g);
 }
 
@@ -1905,280 +1874,6 @@ __global__ __launch_bounds__(kAttnThreads) void attnKernel(AttnArgs a) {
     attnTask<HG, HS, BF16, kAttnThreads>(a, blockIdx.z, blockIdx.x, blockIdx.y, smem);
 }
 
-// ------------------------------------------------------------------------------------------------
-// MFMA attention over a bf16 KV cache (decode rows and prefill rows alike; every row attends to
-// positions [0, pos] of its own slot). Layouts: K row-major [slot][pos][kv0]; V TRANSPOSED
-// [slot][kv0][seqLen] (written so by the QKV epilogues), so every MFMA operand is a contiguous
-// load. Task = (kv head, sequence chunk, row); 4 waves split the chunk; a wave walks tiles of 32
-// keys for all kvMul query heads of the kv head at once (<= 16, padded to the 16 MFMA columns):
-//   S^T = K . Q^T      A = K rows (16 keys x 32 dims, 16-B loads), B = Q^T (registers, bf16)
-//   P^T = exp(S^T - m) C layout: lane (key 4h+i [+16], query l&15) - online softmax per query
-//   O^T += V^T . P^T   A = V^T (16 dims x 32 keys, two 8-B loads), B = P^T straight from the
-//                      C registers of S^T (k order permuted identically on both operands)
-// so every per-query statistic lives in the lanes of that query (l & 15) and no data moves
-// between lanes except the max / sum across the 4 lane groups. Waves merge through LDS; several
-// chunks merge through partO/partML and the last-arriving workgroup (the split combine of the
-// VALU kernel). Output: f32, f16 (batched path) or Q80 (decode path), per head.
-// ------------------------------------------------------------------------------------------------
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-static constexpr int kAttnMThreads = 256, kAttnMWaves = 4, kAttnMChunk = kAttnMChunkKeys;
-
-__device__ __forceinline__ bf16x8 f32x8ToBf16(const float (&v)[8]) {
-    bf16x8 r;
-#pragma unroll
-    for (int j = 0; j < 8; j++) r[j] = (__bf16)v[j];
-    return r;
-}
-
-// Final output of nq heads from LDS fin[nq][HS] -> f32 / f16 / Q80 (32-element blocks) in global.
-template <int HS>
-__device__ __forceinline__ void attnWriteOutN(const AttnArgs &a, int b, int head0, int nq, const float *fin) {
-    const int tid = threadIdx.x, total = nq * HS;  // a multiple of 32: whole lane groups per block
-    if (a.outQ) {
-        for (int base = 0; base < total; base += kAttnMThreads) {
-            const int i = base + tid;
-            const float v = i < total ? fin[i] : 0.f;
-            const float amax = groupMax<32>(fabsf(v));
-            const float d = amax / 127.0f;
-            const float id = d != 0.f ? 1.0f / d : 0.f;
-            int q = (int)rintf(v * id);
-            q = q > 127 ? 127 : (q < -127 ? -127 : q);
-            const float qs = groupSum<32>((float)q);
-            if (i < total) {
-                const int col = head0 * HS + i;
-                a.outQ[(size_t)b * a.ldOut + col] = (int8_t)q;
-                if ((i & 31) == 0) a.outS[(size_t)b * (a.ldOut >> 5) + (col >> 5)] = make_float2(roundF16(d), qs);
-            }
-        }
-    } else if (a.outH) {
-        for (int i = tid; i < total; i += kAttnMThreads) a.outH[(size_t)b * a.ldOut + head0 * HS + i] = (_Float16)fin[i];
-    } else {
-        for (int i = tid; i < total; i += kAttnMThreads) a.out[(size_t)b * a.ldOut + head0 * HS + i] = fin[i];
-    }
-}
-
-template <int HS>
-__global__ __launch_bounds__(kAttnMThreads) void attnMfmaKernel(AttnArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int DS = HS / 32, NT = HS / 16;  // 32-dim k-steps of S, 16-dim tiles of O
-    const int g = blockIdx.x, c = blockIdx.y, b = blockIdx.z;
-    const int nq = a.kvMul, head0 = g * nq;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, col = lane & 15, h = lane >> 4;
-    const int pos = a.pos[b], sl = a.slot[b], len = pos + 1;
-    int nSplit = (len + kAttnMChunk - 1) / kAttnMChunk;
-    if (nSplit > a.splitGrid) nSplit = a.splitGrid;
-    const int ch = ((len + nSplit - 1) / nSplit + kAttnMChunk - 1) / kAttnMChunk * kAttnMChunk;
-    if (c >= nSplit) return;
-    const int wch = ch / kAttnMWaves;  // keys per wave (multiple of 32)
-    const int k0 = c * ch + wave * wch, k1 = min(min(c * ch + (wave + 1) * wch, len), c * ch + ch);
-
-    float *mW = reinterpret_cast<float *>(smem);       // [4][16]
-    float *lW = mW + kAttnMWaves * 16;                  // [4][16]
-    float *oW = lW + kAttnMWaves * 16;                  // [4][16][HS]
-    float *redL = oW + kAttnMWaves * 16 * HS;           // [16][HS]
-    float *mlL = redL + 16 * HS;                        // [16][2]
-    int *flagL = reinterpret_cast<int *>(mlL + 32);
-
-    // Q^T fragments (B operand): lane (query col, k-octet h) holds Q[col][32 s + 8 h .. + 7], scaled
-    const float scale = 1.0f / sqrtf((float)HS);
-    bf16x8 qf[DS];
-#pragma unroll
-    for (int s = 0; s < DS; s++) {
-        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (col < nq) {
-            const float *qp = a.q + (size_t)b * a.ldq + (size_t)(head0 + col) * HS + 32 * s + 8 * h;
-            const float4 x0 = ld4(qp), x1 = ld4(qp + 4);
-            v[0] = x0.x * scale; v[1] = x0.y * scale; v[2] = x0.z * scale; v[3] = x0.w * scale;
-            v[4] = x1.x * scale; v[5] = x1.y * scale; v[6] = x1.z * scale; v[7] = x1.w * scale;
-        }
-        qf[s] = f32x8ToBf16(v);
-    }
-    const __bf16 *kc = reinterpret_cast<const __bf16 *>(a.kcache);
-    const __bf16 *vc = reinterpret_cast<const __bf16 *>(a.vcache);
-    const size_t kBase = (size_t)sl * a.seqLen * a.kv0 + (size_t)g * HS;     // + pos * kv0 + dim
-    const size_t vBase = ((size_t)sl * a.kv0 + (size_t)g * HS) * a.seqLen;  // + dim * seqLen + pos
-    const int last = a.seqLen - 1;
-
-    f32x4 o[NT];
-#pragma unroll
-    for (int n = 0; n < NT; n++) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float m = -INFINITY, lsum = 0.f;
-    for (int t0 = k0; t0 < k1; t0 += 32) {
-        bf16x8 kf[2][DS];
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const int key = min(t0 + 16 * u + col, last);
-#pragma unroll
-            for (int s = 0; s < DS; s++)
-                kf[u][s] = *reinterpret_cast<const bf16x8 *>(kc + kBase + (size_t)key * a.kv0 + 32 * s + 8 * h);
-        }
-        bf16x8 vf[NT];
-        const int p0 = min(t0 + 4 * h, last - 3), p1 = min(t0 + 16 + 4 * h, last - 3);
-#pragma unroll
-        for (int n = 0; n < NT; n++) {
-            const __bf16 *vr = vc + vBase + (size_t)(16 * n + col) * a.seqLen;
-            const bf16x4 lo = *reinterpret_cast<const bf16x4 *>(vr + p0);
-            const bf16x4 hi = *reinterpret_cast<const bf16x4 *>(vr + p1);
-            vf[n] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        }
-        f32x4 st[2];
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-            st[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int s = 0; s < DS; s++) st[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[u][s], qf[s], st[u], 0, 0, 0);
-        }
-        // mask keys past the row's length (and past this wave's range), then the online softmax
-        float mx = -INFINITY;
-#pragma unroll
-        for (int u = 0; u < 2; u++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int key = t0 + 16 * u + 4 * h + i;
-                if (key >= k1) st[u][i] = -INFINITY;
-                mx = fmaxf(mx, st[u][i]);
-            }
-        mx = fmaxf(mx, __shfl_xor(mx, 16));
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
-        const float mn = fmaxf(m, mx);
-        const float corr = m == -INFINITY ? 0.f : __expf(m - mn);
-        float p[2][4], ps = 0.f;
-#pragma unroll
-        for (int u = 0; u < 2; u++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                p[u][i] = st[u][i] == -INFINITY ? 0.f : __expf(st[u][i] - mn);
-                ps += p[u][i];
-            }
-        lsum = lsum * corr + ps;
-        m = mn;
-        const float pv[8] = {p[0][0], p[0][1], p[0][2], p[0][3], p[1][0], p[1][1], p[1][2], p[1][3]};
-        const bf16x8 pf = f32x8ToBf16(pv);
-#pragma unroll
-        for (int n = 0; n < NT; n++) {
-            o[n] *= corr;
-            o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[n], pf, o[n], 0, 0, 0);
-        }
-    }
-    lsum += __shfl_xor(lsum, 16);
-    lsum += __shfl_xor(lsum, 32);
-    // waves -> LDS: O^T C layout: lane holds O[query col][dim 16 n + 4 h + i]
-    if (h == 0) {
-        mW[wave * 16 + col] = m;
-        lW[wave * 16 + col] = lsum;
-    }
-#pragma unroll
-    for (int n = 0; n < NT; n++)
-#pragma unroll
-        for (int i = 0; i < 4; i++) oW[(wave * 16 + col) * HS + 16 * n + 4 * h + i] = o[n][i];
-    __syncthreads();
-    for (int i = tid; i < nq * HS; i += kAttnMThreads) {
-        const int q = i / HS, d = i % HS;
-        float M = -INFINITY;
-#pragma unroll
-        for (int w = 0; w < kAttnMWaves; w++) M = fmaxf(M, mW[w * 16 + q]);
-        float acc = 0.f, Ls = 0.f;
-#pragma unroll
-        for (int w = 0; w < kAttnMWaves; w++) {
-            const float e = M == -INFINITY || mW[w * 16 + q] == -INFINITY ? 0.f : __expf(mW[w * 16 + q] - M);
-            acc += e * oW[(w * 16 + q) * HS + d];
-            Ls += e * lW[w * 16 + q];
-        }
-        redL[i] = acc;
-        if (d == 0) {
-            mlL[q * 2] = M;
-            mlL[q * 2 + 1] = Ls;
-        }
-    }
-    __syncthreads();
-    if (nSplit == 1) {
-        for (int i = tid; i < nq * HS; i += kAttnMThreads) redL[i] = redL[i] / mlL[(i / HS) * 2 + 1];
-        __syncthreads();
-        attnWriteOutN<HS>(a, b, head0, nq, redL);
-        return;
-    }
-    // several chunks: publish this chunk's partial, the last arriver combines (as attnFinish)
-    const int G = a.splitGrid;
-    const size_t pbase = ((size_t)b * a.nHeads0 + head0) * G;  // [nq][G] chunks of these heads
-    for (int i = tid; i < nq * HS; i += kAttnMThreads) {
-        const int q = i / HS, d = i % HS;
-        a.partO[((pbase + (size_t)q * G) + c) * HS + d] = redL[i];
-    }
-    if (tid < nq) {
-        a.partML[((pbase + (size_t)tid * G) + c) * 2] = mlL[tid * 2];
-        a.partML[((pbase + (size_t)tid * G) + c) * 2 + 1] = mlL[tid * 2 + 1];
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int *cnt = a.counters + (size_t)b * (a.nHeads0 / nq) + g;
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        flagL[0] = old == nSplit - 1;
-    }
-    __syncthreads();
-    if (!flagL[0]) return;
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    float *scratch = oW;  // >= 2 * 16 * G floats (G <= 128)
-    for (int i = tid; i < nq * nSplit; i += kAttnMThreads) {
-        const int q = i / nSplit, cc = i % nSplit;
-        const float2 ml = *reinterpret_cast<const float2 *>(a.partML + ((pbase + (size_t)q * G) + cc) * 2);
-        scratch[2 * (q * G + cc)] = ml.x;
-        scratch[2 * (q * G + cc) + 1] = ml.y;
-    }
-    __syncthreads();
-    if (tid < nq) {
-        float M = -INFINITY;
-        for (int cc = 0; cc < nSplit; cc++) M = fmaxf(M, scratch[2 * (tid * G + cc)]);
-        float Ls = 0.f;
-        for (int cc = 0; cc < nSplit; cc++) {
-            float *ml = scratch + 2 * (tid * G + cc);
-            const float w = M == -INFINITY || ml[0] == -INFINITY ? 0.f : __expf(ml[0] - M);
-            ml[0] = w;
-            Ls += w * ml[1];
-        }
-        mlL[tid * 2 + 1] = Ls;
-    }
-    __syncthreads();
-    constexpr int U = 8;
-    for (int i = tid; i < nq * HS; i += kAttnMThreads) {
-        const int q = i / HS, d = i % HS;
-        const float *po = a.partO + (pbase + (size_t)q * G) * HS + d;
-        const float *wv = scratch + 2 * q * G;
-        float acc = 0.f;
-        int cc = 0;
-        for (; cc + U <= nSplit; cc += U) {
-            float v[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) v[u] = po[(size_t)(cc + u) * HS];
-#pragma unroll
-            for (int u = 0; u < U; u++) acc += wv[2 * (cc + u)] * v[u];
-        }
-        for (; cc < nSplit; cc++) acc += wv[2 * cc] * po[(size_t)cc * HS];
-        redL[i] = acc / mlL[q * 2 + 1];
-    }
-    __syncthreads();
-    attnWriteOutN<HS>(a, b, head0, nq, redL);
-}
-
-template <int HS>
-static void attnMfmaLaunch(const AttnArgs &a, int B, hipStream_t s) {
-    const size_t lds = sizeof(float) * (2 * kAttnMWaves * 16 + kAttnMWaves * 16 * HS + 16 * HS + 32) + 16;
-    const dim3 grid(a.nHeads0 / a.kvMul, a.splitGrid, B);
-    hipLaunchKernelGGL((attnMfmaKernel<HS>), grid, dim3(kAttnMThreads), lds, s, a);
-}
-
-bool attnMfmaSupported(int kvMul, int hs, int seqLen) {
-    return kvMul >= 1 && kvMul <= 16 && (hs == 64 || hs == 128) && seqLen % 8 == 0;
-}
-
 template <int HS, bool BF16>
 static void attnDispatchHG(const AttnArgs &a, int B, int HG, hipStream_t s) {
     constexpr int NW = kAttnThreads / 64;
@@ -2195,13 +1890,6 @@ static void attnDispatchHG(const AttnArgs &a, int B, int HG, hipStream_t s) {
 }
 
 void launchAttention(const AttnArgs &a, int B, hipStream_t s) {
-    if (a.kvBf16) {  // bf16 cache: MFMA kernel (V stored transposed); f32 cache: the VALU kernel
-        if (!attnMfmaSupported(a.kvMul, a.hs, a.seqLen))
-            throw Error("bf16 KV attention needs kvMul <= 16, head size 64/128 and seqLen % 8 == 0");
-        if (a.hs == 128) attnMfmaLaunch<128>(a, B, s);
-        else attnMfmaLaunch<64>(a, B, s);
-        return;
-    }
     static const int hgOverride = [] {  // experiments: DL_ATTN_HG forces query heads per workgroup
         const char *e = getenv("DL_ATTN_HG");
         return e ? atoi(e) : 0;
@@ -2320,6 +2008,194 @@ __global__ __launch_bounds__(256) void argmaxKernel(ArgmaxArgs a) {
 
 void launchArgmax(const ArgmaxArgs &a, int B, hipStream_t s) {
     hipLaunchKernelGGL(argmaxKernel, dim3(kArgmaxBlocks, B), dim3(256), 0, s, a);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Device sampling (SampleArgs in kernels.h). Probabilities are recomputed from the logits in
+// every pass (128 K floats per row stay L2-resident): max, sum, then for top-p two radix searches
+// of 4 x 8 bits over the order-preserving key of x = logit / T, each pass building a 256-bin
+// histogram of probability mass (LDS float atomics) among the elements whose key matches the
+// prefix found so far; wave 0 suffix-scans the bins to find where the descending cumulative mass
+// first exceeds the target.
+// ------------------------------------------------------------------------------------------------
+static constexpr int kSampleThreads = 1024;
+
+__device__ __forceinline__ uint32_t orderKey(float x) {
+    const uint32_t u = __float_as_uint(x);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+template <typename F>
+__device__ __forceinline__ float blockReduce1024(float v, float *red, F op) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = op(v, __shfl_xor(v, off));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    float r = red[0];
+    for (int w = 1; w < kSampleThreads / 64; w++) r = op(r, red[w]);
+    return r;
+}
+
+// Radix search among candidates (prob >= cutoff, key >= minKey): the key at which the descending
+// cumulative probability mass first exceeds `target` (the lowest key if it never does), and the
+// mass of every candidate with a key >= that key.
+__device__ void sampleRadix(const float *l, int V, float invT, float m, float invZ, float cutoff, uint32_t minKey,
+                            float target, float *hist, uint32_t *sKey, float *sMass) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    uint32_t prefix = 0;
+    float above = 0.f;
+    for (int pass = 0; pass < 4; pass++) {
+        const int shift = 24 - 8 * pass;
+        if (tid < 256) hist[tid] = 0.f;
+        __syncthreads();
+        for (int i = tid; i < V; i += kSampleThreads) {
+            const float x = l[i] * invT;
+            const float p = expf(x - m) * invZ;
+            const uint32_t k = orderKey(x);
+            if (p < cutoff || k < minKey) continue;
+            if (pass > 0 && (k >> (shift + 8)) != (prefix >> (shift + 8))) continue;
+            atomicAdd(&hist[(k >> shift) & 255], p);
+        }
+        __syncthreads();
+        if (tid < 64) {
+            // lane l owns bins 4l..4l+3; suffix sums from the top bin down
+            const float v0 = hist[4 * lane], v1 = hist[4 * lane + 1], v2 = hist[4 * lane + 2], v3 = hist[4 * lane + 3];
+            const float s3 = v3, s2 = v2 + s3, s1 = v1 + s2, s0 = v0 + s1;
+            float inc = s0;  // inclusive suffix over lanes >= lane
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const float y = __shfl_down(inc, off);
+                if (lane + off < 64) inc += y;
+            }
+            const float ex = inc - s0;  // mass of the bins above this lane's four
+            const float t = target - above;
+            int sel = -1;
+            if (ex + s3 > t && v3 > 0.f) sel = 3;
+            else if (ex + s2 > t && v2 > 0.f) sel = 2;
+            else if (ex + s1 > t && v1 > 0.f) sel = 1;
+            else if (ex + s0 > t && v0 > 0.f) sel = 0;
+            const unsigned long long hit = __ballot(sel >= 0);
+            int bin;
+            float newAbove;
+            if (hit) {
+                const int L = 63 - __builtin_clzll(hit);  // highest lane with a crossing bin
+                const int s = __shfl(sel, L);
+                bin = 4 * L + s;
+                const float exL = __shfl(ex, L);
+                const float sufL[4] = {__shfl(s1, L), __shfl(s2, L), __shfl(s3, L), 0.f};
+                newAbove = above + exL + sufL[s];  // mass of the bins above the selected one
+            } else {  // never exceeded (rounding): take everything, i.e. the lowest non-empty bin
+                const unsigned long long ne = __ballot(s0 > 0.f);
+                const int L = ne ? __builtin_ctzll(ne) : 0;
+                const float w0 = __shfl(v0, L), w1 = __shfl(v1, L), w2 = __shfl(v2, L);
+                const int s = w0 > 0.f ? 0 : (w1 > 0.f ? 1 : (w2 > 0.f ? 2 : 3));
+                bin = 4 * L + s;
+                const float sufL[4] = {__shfl(s1, L), __shfl(s2, L), __shfl(s3, L), 0.f};
+                newAbove = above + __shfl(ex, L) + sufL[s];
+            }
+            if (lane == 0) {
+                sKey[0] = prefix | ((uint32_t)bin << shift);
+                sMass[0] = newAbove;
+                sMass[1] = hist[bin];
+            }
+        }
+        __syncthreads();
+        prefix = sKey[0];
+        above = sMass[0];
+        __syncthreads();
+    }
+    if (tid == 0) sMass[0] = above + sMass[1];  // mass of keys >= the found key
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kSampleThreads) void sampleKernel(SampleArgs a) {
+    __shared__ float hist[256];
+    __shared__ float red[kSampleThreads / 64];
+    __shared__ uint32_t sKey[1];
+    __shared__ float sMass[2];
+    __shared__ int sIdx[1];
+    const int b = blockIdx.x, tid = threadIdx.x, V = a.vocab;
+    const float4 sp = a.spec[b];
+    const float T = sp.x, P = sp.y, coin = sp.z;
+    const float *l = a.logits + (size_t)b * V;
+    if (T < 0.f) {
+        if (tid == 0) a.ids[b] = -1;
+        return;
+    }
+    if (T == 0.f) {  // greedy: lowest index of the maximum
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int i = tid; i < V; i += kSampleThreads) argBetter(bv, bi, l[i], i);
+        const float mv = blockReduce1024(bv, red, [](float x, float y) { return fmaxf(x, y); });
+        if (tid == 0) sIdx[0] = 0x7fffffff;
+        __syncthreads();
+        if (bv == mv) atomicMin(&sIdx[0], bi);
+        __syncthreads();
+        if (tid == 0) a.ids[b] = sIdx[0];
+        return;
+    }
+    const float invT = 1.0f / T;
+    float mx = -INFINITY;
+    for (int i = tid; i < V; i += kSampleThreads) mx = fmaxf(mx, l[i] * invT);
+    const float m = blockReduce1024(mx, red, [](float x, float y) { return fmaxf(x, y); });
+    float z = 0.f;
+    for (int i = tid; i < V; i += kSampleThreads) z += expf(l[i] * invT - m);
+    const float Z = blockReduce1024(z, red, [](float x, float y) { return x + y; });
+    const float invZ = 1.0f / Z;
+    int result;
+    if (P <= 0.f || P >= 1.f) {
+        // multinomial in index order: thread t owns the contiguous chunk [t C, (t + 1) C)
+        const int C = (V + kSampleThreads - 1) / kSampleThreads, i0 = tid * C, i1 = min(i0 + C, V);
+        float s = 0.f;
+        for (int i = i0; i < i1; i++) s += expf(l[i] * invT - m) * invZ;
+        // exclusive prefix over threads: per wave, then over the 16 wave totals
+        float inc = s;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const float y = __shfl_up(inc, off);
+            if ((tid & 63) >= off) inc += y;
+        }
+        __syncthreads();
+        if ((tid & 63) == 63) red[tid >> 6] = inc;
+        if (tid == 0) sIdx[0] = V - 1;
+        __syncthreads();
+        float base = inc - s;
+        for (int w = 0; w < (tid >> 6); w++) base += red[w];
+        if (coin >= base && coin < base + s) {  // the draw falls in this chunk
+            float cdf = base;
+            int pick = i1 - 1;
+            for (int i = i0; i < i1; i++) {
+                cdf += expf(l[i] * invT - m) * invZ;
+                if (coin < cdf) {
+                    pick = i;
+                    break;
+                }
+            }
+            atomicMin(&sIdx[0], pick);
+        }
+        __syncthreads();
+        result = sIdx[0];
+    } else {
+        const float cutoff = (1.0f - P) / (float)(V - 1);
+        sampleRadix(l, V, invT, m, invZ, cutoff, 0u, P, hist, sKey, sMass);  // the nucleus cut
+        const uint32_t cutKey = sKey[0];
+        const float nucleus = sMass[0];
+        __syncthreads();
+        sampleRadix(l, V, invT, m, invZ, cutoff, cutKey, coin * nucleus, hist, sKey, sMass);  // the draw
+        const uint32_t key = sKey[0];
+        if (tid == 0) sIdx[0] = 0x7fffffff;
+        __syncthreads();
+        for (int i = tid; i < V; i += kSampleThreads)
+            if (orderKey(l[i] * invT) == key) atomicMin(&sIdx[0], i);
+        __syncthreads();
+        result = sIdx[0] == 0x7fffffff ? 0 : sIdx[0];
+    }
+    if (tid == 0) a.ids[b] = result;
+}
+
+void launchSample(const SampleArgs &a, int B, hipStream_t s) {
+    hipLaunchKernelGGL(sampleKernel, dim3(B), dim3(kSampleThreads), 0, s, a);
 }
 
 // In-place Q80 round trip of f32 values (32-element blocks, rintf like every Q80 producer here).

@@ -170,7 +170,7 @@ std::vector<float> gemmQ40(const std::vector<uint8_t> &blocks, int rows, int n, 
                            const std::vector<float> &residual, const std::vector<float> &normW, float eps, int M) {
     DL_CHECK(M >= 1 && M <= 64, "gemm tokens must be 1..64");
     DL_CHECK(in.size() == (size_t)M * n, "gemm input size");
-    DL_CHECK(hipk::gemmSupported(n), "gemm input width must be a multiple of 128");
+    DL_CHECK(hipk::gemmSupported(n), "gemm input width must be a multiple of 32");
     checkRows(residual, (size_t)M * n, "residual");
     checkRows(normW, (size_t)n, "norm weights");
     Scratch sc;
@@ -254,24 +254,17 @@ std::vector<float> qkvRope(const std::vector<uint8_t> &blocks, int q0, int kv0, 
     a.kvBf16 = kvBf16 ? 1 : 0;
     hipk::launchGemv(a, B, hipk::PRO_RESNORM, hipk::EPI_QKV, true, sc.s);
     sc.sync();
-    // row `pos[b]` of slot b; bf16 V is stored transposed ([slot][kv0][seqLen], see launchAttention)
-    auto row = [&](void *cache, int b, bool transposed) {
+    auto row = [&](void *cache, int b) {
         std::vector<float> r(kv0);
+        const size_t off = ((size_t)b * seqLen + pos[b]) * kv0;
         if (kvBf16) {
-            std::vector<uint16_t> h(kv0);
-            if (transposed) {
-                const std::vector<uint16_t> all =
-                    sc.download(static_cast<uint16_t *>(cache) + (size_t)b * kv0 * seqLen, (size_t)kv0 * seqLen);
-                for (int i = 0; i < kv0; i++) h[i] = all[(size_t)i * seqLen + pos[b]];
-            } else {
-                h = sc.download(static_cast<uint16_t *>(cache) + ((size_t)b * seqLen + pos[b]) * kv0, kv0);
-            }
+            const std::vector<uint16_t> h = sc.download(static_cast<uint16_t *>(cache) + off, kv0);
             for (int i = 0; i < kv0; i++) {
                 const uint32_t u = (uint32_t)h[i] << 16;
                 std::memcpy(&r[i], &u, 4);
             }
         } else {
-            r = sc.download(static_cast<float *>(cache) + ((size_t)b * seqLen + pos[b]) * kv0, kv0);
+            r = sc.download(static_cast<float *>(cache) + off, kv0);
         }
         return r;
     };
@@ -279,11 +272,11 @@ std::vector<float> qkvRope(const std::vector<uint8_t> &blocks, int q0, int kv0, 
     if (vOut) vOut->clear();
     for (int b = 0; b < B; b++) {
         if (kOut) {
-            const std::vector<float> r = row(kc, b, false);
+            const std::vector<float> r = row(kc, b);
             kOut->insert(kOut->end(), r.begin(), r.end());
         }
         if (vOut) {
-            const std::vector<float> r = row(vc, b, true);
+            const std::vector<float> r = row(vc, b);
             vOut->insert(vOut->end(), r.begin(), r.end());
         }
     }
@@ -302,28 +295,21 @@ std::vector<float> attention(const std::vector<float> &q, const std::vector<floa
     for (int b = 0; b < B; b++)
         DL_CHECK(pos[b] >= 0 && pos[b] < seqLen && slot[b] >= 0 && slot[b] < nSlots, "attention row out of range");
     Scratch sc;
-    // caches come in [slot][seqLen][kv0]; bf16 V goes to the device transposed ([slot][kv0][seqLen])
-    auto cache = [&](const std::vector<float> &x, bool transpose) -> void * {
+    auto cache = [&](const std::vector<float> &x) -> void * {
         if (!kvBf16) return sc.upload(x);
         std::vector<uint16_t> h(x.size());
         for (size_t i = 0; i < x.size(); i++) {  // round to nearest even, as the QKV epilogue stores
             uint32_t u;
             std::memcpy(&u, &x[i], 4);
-            const uint16_t hv = (uint16_t)((u + 0x7FFF + ((u >> 16) & 1)) >> 16);
-            if (!transpose) {
-                h[i] = hv;
-            } else {
-                const size_t e = i % kv0, p = (i / kv0) % seqLen, sl = i / ((size_t)kv0 * seqLen);
-                h[(sl * kv0 + e) * seqLen + p] = hv;
-            }
+            h[i] = (uint16_t)((u + 0x7FFF + ((u >> 16) & 1)) >> 16);
         }
         return sc.upload(h);
     };
     hipk::AttnArgs a;
     a.q = sc.upload(q);
     a.ldq = q0;
-    a.kcache = cache(k, false);
-    a.vcache = cache(v, true);
+    a.kcache = cache(k);
+    a.vcache = cache(v);
     a.pos = sc.upload(pos);
     a.slot = sc.upload(slot);
     a.nHeads0 = nHeads0;
@@ -355,6 +341,20 @@ std::vector<int> argmax(const std::vector<float> &logits, int B, int vocab) {
     g.partI = sc.alloc<int>((size_t)B * 64);
     g.counters = sc.alloc<int>(B);
     hipk::launchArgmax(g, B, sc.s);
+    sc.sync();
+    return sc.download(g.ids, B);
+}
+
+std::vector<int> sample(const std::vector<float> &logits, int B, int vocab, const std::vector<float> &specs) {
+    DL_CHECK(B >= 1 && vocab >= 2 && logits.size() == (size_t)B * vocab && specs.size() == (size_t)B * 4,
+             "sample sizes");
+    Scratch sc;
+    hipk::SampleArgs g;
+    g.logits = sc.upload(logits);
+    g.vocab = vocab;
+    g.spec = reinterpret_cast<const float4 *>(sc.upload(specs));
+    g.ids = sc.alloc<int>(B);
+    hipk::launchSample(g, B, sc.s);
     sc.sync();
     return sc.download(g.ids, B);
 }

@@ -46,6 +46,8 @@ std::vector<float> attention(const std::vector<float> &q, const std::vector<floa
 
 // Parallel argmax over [B][vocab] (ties -> lowest index).
 std::vector<int> argmax(const std::vector<float> &logits, int B, int vocab);
+// device sampler (launchSample): spec rows (temperature, topp, coin, -)
+std::vector<int> sample(const std::vector<float> &logits, int B, int vocab, const std::vector<float> &specs);
 
 // Embedding row gather: table [vocab][dim] -> [B][dim].
 std::vector<float> embedding(const std::vector<float> &table, int vocab, int dim, const std::vector<int> &tokens);

@@ -121,6 +121,20 @@ std::vector<int> runArgmax(Backend &b, const std::vector<int> &tokens, const std
     return out;
 }
 
+// Per-row draws: specs from (temperature, topp, coin) lists.
+std::vector<int> runSample(Backend &b, const std::vector<int> &tokens, const std::vector<int> &positions,
+                           const std::vector<int> &slots, const std::vector<float> &temps,
+                           const std::vector<float> &topps, const std::vector<float> &coins) {
+    const size_t n = tokens.size();
+    DL_CHECK(temps.size() == n && topps.size() == n && coins.size() == n, "one (temperature, topp, coin) per row");
+    std::vector<SampleSpec> specs(n);
+    for (size_t i = 0; i < n; i++) specs[i] = SampleSpec{temps[i], topps[i], coins[i], 0.f};
+    std::vector<int> out(n);
+    py::gil_scoped_release rel;
+    b.forwardSample((int)n, tokens.data(), positions.data(), slots.data(), specs.data(), out.data());
+    return out;
+}
+
 // Device communicator owned from Python (xGMI one-shot collectives); shared with engines.
 struct PyComm {
     std::shared_ptr<DeviceComm> comm;
@@ -223,6 +237,16 @@ void bindOps(py::module_ &m) {
           },
           py::arg("q"), py::arg("k"), py::arg("v"), py::arg("n_slots"), py::arg("seq_len"), py::arg("n_heads0"),
           py::arg("kv_mul"), py::arg("head_size"), py::arg("pos"), py::arg("slot"), py::arg("kv_bf16") = true);
+    o.def("sample",
+          [](py::object logits, int B, py::object specs) {
+              const std::vector<float> l = vec<float>(logits), sp = vec<float>(specs);
+              std::vector<int> ids;
+              {
+                  py::gil_scoped_release rel;
+                  ids = ops::sample(l, B, (int)(l.size() / B), sp);
+              }
+              return ids;
+          });
     o.def("argmax",
           [](py::object logits, int B) {
               const std::vector<float> l = vec<float>(logits);
@@ -284,6 +308,11 @@ PYBIND11_MODULE(_C, m) {
 
     // CPU reference primitives (csrc/cpu/cpu_ops.h) for the reference-golden tests
     py::module_ co = m.def_submodule("cpu_ops", "CPU reference primitives (csrc/cpu/cpu_ops.h)");
+    co.def("sample_host", [](py::array_t<float, py::array::c_style | py::array::forcecast> logits, float temp, float topp,
+                             float coin) {
+        std::vector<float> l(logits.data(), logits.data() + logits.size());
+        return sampleHost(l.data(), (int)l.size(), SampleSpec{temp, topp, coin, 0.f});
+    });
     co.def("inv_rms", [](py::array_t<float, py::array::c_style | py::array::forcecast> x, float eps) {
         return cpu::invRms(x.data(), (u32)x.size(), eps);
     });
@@ -446,6 +475,8 @@ PYBIND11_MODULE(_C, m) {
         .def_property_readonly("name", &Backend::name)
         .def("forward", [](Backend &b, std::vector<int> t, std::vector<int> p, std::vector<int> s) { return runForward(b, t, p, s); },
              py::arg("tokens"), py::arg("positions"), py::arg("slots"))
+        .def("forward_sample", &runSample, py::arg("tokens"), py::arg("positions"), py::arg("slots"),
+             py::arg("temperatures"), py::arg("topps"), py::arg("coins"))
         .def("forward_argmax", [](Backend &b, std::vector<int> t, std::vector<int> p, std::vector<int> s) { return runArgmax(b, t, p, s); },
              py::arg("tokens"), py::arg("positions"), py::arg("slots"))
         .def("last_stats", [](const Backend &b) {
@@ -483,7 +514,7 @@ PYBIND11_MODULE(_C, m) {
           py::arg("passes") = 0, py::arg("copies") = 8, py::arg("iters") = 20,
           "bench_gemv_q40 with per-workgroup s_memrealtime stamps: (us, u64[iters*grid*4])");
     m.def("bench_gemm_q40", &benchGemmQ40, py::arg("rows"), py::arg("n"), py::arg("tokens"), py::arg("epi") = 0,
-          py::arg("copies") = 8, py::arg("iters") = 100, py::arg("probe") = 0, py::call_guard<py::gil_scoped_release>());
+          py::arg("copies") = 8, py::arg("iters") = 100, py::call_guard<py::gil_scoped_release>());
     m.def("bench_attention", &benchAttention, py::arg("n_heads0"), py::arg("kv_mul"), py::arg("head_size"),
           py::arg("seq_len"), py::arg("pos"), py::arg("batch") = 1, py::arg("copies") = 32, py::arg("iters") = 200,
           py::call_guard<py::gil_scoped_release>());
@@ -645,6 +676,11 @@ PYBIND11_MODULE(_C, m) {
         .def_property_readonly("device_bytes", [](const PyHipEngine &e) { return e.engine->deviceBytes(); })
         .def("forward", [](PyHipEngine &e, std::vector<int> t, std::vector<int> p, std::vector<int> s) { return runForward(*e.engine, t, p, s); },
              py::arg("tokens"), py::arg("positions"), py::arg("slots"))
+        .def("forward_sample",
+             [](PyHipEngine &e, std::vector<int> t, std::vector<int> p, std::vector<int> s, std::vector<float> temps,
+                std::vector<float> topps, std::vector<float> coins) { return runSample(*e.engine, t, p, s, temps, topps, coins); },
+             py::arg("tokens"), py::arg("positions"), py::arg("slots"), py::arg("temperatures"), py::arg("topps"),
+             py::arg("coins"))
         .def("forward_argmax", [](PyHipEngine &e, std::vector<int> t, std::vector<int> p, std::vector<int> s) { return runArgmax(*e.engine, t, p, s); },
              py::arg("tokens"), py::arg("positions"), py::arg("slots"))
         .def("decode_greedy",

@@ -255,6 +255,18 @@ void InferenceSession::forwardArgmax(int n, const int *tokens, const int *positi
     recordMetrics("forward_argmax", n, t.elapsedMs());
 }
 
+void InferenceSession::forwardSample(int n, const int *tokens, const int *positions, const int *slots,
+                                     const SampleSpec *specs, int *out) {
+    TraceRange tr("dllama.forward_sample");
+    Timer t;
+    sendControl(Cmd::FORWARD_SAMPLE, n, tokens, positions, slots);
+    if (!workers_.empty()) {  // the specs follow the row arrays (every rank runs the same draw graph)
+        for (auto &s : workers_) s.sendAll(specs, n * sizeof(SampleSpec));
+    }
+    backend_->forwardSample(n, tokens, positions, slots, specs, out);
+    recordMetrics("forward_sample", n, t.elapsedMs());
+}
+
 void InferenceSession::recordMetrics(const char *kind, int n, double ms) {
     MetricsSink &m = MetricsSink::global();
     if (!m.enabled()) return;
@@ -392,6 +404,7 @@ void runWorker(const AppArgs &args) {
             if (logLevel() >= 1) std::printf("💿 Weights loaded\n");
             std::fflush(stdout);
             std::vector<int> buf, ids;
+            std::vector<SampleSpec> specs;
             while (true) {
                 int hdr[2];
                 root.recvAll(hdr, sizeof(hdr));
@@ -408,6 +421,11 @@ void runWorker(const AppArgs &args) {
                 } else if (cmd == Cmd::FORWARD_ARGMAX) {
                     ids.resize(n);
                     backend->forwardArgmax(n, &buf[0], &buf[n], &buf[2 * n], ids.data());
+                } else if (cmd == Cmd::FORWARD_SAMPLE) {
+                    ids.resize(n);
+                    specs.resize(n);
+                    root.recvAll(specs.data(), n * sizeof(SampleSpec));
+                    backend->forwardSample(n, &buf[0], &buf[n], &buf[2 * n], specs.data(), ids.data());
                 }
             }
         } catch (const NetError &e) {

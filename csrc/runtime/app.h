@@ -67,6 +67,9 @@ class InferenceSession {
     // logits: [n][vocab]
     void forward(int n, const int *tokens, const int *positions, const int *slots, float *logits);
     void forwardArgmax(int n, const int *tokens, const int *positions, const int *slots, int *out);
+    // per-row sampling on the backend (device sampler on GPUs: only token ids leave the device)
+    void forwardSample(int n, const int *tokens, const int *positions, const int *slots, const SampleSpec *specs,
+                       int *out);
     ForwardStats lastStats();
     void finish();  // stop workers (they return to listening)
     // GPU only: one eager forward of these rows with a per-kernel-class device-time table.

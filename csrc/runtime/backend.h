@@ -40,6 +40,19 @@ struct ForwardStats {
     u64 recvBytes = 0;
 };
 
+// Per-row sampling request (reference Sampler::sample, tokenizer.cpp:416-502): temperature 0 =
+// greedy, < 0 = row not sampled (prefill rows), otherwise softmax(logits / temperature) then a
+// multinomial draw (topp <= 0 or >= 1) or nucleus (top-p) draw with the given coin in [0, 1).
+struct SampleSpec {
+    float temperature = 0.f;
+    float topp = 0.f;
+    float coin = 0.f;
+    float pad = 0.f;
+};
+
+// Host implementation of one row's draw (the CPU path and the reference for the device sampler).
+int sampleHost(float *logits, int vocab, const SampleSpec &s);
+
 class Backend {
   public:
     virtual ~Backend() = default;
@@ -49,6 +62,10 @@ class Backend {
     virtual void forward(int n, const int *tokens, const int *positions, const int *slots, float *logits) = 0;
     // Greedy decode helper: out[i] = argmax over the full vocabulary (every rank gets it).
     virtual void forwardArgmax(int n, const int *tokens, const int *positions, const int *slots, int *out) = 0;
+    // Forward + per-row sampling: out[i] = the sampled token (-1 for rows with temperature < 0).
+    // Default: full logits to the root, host draw, ids shared through forwardArgmax's channel.
+    virtual void forwardSample(int n, const int *tokens, const int *positions, const int *slots,
+                               const SampleSpec *specs, int *out);
     virtual ForwardStats lastStats() const { return stats_; }
     virtual std::string name() const = 0;
 

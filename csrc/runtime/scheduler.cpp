@@ -193,19 +193,29 @@ bool Scheduler::step() {
     const int n = (int)tokens.size();
     if (n == 0) return false;
 
-    // 3) forward: device argmax when every sampled row is greedy, full logits otherwise
+    // 3) forward: device argmax when every sampled row is greedy; otherwise per-row draws on the
+    //    backend (the device sampler on GPUs) with each request's own temperature / top-p and the
+    //    coin its own seeded generator yields, so only token ids come back
     bool allGreedy = true;
     for (auto &p : picks)
         if (p.sample && p.r->params.temperature != 0.0f) allGreedy = false;
     Timer t;
-    std::vector<int> ids;
+    std::vector<int> ids(n);
     if (allGreedy) {
-        ids.resize(n);
         sess_.forwardArgmax(n, tokens.data(), positions.data(), slots.data(), ids.data());
     } else {
-        logits_.resize((size_t)n * vocab);
-        sess_.forward(n, tokens.data(), positions.data(), slots.data(), logits_.data());
+        std::vector<SampleSpec> specs(n);
+        for (auto &sp : specs) sp.temperature = -1.f;  // rows that are not sampled
+        for (auto &p : picks) {
+            if (!p.sample) continue;
+            SampleSpec &sp = specs[p.row];
+            sp.temperature = p.r->params.temperature;
+            sp.topp = p.r->params.topp;
+            sp.coin = p.r->sampler->drawCoin();
+        }
+        sess_.forwardSample(n, tokens.data(), positions.data(), slots.data(), specs.data(), ids.data());
     }
+    (void)vocab;
     const double ms = t.elapsedMs();
 
     // 4) sample, detect stops, stream deltas
@@ -214,7 +224,7 @@ bool Scheduler::step() {
         GenRequest *r = p.r;
         r->prefilled += p.prefill;
         if (!p.sample) continue;
-        const int token = allGreedy ? ids[p.row] : r->sampler->sample(&logits_[(size_t)p.row * vocab]);
+        const int token = ids[p.row];
         r->generated.push_back(token);
         r->completionTokens = (int)r->generated.size();
         std::string piece, delta;

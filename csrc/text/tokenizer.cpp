@@ -347,11 +347,17 @@ Sampler::Sampler(int vocabSize, float temperature, float topp, u64 seed)
     probIndex_.reserve(vocabSize);
 }
 
+float Sampler::randomF32Impl() { return randomF32(&rng_); }
+
 int Sampler::sample(float *logits) {
+    if (temperature_ == 0.0f) return argmax(logits, vocab_);
+    return sampleWithCoin(logits, randomF32(&rng_));
+}
+
+int Sampler::sampleWithCoin(float *logits, float coin) {
     if (temperature_ == 0.0f) return argmax(logits, vocab_);
     for (int i = 0; i < vocab_; i++) logits[i] /= temperature_;
     softmaxInPlace(logits, vocab_);
-    const float coin = randomF32(&rng_);
     if (topp_ <= 0.f || topp_ >= 1.f) {
         float cdf = 0.f;
         for (int i = 0; i < vocab_; i++) {

@@ -76,12 +76,19 @@ class Sampler {
     Sampler(int vocabSize, float temperature, float topp, u64 seed);
     // NOTE: modifies `logits` in place when temperature > 0 (as the reference does).
     int sample(float *logits);
+    // The random draw sample() makes (advances the generator identically); 0 when greedy. A
+    // device sampler given this coin reproduces sample() (Backend::forwardSample).
+    float drawCoin() { return temperature_ == 0.0f ? 0.0f : randomF32Impl(); }
+    // sample() with an explicit coin (logits modified in place when temperature > 0)
+    int sampleWithCoin(float *logits, float coin);
+    float topp() const { return topp_; }
     void setTemp(float t) { temperature_ = t; }
     void setTopp(float p) { topp_ = p; }
     void setSeed(u64 s) { rng_ = s; }
     float temperature() const { return temperature_; }
 
   private:
+    float randomF32Impl();
     int vocab_;
     float temperature_;
     float topp_;

@@ -80,6 +80,15 @@ def attention(q, k_cache, v_cache, n_heads0: int, kv_mul: int, head_size: int, p
                                                    kv_bf16))
 
 
+def sample(logits, temperatures, topps, coins) -> list:
+    """Device sampler: per row softmax(logits / T) then multinomial (top-p >= 1) or nucleus draw."""
+    x = _np(logits)
+    B = x.shape[0] if x.ndim == 2 else 1
+    spec = np.stack([np.asarray(temperatures, np.float32), np.asarray(topps, np.float32),
+                     np.asarray(coins, np.float32), np.zeros(B, np.float32)], axis=1)
+    return native().ops.sample(x, B, spec)
+
+
 def argmax(logits) -> list:
     x = _np(logits)
     return native().ops.argmax(x, x.shape[0] if x.ndim == 2 else 1)

@@ -20,11 +20,11 @@ shapes = [
     ("w13  tp8", 3584, 4096, EPI_ACT_F16),
     ("w2   tp8", 4096, 1792, EPI_STORE),
 ]
-tokens = [int(x) for x in sys.argv[1:]] or [8, 16, 32]
+tokens = [int(x) for x in sys.argv[1:]] or [8, 16, 32, 64]
 for name, rows, n, epi in shapes:
     mb = rows * n * 0.5625 / 1e6
     line = f"{name} {rows:6d}x{n:5d} {mb:7.1f} MB |"
     for m in tokens:
-        us = C.bench_gemm_q40(rows, n, m, epi, 8 if mb < 100 else 2, 50, int(os.environ.get("PROBE", "0")))
+        us = C.bench_gemm_q40(rows, n, m, epi, 8 if mb < 100 else 2, 50)
         line += f" M={m}: {us:7.2f} us {mb / us:5.2f} TB/s |"
     print(line, flush=True)

@@ -161,3 +161,12 @@ def test_stream_client_disconnect_frees_slot(server):
     assert h["cancelled"] == h0["cancelled"] + 1, h
     assert h["active"] == 0 and h["completed"] == h0["completed"], h
     assert _chat(server, "still serving", max_tokens=3)["choices"][0]["finish_reason"] in ("length", "stop")
+
+
+def test_sampled_requests_reproducible_per_seed(server):
+    """temperature > 0: the scheduler draws each row with the request's own seeded coin on the
+    backend (device sampler on GPUs); the same seed gives the same text, another seed may not."""
+    a = _chat(server, "sample me", max_tokens=10, temperature=0.9, top_p=0.9, seed=42)
+    b = _chat(server, "sample me", max_tokens=10, temperature=0.9, top_p=0.9, seed=42)
+    assert a["choices"][0]["message"]["content"] == b["choices"][0]["message"]["content"]
+    assert a["usage"]["completion_tokens"] >= 1

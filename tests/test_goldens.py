@@ -68,3 +68,30 @@ def test_matmul_q80_q40_golden(C, co):
     y = co.matmul_q40_q80(blocks, d, n, x)
     ref = x.astype(np.float64) @ w.astype(np.float64).T
     assert np.all(np.abs(y - ref) <= np.abs(ref) * 0.035)
+
+
+def test_host_sampler_coin_semantics(C, co):
+    """sampleHost with an explicit coin follows the reference's Sampler::sample: temperature 0 ->
+    argmax, top-p >= 1 -> multinomial in index order, else the nucleus in descending order."""
+    rng = np.random.default_rng(3)
+    logits = rng.standard_normal(1000).astype(np.float32) * 3
+    assert co.sample_host(logits, 0.0, 0.9, 0.5) == int(np.argmax(logits))
+    p = np.exp(logits / 0.7 - (logits / 0.7).max())
+    p /= p.sum()
+    cdf = np.cumsum(p)
+    for coin in (0.0, 0.3, 0.77, 0.999):
+        assert co.sample_host(logits, 0.7, 1.0, coin) == int(np.searchsorted(cdf, coin, side="right"))
+    order = np.argsort(-p, kind="stable")
+    cut = np.searchsorted(np.cumsum(p[order]), 0.5, side="right")
+    nucleus = order[:cut + 1]
+    for coin in (0.0, 0.5, 0.99):
+        assert co.sample_host(logits, 0.7, 0.5, coin) in set(nucleus.tolist())
+
+
+def test_cpu_backend_forward_sample(C, assets):
+    b = C.cpu_backend(assets["q40"], "q80", 2, max_batch=8, n_slots=1)
+    toks, pos = [1, 2, 3], [0, 1, 2]
+    ref = b.forward(toks, pos, [0, 0, 0])
+    got = b.forward_sample(toks, pos, [0, 0, 0], [0.0, -1.0, 0.8], [0.9, 0.9, 0.9], [0.1, 0.2, 0.3])
+    assert got[0] == int(np.argmax(ref[0])) and got[1] == -1
+    assert got[2] == C.cpu_ops.sample_host(ref[2], 0.8, 0.9, 0.3)

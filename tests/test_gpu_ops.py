@@ -128,13 +128,7 @@ def test_attention_decode(ops, kv_bf16, n_heads0, kv_mul, hs, seq, pos):
         k, v = k.bfloat16().float(), v.bfloat16().float()
     out = ops.attention(q, k, v, n_heads0, kv_mul, hs, pos, slots, kv_bf16)
     want = ops.ref_attention(q, k, v, n_heads0, kv_mul, hs, pos, slots)
-    if not kv_bf16:
-        assert rel(out, want) < 1e-4  # f32 cache: the VALU kernel, f32 throughout
-        return
-    # bf16 cache: the MFMA kernel multiplies bf16 Q (scaled) x K and bf16 P x V with f32 accumulation
-    assert rel(out, want) < 6e-3
-    qb = (q.view(B, n_heads0, hs) / hs ** 0.5).bfloat16().float().reshape(B, -1) * hs ** 0.5
-    assert rel(out, ops.ref_attention(qb, k, v, n_heads0, kv_mul, hs, pos, slots)) < 4e-3
+    assert rel(out, want) < 1e-4  # f32 arithmetic on the (bf16-rounded) cache values
 
 
 @pytest.mark.parametrize("n_heads0,kv_mul,hs,seq,pos", [
@@ -142,8 +136,8 @@ def test_attention_decode(ops, kv_bf16, n_heads0, kv_mul, hs, seq, pos):
     (16, 16, 128, 1024, [1000]),                 # 405B-like GQA group of 16 heads
     (8, 2, 64, 2048, [1900, 64]),
 ])
-def test_attention_mfma_edges(ops, n_heads0, kv_mul, hs, seq, pos):
-    """MFMA attention: query padding (kvMul < 16), 32-key tile tails, chunk and split edges."""
+def test_attention_split_edges(ops, n_heads0, kv_mul, hs, seq, pos):
+    """Decode attention at long contexts and chunk / split edges, several rows, GQA 16, hs 64."""
     kv0 = n_heads0 // kv_mul * hs
     g = torch.Generator().manual_seed(13)
     B = len(pos)
@@ -153,7 +147,7 @@ def test_attention_mfma_edges(ops, n_heads0, kv_mul, hs, seq, pos):
     q = torch.randn(B, n_heads0 * hs, generator=g) * 2
     out = ops.attention(q, k, v, n_heads0, kv_mul, hs, pos, slots, True)
     want = ops.ref_attention(q, k, v, n_heads0, kv_mul, hs, pos, slots)
-    assert rel(out, want) < 6e-3
+    assert rel(out, want) < 1e-4
 
 
 def test_argmax_ties_lowest_index(ops):
@@ -185,3 +179,66 @@ def test_gemv_matmul_q80_q40_golden(ops):
     assert bool(((out.double() - ref).abs() <= ref.abs() * 0.035).all())
     cpu = torch.from_numpy(dl.native().cpu_ops.matmul_q40_q80(np.asarray(blocks), d, n, x.numpy()))
     assert rel(out, cpu) < 1e-5
+
+
+def _draw_ok(logits, temp, topp, coin, tok, tol=2e-4):
+    """True when `tok` is a valid draw for `coin` under exact (f64) arithmetic, up to `tol` of
+    cumulative mass: float32 cumulative sums (host sequential, device chunked) differ by ~1e-5,
+    so near a token boundary either neighbour is a correct answer."""
+    import numpy as np
+    x = logits.astype(np.float64)
+    if temp == 0.0:
+        return tok == int(np.argmax(x))
+    p = np.exp(x / temp - (x / temp).max())
+    p /= p.sum()
+    if topp <= 0.0 or topp >= 1.0:
+        cdf = np.cumsum(p)
+        lo = cdf[tok - 1] if tok > 0 else 0.0
+        return lo - tol <= coin <= cdf[tok] + tol
+    cutoff = (1.0 - topp) / (len(p) - 1)
+    cand = np.nonzero(p >= cutoff * (1 - 1e-5))[0]
+    order = cand[np.argsort(-p[cand], kind="stable")]
+    cum = np.cumsum(p[order])
+    last = min(int(np.searchsorted(cum, topp, side="right")), len(order) - 1)
+    r = coin * cum[last]
+    where = np.nonzero(order == tok)[0]
+    if len(where) == 0 or where[0] > last + 1:
+        return False
+    i = where[0]
+    lo = cum[i - 1] if i > 0 else 0.0
+    return lo - tol <= r <= cum[i] + tol
+
+
+@pytest.mark.parametrize("vocab,scale", [(128256, 1.0), (128256, 6.0), (32000, 3.0), (517, 2.0)])
+def test_device_sampler_matches_host(ops, vocab, scale):
+    """Device sampler (multinomial and top-p radix search) vs the host Sampler given the same coin,
+    on flat (random-model) and peaked distributions: every draw valid under exact arithmetic, and
+    (float32 cumulative sums aside) the same tokens as the host."""
+    import distributed_llama_multiusers_amd as dl
+    co = dl.native().cpu_ops
+    g = torch.Generator().manual_seed(14)
+    rows = [(temp, topp) for temp in (0.0, 0.6, 1.0, 1.3) for topp in (0.0, 0.5, 0.9, 0.95, 1.0)]
+    B = len(rows)
+    logits = torch.randn(B, vocab, generator=g) * scale
+    coins = torch.rand(B, generator=g).tolist()
+    got = ops.sample(logits, [r[0] for r in rows], [r[1] for r in rows], coins)
+    want = [co.sample_host(logits[i].numpy(), rows[i][0], rows[i][1], coins[i]) for i in range(B)]
+    for i in range(B):
+        assert _draw_ok(logits[i].numpy(), rows[i][0], rows[i][1], coins[i], got[i]), (i, rows[i], got[i], want[i])
+        assert _draw_ok(logits[i].numpy(), rows[i][0], rows[i][1], coins[i], want[i]), (i, rows[i], want[i])
+    assert sum(a == b for a, b in zip(got, want)) >= 0.8 * B, (got, want)
+    assert ops.sample(logits[:1], [-1.0], [0.9], [0.5]) == [-1]
+
+
+def test_engine_forward_sample_matches_host(C, assets):
+    """HipEngine SAMPLE graph: per-row draws on the device from the engine's own logits."""
+    import numpy as np
+    eng = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=8)
+    toks, pos = [5, 6, 7, 8], [0, 1, 2, 3]
+    logits = eng.forward(toks, pos, [0] * 4)
+    eng2 = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=8)
+    temps, topps, coins = [0.0, 0.7, 1.0, -1.0], [0.9, 0.9, 1.0, 0.9], [0.2, 0.4, 0.6, 0.8]
+    got = eng2.forward_sample(toks, pos, [0] * 4, temps, topps, coins)
+    co = C.cpu_ops
+    want = [co.sample_host(np.asarray(logits[i]), temps[i], topps[i], coins[i]) for i in range(4)]
+    assert got == want, (got, want)
