@@ -1,5 +1,9 @@
 #include "model_file.h"
 
+#include <atomic>
+#include <cerrno>
+#include <thread>
+
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -204,6 +208,63 @@ MappedFile::MappedFile(const std::string &path) {
 MappedFile::~MappedFile() {
     if (data_) ::munmap((void *)data_, size_);
     if (fd_ >= 0) ::close(fd_);
+}
+
+ParallelReader::ParallelReader(const std::string &path, int threads, u64 piece) : piece_(piece), path_(path) {
+    fd_ = ::open(path.c_str(), O_RDONLY);
+    if (fd_ < 0) throw Error("Cannot open file: " + path);
+    if (threads <= 0) {
+        const unsigned hw = std::thread::hardware_concurrency();
+        threads = (int)std::min<unsigned>(hw ? hw : 4, 16);
+    }
+    threads_ = threads;
+}
+
+ParallelReader::~ParallelReader() {
+    if (fd_ >= 0) ::close(fd_);
+}
+
+void ParallelReader::read(u64 off, u64 len, void *dst) { readMany({{off, len, dst}}); }
+
+void ParallelReader::readMany(const std::vector<Range> &ranges) {
+    struct Part {
+        u64 off, len;
+        u8 *dst;
+    };
+    std::vector<Part> parts;
+    u64 total = 0;
+    for (const Range &r : ranges) {
+        total += r.len;
+        for (u64 o = 0; o < r.len; o += piece_)
+            parts.push_back({r.off + o, std::min(piece_, r.len - o), (u8 *)r.dst + o});
+    }
+    std::atomic<size_t> next{0};
+    std::atomic<bool> failed{false};
+    auto work = [&] {
+        for (size_t i = next++; i < parts.size() && !failed; i = next++) {
+            const Part &p = parts[i];
+            u64 done = 0;
+            while (done < p.len) {
+                const ssize_t r = ::pread(fd_, p.dst + done, p.len - done, (off_t)(p.off + done));
+                if (r < 0 && errno == EINTR) continue;
+                if (r <= 0) {
+                    failed = true;
+                    break;
+                }
+                done += (u64)r;
+            }
+        }
+    };
+    const int nt = (int)std::min<size_t>((size_t)threads_, parts.size());
+    if (nt <= 1) {
+        work();
+    } else {
+        std::vector<std::thread> pool;
+        for (int t = 0; t < nt; t++) pool.emplace_back(work);
+        for (auto &t : pool) t.join();
+    }
+    if (failed) throw Error("short read from " + path_);
+    bytes_ += total;
 }
 
 ModelFile::ModelFile(const std::string &path, u32 maxSeqLen) : path_(path) {

@@ -86,6 +86,35 @@ class MappedFile {
     int fd_ = -1;
 };
 
+// Positional reads of a file split over a pool of threads (pread, no page-cache mapping faults
+// on the load path): large weight slices are read in `piece`-byte parts concurrently, which is
+// what lets a multi-GB shard leave NVMe / the page cache at several GB/s (the mapping is
+// single-threaded per fault). Thread-safe for concurrent read() calls on disjoint outputs.
+class ParallelReader {
+  public:
+    explicit ParallelReader(const std::string &path, int threads = 0, u64 piece = 8ull << 20);
+    ~ParallelReader();
+    ParallelReader(const ParallelReader &) = delete;
+    ParallelReader &operator=(const ParallelReader &) = delete;
+    // [off, off + len) of the file into dst; throws on a short read.
+    void read(u64 off, u64 len, void *dst);
+    // Several ranges at once (one parallel batch): ranges[i] = {file offset, length, dst}.
+    struct Range {
+        u64 off, len;
+        void *dst;
+    };
+    void readMany(const std::vector<Range> &ranges);
+    u64 bytesRead() const { return bytes_; }
+    int threads() const { return threads_; }
+
+  private:
+    int fd_ = -1;
+    int threads_ = 1;
+    u64 piece_;
+    u64 bytes_ = 0;
+    std::string path_;
+};
+
 // A model opened for reading: header + table + mapping.
 class ModelFile {
   public:

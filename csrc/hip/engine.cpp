@@ -82,6 +82,8 @@ class HipEngineImpl : public HipEngine {
                        (size_t)2 * cfg.maxBatch <= (size_t)tpArg_.stride;
             tpVec_.q80 = syncQ80_ ? 1 : 0;
         }
+        checkFits();
+        Timer timer;
         allocBuffers();
         if (cfg.synthetic)
             loadSynthetic();
@@ -89,6 +91,33 @@ class HipEngineImpl : public HipEngine {
             loadFromFile();
         uploadRope();
         DL_HIP(hipStreamSynchronize(stream_));
+        load_.ms = timer.elapsedMs();
+        load_.deviceBytes = deviceBytes_;
+    }
+
+    LoadStats loadStats() const override { return load_; }
+
+    // Refuse a configuration whose weights + KV cache cannot be resident, with the numbers, before
+    // allocating anything (KV is preallocated as nSlots x seqLen per layer).
+    void checkFits() {
+        size_t freeB = 0, totalB = 0;
+        DL_HIP(hipMemGetInfo(&freeB, &totalB));
+        const ShardPlan &p = plan_;
+        const double GB = 1e9;
+        const size_t kv = (size_t)h_.nLayers * 2 * cfg_.nSlots * h_.seqLen * p.kv0 * (kvBf16_ ? 2 : 4);
+        size_t w = (size_t)h_.nLayers * (matStageBytes(p.q0 + 2 * p.kv0, h_.dim) + matStageBytes(h_.dim, p.q0) +
+                                         matStageBytes(2 * p.hidden0, h_.dim) + matStageBytes(h_.dim, p.hidden0));
+        w += matStageBytes(p.vocab0, h_.dim) + (size_t)h_.vocabSize * h_.dim * 4;
+        const size_t act = (size_t)cfg_.maxBatch * h_.vocabSize * 4 * 3 + ((size_t)256 << 20);
+        if (kv + w + act > freeB) {
+            char msg[512];
+            std::snprintf(msg, sizeof(msg), "Model does not fit on GPU %d: weights %.2f GB + KV cache %.2f GB (%u slots x %u "
+                                  "positions x %u layers, %s) + buffers %.2f GB > %.2f GB free of %.2f GB. Lower "
+                                  "--max-seq-len or the number of slots, or add tensor-parallel ranks.",
+                                  dev_, w / GB, kv / GB, cfg_.nSlots, h_.seqLen, h_.nLayers, kvBf16_ ? "bf16" : "f32",
+                                  act / GB, freeB / GB, totalB / GB);
+            throw Error(msg);
+        }
     }
 
     ~HipEngineImpl() override {
@@ -326,110 +355,179 @@ class HipEngineImpl : public HipEngine {
     }
 
     // ---------------------------------------------------------------- weight upload
-    // Append rows of a Q40 (AoS on disk) matrix slice to SoA host buffers.
-    static void repackRowsQ40(const u8 *src, u32 cols, u32 r0, u32 nr, u32 c0, u32 nc, std::vector<u8> &qs,
-                              std::vector<u16> &d) {
-        const u32 nbAll = cols / kQBlock, nb0 = c0 / kQBlock, nb = nc / kQBlock;
-        const size_t q0 = qs.size(), d0 = d.size();
-        qs.resize(q0 + (size_t)nr * nb * 16);
-        d.resize(d0 + (size_t)nr * nb);
-        for (u32 r = 0; r < nr; r++) {
-            const BlockQ40 *row = reinterpret_cast<const BlockQ40 *>(src) + (u64)(r0 + r) * nbAll + nb0;
-            u8 *qo = qs.data() + q0 + (size_t)r * nb * 16;
-            u16 *dd = d.data() + d0 + (size_t)r * nb;
-            for (u32 j = 0; j < nb; j++) {
-                std::memcpy(qo + (size_t)j * 16, row[j].qs, 16);
-                dd[j] = row[j].d;
-            }
-        }
-    }
-
-    void uploadMat(DevMat &m, int rows, int n, const std::vector<u8> &qs, const std::vector<u16> &d,
-                   const std::vector<float> &f) {
-        m.rows = rows;
-        m.n = n;
-        if (q40_) {
-            DL_CHECK(qs.size() == (size_t)rows * n / 2 && d.size() == (size_t)rows * n / 32, "repack size");
-            m.lanes = hipk::gemvLanesPerRow(n, rows, 1, true);
-            const hipk::Q40Tiling t = hipk::q40Tiling(rows, n, m.lanes);
-            std::vector<u8> qt(t.qsBytes);
-            std::vector<uint32_t> dt(t.dBytes / 4);
-            hipk::tileQ40(qs.data(), d.data(), rows, n, m.lanes, qt.data(), dt.data());
-            m.qs = dalloc<uint8_t>(qt.size());
-            m.d = dalloc<uint16_t>(t.dBytes / 2);
-            DL_HIP(hipMemcpy(m.qs, qt.data(), qt.size(), hipMemcpyHostToDevice));
-            DL_HIP(hipMemcpy(m.d, dt.data(), t.dBytes, hipMemcpyHostToDevice));
-        } else {
-            DL_CHECK(f.size() == (size_t)rows * n, "f32 slice size");
-            m.f = dalloc<float>(f.size());
-            DL_HIP(hipMemcpy(m.f, f.data(), f.size() * 4, hipMemcpyHostToDevice));
-        }
-    }
-
-    // Build a device matrix from a list of (tensor, rowStart, nRows) row sources, optionally
-    // interleaving two sources row by row, restricted to input columns [c0, c0+nc).
+    // The file load is a three-stage pipeline per matrix:
+    //   1. parallel pread of exactly this rank's rows / row slices (ParallelReader, 16 threads);
+    //   2. multi-threaded repack of the file's AoS Q40 blocks straight into the GEMV's tiled layout,
+    //      written into one of two pinned staging buffers;
+    //   3. hipMemcpyAsync on a dedicated copy stream (DMA at pinned-memory speed), which runs while
+    //      the host reads and tiles the next matrix; a staging buffer is reused only after the
+    //      event of its previous copy has completed.
+    // (Round 1 repacked into std::vectors and uploaded with synchronous pageable hipMemcpy.)
     struct RowSrc {
         const TensorInfo *t;
         u32 r0, nr;
     };
-    void buildMat(DevMat &m, const std::vector<RowSrc> &srcs, bool interleave, u32 c0, u32 nc) {
-        std::vector<u8> qs;
-        std::vector<u16> d;
-        std::vector<float> f;
-        u32 rows = 0;
-        auto addRows = [&](const RowSrc &s, u32 r, u32 cnt) {
-            const u8 *base = file_->ptr(*s.t);
-            if (q40_) {
-                repackRowsQ40(base, s.t->cols, r, cnt, c0, nc, qs, d);
-            } else {
-                for (u32 rr = r; rr < r + cnt; rr++) {
-                    const float *row = reinterpret_cast<const float *>(base) + (u64)rr * s.t->cols + c0;
-                    f.insert(f.end(), row, row + nc);
-                }
+    struct Loader {
+        std::unique_ptr<ParallelReader> reader;
+        hipStream_t copy = nullptr;
+        u8 *stage[2] = {nullptr, nullptr};
+        hipEvent_t done[2] = {nullptr, nullptr};
+        bool busy[2] = {false, false};
+        size_t stageBytes = 0;
+        int cur = 0;
+        std::vector<u8> raw;
+        std::vector<const u8 *> rowPtr;
+    };
+
+    u8 *stageAcquire(Loader &ld) {
+        ld.cur ^= 1;
+        if (ld.busy[ld.cur]) DL_HIP(hipEventSynchronize(ld.done[ld.cur]));
+        ld.busy[ld.cur] = false;
+        return ld.stage[ld.cur];
+    }
+    void stageCopy(Loader &ld, void *dst, const u8 *src, size_t bytes) {
+        DL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ld.copy));
+    }
+    void stageRelease(Loader &ld) {
+        DL_HIP(hipEventRecord(ld.done[ld.cur], ld.copy));
+        ld.busy[ld.cur] = true;
+    }
+
+    // Read the rows of every source (restricted to columns [c0, c0 + nc)) into ld.raw and point
+    // ld.rowPtr at each output row (w1/w3 interleaved row by row when `interleave`).
+    void readRows(Loader &ld, const std::vector<RowSrc> &srcs, bool interleave, u32 c0, u32 nc) {
+        const u64 esz = q40_ ? 0 : 4;
+        auto rowBytes = [&](u32 cols) { return q40_ ? (u64)cols / kQBlock * kQ40BlockBytes : (u64)cols * esz; };
+        const u64 slice = rowBytes(nc);
+        u64 total = 0;
+        for (const auto &s : srcs) total += (u64)s.nr * slice;
+        if (ld.raw.size() < total) ld.raw.resize(total);
+        std::vector<ParallelReader::Range> ranges;
+        std::vector<std::vector<const u8 *>> perSrc(srcs.size());
+        u64 at = 0;
+        for (size_t i = 0; i < srcs.size(); i++) {
+            const RowSrc &s = srcs[i];
+            const u64 full = rowBytes(s.t->cols), skip = rowBytes(c0);
+            u8 *dst = ld.raw.data() + at;
+            if (c0 == 0 && nc == s.t->cols) {  // whole rows: one contiguous range
+                ranges.push_back({s.t->offset + (u64)s.r0 * full, (u64)s.nr * full, dst});
+            } else {  // column slice (row-split wo / w2 of tensor parallelism): one range per row
+                for (u32 r = 0; r < s.nr; r++)
+                    ranges.push_back({s.t->offset + (u64)(s.r0 + r) * full + skip, slice, dst + (u64)r * slice});
             }
-        };
+            for (u32 r = 0; r < s.nr; r++) perSrc[i].push_back(dst + (u64)r * slice);
+            at += (u64)s.nr * slice;
+        }
+        ld.reader->readMany(ranges);
+        ld.rowPtr.clear();
         if (interleave) {
             DL_CHECK(srcs.size() == 2 && srcs[0].nr == srcs[1].nr, "interleave");
             for (u32 i = 0; i < srcs[0].nr; i++) {
-                addRows(srcs[0], srcs[0].r0 + i, 1);
-                addRows(srcs[1], srcs[1].r0 + i, 1);
+                ld.rowPtr.push_back(perSrc[0][i]);
+                ld.rowPtr.push_back(perSrc[1][i]);
             }
-            rows = 2 * srcs[0].nr;
         } else {
-            for (const auto &s : srcs) {
-                addRows(s, s.r0, s.nr);
-                rows += s.nr;
-            }
+            for (auto &v : perSrc) ld.rowPtr.insert(ld.rowPtr.end(), v.begin(), v.end());
         }
-        uploadMat(m, rows, nc, qs, d, f);
     }
 
-    float *uploadF32(const TensorInfo &t) {
+    size_t matStageBytes(u32 rows, u32 n) const {
+        if (!q40_) return (size_t)rows * n * 4;
+        const hipk::Q40Tiling t = hipk::q40Tiling((int)rows, (int)n, hipk::gemvLanesPerRow((int)n, (int)rows, 1, true));
+        return t.qsBytes + t.dBytes;
+    }
+
+    void buildMat(Loader &ld, DevMat &m, const std::vector<RowSrc> &srcs, bool interleave, u32 c0, u32 nc) {
+        readRows(ld, srcs, interleave, c0, nc);
+        const int rows = (int)ld.rowPtr.size();
+        m.rows = rows;
+        m.n = (int)nc;
+        u8 *st = stageAcquire(ld);
+        if (q40_) {
+            m.lanes = hipk::gemvLanesPerRow((int)nc, rows, 1, true);
+            const hipk::Q40Tiling t = hipk::q40Tiling(rows, (int)nc, m.lanes);
+            DL_CHECK(t.qsBytes + t.dBytes <= ld.stageBytes, "staging buffer too small");
+            hipk::tileQ40AoS(ld.rowPtr.data(), rows, (int)nc, m.lanes, st, reinterpret_cast<uint32_t *>(st + t.qsBytes));
+            m.qs = dalloc<uint8_t>(t.qsBytes);
+            m.d = dalloc<uint16_t>(t.dBytes / 2);
+            stageCopy(ld, m.qs, st, t.qsBytes);
+            stageCopy(ld, m.d, st + t.qsBytes, t.dBytes);
+        } else {
+            const size_t rb = (size_t)nc * 4;
+            DL_CHECK((size_t)rows * rb <= ld.stageBytes, "staging buffer too small");
+            for (int r = 0; r < rows; r++) std::memcpy(st + (size_t)r * rb, ld.rowPtr[r], rb);
+            m.f = dalloc<float>((size_t)rows * nc);
+            stageCopy(ld, m.f, st, (size_t)rows * rb);
+        }
+        stageRelease(ld);
+    }
+
+    // A whole f32 tensor (norm weights, embedding), streamed through the staging buffers.
+    float *uploadF32(Loader &ld, const TensorInfo &t) {
+        const size_t bytes = (size_t)t.rows * t.cols * 4;
         float *p = dalloc<float>((size_t)t.rows * t.cols);
-        DL_HIP(hipMemcpy(p, file_->ptr(t), (size_t)t.rows * t.cols * 4, hipMemcpyHostToDevice));
+        for (size_t o = 0; o < bytes; o += ld.stageBytes) {
+            const size_t len = std::min(ld.stageBytes, bytes - o);
+            u8 *st = stageAcquire(ld);
+            ld.reader->read(t.offset + o, len, st);
+            stageCopy(ld, reinterpret_cast<u8 *>(p) + o, st, len);
+            stageRelease(ld);
+        }
         return p;
     }
 
     void loadFromFile() {
         const ShardPlan &p = plan_;
         const ModelFile &f = *file_;
-        for (u32 l = 0; l < h_.nLayers; l++) {
-            DevLayer &L = layers_[l];
-            const TensorInfo &wq = f.find(TensorKind::WQ, l), &wk = f.find(TensorKind::WK, l),
-                             &wv = f.find(TensorKind::WV, l), &wo = f.find(TensorKind::WO, l),
-                             &w1 = f.find(TensorKind::W1, l), &w2 = f.find(TensorKind::W2, l),
-                             &w3 = f.find(TensorKind::W3, l);
-            buildMat(L.qkv, {{&wq, p.qStart(), p.q0}, {&wk, p.kvStart(), p.kv0}, {&wv, p.kvStart(), p.kv0}}, false, 0,
-                     h_.dim);
-            buildMat(L.wo, {{&wo, 0, h_.dim}}, false, p.qStart(), p.q0);
-            buildMat(L.w13, {{&w1, p.hiddenStart(), p.hidden0}, {&w3, p.hiddenStart(), p.hidden0}}, true, 0, h_.dim);
-            buildMat(L.w2, {{&w2, 0, h_.dim}}, false, p.hiddenStart(), p.hidden0);
-            L.rmsAtt = uploadF32(f.find(TensorKind::RMS_ATT, l));
-            L.rmsFfn = uploadF32(f.find(TensorKind::RMS_FFN, l));
+        Loader ld;
+        ld.reader.reset(new ParallelReader(file_->path()));
+        // staging: the largest tiled matrix of this shard (at least 64 MB for the f32 tensors)
+        size_t sb = (size_t)64 << 20;
+        sb = std::max(sb, matStageBytes(p.q0 + 2 * p.kv0, h_.dim));
+        sb = std::max(sb, matStageBytes(h_.dim, p.q0));
+        sb = std::max(sb, matStageBytes(2 * p.hidden0, h_.dim));
+        sb = std::max(sb, matStageBytes(h_.dim, p.hidden0));
+        sb = std::max(sb, matStageBytes(p.vocab0, h_.dim));
+        ld.stageBytes = sb;
+        for (int i = 0; i < 2; i++) {
+            DL_HIP(hipHostMalloc(reinterpret_cast<void **>(&ld.stage[i]), sb, hipHostMallocDefault));
+            DL_HIP(hipEventCreateWithFlags(&ld.done[i], hipEventDisableTiming));
         }
-        emb_ = uploadF32(f.find(TensorKind::EMBEDDING, -1));
-        rmsFinal_ = uploadF32(f.find(TensorKind::RMS_FINAL, -1));
-        buildMat(wcls_, {{&f.find(TensorKind::WCLS, -1), p.vocabStart(), p.vocab0}}, false, 0, h_.dim);
+        DL_HIP(hipStreamCreateWithFlags(&ld.copy, hipStreamNonBlocking));
+        auto cleanup = [&] {
+            (void)hipStreamSynchronize(ld.copy);
+            for (int i = 0; i < 2; i++) {
+                (void)hipHostFree(ld.stage[i]);
+                (void)hipEventDestroy(ld.done[i]);
+            }
+            (void)hipStreamDestroy(ld.copy);
+        };
+        try {
+            for (u32 l = 0; l < h_.nLayers; l++) {
+                DevLayer &L = layers_[l];
+                const TensorInfo &wq = f.find(TensorKind::WQ, l), &wk = f.find(TensorKind::WK, l),
+                                 &wv = f.find(TensorKind::WV, l), &wo = f.find(TensorKind::WO, l),
+                                 &w1 = f.find(TensorKind::W1, l), &w2 = f.find(TensorKind::W2, l),
+                                 &w3 = f.find(TensorKind::W3, l);
+                buildMat(ld, L.qkv, {{&wq, p.qStart(), p.q0}, {&wk, p.kvStart(), p.kv0}, {&wv, p.kvStart(), p.kv0}},
+                         false, 0, h_.dim);
+                buildMat(ld, L.wo, {{&wo, 0, h_.dim}}, false, p.qStart(), p.q0);
+                buildMat(ld, L.w13, {{&w1, p.hiddenStart(), p.hidden0}, {&w3, p.hiddenStart(), p.hidden0}}, true, 0,
+                         h_.dim);
+                buildMat(ld, L.w2, {{&w2, 0, h_.dim}}, false, p.hiddenStart(), p.hidden0);
+                L.rmsAtt = uploadF32(ld, f.find(TensorKind::RMS_ATT, l));
+                L.rmsFfn = uploadF32(ld, f.find(TensorKind::RMS_FFN, l));
+            }
+            emb_ = uploadF32(ld, f.find(TensorKind::EMBEDDING, -1));
+            rmsFinal_ = uploadF32(ld, f.find(TensorKind::RMS_FINAL, -1));
+            buildMat(ld, wcls_, {{&f.find(TensorKind::WCLS, -1), p.vocabStart(), p.vocab0}}, false, 0, h_.dim);
+            DL_HIP(hipStreamSynchronize(ld.copy));
+        } catch (...) {
+            cleanup();
+            throw;
+        }
+        cleanup();
+        load_.fileBytes = ld.reader->bytesRead();
     }
 
     void synthMat(DevMat &m, int rows, int n, u64 seed) {
@@ -891,6 +989,7 @@ class HipEngineImpl : public HipEngine {
     hipk::TpXchg tpVec_, tpArg_;
     std::vector<void *> allocs_, hostAllocs_;
     size_t deviceBytes_ = 0;
+    LoadStats load_;
     std::vector<DevLayer> layers_;
     DevMat wcls_;
     float *emb_ = nullptr, *rmsFinal_ = nullptr;

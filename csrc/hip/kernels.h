@@ -43,6 +43,9 @@ struct Q40Tiling {
 Q40Tiling q40Tiling(int rows, int n, int L);
 // Host repack of row-major SoA blocks (qs [rows][nb][16], d [rows][nb] f16) into the tiled layout.
 void tileQ40(const uint8_t *qs, const uint16_t *d, int rows, int n, int L, uint8_t *qsOut, uint32_t *dOut);
+// Same from the file's AoS blocks (BlockQ40: f16 scale + 16 nibble bytes): rowBlocks[r] points
+// at row r's first block of the column slice being tiled.
+void tileQ40AoS(const uint8_t *const *rowBlocks, int rows, int n, int L, uint8_t *qsOut, uint32_t *dOut);
 
 struct AttnArgs {
     const float *q = nullptr;   // [B][ldq], rotated queries

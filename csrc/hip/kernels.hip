@@ -116,31 +116,11 @@ Q40Tiling q40Tiling(int rows, int n, int L) {
     return t;
 }
 
-static void tileQ40Groups(const uint8_t *qs, const uint16_t *d, int rows, int nb, const Q40Tiling &t, int gBegin,
-                          int gEnd, uint8_t *qsOut, uint32_t *dOut);
-
-void tileQ40(const uint8_t *qs, const uint16_t *d, int rows, int n, int L, uint8_t *qsOut, uint32_t *dOut) {
-    const Q40Tiling t = q40Tiling(rows, n, L);
-    const int nb = n / 32;
-    // pass groups are independent output ranges: split them over host threads (a 405B TP8 shard
-    // is ~28 GB of Q40 per rank, so the repack at load time must not be single-threaded)
-    const int hw = (int)std::thread::hardware_concurrency();
-    const int nThreads = std::max(1, std::min({hw > 0 ? hw : 1, 32, t.groups / 4}));
-    if (nThreads > 1) {
-        std::vector<std::thread> pool;
-        for (int ti = 0; ti < nThreads; ti++)
-            pool.emplace_back([&, ti] {
-                const int g0 = (int)((long)t.groups * ti / nThreads), g1 = (int)((long)t.groups * (ti + 1) / nThreads);
-                tileQ40Groups(qs, d, rows, nb, t, g0, g1, qsOut, dOut);
-            });
-        for (auto &th : pool) th.join();
-        return;
-    }
-    tileQ40Groups(qs, d, rows, nb, t, 0, t.groups, qsOut, dOut);
-}
-
-static void tileQ40Groups(const uint8_t *qs, const uint16_t *d, int rows, int nb, const Q40Tiling &t, int gBegin,
-                          int gEnd, uint8_t *qsOut, uint32_t *dOut) {
+// Tiled layout writer over pass groups [gBegin, gEnd): src(row, j, qs16Out) copies block j of
+// `row` (16 nibble bytes) and returns its f16 scale.
+template <typename Src>
+static void tileQ40Groups(const Src &src, int rows, int nb, const Q40Tiling &t, int gBegin, int gEnd,
+                          uint8_t *qsOut, uint32_t *dOut) {
     const int L = t.L;
     for (int g = gBegin; g < gEnd; g++)
         for (int k = 0; k < t.K; k++) {
@@ -152,17 +132,57 @@ static void tileQ40Groups(const uint8_t *qs, const uint16_t *d, int rows, int nb
                 for (int r = 0; r < 2; r++) {
                     uint8_t *dst = qsOut + ((c * 2 + r) * kThreads + tid) * 16;
                     const int row = row0 + r;
-                    if (row < rows && j < nb) {
-                        const size_t blk = (size_t)row * nb + j;
-                        std::memcpy(dst, qs + blk * 16, 16);
-                        dd |= (uint32_t)d[blk] << (16 * r);
-                    } else {
+                    if (row < rows && j < nb)
+                        dd |= (uint32_t)src(row, j, dst) << (16 * r);
+                    else
                         std::memset(dst, 0, 16);
-                    }
                 }
                 dOut[c * kThreads + tid] = dd;
             }
         }
+}
+
+// Pass groups are independent output ranges: split them over host threads (a 405B TP8 shard is
+// ~28 GB of Q40 per rank, so the repack at load time must not be single-threaded).
+template <typename Src>
+static void tileQ40Parallel(const Src &src, int rows, int n, int L, uint8_t *qsOut, uint32_t *dOut) {
+    const Q40Tiling t = q40Tiling(rows, n, L);
+    const int nb = n / 32;
+    const int hw = (int)std::thread::hardware_concurrency();
+    const int nThreads = std::max(1, std::min({hw > 0 ? hw : 1, 32, t.groups / 4}));
+    if (nThreads > 1) {
+        std::vector<std::thread> pool;
+        for (int ti = 0; ti < nThreads; ti++)
+            pool.emplace_back([&, ti] {
+                const int g0 = (int)((long)t.groups * ti / nThreads), g1 = (int)((long)t.groups * (ti + 1) / nThreads);
+                tileQ40Groups(src, rows, nb, t, g0, g1, qsOut, dOut);
+            });
+        for (auto &th : pool) th.join();
+        return;
+    }
+    tileQ40Groups(src, rows, nb, t, 0, t.groups, qsOut, dOut);
+}
+
+void tileQ40(const uint8_t *qs, const uint16_t *d, int rows, int n, int L, uint8_t *qsOut, uint32_t *dOut) {
+    const size_t nb = (size_t)n / 32;
+    auto src = [&](int row, int j, uint8_t *dst) -> uint16_t {
+        const size_t blk = (size_t)row * nb + j;
+        std::memcpy(dst, qs + blk * 16, 16);
+        return d[blk];
+    };
+    tileQ40Parallel(src, rows, n, L, qsOut, dOut);
+}
+
+void tileQ40AoS(const uint8_t *const *rowBlocks, int rows, int n, int L, uint8_t *qsOut, uint32_t *dOut) {
+    // file layout: per block an f16 scale then 16 nibble bytes (18 B, unaligned)
+    auto src = [&](int row, int j, uint8_t *dst) -> uint16_t {
+        const uint8_t *b = rowBlocks[row] + (size_t)j * 18;
+        std::memcpy(dst, b + 2, 16);
+        uint16_t dv;
+        std::memcpy(&dv, b, 2);
+        return dv;
+    };
+    tileQ40Parallel(src, rows, n, L, qsOut, dOut);
 }
 
 int gemvDefaultPasses(int n, int rows, int B, bool q40, int epi) {

@@ -674,6 +674,15 @@ PYBIND11_MODULE(_C, m) {
              py::arg("sync_type") = "f32")
         .def_property_readonly("header", [](const PyHipEngine &e) { return headerToDict(e.engine->header()); })
         .def_property_readonly("device_bytes", [](const PyHipEngine &e) { return e.engine->deviceBytes(); })
+        .def_property_readonly("load_stats",
+                               [](const PyHipEngine &e) {
+                                   const Backend::LoadStats l = e.engine->loadStats();
+                                   py::dict d;
+                                   d["ms"] = l.ms;
+                                   d["file_bytes"] = l.fileBytes;
+                                   d["device_bytes"] = l.deviceBytes;
+                                   return d;
+                               })
         .def("forward", [](PyHipEngine &e, std::vector<int> t, std::vector<int> p, std::vector<int> s) { return runForward(*e.engine, t, p, s); },
              py::arg("tokens"), py::arg("positions"), py::arg("slots"))
         .def("forward_sample",

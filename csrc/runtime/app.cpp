@@ -211,7 +211,14 @@ InferenceSession::InferenceSession(const AppArgs &args, int nSlots) : args_(args
         const u32 ack = s.recvPod<u32>();
         if (ack != kAck) throw NetError("worker failed to initialize: " + s.recvString());
     }
-    if (logLevel() >= 1) printModelHeader(backend_->header());
+    if (logLevel() >= 1) {
+        printModelHeader(backend_->header());
+        const Backend::LoadStats ls = backend_->loadStats();
+        if (ls.fileBytes > 0)
+            std::printf("💿 Weights: %.2f GB read in %.2f s (%.2f GB/s)%s\n", ls.fileBytes / 1e9, ls.ms / 1e3,
+                        ls.fileBytes / 1e6 / std::max(ls.ms, 1e-3),
+                        ls.deviceBytes ? (", " + std::to_string(ls.deviceBytes >> 20) + " MB on device").c_str() : "");
+    }
     if (!args.tokenizerPath.empty()) {
         tokenizer_.reset(new Tokenizer(args.tokenizerPath, true));
         if ((u32)tokenizer_->vocabSize() != backend_->header().vocabSize)

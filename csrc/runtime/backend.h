@@ -67,6 +67,13 @@ class Backend {
     virtual void forwardSample(int n, const int *tokens, const int *positions, const int *slots,
                                const SampleSpec *specs, int *out);
     virtual ForwardStats lastStats() const { return stats_; }
+    // Weight residency: time to load (file read + repack + upload, or on-device init), bytes read
+    // from the model file by this rank, bytes resident on its device (0 for host backends).
+    struct LoadStats {
+        double ms = 0;
+        u64 fileBytes = 0, deviceBytes = 0;
+    };
+    virtual LoadStats loadStats() const { return {}; }
     virtual std::string name() const = 0;
 
   protected:

@@ -262,3 +262,41 @@ def read_model(path: str) -> tuple:
         if rest:
             raise ValueError(f"Missing bytes in weight file: {-len(rest)}")
     return h, spec, out
+
+
+def write_random_model(path: str, spec: ModelSpec, seed: int = 0, chunk_bytes: int = 64 << 20) -> int:
+    """Write a full-size model of random weights without materialising it: Q40 tensors get random
+    nibbles and scales of 1/sqrt(21.5 n) (unit-variance activations, like the engine's synthetic
+    init), f32 tensors uniform [-1, 1) (norm weights 1). Streams `chunk_bytes` at a time, so an
+    8B-parameter file (4.6 GB) needs ~100 MB of RAM. Returns the file size."""
+    rng = np.random.default_rng(seed)
+    q40 = np.dtype([("d", "<f2"), ("qs", "u1", (16,))])
+    with open(path, "wb") as f:
+        write_header(f, spec.header_params())
+        for name, layer, rows, cols, ftype in tensor_plan(spec):
+            n = rows * cols
+            if ftype == FloatType.Q40:
+                nblk, per = n // 32, max(1, chunk_bytes // 18)
+                scale = np.float16(1.0 / np.sqrt(21.5 * cols))
+                for b0 in range(0, nblk, per):
+                    m = min(per, nblk - b0)
+                    blk = np.empty(m, dtype=q40)
+                    blk["d"] = scale
+                    blk["qs"] = rng.integers(0, 256, size=(m, 16), dtype=np.uint8)
+                    f.write(blk.tobytes())
+            elif ftype == FloatType.F32:
+                if name.startswith("rms"):
+                    f.write(np.ones(n, dtype=np.float32).tobytes())
+                    continue
+                per = max(1, chunk_bytes // 4)
+                for e0 in range(0, n, per):
+                    m = min(per, n - e0)
+                    # uniform [-1, 1) from raw bits: mantissa into [1, 2), then 2 x - 3
+                    u = (rng.integers(0, 1 << 32, size=m, dtype=np.uint32) >> np.uint32(9)) | np.uint32(0x3F800000)
+                    v = u.view(np.float32)
+                    v *= 2
+                    v -= 3
+                    f.write(v.tobytes())
+            else:
+                raise ValueError(f"write_random_model: unsupported float type {ftype}")
+        return f.tell()

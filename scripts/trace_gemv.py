@@ -46,6 +46,24 @@ def analyse(name, us, t, iters):
     avg = {k: np.nanmean([r[k] for r in rows]) * TICK_US for k in rows[0]}
     xcc = (t[-1, :, 3] & 0xF)
     per_xcc = np.bincount(xcc, minlength=8)
+    # where does the tail come from? per-CU load (workgroups sharing a CU), XCC, entry order
+    hw = (t[4:, :, 3] >> 32)
+    cu = (t[4:, :, 3] & 0xF) * 4096 + ((hw >> 8) & 0xF) + 16 * ((hw >> 12) & 0x1) + 32 * ((hw >> 13) & 0x7)
+    ex = (t[4:, :, 2] - t[4:, :, 0].min(axis=1, keepdims=True)) * TICK_US
+    en = (t[4:, :, 0] - t[4:, :, 0].min(axis=1, keepdims=True)) * TICK_US
+    share = np.zeros_like(cu)
+    for i in range(cu.shape[0]):
+        _, inv, cnt = np.unique(cu[i], return_inverse=True, return_counts=True)
+        share[i] = cnt[inv]
+    by_share = {int(k): round(float(ex[share == k].mean()), 2) for k in np.unique(share)}
+    n_share = {int(k): int((share == k).sum() // cu.shape[0]) for k in np.unique(share)}
+    xc = t[4:, :, 3] & 0xF
+    by_xcc = [round(float(ex[xc == k].max(axis=-1).mean() if (xc == k).any() else 0), 2) for k in range(8)]
+    last = ex >= np.percentile(ex, 95, axis=1, keepdims=True)
+    print(f"    exit by WGs/CU {by_share} (WGs {n_share}) | max exit by XCC {by_xcc} | "
+          f"corr(entry, exit) {np.corrcoef(en.ravel(), ex.ravel())[0, 1]:.2f} | last-5% entry {en[last].mean():.2f} vs all {en.mean():.2f} "
+          f"| last-5% share {share[last].mean():.2f} vs all {share.mean():.2f} | blockIdx of last-5% mean {np.nonzero(last)[1].mean():.0f} of {grid}",
+          flush=True)
     print(f"{name:5s} grid {grid:4d} | {us:6.2f} us/launch | span {avg['span']:5.2f} gap {avg['gap']:4.2f} | "
           f"entry spread {avg['entry']:4.2f} | loaded {avg['loaded']:4.2f} | first {avg['first']:4.2f} | ready med {avg['ready_med']:4.2f} p90 {avg['ready_p90']:4.2f} | "
           f"exit min {avg['exit_min']:5.2f} med {avg['exit_med']:5.2f} p90 {avg['exit_p90']:5.2f} | WGs/XCC {per_xcc.tolist()}",

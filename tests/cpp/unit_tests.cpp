@@ -3,6 +3,8 @@
 // Host-only: quantization codecs, the shard plan, RoPE table, CPU primitives, JSON, chat templates,
 // the EOS detector and the TP fused-exchange plan helpers. Built by `make test-cpp`
 // (build/unit_tests) and run by tests/test_cpp_units.py.
+#include <unistd.h>
+
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -10,6 +12,7 @@
 #include <string>
 #include <vector>
 
+#include "../../csrc/core/model_file.h"
 #include "../../csrc/core/plan.h"
 #include "../../csrc/core/quant.h"
 #include "../../csrc/cpu/cpu_ops.h"
@@ -158,6 +161,37 @@ int main() {
         eos.reset();  // the caller emits the delta and resets after NOT_EOS (scheduler.cpp)
         CHECK(eos.append(2, "ST") == EosResult::MAYBE_EOS);
         CHECK(eos.append(3, "OP") == EosResult::EOS);
+        return ok;
+    });
+    run("parallel_reader", [] {
+        // 3 MB file read back through 1 KB pieces on 8 threads, whole and as scattered ranges
+        bool ok = true;
+        char path[] = "/tmp/dl_unit_reader_XXXXXX";
+        const int fd = mkstemp(path);
+        CHECK(fd >= 0);
+        std::vector<u8> data(3 << 20);
+        for (size_t i = 0; i < data.size(); i++) data[i] = (u8)(i * 2654435761u >> 13);
+        CHECK(::write(fd, data.data(), data.size()) == (ssize_t)data.size());
+        ::close(fd);
+        {
+            ParallelReader r(path, 8, 1024);
+            std::vector<u8> out(data.size());
+            r.read(0, out.size(), out.data());
+            CHECK(out == data);
+            std::vector<u8> a(5000), b(77);
+            r.readMany({{12345, a.size(), a.data()}, {data.size() - 77, b.size(), b.data()}});
+            CHECK(std::memcmp(a.data(), data.data() + 12345, a.size()) == 0);
+            CHECK(std::memcmp(b.data(), data.data() + data.size() - 77, b.size()) == 0);
+            CHECK(r.bytesRead() == data.size() + 5077);
+            bool threw = false;
+            try {
+                r.read(data.size() - 10, 100, a.data());
+            } catch (const Error &) {
+                threw = true;
+            }
+            CHECK(threw);  // short read past the end of the file
+        }
+        ::unlink(path);
         return ok;
     });
     std::printf("%d/%d native unit tests passed\n", gRun - gFailed, gRun);

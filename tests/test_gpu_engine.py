@@ -164,3 +164,13 @@ def test_simulated_tensor_parallel_matches_single(C, kv4_gpu, world):
     got = C.simulate_tp(kv4_gpu, "q80", world, tokens)
     assert _rel(got, ref) < 3e-2
     assert (got.argmax(-1) == ref.argmax(-1)).all()
+
+
+@pytest.mark.gpu
+def test_kv_cache_larger_than_hbm_is_refused(C):
+    """64 slots x 131072 positions of bf16 KV for the 8B is ~1.1 TB: refused before allocating,
+    with the numbers and what to lower, instead of an out-of-memory fault mid-load."""
+    with pytest.raises(RuntimeError, match="does not fit on GPU"):
+        h = dict(dim=4096, hidden_dim=14336, n_layers=32, n_heads=32, n_kv_heads=8, vocab_size=128256,
+                 seq_len=131072, rope_theta=500000, weight_type=2)
+        C.HipEngine("", "q80", synthetic=h, max_seq_len=131072, n_slots=64, max_batch=1)
