@@ -86,6 +86,7 @@ def main() -> int:
     ap.add_argument("--long-ctx", type=int, default=4096, help="position of the long-context decode point (0: off)")
     ap.add_argument("--no-cli", action="store_true", help="skip the dllama CLI product-path point (1 GPU)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-f32kv", action="store_true", help="skip the f32 KV-cache decode point")
     args = ap.parse_args()
 
     import torch
@@ -126,10 +127,11 @@ def main() -> int:
         from distributed_llama_multiusers_amd.models.synthetic import LLAMA_SHAPES
         shape = dict(LLAMA31_8B, **LLAMA_SHAPES[args.shape])
 
-    def make_engine(max_seq=seq_len):
+    def make_engine(max_seq=seq_len, kv_bf16=True):
         # the context length is sized to the run (attention split grids follow it)
         synthetic = None if args.model else dict(shape, seq_len=max_seq)
         return C.HipEngine(args.model, "q80", max_seq_len=max_seq, max_batch=max_batch, n_slots=args.batch,
+                           kv_bf16=kv_bf16,
                            gpu_index=local, use_graphs=not args.no_graphs, synthetic=synthetic, seed=1234, rank=rank,
                            world=world, uid=uid, comm=comm, sync_type=args.sync_type)
 
@@ -214,10 +216,25 @@ def main() -> int:
         long_ms = (time.perf_counter() - tl) * 1000.0 / 16
         barrier()
 
+    f32kv_ms = None
+    if not args.no_f32kv:  # the reference keeps its KV cache in f32: same decode with an f32 cache
+        del eng
+        eng = make_engine(kv_bf16=False)
+        eng.decode_greedy(4, tokens, [pos0] * B, list(range(B)))
+        barrier()
+        torch.cuda.synchronize()
+        tf = time.perf_counter()
+        eng.decode_greedy(16, tokens, [pos0 + 4] * B, list(range(B)))
+        torch.cuda.synchronize()
+        f32kv_ms = (time.perf_counter() - tf) * 1000.0 / 16
+        barrier()
+
     if dist is not None:
-        t = torch.tensor([elapsed, eval_s, long_ms or 0.0], dtype=torch.float64)
+        t = torch.tensor([elapsed, eval_s, long_ms or 0.0, f32kv_ms or 0.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, eval_s, long_ms = float(t[0]), float(t[1]), (float(t[2]) if long_ms is not None else None)
+        elapsed, eval_s = float(t[0]), float(t[1])
+        long_ms = float(t[2]) if long_ms is not None else None
+        f32kv_ms = float(t[3]) if f32kv_ms is not None else None
 
     ms_per_step = elapsed * 1000.0 / args.steps
     pred_ms_tok = ms_per_step / B
@@ -260,6 +277,7 @@ def main() -> int:
             "device_ms_per_step": round(dev_ms / args.steps, 4),
             "long_ctx_pos": long_pos or None,
             "long_ctx_pred_ms_per_token": round(long_ms / B, 4) if long_ms is not None else None,
+            "f32_kv_pred_ms_per_token": round(f32kv_ms / B, 4) if f32kv_ms is not None else None,
             "load_s": round(load_s, 2),
             "hip_graphs": not args.no_graphs,
             "tp_comm": comm_kind if world > 1 else None,

@@ -17,6 +17,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <condition_variable>
+#include <mutex>
 #include <vector>
 
 #include "../core/quant.h"
@@ -28,6 +30,74 @@ namespace dl {
 
 void LocalComm::gatherToRoot(const float *local, u64 nLocal, float *out) {
     if (out && out != local) std::memcpy(out, local, nLocal * sizeof(float));
+}
+
+struct ThreadGroupComm::Group {
+    int world;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    u64 generation = 0;
+    std::vector<const void *> ptr;
+    std::vector<std::vector<BlockQ80>> q80;
+    explicit Group(int w) : world(w), ptr(w), q80(w) {}
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const u64 gen = generation;
+        if (++arrived == world) {
+            arrived = 0;
+            generation++;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return generation != gen; });
+        }
+    }
+};
+
+std::vector<std::unique_ptr<ThreadGroupComm>> ThreadGroupComm::make(int world) {
+    auto g = std::make_shared<Group>(world);
+    std::vector<std::unique_ptr<ThreadGroupComm>> out;
+    for (int r = 0; r < world; r++) out.emplace_back(new ThreadGroupComm(g, r));
+    return out;
+}
+
+int ThreadGroupComm::size() const { return g_->world; }
+
+void ThreadGroupComm::allReduceSum(float *data, u64 n) {
+    g_->ptr[rank_] = data;
+    g_->barrier();
+    tmp_.assign(n, 0.f);
+    for (int r = 0; r < g_->world; r++) {
+        const float *p = static_cast<const float *>(g_->ptr[r]);
+        for (u64 i = 0; i < n; i++) tmp_[i] += p[i];
+    }
+    g_->barrier();  // every rank has read every partial before any overwrites its own
+    std::memcpy(data, tmp_.data(), n * sizeof(float));
+}
+
+void ThreadGroupComm::allReduceSumQ80(float *data, u64 n) {
+    DL_CHECK(n % kQBlock == 0, "Q80 sync needs 32-aligned vectors");
+    auto &mine = g_->q80[rank_];
+    mine.resize(n / kQBlock);
+    quantizeQ80(data, mine.data(), n);
+    g_->barrier();
+    tmp_.resize(n);
+    std::vector<float> acc(n, 0.f);
+    for (int r = 0; r < g_->world; r++) {
+        dequantizeQ80(g_->q80[r].data(), tmp_.data(), n);
+        for (u64 i = 0; i < n; i++) acc[i] += tmp_[i];
+    }
+    g_->barrier();
+    std::memcpy(data, acc.data(), n * sizeof(float));
+}
+
+void ThreadGroupComm::gatherToRoot(const float *local, u64 nLocal, float *out) {
+    g_->ptr[rank_] = local;
+    g_->barrier();
+    if (rank_ == 0 && out)
+        for (int r = 0; r < g_->world; r++)
+            std::memcpy(out + (u64)r * nLocal, g_->ptr[r], nLocal * sizeof(float));
+    g_->barrier();
 }
 
 namespace {

@@ -494,6 +494,68 @@ PYBIND11_MODULE(_C, m) {
           py::arg("model"), py::arg("buffer_type") = "q80", py::arg("nthreads") = 1, py::arg("max_seq_len") = 0,
           py::arg("max_batch") = 32, py::arg("n_slots") = 1);
 
+    // CPU tensor parallelism in one process (ThreadGroupComm): rank 0's logits of sequential
+    // single-token forwards of `tokens` at positions 0.., [n][vocab], and the greedy continuation
+    // of `steps` tokens after them (every rank agrees on it).
+    m.def("cpu_simulate_tp",
+          [](const std::string &model, const std::string &bufferType, int world, std::vector<int> tokens,
+             const std::string &syncType, int steps, int nThreads) {
+              EngineConfig c = makeConfig(model, bufferType, nThreads, 0, 8, 1, -1, false, false, py::none(), 1);
+              c.syncType = parseFloatType(syncType);
+              std::vector<float> logits;
+              std::vector<int> greedy;
+              u32 vocab = 0;
+              {
+                  py::gil_scoped_release rel;
+                  auto comms = ThreadGroupComm::make(world);
+                  std::vector<std::unique_ptr<Backend>> bes(world);
+                  std::vector<std::string> errs(world);
+                  std::vector<std::thread> th;
+                  for (int r = 0; r < world; r++)
+                      th.emplace_back([&, r] {
+                          try {
+                              bes[r] = makeCpuBackend(c, comms[r].get());
+                              const u32 V = bes[r]->header().vocabSize;
+                              std::vector<float> lg(V);
+                              int pos = 0, slot0 = 0;
+                              for (int t : tokens) {
+                                  bes[r]->forward(1, &t, &pos, &slot0, r == 0 ? lg.data() : nullptr);
+                                  if (r == 0) {
+                                      vocab = V;
+                                      logits.insert(logits.end(), lg.begin(), lg.end());
+                                  }
+                                  pos++;
+                              }
+                              if (steps > 0) {
+                                  // first continuation token from the prompt's last logits (rank 0),
+                                  // shared with the other ranks through the comm (exact for ids)
+                                  float id = r == 0 ? (float)(std::max_element(lg.begin(), lg.end()) - lg.begin()) : 0.f;
+                                  comms[r]->allReduceSum(&id, 1);
+                                  int tok = (int)id;
+                                  if (r == 0) greedy.push_back(tok);
+                                  for (int s = 1; s < steps; s++) {
+                                      int next = 0;
+                                      bes[r]->forwardArgmax(1, &tok, &pos, &slot0, &next);
+                                      pos++;
+                                      tok = next;
+                                      if (r == 0) greedy.push_back(tok);
+                                  }
+                              }
+                          } catch (const std::exception &e) {
+                              errs[r] = e.what();
+                          }
+                      });
+                  for (auto &t : th) t.join();
+                  for (auto &e : errs)
+                      if (!e.empty()) throw Error("cpu_simulate_tp: " + e);
+              }
+              py::array_t<float> a({(py::ssize_t)tokens.size(), (py::ssize_t)vocab});
+              std::memcpy(a.mutable_data(), logits.data(), logits.size() * 4);
+              return py::make_tuple(a, greedy);
+          },
+          py::arg("model"), py::arg("buffer_type"), py::arg("world"), py::arg("tokens"), py::arg("sync_type") = "f32",
+          py::arg("steps") = 0, py::arg("nthreads") = 1);
+
     m.def("bench_gemv_q40",
           [](int rows, int n, int pro, int epi, int B, int lanes, int passes, int copies, int iters) {
               return benchGemvQ40(rows, n, pro, epi, B, lanes, passes, copies, iters);

@@ -107,6 +107,27 @@ class LocalComm : public HostComm {
     void gatherToRoot(const float *local, u64 nLocal, float *out) override;
 };
 
+// `world` ranks of one process (threads) exchanging through shared memory with exactly the TCP
+// data plane's arithmetic (f32 sum in rank order; Q80: every partial quantized once, dequantized
+// sums in rank order). Used to pin the GPU tensor-parallel paths against the CPU reference in
+// tests without sockets.
+class ThreadGroupComm : public HostComm {
+  public:
+    struct Group;
+    static std::vector<std::unique_ptr<ThreadGroupComm>> make(int world);
+    int rank() const override { return rank_; }
+    int size() const override;
+    void allReduceSum(float *data, u64 n) override;
+    void allReduceSumQ80(float *data, u64 n) override;
+    void gatherToRoot(const float *local, u64 nLocal, float *out) override;
+
+  private:
+    ThreadGroupComm(std::shared_ptr<Group> g, int rank) : g_(std::move(g)), rank_(rank) {}
+    std::shared_ptr<Group> g_;
+    int rank_;
+    std::vector<float> tmp_;
+};
+
 std::unique_ptr<Backend> makeCpuBackend(const EngineConfig &cfg, HostComm *comm);
 
 }  // namespace dl

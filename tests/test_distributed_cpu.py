@@ -237,3 +237,21 @@ def test_chat_mode_multi_turn(assets):
     assert r.returncode == 0, out
     assert out.count("🤖 Assistant") == 1 and out.count("👱 User") == 1
     assert out.rstrip().endswith("(end of context)")
+
+
+@pytest.mark.parametrize("world,sync", [(1, "f32"), (2, "f32"), (4, "f32"), (2, "q80"), (4, "q80")])
+def test_thread_group_tp_matches_single(C, kv4, world, sync):
+    """In-process CPU tensor parallelism (ThreadGroupComm, the TCP plane's arithmetic without
+    sockets; used to pin the GPU TP paths): logits and greedy continuation vs one rank."""
+    import numpy as np
+    tokens = [5, 99, 300, 7, 100, 2]
+    ref, ref_g = C.cpu_simulate_tp(kv4["q40"], "q80", 1, tokens, "f32", 16)
+    got, got_g = C.cpu_simulate_tp(kv4["q40"], "q80", world, tokens, sync, 16)
+    cpu = C.cpu_backend(kv4["q40"], "q80", 1)
+    single = np.stack([cpu.forward([t], [p], [0])[0] for p, t in enumerate(tokens)])
+    assert np.array_equal(ref, single)
+    rel = np.abs(got - ref).max() / np.abs(ref).max()
+    assert rel < (1e-5 if sync == "f32" else 3e-2), rel
+    assert len(got_g) == 16
+    if sync == "f32":
+        assert got_g == ref_g

@@ -39,6 +39,48 @@ def test_engine_matches_cpu(C, assets, kind, kv_bf16):
     assert (got.argmax(-1) == ref.argmax(-1)).mean() >= 0.8
 
 
+def _first_divergence(got, ref):
+    for i, (a, b) in enumerate(zip(got, ref)):
+        if a != b:
+            return i
+    return None
+
+
+@pytest.mark.parametrize("kind", ["f32", "q40"])
+def test_greedy_64_tokens_equal_cpu(C, assets, kind):
+    """Free-running greedy decode, f32 KV: the GPU (prompt forwards, then the captured
+    forward->argmax chain) emits exactly the CPU reference's 64 tokens. A divergence is accepted
+    only where the CPU's own logits are a near-tie between the two candidates (f32 weights: 1e-4 of
+    the logit range; Q40 weights x Q80 activations, where a 1-ulp input difference can move a Q80
+    rounding: 3e-2), and for f32 weights not before token 48."""
+    buf = "q80" if kind == "q40" else "f32"
+    cpu = C.cpu_backend(assets[kind], buf, 4)
+    gpu = C.HipEngine(assets[kind], buf, kv_bf16=False, max_batch=8)
+    prompt, steps = [3, 17, 101, 7], 64
+    for p, t in enumerate(prompt):
+        lg = cpu.forward([t], [p], [0])[0]
+    ref, ref_lg = [], []
+    tok = int(lg.argmax())
+    for s in range(steps):
+        ref.append(tok)
+        ref_lg.append(lg)
+        lg = cpu.forward([tok], [len(prompt) + s], [0])[0]
+        tok = int(lg.argmax())
+    for p, t in enumerate(prompt):
+        glg = gpu.forward([t], [p], [0])[0]
+    g0 = int(glg.argmax())
+    _, rest = gpu.decode_greedy(steps - 1, [g0], [len(prompt)], [0])
+    got = [g0] + list(rest)
+    i = _first_divergence(got, ref)
+    if i is None:
+        return
+    scale = float(np.abs(ref_lg[i]).max())
+    margin = float(ref_lg[i][ref[i]] - ref_lg[i][got[i]])
+    assert margin <= (1e-4 if kind == "f32" else 3e-2) * scale, (i, margin, scale, got, ref)
+    if kind == "f32":
+        assert i >= 48, (i, got, ref)
+
+
 def test_engine_medium_matches_cpu(C, medium):
     cpu = C.cpu_backend(medium, "q80", 8)
     gpu = C.HipEngine(medium, "q80", kv_bf16=False, max_batch=8)

@@ -148,6 +148,29 @@ def test_xgmi_engine_tp_matches_single(C, tmp_path, world, sync_type):
     assert agree >= steps - 2 and res[0][1][:4] == list(ref_toks[:4]), (res[0][1], ref_toks)
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_q80_tp_matches_cpu_q80_tp(C, tmp_path, world):
+    """GPU TP with the Q80 exchange (fused GEMV-tail exchange of Q80-quantized partials) vs the CPU
+    reference data plane with --sync-type q80 semantics at the same world size (in-process
+    ThreadGroupComm: every partial quantized once, dequantized sums in rank order)."""
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=9, dim=512, n_heads=8,
+                               n_kv_heads=4, hidden_dim=1024, vocab_size=1024)
+    tokens = [5, 99, 300, 7, 1000, 2]
+    steps = 12
+    cpu_lg, cpu_toks = C.cpu_simulate_tp(m, "q80", world, tokens + [tokens[-1]], "q80", steps, 2)
+    res = _run(_engine_tp, world, m, tokens, kwargs=dict(sync_type="q80", steps=steps))
+    assert all(isinstance(v, tuple) for v in res.values()), res
+    got = res[0][0]
+    ref = cpu_lg[:len(tokens)]
+    rel = np.abs(got - ref).max() / np.abs(ref).max()
+    assert rel < 3e-2, rel
+    assert (got.argmax(-1) == ref.argmax(-1)).all()
+    agree = sum(a == b for a, b in zip(res[0][1], cpu_toks))
+    assert agree >= steps - 2 and res[0][1][:4] == list(cpu_toks[:4]), (res[0][1], cpu_toks)
+
+
 @pytest.mark.parametrize("n_workers", [1, 3])
 def test_cli_root_workers_over_xgmi(tmp_path, n_workers):
     """`dllama inference` root + `dllama worker` processes (all on GPU 0 here): the TCP control plane
