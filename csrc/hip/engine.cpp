@@ -322,6 +322,11 @@ class HipEngineImpl : public HipEngine {
         DL_HIP(hipMemsetAsync(dAttCnt_, 0, sizeof(int) * (size_t)MB * p.nHeads0, stream_));
         dArgV_ = dalloc<float>((size_t)MB * 64);
         dArgI_ = dalloc<int>((size_t)MB * 64);
+        {
+            void *ss = dalloc<uint8_t>(hipk::SampleScratch::bytes((int)MB));
+            DL_HIP(hipMemsetAsync(ss, 0, hipk::SampleScratch::bytes((int)MB), stream_));
+            sampleScratch_.carve(ss, (int)MB);
+        }
         dArgCnt_ = dalloc<int>(MB);
         DL_HIP(hipMemsetAsync(dArgCnt_, 0, sizeof(int) * MB, stream_));
         dLogits_ = dalloc<float>((size_t)MB * p.vocab0);
@@ -945,6 +950,7 @@ class HipEngineImpl : public HipEngine {
             g.vocab = h_.vocabSize;
             g.spec = dSpec_;
             g.ids = dIds_;
+            g.scratch = sampleScratch_;
             hipk::launchSample(g, n, stream_);
         } else if (kind != GraphKind::LOGITS) {
             ProfScope ps(this, "argmax");
@@ -990,6 +996,7 @@ class HipEngineImpl : public HipEngine {
     std::vector<void *> allocs_, hostAllocs_;
     size_t deviceBytes_ = 0;
     LoadStats load_;
+    hipk::SampleScratch sampleScratch_;
     std::vector<DevLayer> layers_;
     DevMat wcls_;
     float *emb_ = nullptr, *rmsFinal_ = nullptr;

@@ -14,6 +14,7 @@
 //   argmax                         greedy sampling on device (+ token feedback for decode chains)
 #pragma once
 
+#include <algorithm>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -205,13 +206,38 @@ struct ArgmaxArgs {
 // logits / temperature -> softmax -> coin -> multinomial in index order, or top-p: candidates
 // >= (1 - p) / (V - 1), descending by probability, cut where the cumulative mass first exceeds p,
 // draw r = coin * nucleus mass). spec[b] = (temperature, topp, coin, -): temperature 0 -> argmax,
-// < 0 -> no draw (ids[b] = -1). One 1024-thread workgroup per row; the top-p cut and the draw are
-// found by 8-bit radix searches over the order-preserving key of logit / temperature.
+// < 0 -> no draw (ids[b] = -1). sampleGroups(B) workgroups per row run 8 dependent phases; the
+// top-p cut and the draw are 11/11/10-bit radix searches over the order-preserving key of
+// logit / temperature. The scratch must be zero-initialised once; every call leaves it zero.
+constexpr int kSampleMaxGroups = 64;
+constexpr int kSampleStateWords = 16;
+int sampleGroups(int B);
+struct SampleScratch {
+    float *hist = nullptr;  // [rows][G][2048] partial histograms (G = sampleGroups(rows))
+    float *part = nullptr;  // [B][kSampleMaxGroups]
+    int *partI = nullptr;   // [B][kSampleMaxGroups]
+    uint32_t *state = nullptr;  // [B][kSampleStateWords]
+    // partial-histogram slots for any batch of up to B rows
+    static size_t histFloats(int B) {
+        size_t m = 0;
+        for (int r = 1; r <= B; r++) m = std::max(m, (size_t)r * sampleGroups(r));
+        return m * 2048;
+    }
+    static size_t bytes(int B) { return (histFloats(B) + (size_t)B * (2 * kSampleMaxGroups + kSampleStateWords)) * 4; }
+    void carve(void *base, int B) {
+        float *f = static_cast<float *>(base);
+        hist = f;
+        part = f + histFloats(B);
+        partI = reinterpret_cast<int *>(part + (size_t)B * kSampleMaxGroups);
+        state = reinterpret_cast<uint32_t *>(partI + (size_t)B * kSampleMaxGroups);
+    }
+};
 struct SampleArgs {
     const float *logits = nullptr;
     int vocab = 0;
     const float4 *spec = nullptr;
     int *ids = nullptr;
+    SampleScratch scratch;
 };
 void launchSample(const SampleArgs &a, int B, hipStream_t s);
 

@@ -354,6 +354,9 @@ std::vector<int> sample(const std::vector<float> &logits, int B, int vocab, cons
     g.vocab = vocab;
     g.spec = reinterpret_cast<const float4 *>(sc.upload(specs));
     g.ids = sc.alloc<int>(B);
+    void *ss = sc.alloc<uint8_t>(hipk::SampleScratch::bytes(B));
+    DL_HIP(hipMemsetAsync(ss, 0, hipk::SampleScratch::bytes(B), sc.s));
+    g.scratch.carve(ss, B);
     hipk::launchSample(g, B, sc.s);
     sc.sync();
     return sc.download(g.ids, B);

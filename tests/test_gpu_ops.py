@@ -209,7 +209,7 @@ def _draw_ok(logits, temp, topp, coin, tok, tol=2e-4):
     return lo - tol <= r <= cum[i] + tol
 
 
-@pytest.mark.parametrize("vocab,scale", [(128256, 1.0), (128256, 6.0), (32000, 3.0), (517, 2.0)])
+@pytest.mark.parametrize("vocab,scale", [(128256, 1.0), (128256, 6.0), (32000, 3.0), (517, 2.0), (50, 2.0)])
 def test_device_sampler_matches_host(ops, vocab, scale):
     """Device sampler (multinomial and top-p radix search) vs the host Sampler given the same coin,
     on flat (random-model) and peaked distributions: every draw valid under exact arithmetic, and
@@ -242,3 +242,5 @@ def test_engine_forward_sample_matches_host(C, assets):
     co = C.cpu_ops
     want = [co.sample_host(np.asarray(logits[i]), temps[i], topps[i], coins[i]) for i in range(4)]
     assert got == want, (got, want)
+    # the engine's sampler scratch is reused: a second identical call draws the same tokens
+    assert eng2.forward_sample(toks, pos, [0] * 4, temps, topps, coins) == got
