@@ -87,6 +87,7 @@ def main() -> int:
     ap.add_argument("--no-cli", action="store_true", help="skip the dllama CLI product-path point (1 GPU)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-f32kv", action="store_true", help="skip the f32 KV-cache decode point")
+    ap.add_argument("--no-prefill4k", action="store_true", help="skip the 4096-token prompt-eval point")
     args = ap.parse_args()
 
     import torch
@@ -229,12 +230,28 @@ def main() -> int:
         f32kv_ms = (time.perf_counter() - tf) * 1000.0 / 16
         barrier()
 
+    p4k_ms = None
+    if not args.no_prefill4k:  # a 4096-token prompt evaluated in 32-token chunks (attention grows with it)
+        del eng
+        eng = make_engine(4096 + 8)
+        p4k = [(i * 7919 + 13) % 128000 for i in range(4096)]
+        eng.forward_argmax(p4k[:32], list(range(32)), [0] * 32)  # graph capture outside the timing
+        barrier()
+        torch.cuda.synchronize()
+        tp4 = time.perf_counter()
+        for s0 in range(0, 4096, 32):
+            eng.forward_argmax(p4k[s0:s0 + 32], list(range(s0, s0 + 32)), [0] * 32)
+        torch.cuda.synchronize()
+        p4k_ms = (time.perf_counter() - tp4) * 1000.0 / 4096
+        barrier()
+
     if dist is not None:
-        t = torch.tensor([elapsed, eval_s, long_ms or 0.0, f32kv_ms or 0.0], dtype=torch.float64)
+        t = torch.tensor([elapsed, eval_s, long_ms or 0.0, f32kv_ms or 0.0, p4k_ms or 0.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, eval_s = float(t[0]), float(t[1])
         long_ms = float(t[2]) if long_ms is not None else None
         f32kv_ms = float(t[3]) if f32kv_ms is not None else None
+        p4k_ms = float(t[4]) if p4k_ms is not None else None
 
     ms_per_step = elapsed * 1000.0 / args.steps
     pred_ms_tok = ms_per_step / B
@@ -278,6 +295,7 @@ def main() -> int:
             "long_ctx_pos": long_pos or None,
             "long_ctx_pred_ms_per_token": round(long_ms / B, 4) if long_ms is not None else None,
             "f32_kv_pred_ms_per_token": round(f32kv_ms / B, 4) if f32kv_ms is not None else None,
+            "prompt_4k_eval_ms_per_token": round(p4k_ms, 4) if p4k_ms is not None else None,
             "load_s": round(load_s, 2),
             "hip_graphs": not args.no_graphs,
             "tp_comm": comm_kind if world > 1 else None,

@@ -1465,18 +1465,24 @@ __global__ __launch_bounds__(kThreads) void normF16Kernel(GemvArgs a, _Float16 *
     float *xo = a.xNext ? a.xNext + (size_t)b * a.ldIn : nullptr;
     _Float16 *o = out + (size_t)b * n;
     const bool inReg = n <= kThreads * 4 * PV;
-    float4 v[PV];
+    float4 v[PV], gw[PV];
     float ss = 0.f;
     if (inReg) {
+        // every load (x, the residual delta and the norm weights) is issued before any is used:
+        // one memory round trip before the reduction instead of three
+        float4 w[PV];
+#pragma unroll
+        for (int k = 0; k < PV; k++) {
+            const int i = min((tid + k * kThreads) * 4, n - 4);
+            v[k] = ld4(x + i);
+            w[k] = y ? ld4(y + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+            gw[k] = a.normW ? ld4(a.normW + i) : make_float4(1.f, 1.f, 1.f, 1.f);
+        }
 #pragma unroll
         for (int k = 0; k < PV; k++) {
             const int i = (tid + k * kThreads) * 4;
             if (i < n) {
-                v[k] = ld4(x + i);
-                if (y) {
-                    const float4 w = ld4(y + i);
-                    v[k].x += w.x; v[k].y += w.y; v[k].z += w.z; v[k].w += w.w;
-                }
+                v[k].x += w[k].x; v[k].y += w[k].y; v[k].z += w[k].z; v[k].w += w[k].w;
                 if (xo) st4(xo + i, v[k]);
                 ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
             }
@@ -1497,8 +1503,8 @@ __global__ __launch_bounds__(kThreads) void normF16Kernel(GemvArgs a, _Float16 *
         ss = blockSum<kThreads>(ss, scratch);
         inv = 1.0f / sqrtf(ss / (float)n + a.eps);
     }
-    auto emit = [&](int i, float4 u) {
-        const float4 g = a.normW ? ld4(a.normW + i) : make_float4(1.f, 1.f, 1.f, 1.f);
+    auto emit = [&](int i, float4 u, const float4 *gp) {
+        const float4 g = gp ? *gp : (a.normW ? ld4(a.normW + i) : make_float4(1.f, 1.f, 1.f, 1.f));
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         const h4 r = {(_Float16)(g.x * (inv * u.x)), (_Float16)(g.y * (inv * u.y)), (_Float16)(g.z * (inv * u.z)),
                       (_Float16)(g.w * (inv * u.w))};
@@ -1508,7 +1514,7 @@ __global__ __launch_bounds__(kThreads) void normF16Kernel(GemvArgs a, _Float16 *
 #pragma unroll
         for (int k = 0; k < PV; k++) {
             const int i = (tid + k * kThreads) * 4;
-            if (i < n) emit(i, v[k]);
+            if (i < n) emit(i, v[k], &gw[k]);
         }
     } else {
         for (int i = tid * 4; i < n; i += kThreads * 4) {
@@ -1517,7 +1523,7 @@ __global__ __launch_bounds__(kThreads) void normF16Kernel(GemvArgs a, _Float16 *
                 const float4 w = ld4(y + i);
                 u.x += w.x; u.y += w.y; u.z += w.z; u.w += w.w;
             }
-            emit(i, u);
+            emit(i, u, nullptr);
         }
     }
 }
