@@ -591,6 +591,10 @@ class HipEngineImpl : public HipEngine {
         std::memcpy(hIn_ + MB, positions, n * sizeof(int));
         std::memcpy(hIn_ + 2 * MB, slots, n * sizeof(int));
         size_t words = 2 * (size_t)MB + n;
+        // prefill attention on MFMA: every block of rows it assigns to one workgroup is one slot
+        prefillOk_ = kvBf16_ && hipk::attnPrefillSupported(plan_.headSize, plan_.kvMul, true);
+        const int rpb = prefillOk_ ? hipk::attnPrefillRowsPerBlock(plan_.kvMul) : 1;
+        for (int b = 0; prefillOk_ && b < n; b++) prefillOk_ = slots[b] == slots[b - b % rpb];
         if (specs) {
             static_assert(sizeof(SampleSpec) == 4 * sizeof(float), "spec layout");
             std::memcpy(hIn_ + 3 * MB, specs, n * sizeof(SampleSpec));
@@ -606,7 +610,7 @@ class HipEngineImpl : public HipEngine {
             enqueueForward(n, kind);
             return;
         }
-        const int key = n * 4 + (int)kind;
+        const int key = (n * 4 + (int)kind) * 2 + (prefillOk_ ? 1 : 0);
         auto it = graphs_.find(key);
         if (it == graphs_.end()) {
             hipGraphExec_t ge = captureForward(n, kind);
@@ -884,7 +888,10 @@ class HipEngineImpl : public HipEngine {
                     a.pf1Bytes = std::min(t13.qsBytes, mallPrefetchBytes());
                     a.pfBlocks = 256;
                 }
-                hipk::launchAttention(a, n, stream_);
+                if (bat && prefillOk_)
+                    hipk::launchAttentionPrefill(a, n, stream_);
+                else
+                    hipk::launchAttention(a, n, stream_);
             }
             {
                 ProfScope ps(this, "gemv_wo");
@@ -1014,6 +1021,7 @@ class HipEngineImpl : public HipEngine {
     float *dArgV_ = nullptr;
     float2 *dRope_ = nullptr;
     int splitGrid_ = 1, chunkMax_ = 256;
+    bool prefillOk_ = false;  // this forward's rows qualify for the MFMA prefill attention
     std::map<int, hipGraphExec_t> graphs_;
     bool profile_ = false;
     bool graphsBroken_ = false;

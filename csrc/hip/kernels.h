@@ -182,6 +182,11 @@ size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg, int pro);
 int gemvDefaultPasses(int n, int rows, int B, bool q40, int epi);
 
 void launchAttention(const AttnArgs &a, int B, hipStream_t s);
+// Prefill rows on MFMA (bf16 caches): blocks of attnPrefillRowsPerBlock(kvMul) consecutive rows
+// must share one slot (positions arbitrary, causal per row); counters >= blocks x KV heads.
+void launchAttentionPrefill(const AttnArgs &a, int nRows, hipStream_t s);
+int attnPrefillRowsPerBlock(int kvMul);
+bool attnPrefillSupported(int hs, int kvMul, bool kvBf16);
 int attnSplitGrid(int seqLen);
 int attnChunkMax(int seqLen, int splitGrid);
 

@@ -285,9 +285,14 @@ std::vector<float> qkvRope(const std::vector<uint8_t> &blocks, int q0, int kv0, 
 
 std::vector<float> attention(const std::vector<float> &q, const std::vector<float> &k, const std::vector<float> &v,
                              int nSlots, int seqLen, int nHeads0, int kvMul, int hs, const std::vector<int> &pos,
-                             const std::vector<int> &slot, bool kvBf16) {
+                             const std::vector<int> &slot, bool kvBf16, bool prefill) {
     const int B = (int)pos.size();
     DL_CHECK(B >= 1 && slot.size() == pos.size(), "attention rows");
+    if (prefill) {
+        DL_CHECK(hipk::attnPrefillSupported(hs, kvMul, kvBf16), "prefill attention needs a bf16 cache");
+        const int rpb = hipk::attnPrefillRowsPerBlock(kvMul);
+        for (int b = 0; b < B; b++) DL_CHECK(slot[b] == slot[b - b % rpb], "prefill row blocks must share a slot");
+    }
     DL_CHECK(kvMul >= 1 && nHeads0 % kvMul == 0 && (hs == 64 || hs == 128), "attention head layout");
     const int q0 = nHeads0 * hs, kv0 = nHeads0 / kvMul * hs;
     const size_t cacheElems = (size_t)nSlots * seqLen * kv0;
@@ -325,7 +330,11 @@ std::vector<float> attention(const std::vector<float> &q, const std::vector<floa
     a.ldOut = q0;
     a.kvBf16 = kvBf16 ? 1 : 0;
     a.counters = sc.alloc<int>((size_t)B * nHeads0);
-    hipk::launchAttention(a, B, sc.s);
+    DL_HIP(hipMemsetAsync(a.counters, 0, sizeof(int) * (size_t)B * nHeads0, sc.s));
+    if (prefill)
+        hipk::launchAttentionPrefill(a, B, sc.s);
+    else
+        hipk::launchAttention(a, B, sc.s);
     sc.sync();
     return sc.download(a.out, (size_t)B * q0);
 }

@@ -42,7 +42,7 @@ std::vector<float> qkvRope(const std::vector<uint8_t> &blocks, int q0, int kv0, 
 // q [B][nHeads0*hs] (already rotated), row b at position pos[b] in slot slot[b]. Returns f32 [B][q0].
 std::vector<float> attention(const std::vector<float> &q, const std::vector<float> &k, const std::vector<float> &v,
                              int nSlots, int seqLen, int nHeads0, int kvMul, int hs, const std::vector<int> &pos,
-                             const std::vector<int> &slot, bool kvBf16);
+                             const std::vector<int> &slot, bool kvBf16, bool prefill = false);
 
 // Parallel argmax over [B][vocab] (ties -> lowest index).
 std::vector<int> argmax(const std::vector<float> &logits, int B, int vocab);

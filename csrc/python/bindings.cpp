@@ -226,17 +226,18 @@ void bindOps(py::module_ &m) {
           py::arg("norm_w"), py::arg("eps"), py::arg("rope"), py::arg("seq_len"), py::arg("pos"), py::arg("kv_bf16") = true);
     o.def("attention",
           [](py::object q, py::object k, py::object v, int nSlots, int seqLen, int nHeads0, int kvMul, int hs,
-             std::vector<int> pos, std::vector<int> slot, bool kvBf16) {
+             std::vector<int> pos, std::vector<int> slot, bool kvBf16, bool prefill) {
               const std::vector<float> qv = vec<float>(q), kv = vec<float>(k), vv = vec<float>(v);
               std::vector<float> out;
               {
                   py::gil_scoped_release rel;
-                  out = ops::attention(qv, kv, vv, nSlots, seqLen, nHeads0, kvMul, hs, pos, slot, kvBf16);
+                  out = ops::attention(qv, kv, vv, nSlots, seqLen, nHeads0, kvMul, hs, pos, slot, kvBf16, prefill);
               }
               return arr(out, {(py::ssize_t)pos.size(), (py::ssize_t)nHeads0 * hs});
           },
           py::arg("q"), py::arg("k"), py::arg("v"), py::arg("n_slots"), py::arg("seq_len"), py::arg("n_heads0"),
-          py::arg("kv_mul"), py::arg("head_size"), py::arg("pos"), py::arg("slot"), py::arg("kv_bf16") = true);
+          py::arg("kv_mul"), py::arg("head_size"), py::arg("pos"), py::arg("slot"), py::arg("kv_bf16") = true,
+          py::arg("prefill") = false);
     o.def("sample",
           [](py::object logits, int B, py::object specs) {
               const std::vector<float> l = vec<float>(logits), sp = vec<float>(specs);

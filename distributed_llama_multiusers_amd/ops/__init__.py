@@ -72,12 +72,13 @@ def qkv_rope(blocks, q0: int, kv0: int, head_size: int, n: int, x, norm_w, eps: 
 
 
 def attention(q, k_cache, v_cache, n_heads0: int, kv_mul: int, head_size: int, pos, slot,
-              kv_bf16: bool = True) -> torch.Tensor:
-    """Decode attention. k_cache / v_cache: [slots, seq_len, kv0]; q: [B, n_heads0 * head_size]."""
+              kv_bf16: bool = True, prefill: bool = False) -> torch.Tensor:
+    """Decode attention. k_cache / v_cache: [slots, seq_len, kv0]; q: [B, n_heads0 * head_size].
+    prefill=True: the MFMA prefill kernel (bf16 cache; row blocks of 64 / kv_mul rows share a slot)."""
     n_slots, seq_len, _ = k_cache.shape
     return torch.from_numpy(native().ops.attention(_np(q), _np(k_cache), _np(v_cache), n_slots, seq_len, n_heads0,
                                                    kv_mul, head_size, [int(p) for p in pos], [int(s) for s in slot],
-                                                   kv_bf16))
+                                                   kv_bf16, prefill))
 
 
 def sample(logits, temperatures, topps, coins) -> list:

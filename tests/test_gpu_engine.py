@@ -216,3 +216,21 @@ def test_kv_cache_larger_than_hbm_is_refused(C):
         h = dict(dim=4096, hidden_dim=14336, n_layers=32, n_heads=32, n_kv_heads=8, vocab_size=128256,
                  seq_len=131072, rope_theta=500000, weight_type=2)
         C.HipEngine("", "q80", synthetic=h, max_seq_len=131072, n_slots=64, max_batch=1)
+
+
+@pytest.mark.parametrize("n", [8, 32, 64])
+def test_engine_prefill_mfma_attention(C, medium, n, monkeypatch):
+    """Batched forward with a bf16 cache (MFMA prefill attention over the chunk's rows, one slot) ==
+    sequential decodes (per-row attention), and a second chunk on top of the first (keys of the
+    earlier chunk + causal keys of its own)."""
+    monkeypatch.setenv("DL_GEMM_MIN", "2")
+    rng = np.random.default_rng(n)
+    toks = [int(t) for t in rng.integers(0, 2048, 2 * n)]
+    a = C.HipEngine(medium, "q80", kv_bf16=True, max_batch=64)
+    b = C.HipEngine(medium, "q80", kv_bf16=True, max_batch=64)
+    seq = _seq(a, toks)
+    first = b.forward(toks[:n], list(range(n)), [0] * n)
+    second = b.forward(toks[n:], list(range(n, 2 * n)), [0] * n)
+    bat = np.concatenate([first, second])
+    assert _rel(bat, seq) < 3e-2
+    assert (bat.argmax(-1) == seq.argmax(-1)).mean() >= 0.85

@@ -131,6 +131,32 @@ def test_attention_decode(ops, kv_bf16, n_heads0, kv_mul, hs, seq, pos):
     assert rel(out, want) < 1e-4  # f32 arithmetic on the (bf16-rounded) cache values
 
 
+@pytest.mark.parametrize("n_heads0,kv_mul,hs,seq,p0,rows", [
+    (32, 4, 128, 512, 0, 32),       # 8B shard, prompt start: causal within the chunk only
+    (32, 4, 128, 4608, 4000, 32),   # deep chunk: 16 key splits + combine
+    (8, 8, 128, 1024, 700, 20),     # 70B-like GQA 8, partial row block
+    (16, 16, 128, 1024, 100, 7),    # 405B-like GQA 16
+    (8, 2, 64, 2048, 1500, 40),     # head size 64, 2-head groups, 40 rows = 2 row blocks (32 rows each)
+    (8, 1, 64, 640, 300, 70),       # MHA: 64-row blocks, two blocks
+])
+def test_attention_prefill_mfma(ops, n_heads0, kv_mul, hs, seq, p0, rows):
+    """MFMA prefill attention (one KV read per row block, S^T = K.Q^T and O^T = V^T.P^T on bf16
+    MFMAs, causal mask per row) vs the fp32 reference over a chunk of consecutive positions of one
+    slot; bf16 Q and P bound the error (the cache values are bf16 on both sides)."""
+    kv0 = n_heads0 // kv_mul * hs
+    g = torch.Generator().manual_seed(21)
+    k = torch.randn(2, seq, kv0, generator=g).bfloat16().float()
+    v = torch.randn(2, seq, kv0, generator=g).bfloat16().float()
+    q = torch.randn(rows, n_heads0 * hs, generator=g)
+    pos = list(range(p0, p0 + rows))
+    slots = [1] * rows
+    out = ops.attention(q, k, v, n_heads0, kv_mul, hs, pos, slots, True, prefill=True)
+    want = ops.ref_attention(q, k, v, n_heads0, kv_mul, hs, pos, slots)
+    assert rel(out, want) < 1.2e-2, rel(out, want)
+    # the per-row VALU kernel on the same rows agrees too
+    assert rel(ops.attention(q, k, v, n_heads0, kv_mul, hs, pos, slots, True), want) < 1e-4
+
+
 @pytest.mark.parametrize("n_heads0,kv_mul,hs,seq,pos", [
     (4, 4, 128, 8192, [8100, 3, 511, 512, 513]),  # long context, chunk edges, several rows
     (16, 16, 128, 1024, [1000]),                 # 405B-like GQA group of 16 heads
