@@ -297,7 +297,7 @@ class HipEngineImpl : public HipEngine {
         dAttS_ = dalloc<float2>((size_t)MB * p.q0 / 32);
         dHQ_ = dalloc<int8_t>((size_t)MB * p.hidden0);
         dHS_ = dalloc<float2>((size_t)MB * p.hidden0 / 32);
-        if (q40_) {  // batched (MFMA) path: f16 activations, split-K partials, counters
+        {  // batched (MFMA) path, Q40 and F32 weights: f16 activations, split-K partials, counters
             const size_t rowsH = ((size_t)MB + 2 * kGemmMaxTokens - 1) / kGemmMaxTokens * kGemmMaxTokens;
             dXh_ = dalloc<_Float16>(rowsH * h_.dim);
             dAttH_ = dalloc<_Float16>(rowsH * p.q0);
@@ -750,7 +750,7 @@ class HipEngineImpl : public HipEngine {
     }
 
     bool batchedPath(int n) const {
-        return q40_ && n >= gemmMinTokens() && hipk::gemmSupported(h_.dim) && hipk::gemmSupported(plan_.q0) &&
+        return n >= gemmMinTokens() && hipk::gemmSupported(h_.dim) && hipk::gemmSupported(plan_.q0) &&
                hipk::gemmSupported(plan_.hidden0);
     }
 
@@ -765,7 +765,7 @@ class HipEngineImpl : public HipEngine {
         return (size_t)(e && *e ? std::atoi(e) : 24) << 20;
     }
 
-    // Batched path (>= gemmMinTokens rows, Q40): per chunk of <= 64 tokens, a norm kernel (f32 ->
+    // Batched path (>= gemmMinTokens rows, Q40 or F32 weights): per chunk of <= 64 tokens, a norm kernel (f32 ->
     // f16, RESNORM) or the producer's f16 rows (xh) feed the MFMA GEMM with the fused epilogue.
     void gemmBatched(const DevMat &m, int n, int epi, const float *in, int ldIn, const float *add, float *xNext,
                      const float *normW, const _Float16 *xh, float *out, int ldOut, _Float16 *outH,
@@ -776,6 +776,7 @@ class HipEngineImpl : public HipEngine {
             hipk::GemvArgs &a = g.e;
             a.qs = m.qs;
             a.wd = m.d;
+            a.wf = m.f;
             a.rows = m.rows;
             a.n = m.n;
             a.lanes = m.lanes;
@@ -813,7 +814,10 @@ class HipEngineImpl : public HipEngine {
             g.splits = hipk::gemmSplits(m.rows, m.n, bc);
             g.part = dPart_;
             g.counters = dGemmCnt_;
-            hipk::launchGemmQ40(g, epi, stream_);
+            if (q40_)
+                hipk::launchGemmQ40(g, epi, stream_);
+            else
+                hipk::launchGemmF32(g, epi, stream_);
         }
     }
 

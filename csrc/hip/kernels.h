@@ -148,6 +148,8 @@ struct GemmArgs {
     int *counters = nullptr;
 };
 void launchGemmQ40(const GemmArgs &a, int epi, hipStream_t s);
+// Same contract for F32 weights (`e.wf` [rows][n] row-major; EPI_ACT_Q80 not supported).
+void launchGemmF32(const GemmArgs &a, int epi, hipStream_t s);
 // Tile / split-K plan of one matrix (rt = 16-row tiles per wave: 64 * rt rows per workgroup).
 struct GemmPlan {
     int rt = 1, tiles = 0, splits = 1;

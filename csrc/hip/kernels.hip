@@ -1228,13 +1228,101 @@ __device__ __forceinline__ void glds4(const void *g, void *lds) {
                                          reinterpret_cast<uintptr_t>(lds)), 4, 0, 0);
 }
 
+// Split-K combine and fused epilogues shared by the batched GEMMs (Q40 and f32): `acc` holds this
+// lane's C fragments (weight row (local) wave*16 + col, token t*16 + h*4 + i); `smem` must hold
+// MP x 64 floats and is free (all K-loop LDS reads retired behind a barrier); `flag` one int.
+template <int MT, int EPI>
+__device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc)[MT], char *smem, int *flag) {
+    const GemvArgs &a = ga.e;
+    constexpr int MP = MT * 16;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int col = lane & 15, h = lane >> 4, rl = wave * 16 + col;
+    const int tileIdx = blockIdx.x, sp = blockIdx.y, S = ga.splits;
+    const int R0 = tileIdx * kGemmRows;
+    float *tile = reinterpret_cast<float *>(smem);  // [MP][64], stages are free now
+    // C layout: weight row (local) wave*16 + col, token t*16 + h*4 + i
+    if (S == 1) {
+#pragma unroll
+        for (int t = 0; t < MT; t++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) tile[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
+    } else {
+        const int tiles = gridDim.x;
+        float *part = ga.part + ((size_t)sp * tiles + tileIdx) * MP * kGemmRows;
+#pragma unroll
+        for (int t = 0; t < MT; t++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) part[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            const int old = __hip_atomic_fetch_add(ga.counters + tileIdx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            flag[0] = old == S - 1;
+        }
+        __syncthreads();
+        if (!flag[0]) return;
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            __hip_atomic_store(ga.counters + tileIdx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        // combine in split order (deterministic), 16-B loads with all of a thread's splits in
+        // flight at once: this tail runs on one workgroup per tile after the others finished
+        const f32x4 *P = reinterpret_cast<const f32x4 *>(ga.part) + (size_t)tileIdx * MP * kGemmRows / 4;
+        const size_t st4 = (size_t)tiles * MP * kGemmRows / 4;
+        f32x4 *tile4 = reinterpret_cast<f32x4 *>(tile);
+        for (int i = tid; i < MP * kGemmRows / 4; i += kThreads) {
+            f32x4 v[8];
+#pragma unroll
+            for (int s2 = 0; s2 < 8; s2++)
+                if (s2 < S) v[s2] = P[s2 * st4 + i];
+            f32x4 r = v[0];
+#pragma unroll
+            for (int s2 = 1; s2 < 8; s2++)
+                if (s2 < S) r += v[s2];
+            for (int s2 = 8; s2 < S; s2++) r += P[s2 * st4 + i];
+            tile4[i] = r;
+        }
+    }
+    __syncthreads();
+    // fused epilogues on row pairs (2k, 2k+1) of the tile, 32 pairs per token
+    for (int i = tid; i < ga.M * 32; i += kThreads) {
+        const int t = i >> 5, k = i & 31, r0 = R0 + 2 * k;
+        const float v0 = tile[t * kGemmRows + 2 * k], v1 = tile[t * kGemmRows + 2 * k + 1];
+        if constexpr (EPI == EPI_STORE) {
+            if (r0 < a.rows) a.out[(size_t)t * a.ldOut + r0] = v0;
+            if (r0 + 1 < a.rows) a.out[(size_t)t * a.ldOut + r0 + 1] = v1;
+        } else if constexpr (EPI == EPI_ACT) {
+            if (r0 < a.rows) a.out[(size_t)t * a.ldOut + (r0 >> 1)] = gateAct(a, v0) * v1;
+        } else if constexpr (EPI == EPI_ACT_F16) {
+            if (r0 < a.rows) ga.outH[(size_t)t * a.ldOut + (r0 >> 1)] = (_Float16)(gateAct(a, v0) * v1);
+        } else if constexpr (EPI == EPI_ACT_Q80) {
+            const int hBase = R0 >> 1;
+            if (hBase >= (a.rows >> 1)) continue;  // whole 32-unit block: uniform per lane group
+            const float hv = gateAct(a, v0) * v1;
+            const float amax = groupMax<32>(fabsf(hv));
+            const float d = amax / 127.0f;
+            const float id = d != 0.f ? 1.0f / d : 0.f;
+            int q = (int)rintf(hv * id);
+            q = q > 127 ? 127 : (q < -127 ? -127 : q);
+            a.oq[(size_t)t * a.ldOut + hBase + k] = (int8_t)q;
+            const float qsum = groupSum<32>((float)q);
+            if (k == 0) a.os[(size_t)t * (a.ldOut >> 5) + (hBase >> 5)] = make_float2(roundF16(d), qsum);
+        } else {
+            if (r0 < a.rows)
+                qkvPairStore(a, r0, v0, v1, a.rope + (size_t)a.pos[t] * (a.hs >> 1), a.pos[t], a.slot[t],
+                             a.out + (size_t)t * a.ldOut);
+        }
+    }
+}
+
 // STG = stage buffers: 2 double-buffers the chunk stream inside a workgroup; 1 (the 64-token
 // tile) drops that to fit 3 workgroups per CU, which then overlap each other's loads.
 template <int MT, int EPI, int STG>
 __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     const GemvArgs &a = ga.e;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int MP = MT * 16;
     constexpr int SB = gemmStageBytes(MT);
     constexpr int NW = kGemmRows * kGemmCh / kThreads, NX = MT * 16 * kGemmCh * 4 / kThreads;
     constexpr int NLD = NW + 1 + NX;  // glds instructions per thread per stage
@@ -1331,82 +1419,7 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
         __builtin_amdgcn_s_barrier();  // stage c % STG is refilled at iteration c + 1
     }
 
-    float *tile = reinterpret_cast<float *>(smem);  // [MP][64], stages are free now
-    // C layout: weight row (local) wave*16 + col, token t*16 + h*4 + i
-    if (S == 1) {
-#pragma unroll
-        for (int t = 0; t < MT; t++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) tile[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
-    } else {
-        const int tiles = gridDim.x;
-        float *part = ga.part + ((size_t)sp * tiles + tileIdx) * MP * kGemmRows;
-#pragma unroll
-        for (int t = 0; t < MT; t++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) part[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            const int old = __hip_atomic_fetch_add(ga.counters + tileIdx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            flag[0] = old == S - 1;
-        }
-        __syncthreads();
-        if (!flag[0]) return;
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            __hip_atomic_store(ga.counters + tileIdx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        // combine in split order (deterministic), 16-B loads with all of a thread's splits in
-        // flight at once: this tail runs on one workgroup per tile after the others finished
-        const f32x4 *P = reinterpret_cast<const f32x4 *>(ga.part) + (size_t)tileIdx * MP * kGemmRows / 4;
-        const size_t st4 = (size_t)tiles * MP * kGemmRows / 4;
-        f32x4 *tile4 = reinterpret_cast<f32x4 *>(tile);
-        for (int i = tid; i < MP * kGemmRows / 4; i += kThreads) {
-            f32x4 v[8];
-#pragma unroll
-            for (int s2 = 0; s2 < 8; s2++)
-                if (s2 < S) v[s2] = P[s2 * st4 + i];
-            f32x4 r = v[0];
-#pragma unroll
-            for (int s2 = 1; s2 < 8; s2++)
-                if (s2 < S) r += v[s2];
-            for (int s2 = 8; s2 < S; s2++) r += P[s2 * st4 + i];
-            tile4[i] = r;
-        }
-    }
-    __syncthreads();
-    // fused epilogues on row pairs (2k, 2k+1) of the tile, 32 pairs per token
-    for (int i = tid; i < ga.M * 32; i += kThreads) {
-        const int t = i >> 5, k = i & 31, r0 = R0 + 2 * k;
-        const float v0 = tile[t * kGemmRows + 2 * k], v1 = tile[t * kGemmRows + 2 * k + 1];
-        if constexpr (EPI == EPI_STORE) {
-            if (r0 < a.rows) a.out[(size_t)t * a.ldOut + r0] = v0;
-            if (r0 + 1 < a.rows) a.out[(size_t)t * a.ldOut + r0 + 1] = v1;
-        } else if constexpr (EPI == EPI_ACT) {
-            if (r0 < a.rows) a.out[(size_t)t * a.ldOut + (r0 >> 1)] = gateAct(a, v0) * v1;
-        } else if constexpr (EPI == EPI_ACT_F16) {
-            if (r0 < a.rows) ga.outH[(size_t)t * a.ldOut + (r0 >> 1)] = (_Float16)(gateAct(a, v0) * v1);
-        } else if constexpr (EPI == EPI_ACT_Q80) {
-            const int hBase = R0 >> 1;
-            if (hBase >= (a.rows >> 1)) continue;  // whole 32-unit block: uniform per lane group
-            const float hv = gateAct(a, v0) * v1;
-            const float amax = groupMax<32>(fabsf(hv));
-            const float d = amax / 127.0f;
-            const float id = d != 0.f ? 1.0f / d : 0.f;
-            int q = (int)rintf(hv * id);
-            q = q > 127 ? 127 : (q < -127 ? -127 : q);
-            a.oq[(size_t)t * a.ldOut + hBase + k] = (int8_t)q;
-            const float qsum = groupSum<32>((float)q);
-            if (k == 0) a.os[(size_t)t * (a.ldOut >> 5) + (hBase >> 5)] = make_float2(roundF16(d), qsum);
-        } else {
-            if (r0 < a.rows)
-                qkvPairStore(a, r0, v0, v1, a.rope + (size_t)a.pos[t] * (a.hs >> 1), a.pos[t], a.slot[t],
-                             a.out + (size_t)t * a.ldOut);
-        }
-    }
+    gemmFinish<MT, EPI>(ga, acc, smem, flag);
 }
 
 static int gemmStages4() {  // stage buffers of the 64-token tile (DL_GEMM_STG4, read once)
@@ -1452,6 +1465,81 @@ void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
     DL_GEMM_CASES(1, kGemmStages) DL_GEMM_CASES(1, 3) DL_GEMM_CASES(1, 4) DL_GEMM_CASES(2, kGemmStages) DL_GEMM_CASES(2, 1) DL_GEMM_CASES(4, 1) DL_GEMM_CASES(4, 2)
 #undef DL_GEMM_CASES
 #undef DL_GEMM_CASE
+}
+
+// Batched matmul for F32 weights on MFMA (the reference runs F32 batches through
+// llamafile_sgemm, nn-cpu-ops.cpp:1018-1037): out[t][row] = sum_k W[row][k] x[t][k], W f32
+// row-major [rows][n] (exact: v_mfma_f32_16x16x4_f32), x f16 as on the Q40 path (the only
+// rounding). A wave owns 16 rows; per 32-k step lane (col, h) streams 32 B of its row col
+// (k = 8h .. 8h+7: 4 lanes cover a 128-B line) straight into VGPRs - no LDS for the weights,
+// which are read once - and the matching 16 B of f16 activations per token tile (L2-resident,
+// shared by the workgroup's waves). Element e of those 8 feeds MFMA e on both operands (k = 8h+e,
+// a permutation of k). 4 steps are issued per iteration so 4 x 32 B per lane stay in flight.
+// Split-K, the deterministic combine and the fused epilogues are the Q40 GEMM's (gemmFinish).
+template <int MT, int EPI>
+__global__ __launch_bounds__(kThreads) void gemmF32Kernel(GemmArgs ga) {
+    const GemvArgs &a = ga.e;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int *flag = reinterpret_cast<int *>(smem + MT * 16 * kGemmRows * 4);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, col = lane & 15, h = lane >> 4;
+    const int n = a.n, kps = n / ga.splits, k0 = blockIdx.y * kps;
+    const int row = min(blockIdx.x * kGemmRows + wave * 16 + col, a.rows - 1);  // clamped: outputs dropped
+    const float *wp = a.wf + (size_t)row * n + k0 + 8 * h;
+    const _Float16 *xp = ga.x + (size_t)col * n + k0 + 8 * h;
+    f32x4 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int U = 4;
+    int k = 0;
+    for (; k + 32 * U <= kps; k += 32 * U) {
+        f32x4 w[U][2];
+        half8 xv[U][MT];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            w[u][0] = *reinterpret_cast<const f32x4 *>(wp + k + 32 * u);
+            w[u][1] = *reinterpret_cast<const f32x4 *>(wp + k + 32 * u + 4);
+#pragma unroll
+            for (int t = 0; t < MT; t++) xv[u][t] = *reinterpret_cast<const half8 *>(xp + (size_t)t * 16 * n + k + 32 * u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int e = 0; e < 8; e++)
+#pragma unroll
+                for (int t = 0; t < MT; t++)
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)xv[u][t][e], w[u][e >> 2][e & 3], acc[t], 0, 0, 0);
+    }
+    for (; k < kps; k += 32) {  // remainder steps (kps is a multiple of 32)
+        const f32x4 w0 = *reinterpret_cast<const f32x4 *>(wp + k), w1 = *reinterpret_cast<const f32x4 *>(wp + k + 4);
+#pragma unroll
+        for (int t = 0; t < MT; t++) {
+            const half8 xv = *reinterpret_cast<const half8 *>(xp + (size_t)t * 16 * n + k);
+#pragma unroll
+            for (int e = 0; e < 8; e++)
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)xv[e], e < 4 ? w0[e] : w1[e - 4], acc[t], 0, 0, 0);
+        }
+    }
+    gemmFinish<MT, EPI>(ga, acc, smem, flag);
+}
+
+void launchGemmF32(const GemmArgs &ga, int epi, hipStream_t s) {
+    const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
+    const int MT = gemmTokenPad(ga.M) / 16;
+    const dim3 grid(tiles, ga.splits);
+    const size_t lds = (size_t)MT * 16 * kGemmRows * 4 + 16;
+#define DL_GEMMF_CASE(M_, E)                                                              \
+    if (MT == M_ && epi == E) {                                                           \
+        if (lds > 65536) allowLds((const void *)gemmF32Kernel<M_, E>, lds);               \
+        hipLaunchKernelGGL((gemmF32Kernel<M_, E>), grid, dim3(kThreads), lds, s, ga);     \
+        return;                                                                           \
+    }
+#define DL_GEMMF_CASES(M_)                                                                \
+    DL_GEMMF_CASE(M_, EPI_STORE) DL_GEMMF_CASE(M_, EPI_ACT) DL_GEMMF_CASE(M_, EPI_QKV)    \
+    DL_GEMMF_CASE(M_, EPI_ACT_F16)
+    DL_GEMMF_CASES(1) DL_GEMMF_CASES(2) DL_GEMMF_CASES(4)
+#undef DL_GEMMF_CASES
+#undef DL_GEMMF_CASE
+    throw Error("launchGemmF32: unsupported epilogue");
 }
 
 // Residual add + RMS norm (optional) of M rows -> f16 (one workgroup per row): the batched

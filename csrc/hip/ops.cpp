@@ -212,6 +212,47 @@ std::vector<float> gemmQ40(const std::vector<uint8_t> &blocks, int rows, int n, 
     return sc.download(out, (size_t)M * rows);
 }
 
+// Batched F32-weight GEMM (K5): RMS norm -> f16 activations -> gemmF32Kernel, EPI_STORE.
+std::vector<float> gemmF32(const std::vector<float> &w, int rows, int n, const std::vector<float> &in,
+                           const std::vector<float> &normW, float eps, int M) {
+    DL_CHECK(M >= 1 && M <= 256, "gemm tokens must be 1..256");
+    DL_CHECK(w.size() == (size_t)rows * n && in.size() == (size_t)M * n, "gemm operand sizes");
+    DL_CHECK(hipk::gemmSupported(n), "gemm input width must be a multiple of 32");
+    checkRows(normW, (size_t)n, "norm weights");
+    Scratch sc;
+    hipk::GemvArgs nq;
+    nq.n = n;
+    nq.in = sc.upload(in);
+    nq.ldIn = n;
+    nq.normW = sc.upload(normW);
+    nq.eps = eps;
+    const int rowsPad = (M + hipk::kGemmMaxTokens - 1) / hipk::kGemmMaxTokens * hipk::kGemmMaxTokens;
+    _Float16 *xh = sc.alloc<_Float16>((size_t)rowsPad * n);
+    hipk::launchNormF16(nq, xh, M, sc.s);
+    const float *wd = sc.upload(w);
+    float *out = sc.alloc<float>((size_t)M * rows);
+    const size_t part = hipk::gemmPartFloats(rows, n, M);
+    float *partBuf = part ? sc.alloc<float>(part) : nullptr;
+    int *counters = sc.alloc<int>((size_t)(rows + 63) / 64 + 1);
+    for (int c0 = 0; c0 < M; c0 += hipk::kGemmMaxTokens) {
+        const int bc = std::min(hipk::kGemmMaxTokens, M - c0);
+        hipk::GemmArgs g;
+        g.e.wf = wd;
+        g.e.rows = rows;
+        g.e.n = n;
+        g.e.out = out + (size_t)c0 * rows;
+        g.e.ldOut = rows;
+        g.x = xh + (size_t)c0 * n;
+        g.M = bc;
+        g.splits = hipk::gemmSplits(rows, n, bc);
+        g.part = partBuf;
+        g.counters = counters;
+        hipk::launchGemmF32(g, hipk::EPI_STORE, sc.s);
+    }
+    sc.sync();
+    return sc.download(out, (size_t)M * rows);
+}
+
 std::vector<float> qkvRope(const std::vector<uint8_t> &blocks, int q0, int kv0, int hs, int n,
                            const std::vector<float> &in, const std::vector<float> &normW, float eps,
                            const std::vector<float> &rope, int seqLen, const std::vector<int> &pos, bool kvBf16,

@@ -27,6 +27,8 @@ std::vector<float> gemvQ40Q80In(const std::vector<uint8_t> &blocks, int rows, in
 
 // Batched Q40 matmul on MFMA (M = 2..32 tokens): norm kernel (in + residual -> RMS norm -> f16)
 // then the MFMA GEMM with the plain store epilogue.
+std::vector<float> gemmF32(const std::vector<float> &w, int rows, int n, const std::vector<float> &in,
+                           const std::vector<float> &normW, float eps, int M);
 std::vector<float> gemmQ40(const std::vector<uint8_t> &blocks, int rows, int n, const std::vector<float> &in,
                            const std::vector<float> &residual, const std::vector<float> &normW, float eps, int M);
 

@@ -209,6 +209,19 @@ void bindOps(py::module_ &m) {
           },
           py::arg("blocks"), py::arg("rows"), py::arg("n"), py::arg("x"), py::arg("residual") = py::none(),
           py::arg("norm_w") = py::none(), py::arg("eps") = 1e-5f);
+    o.def("gemm_f32",
+          [](py::object wts, int rows, int n, py::object x, py::object normW, float eps) {
+              const std::vector<float> w = vec<float>(wts), in = vec<float>(x), nw = vec<float>(normW);
+              const int M = (int)(in.size() / n);
+              std::vector<float> out;
+              {
+                  py::gil_scoped_release rel;
+                  out = ops::gemmF32(w, rows, n, in, nw, eps, M);
+              }
+              return arr(out, {M, rows});
+          },
+          py::arg("w"), py::arg("rows"), py::arg("n"), py::arg("x"), py::arg("norm_w") = py::none(),
+          py::arg("eps") = 1e-5f);
     o.def("qkv_rope",
           [](py::object blocks, int q0, int kv0, int hs, int n, py::object x, py::object normW, float eps, py::object rope,
              int seqLen, std::vector<int> pos, bool kvBf16) {

@@ -63,6 +63,13 @@ def gemm_q40(blocks, rows: int, n: int, x, residual=None, norm_w=None, eps: floa
                                                   _np(norm_w), eps))
 
 
+def gemm_f32(w, x, norm_w=None, eps: float = 1e-5) -> torch.Tensor:
+    """Batched (MFMA, v_mfma_f32_16x16x4_f32) matmul for F32 weights [rows][n], 1..256 tokens:
+    x -> RMS norm -> f16 -> W.x (weights exact in f32, f32 accumulate)."""
+    rows, n = w.shape
+    return torch.from_numpy(native().ops.gemm_f32(_np(w), rows, n, _np(x), _np(norm_w), eps))
+
+
 def qkv_rope(blocks, q0: int, kv0: int, head_size: int, n: int, x, norm_w, eps: float, rope, seq_len: int,
              pos, kv_bf16: bool = True):
     """QKV GEMV with the RoPE + KV-cache-append epilogue. Returns (q rotated, k row, v row)."""

@@ -121,6 +121,22 @@ def test_engine_batched_prefill_mfma(C, assets, graphs, n, monkeypatch):
     assert _rel(bat, ref) < 3e-2
 
 
+@pytest.mark.parametrize("n", [7, 40, 72])
+def test_engine_batched_prefill_f32(C, assets, n, monkeypatch):
+    """F32-weight models on the batched path (K5: gemmF32Kernel + fused epilogues) vs sequential
+    f32 GEMV decodes and the CPU reference (the batched path's only rounding: f16 activations)."""
+    rng = np.random.default_rng(100 + n)
+    tokens = [int(t) for t in rng.integers(0, 512, n)]
+    a = C.HipEngine(assets["f32"], "f32", kv_bf16=False, max_batch=128)
+    b = C.HipEngine(assets["f32"], "f32", kv_bf16=False, max_batch=128)
+    seq = _seq(a, tokens)
+    bat = b.forward(tokens, list(range(n)), [0] * n)
+    assert _rel(bat, seq) < 1e-2
+    assert (bat.argmax(-1) == seq.argmax(-1)).mean() >= 0.9
+    cpu = C.cpu_backend(assets["f32"], "f32", 2, max_batch=128)
+    assert _rel(bat, cpu.forward(tokens, list(range(n)), [0] * n)) < 1e-2
+
+
 @pytest.mark.parametrize("gemm_min,tol", [("1000", 1e-4), ("2", 2e-2)])
 def test_engine_slots_independent(C, assets, monkeypatch, gemm_min, tol):
     """Two sequences in different KV slots in one batch == each alone (GEMV batch path exactly,

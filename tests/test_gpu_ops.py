@@ -82,6 +82,21 @@ def test_gemm_q40_mfma(ops, M):
     assert rel(out, ops.ref_rmsnorm(x + r, nw) @ w.T) < 0.12
 
 
+@pytest.mark.parametrize("M", [5, 16, 33, 64, 100])
+def test_gemm_f32_mfma(ops, M):
+    """K5: F32-weight batched matmul on v_mfma_f32_16x16x4_f32 (weights exact, activations f16)
+    vs the fp32 torch reference; 100 tokens take two launches, 1536 rows x 2048 exercise split-K."""
+    rows, n = 1536, 2048
+    w = make_w(rows, n, 11)
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(M, n, generator=g)
+    nw = torch.rand(n, generator=g) + 0.5
+    out = ops.gemm_f32(w, x, nw)
+    xn = ops.ref_rmsnorm(x, nw)
+    assert rel(out, xn.half().float() @ w.T) < 1e-5  # only the f16 activations are rounded
+    assert rel(out, xn @ w.T) < 2e-3
+
+
 @pytest.mark.parametrize("kv_bf16", [True, False])
 def test_qkv_rope_kv_append(ops, kv_bf16):
     hs, q0, kv0, n, seq = 128, 512, 128, 1024, 64
