@@ -1231,13 +1231,15 @@ __device__ __forceinline__ void glds4(const void *g, void *lds) {
 // Split-K combine and fused epilogues shared by the batched GEMMs (Q40 and f32): `acc` holds this
 // lane's C fragments (weight row (local) wave*16 + col, token t*16 + h*4 + i); `smem` must hold
 // MP x 64 floats and is free (all K-loop LDS reads retired behind a barrier); `flag` one int.
+// tileIdx / tiles: this 64-row tile and the launch's tile count (split-K partial slots, counters).
 template <int MT, int EPI>
-__device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc)[MT], char *smem, int *flag) {
+__device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc)[MT], char *smem, int *flag,
+                                           int tileIdx, int tiles) {
     const GemvArgs &a = ga.e;
     constexpr int MP = MT * 16;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int col = lane & 15, h = lane >> 4, rl = wave * 16 + col;
-    const int tileIdx = blockIdx.x, sp = blockIdx.y, S = ga.splits;
+    const int sp = blockIdx.y, S = ga.splits;
     const int R0 = tileIdx * kGemmRows;
     float *tile = reinterpret_cast<float *>(smem);  // [MP][64], stages are free now
     // C layout: weight row (local) wave*16 + col, token t*16 + h*4 + i
@@ -1247,7 +1249,6 @@ __device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc
 #pragma unroll
             for (int i = 0; i < 4; i++) tile[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
     } else {
-        const int tiles = gridDim.x;
         float *part = ga.part + ((size_t)sp * tiles + tileIdx) * MP * kGemmRows;
 #pragma unroll
         for (int t = 0; t < MT; t++)
@@ -1257,6 +1258,7 @@ __device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc
         __syncthreads();
         if (tid == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the fence's own wait may be dropped
             const int old = __hip_atomic_fetch_add(ga.counters + tileIdx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             flag[0] = old == S - 1;
         }
@@ -1264,6 +1266,7 @@ __device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc
         if (!flag[0]) return;
         if (tid == 0) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(ga.counters + tileIdx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
@@ -1419,7 +1422,7 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
         __builtin_amdgcn_s_barrier();  // stage c % STG is refilled at iteration c + 1
     }
 
-    gemmFinish<MT, EPI>(ga, acc, smem, flag);
+    gemmFinish<MT, EPI>(ga, acc, smem, flag, blockIdx.x, gridDim.x);
 }
 
 static int gemmStages4() {  // stage buffers of the 64-token tile (DL_GEMM_STG4, read once)
@@ -1519,7 +1522,7 @@ __global__ __launch_bounds__(kThreads) void gemmF32Kernel(GemmArgs ga) {
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)xv[e], e < 4 ? w0[e] : w1[e - 4], acc[t], 0, 0, 0);
         }
     }
-    gemmFinish<MT, EPI>(ga, acc, smem, flag);
+    gemmFinish<MT, EPI>(ga, acc, smem, flag, blockIdx.x, gridDim.x);
 }
 
 void launchGemmF32(const GemmArgs &ga, int epi, hipStream_t s) {
