@@ -1249,43 +1249,50 @@ __device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc
 #pragma unroll
             for (int i = 0; i < 4; i++) tile[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
     } else {
+        // Partials are written and read with agent-scope atomic accesses (global_store / load sc1:
+        // performed at the coherence point, never held in or served from one XCD's L2), so the
+        // hand-off needs no fence: an agent-scope release / acquire fence is a whole-L2 writeback
+        // (buffer_wbl2) / invalidate (buffer_inv) on gfx950, which measured ~28 us per split level
+        // on w13 (448 -> 896 workgroups) and evicted the other workgroups' cached activations.
+        // vmcnt(0) before the arrival count: every partial store has been performed.
         float *part = ga.part + ((size_t)sp * tiles + tileIdx) * MP * kGemmRows;
 #pragma unroll
         for (int t = 0; t < MT; t++)
 #pragma unroll
-            for (int i = 0; i < 4; i++) part[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
+            for (int i = 0; i < 4; i++)
+                __hip_atomic_store(part + (t * 16 + h * 4 + i) * kGemmRows + rl, acc[t][i], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the fence's own wait may be dropped
             const int old = __hip_atomic_fetch_add(ga.counters + tileIdx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             flag[0] = old == S - 1;
         }
         __syncthreads();
         if (!flag[0]) return;
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(ga.counters + tileIdx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __syncthreads();
-        // combine in split order (deterministic), 16-B loads with all of a thread's splits in
-        // flight at once: this tail runs on one workgroup per tile after the others finished
-        const f32x4 *P = reinterpret_cast<const f32x4 *>(ga.part) + (size_t)tileIdx * MP * kGemmRows / 4;
-        const size_t st4 = (size_t)tiles * MP * kGemmRows / 4;
-        f32x4 *tile4 = reinterpret_cast<f32x4 *>(tile);
+        if (tid == 0) __hip_atomic_store(ga.counters + tileIdx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // combine in split order (deterministic), all of a thread's splits in flight at once: this
+        // tail runs on one workgroup per tile after the others finished
+        const float *P = ga.part + (size_t)tileIdx * MP * kGemmRows;
+        const size_t stp = (size_t)tiles * MP * kGemmRows;
+        auto ld = [](const float *q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
         for (int i = tid; i < MP * kGemmRows / 4; i += kThreads) {
             f32x4 v[8];
 #pragma unroll
             for (int s2 = 0; s2 < 8; s2++)
-                if (s2 < S) v[s2] = P[s2 * st4 + i];
+                if (s2 < S) {
+                    const float *q = P + s2 * stp + 4 * i;
+                    v[s2] = f32x4{ld(q), ld(q + 1), ld(q + 2), ld(q + 3)};
+                }
             f32x4 r = v[0];
 #pragma unroll
             for (int s2 = 1; s2 < 8; s2++)
                 if (s2 < S) r += v[s2];
-            for (int s2 = 8; s2 < S; s2++) r += P[s2 * st4 + i];
-            tile4[i] = r;
+            for (int s2 = 8; s2 < S; s2++) {
+                const float *q = P + s2 * stp + 4 * i;
+                r += f32x4{ld(q), ld(q + 1), ld(q + 2), ld(q + 3)};
+            }
+            reinterpret_cast<f32x4 *>(tile)[i] = r;
         }
     }
     __syncthreads();
