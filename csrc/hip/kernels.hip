@@ -1443,7 +1443,8 @@ static int gemmStages4() {  // stage buffers of the 64-token tile (DL_GEMM_STG4,
 static int gemmStages2() {  // stage buffers of the 32-token tile (DL_GEMM_STG2, read once)
     static const int v = [] {
         const char *e = std::getenv("DL_GEMM_STG2");
-        return e && std::atoi(e) == 1 ? 1 : kGemmStages;
+        const int k = e ? std::atoi(e) : kGemmStages;
+        return k >= 1 && k <= 3 ? k : kGemmStages;
     }();
     return v;
 }
@@ -1472,7 +1473,7 @@ void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
 #define DL_GEMM_CASES(M_, G)                                                                      \
     DL_GEMM_CASE(M_, EPI_STORE, G) DL_GEMM_CASE(M_, EPI_ACT, G) DL_GEMM_CASE(M_, EPI_ACT_Q80, G)  \
     DL_GEMM_CASE(M_, EPI_QKV, G) DL_GEMM_CASE(M_, EPI_ACT_F16, G)
-    DL_GEMM_CASES(1, kGemmStages) DL_GEMM_CASES(1, 3) DL_GEMM_CASES(1, 4) DL_GEMM_CASES(2, kGemmStages) DL_GEMM_CASES(2, 1) DL_GEMM_CASES(4, 1) DL_GEMM_CASES(4, 2)
+    DL_GEMM_CASES(1, kGemmStages) DL_GEMM_CASES(1, 3) DL_GEMM_CASES(1, 4) DL_GEMM_CASES(2, kGemmStages) DL_GEMM_CASES(2, 1) DL_GEMM_CASES(2, 3) DL_GEMM_CASES(4, 1) DL_GEMM_CASES(4, 2)
 #undef DL_GEMM_CASES
 #undef DL_GEMM_CASE
 }
@@ -1735,37 +1736,35 @@ __device__ __forceinline__ bool attnFinish(const AttnArgs &a, int b, int hgIdx, 
     }
     const int G = a.splitGrid;
     const size_t pbase = ((size_t)b * a.nHeads0 + head0) * G;  // [HG][G] chunks of this head group
+    // fence-free hand-off (as gemmFinish): partials stored and read back with agent-scope atomic
+    // accesses (sc1, performed at the coherence point), vmcnt(0) before the arrival count; an
+    // agent-scope fence would write back / invalidate this XCD's whole L2
+    auto st = [](float *q, float v) { __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto ld = [](const float *q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     for (int i = tid; i < HG * HS; i += AT) {
         const int h = i / HS, d = i % HS;
-        a.partO[((pbase + (size_t)h * G) + c) * HS + d] = redL[i];
+        st(a.partO + ((pbase + (size_t)h * G) + c) * HS + d, redL[i]);
     }
     if (tid < HG) {
-        a.partML[((pbase + (size_t)tid * G) + c) * 2] = mlL[tid * 2];
-        a.partML[((pbase + (size_t)tid * G) + c) * 2 + 1] = mlL[tid * 2 + 1];
+        st(a.partML + ((pbase + (size_t)tid * G) + c) * 2, mlL[tid * 2]);
+        st(a.partML + ((pbase + (size_t)tid * G) + c) * 2 + 1, mlL[tid * 2 + 1]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int *cnt = a.counters + (size_t)b * (a.nHeads0 / HG) + hgIdx;
     if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         flagL[0] = old == nSplit - 1;
     }
     __syncthreads();
     if (!flagL[0]) return false;
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
+    if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // every chunk's (max, sum) -> LDS, then per head: global max and chunk weights w = exp(m - M)
     for (int i = tid; i < HG * nSplit; i += AT) {
         const int h = i / nSplit, cc = i % nSplit;
-        const float2 ml = *reinterpret_cast<const float2 *>(a.partML + ((pbase + (size_t)h * G) + cc) * 2);
-        scratch[2 * (h * G + cc)] = ml.x;
-        scratch[2 * (h * G + cc) + 1] = ml.y;
+        const float *ml = a.partML + ((pbase + (size_t)h * G) + cc) * 2;
+        scratch[2 * (h * G + cc)] = ld(ml);
+        scratch[2 * (h * G + cc) + 1] = ld(ml + 1);
     }
     __syncthreads();
     if (tid < HG) {
@@ -1791,11 +1790,11 @@ __device__ __forceinline__ bool attnFinish(const AttnArgs &a, int b, int hgIdx, 
         for (; cc + U <= nSplit; cc += U) {
             float v[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) v[u] = po[(size_t)(cc + u) * HS];
+            for (int u = 0; u < U; u++) v[u] = ld(po + (size_t)(cc + u) * HS);
 #pragma unroll
             for (int u = 0; u < U; u++) acc += wv[2 * (cc + u)] * v[u];
         }
-        for (; cc < nSplit; cc++) acc += wv[2 * cc] * po[(size_t)cc * HS];
+        for (; cc < nSplit; cc++) acc += wv[2 * cc] * ld(po + (size_t)cc * HS);
         redL[i] = acc / mlL[h * 2 + 1];
     }
     __syncthreads();
@@ -2220,32 +2219,27 @@ __global__ __launch_bounds__(kPfThreads) void attnPrefillKernel(AttnArgs a, int 
     // several chunks: publish (every column of the block, masked ones as (-inf, 0, 0)), count in,
     // the last arriver combines
     const int G = a.splitGrid;
+    // fence-free hand-off (see gemmFinish): agent-scope atomic stores here, atomic loads below
+    auto st = [](float *q, float v) { __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto ld = [](const float *q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     if (rowOk) {
         const size_t pb = ((size_t)row * a.nHeads0 + head) * G + c;
 #pragma unroll
         for (int n = 0; n < NT; n++)
-            *reinterpret_cast<float4 *>(a.partO + pb * HS + 16 * n + 4 * h) = make_float4(o[n][0], o[n][1], o[n][2], o[n][3]);
+#pragma unroll
+            for (int e = 0; e < 4; e++) st(a.partO + pb * HS + 16 * n + 4 * h + e, o[n][e]);
         if (h == 0) {
-            a.partML[pb * 2] = m;
-            a.partML[pb * 2 + 1] = lsum;
+            st(a.partML + pb * 2, m);
+            st(a.partML + pb * 2 + 1, lsum);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int *cnt = a.counters + (size_t)rb * nKv + g;
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        flagL = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nSplit - 1;
-    }
+    if (tid == 0) flagL = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nSplit - 1;
     __syncthreads();
     if (!flagL) return;
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
+    if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // per column: chunk weights exp(m_c - M) and the total sum (LDS: the tiles are free now)
     const int nCol = rpb * kvMul;  // 64 columns
     float *wts = reinterpret_cast<float *>(&kT[0][0]);  // [nCol][nSplit]
@@ -2255,11 +2249,12 @@ __global__ __launch_bounds__(kPfThreads) void attnPrefillKernel(AttnArgs a, int 
         float M = -INFINITY, L = 0.f;
         if (r < nRows) {
             const float *ml = a.partML + ((size_t)r * a.nHeads0 + hd) * G * 2;
-            for (int cc = 0; cc < nSplit; cc++) M = fmaxf(M, ml[2 * cc]);
+            for (int cc = 0; cc < nSplit; cc++) M = fmaxf(M, ld(ml + 2 * cc));
             for (int cc = 0; cc < nSplit; cc++) {
-                const float w = (M == -INFINITY || ml[2 * cc] == -INFINITY) ? 0.f : __expf(ml[2 * cc] - M);
+                const float mc = ld(ml + 2 * cc);
+                const float w = (M == -INFINITY || mc == -INFINITY) ? 0.f : __expf(mc - M);
                 wts[tid * nSplit + cc] = w;
-                L += w * ml[2 * cc + 1];
+                L += w * ld(ml + 2 * cc + 1);
             }
         }
         tot[tid] = L;
@@ -2273,8 +2268,8 @@ __global__ __launch_bounds__(kPfThreads) void attnPrefillKernel(AttnArgs a, int 
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
         for (int cc = 0; cc < nSplit; cc++) {
             const float w = wts[cl * nSplit + cc];
-            const float4 x = *reinterpret_cast<const float4 *>(po + (size_t)cc * HS);
-            acc[0] += w * x.x; acc[1] += w * x.y; acc[2] += w * x.z; acc[3] += w * x.w;
+            const float *x = po + (size_t)cc * HS;
+            acc[0] += w * ld(x); acc[1] += w * ld(x + 1); acc[2] += w * ld(x + 2); acc[3] += w * ld(x + 3);
         }
         const float il = tot[cl] > 0.f ? 1.0f / tot[cl] : 0.f;
         const float v[4] = {acc[0] * il, acc[1] * il, acc[2] * il, acc[3] * il};
@@ -2337,26 +2332,22 @@ __global__ __launch_bounds__(256) void argmaxKernel(ArgmaxArgs a) {
     int bi = 0x7fffffff;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.vocab; i += gridDim.x * blockDim.x) argBetter(bv, bi, x[i], i);
     blockArgmax(bv, bi, sv, si);
+    // fence-free hand-off (see gemmFinish): agent-scope atomic stores / loads of the partials
     if (threadIdx.x == 0) {
-        a.partV[b * kArgmaxBlocks + blockIdx.x] = bv;
-        a.partI[b * kArgmaxBlocks + blockIdx.x] = bi;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(a.partV + b * kArgmaxBlocks + blockIdx.x, bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.partI + b * kArgmaxBlocks + blockIdx.x, bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int old = __hip_atomic_fetch_add(a.counters + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last = old == (int)gridDim.x - 1;
     }
     __syncthreads();
     if (!last) return;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(a.counters + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(a.counters + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     bv = -INFINITY;
     bi = 0x7fffffff;
     for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x)
-        argBetter(bv, bi, a.partV[b * kArgmaxBlocks + i], a.partI[b * kArgmaxBlocks + i]);
+        argBetter(bv, bi, __hip_atomic_load(a.partV + b * kArgmaxBlocks + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                  __hip_atomic_load(a.partI + b * kArgmaxBlocks + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     blockArgmax(bv, bi, sv, si);
     if (threadIdx.x == 0 && a.tp.world > 1) {
         // tensor parallel: every rank offers its slice's winner (value, global index); all ranks
