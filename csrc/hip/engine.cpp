@@ -316,6 +316,9 @@ class HipEngineImpl : public HipEngine {
             if (part) dPart_ = dalloc<float>(part);
             const int maxTiles = (std::max<int>({(int)(p.q0 + 2 * p.kv0), (int)h_.dim, (int)(2 * p.hidden0), (int)p.vocab0}) + 63) / 64;
             dGemmCnt_ = dalloc<int>(maxTiles);
+            // fused residual + norm hand-off between batched GEMMs (TP1): per 64-row tile of dim,
+            // per token, the partial sum of squares
+            dSS_ = dalloc<float>((size_t)((h_.dim + 63) / 64) * MB);
             DL_HIP(hipMemsetAsync(dGemmCnt_, 0, sizeof(int) * maxTiles, stream_));
         }
         dAttCnt_ = dalloc<int>((size_t)MB * p.nHeads0);
@@ -767,9 +770,22 @@ class HipEngineImpl : public HipEngine {
 
     // Batched path (>= gemmMinTokens rows, Q40 or F32 weights): per chunk of <= 64 tokens, a norm kernel (f32 ->
     // f16, RESNORM) or the producer's f16 rows (xh) feed the MFMA GEMM with the fused epilogue.
+    // Residual + norm fusion between batched GEMMs at TP1 (DL_GEMM_FUSE_NORM=0 disables, read per
+    // call): wo / w2 end with EPI_RES (x' = x + out, x' * normW -> f16, per-tile sums of squares)
+    // and the next GEMM applies the RMS scale per token in its epilogue: no norm kernel between.
+    struct ResFuse {
+        const float *resIn;
+        float *resOut;
+        const float *w;
+    };
+    bool fuseNorm() const {
+        const char *e = std::getenv("DL_GEMM_FUSE_NORM");
+        return plan_.nRanks == 1 && !(e && *e == '0');
+    }
+
     void gemmBatched(const DevMat &m, int n, int epi, const float *in, int ldIn, const float *add, float *xNext,
                      const float *normW, const _Float16 *xh, float *out, int ldOut, _Float16 *outH,
-                     const DevLayer *L) {
+                     const DevLayer *L, const ResFuse *rf = nullptr, bool ssIn = false) {
         for (int c0 = 0; c0 < n; c0 += kGemmMaxTokens) {
             const int bc = std::min(kGemmMaxTokens, n - c0);
             hipk::GemmArgs g;
@@ -780,7 +796,13 @@ class HipEngineImpl : public HipEngine {
             a.rows = m.rows;
             a.n = m.n;
             a.lanes = m.lanes;
-            if (!xh) {
+            a.eps = h_.normEpsilon;
+            if (ssIn) {  // input = the producer's x' * normW rows; RMS scale applied per token
+                g.x = dXh_ + (size_t)c0 * m.n;
+                g.ssIn = dSS_ + c0;
+                g.ssTiles = (h_.dim + 63) / 64;
+                g.ldSS = (int)cfg_.maxBatch;
+            } else if (!xh) {
                 hipk::GemvArgs nq;
                 nq.n = m.n;
                 nq.in = in + (size_t)c0 * ldIn;
@@ -809,6 +831,14 @@ class HipEngineImpl : public HipEngine {
                 a.kcache = L->k;
                 a.vcache = L->v;
                 a.kvBf16 = kvBf16_ ? 1 : 0;
+            }
+            if (rf) {
+                g.resIn = rf->resIn + (size_t)c0 * ldOut;
+                g.resOut = rf->resOut + (size_t)c0 * ldOut;
+                g.resW = rf->w;
+                g.resX = dXh_ + (size_t)c0 * ldOut;
+                g.ssOut = dSS_ + c0;
+                g.ldSS = (int)cfg_.maxBatch;
             }
             g.M = bc;
             g.splits = hipk::gemmSplits(m.rows, m.n, bc);
@@ -842,12 +872,16 @@ class HipEngineImpl : public HipEngine {
             hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_);
         }
         const bool bat = batchedPath(n);  // MFMA GEMMs on f16 activations instead of GEMVs
+        const bool fz = bat && fuseNorm();  // residual + norm carried by the GEMM epilogues
         for (u32 l = 0; l < h_.nLayers; l++) {
             DevLayer &L = layers_[l];
             const bool hasDelta = l > 0;
             {
                 ProfScope ps(this, "gemv_qkv");
-                if (bat)
+                if (fz && hasDelta)
+                    gemmBatched(L.qkv, n, hipk::EPI_QKV, nullptr, dim, nullptr, nullptr, nullptr, nullptr, dQ_, p.q0,
+                                nullptr, &L, nullptr, true);
+                else if (bat)
                     gemmBatched(L.qkv, n, hipk::EPI_QKV, dX_[cur], dim, hasDelta ? dY_ : nullptr,
                                 hasDelta ? dX_[cur ^ 1] : nullptr, L.rmsAtt, nullptr, dQ_, p.q0, nullptr, &L);
                 else
@@ -899,7 +933,11 @@ class HipEngineImpl : public HipEngine {
             }
             {
                 ProfScope ps(this, "gemv_wo");
-                if (bat)
+                if (fz) {
+                    const ResFuse rf{dX_[cur], dX_[cur ^ 1], L.rmsFfn};
+                    gemmBatched(L.wo, n, hipk::EPI_RES, nullptr, 0, nullptr, nullptr, nullptr, dAttH_, nullptr, dim,
+                                nullptr, nullptr, &rf);
+                } else if (bat)
                     gemmBatched(L.wo, n, hipk::EPI_STORE, nullptr, 0, nullptr, nullptr, nullptr, dAttH_, dY_, dim,
                                 nullptr, nullptr);
                 else
@@ -912,7 +950,10 @@ class HipEngineImpl : public HipEngine {
             const bool hQ80 = q40_ && p.hidden0 / 32 >= 192;
             {
                 ProfScope ps(this, "gemv_w13");
-                if (bat)
+                if (fz)
+                    gemmBatched(L.w13, n, hipk::EPI_ACT_F16, nullptr, dim, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                p.hidden0, dHh_, nullptr, nullptr, true);
+                else if (bat)
                     gemmBatched(L.w13, n, hipk::EPI_ACT_F16, dX_[cur], dim, dY_, dX_[cur ^ 1], L.rmsFfn, nullptr,
                                 nullptr, p.hidden0, dHh_, nullptr);
                 else
@@ -922,7 +963,12 @@ class HipEngineImpl : public HipEngine {
             cur ^= 1;
             {
                 ProfScope ps(this, "gemv_w2");
-                if (bat)
+                if (fz) {
+                    const float *wNext = l + 1 < h_.nLayers ? layers_[l + 1].rmsAtt : rmsFinal_;
+                    const ResFuse rf{dX_[cur], dX_[cur ^ 1], wNext};
+                    gemmBatched(L.w2, n, hipk::EPI_RES, nullptr, 0, nullptr, nullptr, nullptr, dHh_, nullptr, dim,
+                                nullptr, nullptr, &rf);
+                } else if (bat)
                     gemmBatched(L.w2, n, hipk::EPI_STORE, nullptr, 0, nullptr, nullptr, nullptr, dHh_, dY_, dim,
                                 nullptr, nullptr);
                 else if (hQ80 || !q40_)
@@ -936,7 +982,10 @@ class HipEngineImpl : public HipEngine {
         }
         {
             ProfScope ps(this, "gemv_logits");
-            if (bat)
+            if (fz)
+                gemmBatched(wcls_, n, hipk::EPI_STORE, nullptr, dim, nullptr, nullptr, nullptr, nullptr, dLogits_,
+                            p.vocab0, nullptr, nullptr, nullptr, true);
+            else if (bat)
                 gemmBatched(wcls_, n, hipk::EPI_STORE, dX_[cur], dim, dY_, nullptr, rmsFinal_, nullptr, dLogits_,
                             p.vocab0, nullptr, nullptr);
             else
@@ -993,6 +1042,7 @@ class HipEngineImpl : public HipEngine {
     _Float16 *dXh_ = nullptr, *dAttH_ = nullptr, *dHh_ = nullptr;
     float *dPart_ = nullptr;
     int *dGemmCnt_ = nullptr;
+    float *dSS_ = nullptr;
 
     EngineConfig cfg_;
     DeviceComm *comm_;

@@ -28,7 +28,9 @@ namespace hipk {
 enum Prologue : int { PRO_GLOBAL = 0, PRO_RESNORM = 1 };
 // EPI_ACT_Q80: act(w1 x) * (w3 x), quantized to Q80 blocks for the next GEMV (32 hidden units/block).
 // EPI_STORE_TP: EPI_STORE whose rows are first all-reduced over the tensor-parallel ranks (GemvArgs::tp).
-enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2, EPI_ACT_Q80 = 3, EPI_ACT_F16 = 4, EPI_STORE_TP = 5 };
+// EPI_RES (batched GEMMs): residual update fused with the next RMS norm's elementwise half - see
+// GemmArgs::resIn.
+enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2, EPI_ACT_Q80 = 3, EPI_ACT_F16 = 4, EPI_STORE_TP = 5, EPI_RES = 6 };
 
 // Q40 weights live on the device TILED in the ring GEMV's consumption order, for a lanes-per-row
 // count L fixed per matrix (NG = 256/L row pairs per workgroup pass, K = ceil(nb/L) steps):
@@ -146,6 +148,18 @@ struct GemmArgs {
     int splits = 1;
     float *part = nullptr;
     int *counters = nullptr;
+    // EPI_RES (producer of the next norm's input, wo / w2 at TP1): x' = resIn + out -> resOut (f32,
+    // [M][ldOut]), resX = x' * resW as f16 (the norm's per-column half) and per 64-row tile the
+    // partial sum of squares ssOut[tile * ldSS + t]: the RMS reduction is left to the consumer.
+    const float *resIn = nullptr;
+    float *resOut = nullptr;
+    const float *resW = nullptr;
+    _Float16 *resX = nullptr;
+    float *ssOut = nullptr;
+    // consumer side (x = a producer's resX): ssIn != null -> each output row t is scaled by
+    // 1 / sqrt(sum_j ssIn[j * ldSS + t] / n + eps) (ssTiles partials, summed in tile order)
+    const float *ssIn = nullptr;
+    int ssTiles = 0, ldSS = 0;
 };
 void launchGemmQ40(const GemmArgs &a, int epi, hipStream_t s);
 // Same contract for F32 weights (`e.wf` [rows][n] row-major; EPI_ACT_Q80 not supported).

@@ -1175,6 +1175,9 @@ int gemmSplits(int rows, int n, int M) {
     const int target = gemmWgTarget(), maxS = gemmMaxSplits();
     int S = 1;
     while (2 * S <= maxS && tiles * S < target && nb % (2 * S) == 0 && nb / (2 * S) >= kGemmCh) S *= 2;
+    // deep K (w2: 4096 x 14336): keep splitting up to two workgroups per CU while every split
+    // still streams >= 4 chunks (measured w2 M=8 23.9 -> 19.6 us; shallower matrices lose)
+    while (2 * S <= maxS && tiles * 2 * S <= 2 * target && nb % (2 * S) == 0 && nb / (2 * S) >= 4 * kGemmCh) S *= 2;
     return S;
 }
 
@@ -1193,7 +1196,7 @@ __host__ __device__ static constexpr int gemmStageBytes(int MT) { return kStW + 
 #define DL_GEMM_STAGES 2  // 3 stages (2 WGs/CU) measured slower: batch-32 8.1k vs 8.8k tok/s
 #endif
 static constexpr int kGemmStages = DL_GEMM_STAGES;  // stage buffers (kGemmStages-1 chunks in flight)
-static size_t gemmLds(int MT, int stages) { return stages * (size_t)gemmStageBytes(MT) + 16; }
+static size_t gemmLds(int MT, int stages) { return stages * (size_t)gemmStageBytes(MT) + 16 + 320 * 4; }  // + flag, row scales
 
 // 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d via the 0x6400 | q magic (1024 + q)
 __device__ __forceinline__ half8 dequantQ40x8(u32x2 wv, int nibHi, uint32_t d16) {
@@ -1295,12 +1298,50 @@ __device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc
             reinterpret_cast<f32x4 *>(tile)[i] = r;
         }
     }
+    // consumer of a fused residual + norm: per-token RMS scale from the producer's tile partials
+    float *rsL = reinterpret_cast<float *>(flag + 4);  // [64]
+    if (ga.ssIn) {
+        // TPT threads per token each sum a strided slice of the tile partials (independent loads
+        // in flight), then one thread per token adds the TPT slices in order (deterministic)
+        float *slL = rsL + 64;  // [256]
+        constexpr int TPT = kThreads / MP;
+        const int t = tid / TPT, q = tid % TPT;
+        float ssum = 0.f;
+        if (t < ga.M) {
+#pragma unroll 8
+            for (int j = q; j < ga.ssTiles; j += TPT) ssum += ga.ssIn[(size_t)j * ga.ldSS + t];
+        }
+        slL[tid] = ssum;
+        __syncthreads();
+        if (tid < ga.M) {
+            float tot = 0.f;
+            for (int i = 0; i < TPT; i++) tot += slL[tid * TPT + i];
+            rsL[tid] = 1.0f / sqrtf(tot / (float)a.n + a.eps);
+        }
+    }
     __syncthreads();
     // fused epilogues on row pairs (2k, 2k+1) of the tile, 32 pairs per token
     for (int i = tid; i < ga.M * 32; i += kThreads) {
         const int t = i >> 5, k = i & 31, r0 = R0 + 2 * k;
-        const float v0 = tile[t * kGemmRows + 2 * k], v1 = tile[t * kGemmRows + 2 * k + 1];
-        if constexpr (EPI == EPI_STORE) {
+        float v0 = tile[t * kGemmRows + 2 * k], v1 = tile[t * kGemmRows + 2 * k + 1];
+        if (ga.ssIn) {
+            v0 *= rsL[t];
+            v1 *= rsL[t];
+        }
+        if constexpr (EPI == EPI_RES) {
+            float x0 = 0.f, x1 = 0.f;
+            if (r0 < a.rows) {  // a.rows even: whole pairs
+                const size_t o = (size_t)t * a.ldOut + r0;
+                x0 = ga.resIn[o] + v0;
+                x1 = ga.resIn[o + 1] + v1;
+                ga.resOut[o] = x0;
+                ga.resOut[o + 1] = x1;
+                ga.resX[o] = (_Float16)(x0 * ga.resW[r0]);
+                ga.resX[o + 1] = (_Float16)(x1 * ga.resW[r0 + 1]);
+            }
+            const float ssq = groupSum<32>(x0 * x0 + x1 * x1);  // the 32 pairs of token t, in lane order
+            if (k == 0) ga.ssOut[(size_t)tileIdx * ga.ldSS + t] = ssq;
+        } else if constexpr (EPI == EPI_STORE) {
             if (r0 < a.rows) a.out[(size_t)t * a.ldOut + r0] = v0;
             if (r0 + 1 < a.rows) a.out[(size_t)t * a.ldOut + r0 + 1] = v1;
         } else if constexpr (EPI == EPI_ACT) {
@@ -1472,7 +1513,7 @@ void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
     }
 #define DL_GEMM_CASES(M_, G)                                                                      \
     DL_GEMM_CASE(M_, EPI_STORE, G) DL_GEMM_CASE(M_, EPI_ACT, G) DL_GEMM_CASE(M_, EPI_ACT_Q80, G)  \
-    DL_GEMM_CASE(M_, EPI_QKV, G) DL_GEMM_CASE(M_, EPI_ACT_F16, G)
+    DL_GEMM_CASE(M_, EPI_QKV, G) DL_GEMM_CASE(M_, EPI_ACT_F16, G) DL_GEMM_CASE(M_, EPI_RES, G)
     DL_GEMM_CASES(1, kGemmStages) DL_GEMM_CASES(1, 3) DL_GEMM_CASES(1, 4) DL_GEMM_CASES(2, kGemmStages) DL_GEMM_CASES(2, 1) DL_GEMM_CASES(2, 3) DL_GEMM_CASES(4, 1) DL_GEMM_CASES(4, 2)
 #undef DL_GEMM_CASES
 #undef DL_GEMM_CASE
@@ -1537,7 +1578,7 @@ void launchGemmF32(const GemmArgs &ga, int epi, hipStream_t s) {
     const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
     const int MT = gemmTokenPad(ga.M) / 16;
     const dim3 grid(tiles, ga.splits);
-    const size_t lds = (size_t)MT * 16 * kGemmRows * 4 + 16;
+    const size_t lds = (size_t)MT * 16 * kGemmRows * 4 + 16 + 320 * 4;  // + flag, row scales
 #define DL_GEMMF_CASE(M_, E)                                                              \
     if (MT == M_ && epi == E) {                                                           \
         if (lds > 65536) allowLds((const void *)gemmF32Kernel<M_, E>, lds);               \
@@ -1546,7 +1587,7 @@ void launchGemmF32(const GemmArgs &ga, int epi, hipStream_t s) {
     }
 #define DL_GEMMF_CASES(M_)                                                                \
     DL_GEMMF_CASE(M_, EPI_STORE) DL_GEMMF_CASE(M_, EPI_ACT) DL_GEMMF_CASE(M_, EPI_QKV)    \
-    DL_GEMMF_CASE(M_, EPI_ACT_F16)
+    DL_GEMMF_CASE(M_, EPI_ACT_F16) DL_GEMMF_CASE(M_, EPI_RES)
     DL_GEMMF_CASES(1) DL_GEMMF_CASES(2) DL_GEMMF_CASES(4)
 #undef DL_GEMMF_CASES
 #undef DL_GEMMF_CASE
