@@ -30,14 +30,16 @@ struct Bar {
 __device__ __forceinline__ long long rt() { return (long long)__builtin_amdgcn_s_memrealtime(); }
 
 // Sense-reversal barrier; HIER = per-XCD (blockIdx % 8) counters first, then one top counter.
-template <bool HIER>
+// FENCE = agent-scope release/acquire fences around it (on gfx950: whole-L2 writeback /
+// invalidate); without, stage data must be handed over with agent-scope atomic (sc1) accesses.
+template <bool HIER, bool FENCE = true>
 __device__ __forceinline__ bool gridBarrier(Bar *b) {
     __shared__ int ok;
     __syncthreads();
     if (threadIdx.x == 0) {
         ok = 1;
         const unsigned g = __hip_atomic_load(&b->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (FENCE) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         bool last;
         if (HIER) {
             const int grp = blockIdx.x & 7;
@@ -54,7 +56,8 @@ __device__ __forceinline__ bool gridBarrier(Bar *b) {
             if (last) __hip_atomic_store(&b->top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (last) {
-            __hip_atomic_store(&b->gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            if (FENCE) __hip_atomic_store(&b->gen, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            else __hip_atomic_store(&b->gen, g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
             const long long t0 = rt();
             while (__hip_atomic_load(&b->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
@@ -67,16 +70,16 @@ __device__ __forceinline__ bool gridBarrier(Bar *b) {
                 }
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
     return ok;
 }
 
-template <bool HIER>
+template <bool HIER, bool FENCE = true>
 __global__ __launch_bounds__(256) void barrierLoop(Bar *b, int iters, unsigned *out) {
     for (int i = 0; i < iters; i++)
-        if (!gridBarrier<HIER>(b)) return;
+        if (!gridBarrier<HIER, FENCE>(b)) return;
     if (threadIdx.x == 0 && blockIdx.x == 0) out[0] = 1;
 }
 
@@ -99,13 +102,13 @@ __device__ __forceinline__ unsigned streamShare(const u32x4 *p, size_t n16) {
     return acc;
 }
 
-template <bool HIER>
+template <bool HIER, bool FENCE = true>
 __global__ __launch_bounds__(256) void persistentStages(const u32x4 *const *bufs, int nBufs, size_t n16, int stages,
                                                         Bar *b, unsigned *out) {
     unsigned acc = 0;
     for (int s = 0; s < stages; s++) {
         acc ^= streamShare(bufs[s % nBufs], n16);
-        if (!gridBarrier<HIER>(b)) return;
+        if (!gridBarrier<HIER, FENCE>(b)) return;
     }
     if (acc == 0x12345678) out[1] = acc;
 }
@@ -132,10 +135,12 @@ int main() {
 
     const int iters = 2000;
     for (int G : {cus, 2 * cus}) {
-        for (int hier = 0; hier < 2; hier++) {
+        for (int hier = 0; hier < 4; hier++) {  // 0/1 flat/hier with fences, 2/3 fence-free
             auto run = [&]() {
-                if (hier) hipLaunchKernelGGL(barrierLoop<true>, dim3(G), dim3(256), 0, s, bar, iters, out);
-                else hipLaunchKernelGGL(barrierLoop<false>, dim3(G), dim3(256), 0, s, bar, iters, out);
+                if (hier == 1) hipLaunchKernelGGL((barrierLoop<true, true>), dim3(G), dim3(256), 0, s, bar, iters, out);
+                else if (hier == 0) hipLaunchKernelGGL((barrierLoop<false, true>), dim3(G), dim3(256), 0, s, bar, iters, out);
+                else if (hier == 3) hipLaunchKernelGGL((barrierLoop<true, false>), dim3(G), dim3(256), 0, s, bar, iters, out);
+                else hipLaunchKernelGGL((barrierLoop<false, false>), dim3(G), dim3(256), 0, s, bar, iters, out);
             };
             run();
             CK(hipStreamSynchronize(s));
@@ -147,7 +152,8 @@ int main() {
             CK(hipEventElapsedTime(&ms, e0, e1));
             unsigned ab = 0;
             CK(hipMemcpy(&ab, &bar->abort, 4, hipMemcpyDeviceToHost));
-            printf("barrier G=%d %s: %.3f us per barrier%s\n", G, hier ? "hier" : "flat", ms * 1000 / iters,
+            printf("barrier G=%d %s%s: %.3f us per barrier%s\n", G, (hier & 1) ? "hier" : "flat",
+                   hier >= 2 ? " fence-free" : "", ms * 1000 / iters,
                    ab ? " (ABORTED)" : "");
             if (ab) return 1;
         }
@@ -166,11 +172,13 @@ int main() {
         CK(hipMalloc(&dBufs, nBufs * sizeof(void *)));
         CK(hipMemcpy(dBufs, bufs.data(), nBufs * sizeof(void *), hipMemcpyHostToDevice));
         const size_t n16 = bytes / 16;
-        float msP[2] = {0, 0};
-        for (int hier = 0; hier < 2; hier++) {
+        float msP[4] = {0, 0, 0, 0};
+        for (int hier = 0; hier < 4; hier++) {
             auto run = [&]() {
-                if (hier) hipLaunchKernelGGL(persistentStages<true>, dim3(cus), dim3(256), 0, s, dBufs, nBufs, n16, stages, bar, out);
-                else hipLaunchKernelGGL(persistentStages<false>, dim3(cus), dim3(256), 0, s, dBufs, nBufs, n16, stages, bar, out);
+                if (hier == 1) hipLaunchKernelGGL((persistentStages<true, true>), dim3(cus), dim3(256), 0, s, dBufs, nBufs, n16, stages, bar, out);
+                else if (hier == 0) hipLaunchKernelGGL((persistentStages<false, true>), dim3(cus), dim3(256), 0, s, dBufs, nBufs, n16, stages, bar, out);
+                else if (hier == 3) hipLaunchKernelGGL((persistentStages<true, false>), dim3(cus), dim3(256), 0, s, dBufs, nBufs, n16, stages, bar, out);
+                else hipLaunchKernelGGL((persistentStages<false, false>), dim3(cus), dim3(256), 0, s, dBufs, nBufs, n16, stages, bar, out);
             };
             run();
             CK(hipStreamSynchronize(s));
@@ -194,8 +202,9 @@ int main() {
         CK(hipEventSynchronize(e1));
         float msG = 0;
         CK(hipEventElapsedTime(&msG, e0, e1));
-        printf("stage %5.1f MB: persistent flat %.2f us, hier %.2f us | graph of kernels %.2f us per stage\n", mb,
-               msP[0] * 1000 / stages, msP[1] * 1000 / stages, msG * 1000 / stages);
+        printf("stage %5.1f MB: persistent flat %.2f us, hier %.2f us, fence-free flat %.2f us, hier %.2f us | graph of "
+               "kernels %.2f us per stage\n", mb, msP[0] * 1000 / stages, msP[1] * 1000 / stages, msP[2] * 1000 / stages,
+               msP[3] * 1000 / stages, msG * 1000 / stages);
         CK(hipGraphExecDestroy(ge));
         CK(hipGraphDestroy(g));
         for (auto p : bufs) CK(hipFree(p));
