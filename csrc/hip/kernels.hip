@@ -2332,7 +2332,21 @@ __global__ void embeddingKernel(const float *table, const int *tokens, float *x,
     const int b = blockIdx.x;
     const float *src = table + (size_t)tokens[b] * dim;
     float *dst = x + (size_t)b * dim;
-    for (int i = threadIdx.x * 4; i < dim; i += blockDim.x * 4) st4(dst + i, ld4(src + i));
+    // all of a thread's row loads in flight before the first store (one HBM round trip, not four)
+    constexpr int U = 4;
+    for (int i0 = threadIdx.x * 4; i0 < dim; i0 += U * blockDim.x * 4) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int i = i0 + u * blockDim.x * 4;
+            if (i < dim) v[u] = ld4(src + i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int i = i0 + u * blockDim.x * 4;
+            if (i < dim) st4(dst + i, v[u]);
+        }
+    }
 }
 
 void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s) {
@@ -2371,7 +2385,22 @@ __global__ __launch_bounds__(256) void argmaxKernel(ArgmaxArgs a) {
     const float *x = a.logits + (size_t)b * a.vocab;
     float bv = -INFINITY;
     int bi = 0x7fffffff;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.vocab; i += gridDim.x * blockDim.x) argBetter(bv, bi, x[i], i);
+    // 8 loads in flight per thread per round (a plain grid-stride loop waits for each load in turn)
+    constexpr int U = 8;
+    const int stride = gridDim.x * blockDim.x;
+    for (int i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < a.vocab; i0 += U * stride) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int i = i0 + u * stride;
+            v[u] = i < a.vocab ? x[i] : -INFINITY;
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int i = i0 + u * stride;
+            if (i < a.vocab) argBetter(bv, bi, v[u], i);
+        }
+    }
     blockArgmax(bv, bi, sv, si);
     // fence-free hand-off (see gemmFinish): agent-scope atomic stores / loads of the partials
     if (threadIdx.x == 0) {
