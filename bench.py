@@ -175,10 +175,12 @@ def main() -> int:
             eng = make_engine()
 
     # eval: prefill the prompt (chunks of 32 rows per forward, like the reference nBatches=32);
-    # one untimed chunk first so the batch-32 graph is captured outside the timed region
+    # two untimed chunks first (the engine runs a row count eagerly on first use and captures its
+    # graph on the second) so the timed chunks replay the batch-32 graph
     if len(prompt) >= 32:
-        for b in range(B):
-            eng.forward_argmax(prompt[:32], list(range(32)), [b] * 32)
+        for _ in range(2):
+            for b in range(B):
+                eng.forward_argmax(prompt[:32], list(range(32)), [b] * 32)
     torch.cuda.synchronize()
     barrier()
     te = time.perf_counter()
@@ -235,7 +237,8 @@ def main() -> int:
         del eng
         eng = make_engine(4096 + 8)
         p4k = [(i * 7919 + 13) % 128000 for i in range(4096)]
-        eng.forward_argmax(p4k[:32], list(range(32)), [0] * 32)  # graph capture outside the timing
+        for _ in range(2):  # eager first use, then graph capture - both outside the timing
+            eng.forward_argmax(p4k[:32], list(range(32)), [0] * 32)
         barrier()
         torch.cuda.synchronize()
         tp4 = time.perf_counter()

@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <unordered_set>
 #include <vector>
 
 #include "../core/quant.h"
@@ -616,6 +617,13 @@ class HipEngineImpl : public HipEngine {
         const int key = (n * 4 + (int)kind) * 2 + (prefillOk_ ? 1 : 0);
         auto it = graphs_.find(key);
         if (it == graphs_.end()) {
+            // capture on the second use of a shape: a one-off row count (the tail chunk of a prompt,
+            // a serving batch seen once) runs eagerly instead of paying capture + instantiation
+            // (several ms for ~170 kernel nodes) for a graph that would never be replayed
+            if (graphSeen_.insert(key).second) {
+                enqueueForward(n, kind);
+                return;
+            }
             hipGraphExec_t ge = captureForward(n, kind);
             if (!ge) {
                 // e.g. a collective library build that cannot be stream-captured: stay correct, run eagerly
@@ -1042,6 +1050,7 @@ class HipEngineImpl : public HipEngine {
     _Float16 *dXh_ = nullptr, *dAttH_ = nullptr, *dHh_ = nullptr;
     float *dPart_ = nullptr;
     int *dGemmCnt_ = nullptr;
+    std::unordered_set<int> graphSeen_;  // graph keys used once (captured on the second use)
     float *dSS_ = nullptr;
 
     EngineConfig cfg_;
