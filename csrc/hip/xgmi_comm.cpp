@@ -18,7 +18,7 @@
 // and each rank polls its OWN buffer until every word carries the current epoch, then sums the
 // ranks' values in rank order. Data and flag travel in the same atomic 8-byte store, so there is
 // no release fence, no separate flag store and no remote read: one one-way xGMI trip per call
-// (the pull protocol below needs a fence, a flag trip and a remote read round trip). Receive
+// (the pull protocol below needs a flag trip and a remote read round trip, no fence). Receive
 // buffers alternate by epoch parity per chunk; a rank can only write epoch e+2 into a peer's
 // buffer after finishing call e+1, which needed that peer's e+1 data, which the peer only sends
 // after it finished reading epoch e.
@@ -90,19 +90,28 @@ __global__ __launch_bounds__(kThreads) void xgmiKernel(XgmiCall a) {
     __syncthreads();
     const int e = sEpoch, q = e & 1;
     float *myPub = a.peers.pub[a.rank] + (long long)q * a.maxFloats;
+    // Published data is written and read with system-scope atomic accesses (performed at the
+    // memory side, never served from a cached line), so no fence is needed around the flags: a
+    // system-scope release / acquire fence is a whole-L2 writeback / invalidate on gfx950.
+    auto pst = [](float *p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+    auto pld = [](const float *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
     // 1. publish my chunks
     for (long long c = g; c < nChunks; c += kSlots) {
         const long long i = c * kChunk + tid * 4;
         if (i + 3 < a.n) {
-            *reinterpret_cast<float4 *>(myPub + i) = *reinterpret_cast<const float4 *>(a.in + i);
+            const float4 v = *reinterpret_cast<const float4 *>(a.in + i);
+            pst(myPub + i, v.x);
+            pst(myPub + i + 1, v.y);
+            pst(myPub + i + 2, v.z);
+            pst(myPub + i + 3, v.w);
         } else {
-            for (long long k = i; k < a.n; k++) myPub[k] = a.in[k];
+            for (long long k = i; k < a.n; k++) pst(myPub + k, a.in[k]);
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every publish store performed
     __syncthreads();
     // 2. signal every peer, then wait for every peer's signal (one lane per peer)
     if (tid < a.world) {
-        __threadfence_system();  // release: my chunks are visible at system scope
         if (tid != a.rank) {
             int *remote = a.peers.flags[tid] + a.rank * kSlots + g;
             __hip_atomic_store(remote, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -118,7 +127,6 @@ __global__ __launch_bounds__(kThreads) void xgmiKernel(XgmiCall a) {
                 }
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system-scope acquire: drop stale lines
     }
     __syncthreads();
     // 3. reduce (rank order, identical on every rank) or gather
@@ -132,8 +140,10 @@ __global__ __launch_bounds__(kThreads) void xgmiKernel(XgmiCall a) {
                 float4 v[kMaxRanks];  // all peers' loads in flight at once
 #pragma unroll
                 for (int p = 0; p < kMaxRanks; p++)
-                    if (p < a.world)
-                        v[p] = *reinterpret_cast<const float4 *>(a.peers.pub[p] + (long long)q * a.maxFloats + i);
+                    if (p < a.world) {
+                        const float *src = a.peers.pub[p] + (long long)q * a.maxFloats + i;
+                        v[p] = make_float4(pld(src), pld(src + 1), pld(src + 2), pld(src + 3));
+                    }
 #pragma unroll
                 for (int p = 0; p < kMaxRanks; p++)
                     if (p < a.world) {
@@ -146,7 +156,7 @@ __global__ __launch_bounds__(kThreads) void xgmiKernel(XgmiCall a) {
             } else {
                 for (long long k = 0; k < cnt; k++) {
                     float s = 0.f;
-                    for (int p = 0; p < a.world; p++) s += a.peers.pub[p][(long long)q * a.maxFloats + i + k];
+                    for (int p = 0; p < a.world; p++) s += pld(a.peers.pub[p] + (long long)q * a.maxFloats + i + k);
                     a.out[i + k] = s;
                 }
             }
@@ -154,10 +164,7 @@ __global__ __launch_bounds__(kThreads) void xgmiKernel(XgmiCall a) {
             for (int p = 0; p < a.world; p++) {
                 const float *src = a.peers.pub[p] + (long long)q * a.maxFloats + i;
                 float *dst = a.out + (long long)p * a.n + i;
-                if (cnt == 4)
-                    *reinterpret_cast<float4 *>(dst) = *reinterpret_cast<const float4 *>(src);
-                else
-                    for (long long k = 0; k < cnt; k++) dst[k] = src[k];
+                for (long long k = 0; k < cnt; k++) dst[k] = pld(src + k);
             }
         }
     }
