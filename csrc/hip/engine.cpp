@@ -755,9 +755,12 @@ class HipEngineImpl : public HipEngine {
 
     // rows per forward from which the MFMA GEMM replaces the GEMV (DL_GEMM_MIN, read per call so
     // tests can compare both paths in one process)
-    static int gemmMinTokens() {
+    // Default: GEMV up to 2 rows at TP1 (8B ms/step GEMV vs MFMA GEMM: 1.90 vs 2.64 at 2 rows, 3.15 vs
+    // 2.67 at 3, 2.92 vs 2.66 at 4, after the fence-free split-K); up to 4 rows at TP > 1, where the
+    // GEMV path carries the fused exchange.
+    int gemmMinTokens() const {
         const char *e = std::getenv("DL_GEMM_MIN");
-        return e && *e ? std::atoi(e) : 5;  // GEMV up to 4 rows: 1.78 vs 3.44 ms/step at 2, 2.77 vs 3.47 at 4 (8B)
+        return e && *e ? std::atoi(e) : (plan_.nRanks > 1 ? 5 : 3);
     }
 
     bool batchedPath(int n) const {
