@@ -1406,11 +1406,11 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     auto issue = [&](int c, int b) {
         char *st = smem + b * SB;
         const int c0 = j0 + c * kGemmCh;
-        // weights: unit u = s*256 + tid -> (row_l = u/8, position p = u%8) holds block p ^ (row_l&7)
+        // weights: unit u = s*256 + tid -> (row_l = u/8, position p = u%8) holds block p ^ ((row_l>>1)&7)
 #pragma unroll
         for (int s = 0; s < NW; s++) {
             const int u = s * kThreads + tid, rl = u / kGemmCh, pp = u % kGemmCh;
-            const size_t unit = unitOf(R0 + rl, c0 + (pp ^ (rl & (kGemmCh - 1))));
+            const size_t unit = unitOf(R0 + rl, c0 + (pp ^ ((rl >> 1) & (kGemmCh - 1))));
             glds16(qs + unit * 16, st + (size_t)(s * kThreads + wave * 64) * 16);
         }
         // pair scales: u = tid -> (pair_l = u/8, block u%8), 4 B each
@@ -1454,7 +1454,10 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
         const int cn = min(kGemmCh, bps - c * kGemmCh);
 #pragma unroll
         for (int jj = 0; jj < kGemmCh; jj++) {
-            const int pp = jj ^ (rl & (kGemmCh - 1));
+            // swizzle key (rl >> 1) & 7: the 16 rows of a wave's ds_read_b64 (two 8-B halves per
+            // 16-B unit) land on 32 distinct bank pairs (rows 128 B apart alias every other row;
+            // the old key rl & 7 left 2-way conflicts: SQ_LDS_BANK_CONFLICT 25 % of LDS cycles)
+            const int pp = jj ^ ((rl >> 1) & (kGemmCh - 1));
             const u32x2 wv = *reinterpret_cast<const u32x2 *>(st + (size_t)(rl * kGemmCh + pp) * 16 + byteHalf * 8);
             const uint32_t dw = *reinterpret_cast<const uint32_t *>(st + kStW + (size_t)((rl >> 1) * kGemmCh + jj) * 4);
             const uint32_t d16 = jj < cn ? ((rl & 1) ? dw >> 16 : dw & 0xFFFFu) : 0u;
