@@ -16,8 +16,17 @@ the product path through `build/dllama inference --synthetic llama3_1_8b` (cli_*
 round trips included).
 
     python bench.py --gpus 1 --steps 128 --warmup 16
+    python bench.py --gpus 8 --steps 128 --warmup 16        # launches its own 8 ranks
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 bench.py --gpus 8 --steps 128 --warmup 16
+
+Multi-GPU: one process per GPU. Started without a launcher (no WORLD_SIZE) and --gpus N > 1, the
+parent spawns the N ranks itself (before touching any GPU), relays rank 0's JSON line and fails if
+any rank fails - the reference's root drives its workers the same way (src/app.cpp:233-312).
+`n_gpus` is the number of distinct devices the ranks ran on: DL_BENCH_SAME_GPU=1 rehearses N ranks on
+one GPU, labelled "same_gpu_rehearsal": true with n_gpus 1 and no vs_baseline.
+TP partial sums default to the reference's wire format, Q80 blocks (syncType = bufferFloatType,
+src/app.cpp:81, llm.cpp:150); the exact f32 exchange is reported next to it (tp_f32_*).
 """
 from __future__ import annotations
 
@@ -71,6 +80,61 @@ def _cli_point(local: int, prompt_tokens: int, steps: int) -> dict:
             "cli_avg_tokens_per_s": round(1000.0 / ((float(m[0][1]) + float(m[1][1])) / 2), 2)}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch_ranks(n: int) -> int:
+    """--gpus N without a launcher: start N ranks of this script (one per GPU, LOCAL_RANK = GPU
+    ordinal), relay rank 0's JSON line, fail if any rank fails. Runs before anything in this
+    process touches a GPU (torch.cuda.device_count() only counts devices on this image)."""
+    import subprocess
+    import tempfile
+    import torch
+    same = os.environ.get("DL_BENCH_SAME_GPU") == "1"
+    ndev = torch.cuda.device_count()
+    if not same and ndev < n:
+        print(f"bench.py: --gpus {n} but only {ndev} GPU(s) visible; set DL_BENCH_SAME_GPU=1 to rehearse "
+              f"{n} ranks on one GPU (not a scaling point)", file=sys.stderr)
+        return 2
+    port = _free_port()
+    out = tempfile.TemporaryFile(mode="w+")
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      stdout=out if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    try:
+        alive = set(range(n))
+        while alive:
+            for r in list(alive):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                alive.discard(r)
+                if c != 0 and rc == 0:
+                    rc = c
+                    print(f"bench.py: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr)
+                    for q in alive:
+                        procs[q].terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    out.seek(0)
+    lines = [l for l in out.read().splitlines() if l.startswith("{")]
+    if rc == 0 and lines:
+        print(lines[-1], flush=True)
+    return rc if rc else (0 if lines else 1)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -81,14 +145,17 @@ def main() -> int:
     ap.add_argument("--model", default="", help="optional .m file instead of synthetic 8B weights")
     ap.add_argument("--shape", default="llama3_1_8b",
                     help="synthetic shape (models/synthetic.py LLAMA_SHAPES); the headline metric is llama3_1_8b")
-    ap.add_argument("--sync-type", default=os.environ.get("DL_SYNC_TYPE", "f32"), choices=["f32", "q80"],
-                    help="TP partial-sum exchange: f32 (exact, measured faster) or q80 (the reference ZQ wire format)")
+    ap.add_argument("--sync-type", default=os.environ.get("DL_SYNC_TYPE", "q80"), choices=["f32", "q80"],
+                    help="TP partial-sum exchange: q80 (the reference's ZQ wire format, default) or f32 (exact)")
     ap.add_argument("--long-ctx", type=int, default=4096, help="position of the long-context decode point (0: off)")
     ap.add_argument("--no-cli", action="store_true", help="skip the dllama CLI product-path point (1 GPU)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-f32kv", action="store_true", help="skip the f32 KV-cache decode point")
     ap.add_argument("--no-prefill4k", action="store_true", help="skip the 4096-token prompt-eval point")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _launch_ranks(args.gpus)
 
     import torch
     import distributed_llama_multiusers_amd as dl
@@ -97,7 +164,8 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if os.environ.get("DL_BENCH_SAME_GPU") == "1":  # rehearsal of the multi-rank path on one GPU
+    same_gpu = world > 1 and os.environ.get("DL_BENCH_SAME_GPU") == "1"
+    if same_gpu:  # rehearsal of the multi-rank path on one GPU (not a scaling point)
         local = 0
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
@@ -128,17 +196,18 @@ def main() -> int:
         from distributed_llama_multiusers_amd.models.synthetic import LLAMA_SHAPES
         shape = dict(LLAMA31_8B, **LLAMA_SHAPES[args.shape])
 
-    def make_engine(max_seq=seq_len, kv_bf16=True):
+    def make_engine(max_seq=seq_len, kv_bf16=True, sync=None):
         # the context length is sized to the run (attention split grids follow it)
         synthetic = None if args.model else dict(shape, seq_len=max_seq)
         return C.HipEngine(args.model, "q80", max_seq_len=max_seq, max_batch=max_batch, n_slots=args.batch,
                            kv_bf16=kv_bf16,
                            gpu_index=local, use_graphs=not args.no_graphs, synthetic=synthetic, seed=1234, rank=rank,
-                           world=world, uid=uid, comm=comm, sync_type=args.sync_type)
+                           world=world, uid=uid, comm=comm, sync_type=sync or args.sync_type)
 
     t0 = time.time()
     eng = make_engine()
     load_s = time.time() - t0
+    tp_fused = bool(eng.tp_fused) if world > 1 else None
     B = args.batch
 
     def barrier():
@@ -232,6 +301,19 @@ def main() -> int:
         f32kv_ms = (time.perf_counter() - tf) * 1000.0 / 16
         barrier()
 
+    tpf32_ms = None
+    if world > 1 and args.sync_type != "f32":  # the exact f32 exchange next to the Q80 wire format
+        del eng
+        eng = make_engine(sync="f32")
+        eng.decode_greedy(4, tokens, [pos0] * B, list(range(B)))
+        barrier()
+        torch.cuda.synchronize()
+        tt = time.perf_counter()
+        eng.decode_greedy(32, tokens, [pos0 + 4] * B, list(range(B)))
+        torch.cuda.synchronize()
+        tpf32_ms = (time.perf_counter() - tt) * 1000.0 / 32
+        barrier()
+
     p4k_ms = None
     if not args.no_prefill4k:  # a 4096-token prompt evaluated in 32-token chunks (attention grows with it)
         del eng
@@ -249,12 +331,14 @@ def main() -> int:
         barrier()
 
     if dist is not None:
-        t = torch.tensor([elapsed, eval_s, long_ms or 0.0, f32kv_ms or 0.0, p4k_ms or 0.0], dtype=torch.float64)
+        t = torch.tensor([elapsed, eval_s, long_ms or 0.0, f32kv_ms or 0.0, p4k_ms or 0.0, tpf32_ms or 0.0],
+                         dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, eval_s = float(t[0]), float(t[1])
         long_ms = float(t[2]) if long_ms is not None else None
         f32kv_ms = float(t[3]) if f32kv_ms is not None else None
         p4k_ms = float(t[4]) if p4k_ms is not None else None
+        tpf32_ms = float(t[5]) if tpf32_ms is not None else None
 
     ms_per_step = elapsed * 1000.0 / args.steps
     pred_ms_tok = ms_per_step / B
@@ -264,6 +348,8 @@ def main() -> int:
     # the published baselines are per model family: 7B/8B at 1/2/4/8 devices, 70B at 8 devices
     base = (BASELINE_MS.get(world) if args.shape == "llama3_1_8b" and not args.model
             else BASELINE_MS_70B.get(world) if args.shape == "llama3_3_70b" and not args.model else None)
+    if same_gpu:
+        base = None  # a rehearsal on one device is not a point of the scaling curve
     cli = {}
     if world == 1 and not args.no_cli and args.shape == "llama3_1_8b" and not args.model:
         del eng
@@ -272,7 +358,7 @@ def main() -> int:
         "metric": METRIC,
         "value": round(tok_s, 3),
         "unit": "tokens/s",
-        "n_gpus": world,
+        "n_gpus": 1 if same_gpu else world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
@@ -301,11 +387,16 @@ def main() -> int:
             "prompt_4k_eval_ms_per_token": round(p4k_ms, 4) if p4k_ms is not None else None,
             "load_s": round(load_s, 2),
             "hip_graphs": not args.no_graphs,
+            "tp_ranks": world,
             "tp_comm": comm_kind if world > 1 else None,
             "tp_sync": args.sync_type if world > 1 else None,
+            "tp_fused_exchange": tp_fused,
+            "tp_f32_pred_ms_per_token": round(tpf32_ms / B, 4) if tpf32_ms is not None else None,
             **cli,
         },
     }
+    if same_gpu:
+        result["same_gpu_rehearsal"] = True
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:

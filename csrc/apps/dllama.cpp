@@ -181,7 +181,7 @@ static void usage() {
                  "Usage: dllama {inference|chat|worker} {--model <path>} {--tokenizer <path>} [options]\n"
                  "  --prompt <p> --steps <n>            (inference)\n"
                  "  --buffer-float-type {f32|f16|q40|q80}\n"
-                 "  --sync-type {f32|q80}               (CPU tensor-parallel partial sums; default f32)\n"
+                 "  --sync-type {f32|q80}               (tensor-parallel partial sums; default: the buffer type)\n"
                  "  --workers <host:port> ...           (root of a tensor-parallel group)\n"
                  "  --port <p>                          (worker)\n"
                  "  --nthreads <n>                      (CPU backend threads)\n"

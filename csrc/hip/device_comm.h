@@ -33,6 +33,9 @@ class DeviceComm {
     virtual std::string asyncError() { return ""; }
     // Release the communicator without waiting for peers (used after an error).
     virtual void shutdownNow() {}
+    // Ranks of this communicator that run on this rank's GPU (1 on a real multi-GPU node; all of
+    // them in a same-GPU rehearsal): they share the device's resident workgroup slots.
+    virtual int ranksOnDevice() const { return 1; }
     // Targets of the exchange fused into producer kernels (hipk::TpXchg): region 0 = residual
     // partial sums (elements b * dim + row, up to 65536), region 1 = argmax winners (2 words per
     // row). False when the transport has none (RCCL): the engine launches separate collectives.
@@ -63,5 +66,10 @@ void xgmiConnect(DeviceComm *c, const std::vector<std::string> &handles);
 bool xgmiTimedOut(DeviceComm *c);
 void xgmiSetLowLatency(DeviceComm *c, bool on);  // LL push protocol for small all-reduces (default on)
 void xgmiResetError(DeviceComm *c);
+// Peers on other GPUs (PCI bus ids differ)? Then the pull protocol runs with system-scope fences
+// around its flags unless DL_XGMI_FENCE=0 (the LL / fused exchanges carry data and epoch in one
+// 64-bit word and need no fence on any topology).
+bool xgmiCrossDevice(DeviceComm *c);
+bool xgmiFenced(DeviceComm *c);
 
 }  // namespace dl

@@ -84,6 +84,13 @@ class HipEngineImpl : public HipEngine {
             tpVec_.q80 = syncQ80_ ? 1 : 0;
         }
         checkFits();
+        if (tpFused_) checkFusedResidency();
+        {  // path knobs, read once: a captured graph replays the path it was captured with
+            const char *e = std::getenv("DL_GEMM_MIN");
+            gemmMin_ = e && *e ? std::atoi(e) : (plan_.nRanks > 1 ? 5 : 3);
+            const char *f = std::getenv("DL_GEMM_FUSE_NORM");
+            fuseNormEnv_ = !(f && *f == '0');
+        }
         Timer timer;
         allocBuffers();
         if (cfg.synthetic)
@@ -120,6 +127,62 @@ class HipEngineImpl : public HipEngine {
             throw Error(msg);
         }
     }
+
+    // The fused TP exchange spins inside the wo / w2 GEMV workgroups until every peer published the
+    // same rows: deadlock-free only if every workgroup of such a launch is resident at once (a
+    // waiting workgroup must never keep a peer's producer, or its own rank's later workgroups, off
+    // the CUs). Check every launch shape the fused path can take against the device's occupancy
+    // (hipOccupancyMaxActiveBlocksPerMultiprocessor x CUs at the launch's LDS size); if any would
+    // not fit, fall back to the separate all-reduce kernels, whose grids are a few workgroups.
+    void checkFusedResidency() {
+        const ShardPlan &p = plan_;
+        // ranks sharing this GPU (same-GPU rehearsals) share its resident slots; DL_FUSED_RESIDENT
+        // overrides the limit (diagnostics / tests of the fallback)
+        const int share = std::max(1, comm_->ranksOnDevice());
+        const char *ov = std::getenv("DL_FUSED_RESIDENT");
+        const bool hQ80 = p.hidden0 / 32 >= 192;
+        struct Shape {
+            int rows, n, pro;
+        } shapes[2] = {{(int)h_.dim, (int)p.q0, hipk::PRO_GLOBAL},
+                       {(int)h_.dim, (int)p.hidden0, hQ80 ? hipk::PRO_GLOBAL : hipk::PRO_RESNORM}};
+        for (const Shape &sh : shapes) {
+            DevMat m;
+            m.rows = sh.rows;
+            m.n = sh.n;
+            m.lanes = hipk::gemvLanesPerRow(sh.n, sh.rows, 1, true);
+            const int bcMax = std::min<int>(batchChunk(m, sh.pro, hipk::EPI_STORE_TP), (int)cfg_.maxBatch);
+            for (int bc = 1; bc <= bcMax; bc *= 2) {
+                hipk::GemvArgs a;
+                a.rows = m.rows;
+                a.n = m.n;
+                a.lanes = m.lanes;
+                a.passes = tpPasses(m, bc);
+                a.tp = tpVec_;
+                const hipk::GemvResidency r = hipk::gemvResidency(a, bc, sh.pro, hipk::EPI_STORE_TP, true);
+                const int limit = ov && *ov ? std::atoi(ov) : r.maxResident / share;
+                fusedGridMax_ = std::max(fusedGridMax_, r.grid);
+                if (limit <= 0 || r.grid > limit) {
+                    std::fprintf(stderr,
+                                 "⚠️  fused TP exchange disabled: a %dx%d GEMV at batch %d needs %d co-resident "
+                                 "workgroups, this rank may hold %d (%d per device, %d rank(s) on it); using "
+                                 "separate all-reduce kernels\n",
+                                 sh.rows, sh.n, bc, r.grid, limit, r.maxResident, share);
+                    tpFused_ = false;
+                    return;
+                }
+            }
+        }
+    }
+    int tpPasses(const DevMat &m, int bc) const {
+        int passes = passesFor(m, hipk::EPI_STORE_TP, bc);
+        if (tpVec_.q80)  // whole Q80 blocks of 32 rows per workgroup
+            while ((256 / m.lanes * 2 * passes) % 32) passes++;
+        return passes;
+    }
+
+  public:
+    bool tpFused() const override { return tpFused_; }
+    int fusedGridMax() const override { return fusedGridMax_; }
 
     ~HipEngineImpl() override {
         (void)hipSetDevice(dev_);
@@ -716,13 +779,9 @@ class HipEngineImpl : public HipEngine {
             a.wf = m.f;
             a.rows = m.rows;
             a.n = m.n;
-            a.passes = passesFor(m, epi, bc);
+            a.passes = tp ? tpPasses(m, bc) : passesFor(m, epi, bc);
             a.lanes = m.lanes;
-            if (tp) {
-                a.tp = tpVec_;
-                if (tpVec_.q80)  // whole Q80 blocks of 32 rows per workgroup
-                    while ((256 / m.lanes * 2 * a.passes) % 32) a.passes++;
-            }
+            if (tp) a.tp = tpVec_;
             a.in = in ? in + (size_t)c0 * ldIn : nullptr;
             a.aq = aq ? aq + (size_t)c0 * m.n : nullptr;
             a.as = as ? as + (size_t)c0 * (m.n / 32) : nullptr;
@@ -753,15 +812,11 @@ class HipEngineImpl : public HipEngine {
         }
     }
 
-    // rows per forward from which the MFMA GEMM replaces the GEMV (DL_GEMM_MIN, read per call so
-    // tests can compare both paths in one process)
+    // rows per forward from which the MFMA GEMM replaces the GEMV (DL_GEMM_MIN, read at construction)
     // Default: GEMV up to 2 rows at TP1 (8B ms/step GEMV vs MFMA GEMM: 1.90 vs 2.64 at 2 rows, 3.15 vs
     // 2.67 at 3, 2.92 vs 2.66 at 4, after the fence-free split-K); up to 4 rows at TP > 1, where the
     // GEMV path carries the fused exchange.
-    int gemmMinTokens() const {
-        const char *e = std::getenv("DL_GEMM_MIN");
-        return e && *e ? std::atoi(e) : (plan_.nRanks > 1 ? 5 : 3);
-    }
+    int gemmMinTokens() const { return gemmMin_; }
 
     bool batchedPath(int n) const {
         return n >= gemmMinTokens() && hipk::gemmSupported(h_.dim) && hipk::gemmSupported(plan_.q0) &&
@@ -781,18 +836,15 @@ class HipEngineImpl : public HipEngine {
 
     // Batched path (>= gemmMinTokens rows, Q40 or F32 weights): per chunk of <= 64 tokens, a norm kernel (f32 ->
     // f16, RESNORM) or the producer's f16 rows (xh) feed the MFMA GEMM with the fused epilogue.
-    // Residual + norm fusion between batched GEMMs at TP1 (DL_GEMM_FUSE_NORM=0 disables, read per
-    // call): wo / w2 end with EPI_RES (x' = x + out, x' * normW -> f16, per-tile sums of squares)
+    // Residual + norm fusion between batched GEMMs at TP1 (DL_GEMM_FUSE_NORM=0 disables, read at
+    // construction): wo / w2 end with EPI_RES (x' = x + out, x' * normW -> f16, per-tile sums of squares)
     // and the next GEMM applies the RMS scale per token in its epilogue: no norm kernel between.
     struct ResFuse {
         const float *resIn;
         float *resOut;
         const float *w;
     };
-    bool fuseNorm() const {
-        const char *e = std::getenv("DL_GEMM_FUSE_NORM");
-        return plan_.nRanks == 1 && !(e && *e == '0');
-    }
+    bool fuseNorm() const { return plan_.nRanks == 1 && fuseNormEnv_; }
 
     void gemmBatched(const DevMat &m, int n, int epi, const float *in, int ldIn, const float *add, float *xNext,
                      const float *normW, const _Float16 *xh, float *out, int ldOut, _Float16 *outH,
@@ -1065,6 +1117,9 @@ class HipEngineImpl : public HipEngine {
     ModelHeader h_;
     ShardPlan plan_;
     bool q40_ = true, kvBf16_ = true, syncQ80_ = false, tpFused_ = false;
+    int fusedGridMax_ = 0;  // largest grid of a fused-exchange GEMV launch (checked co-resident)
+    int gemmMin_ = 3;       // DL_GEMM_MIN: rows per forward from which the batched MFMA path runs
+    bool fuseNormEnv_ = true;  // DL_GEMM_FUSE_NORM
     hipk::TpXchg tpVec_, tpArg_;
     std::vector<void *> allocs_, hostAllocs_;
     size_t deviceBytes_ = 0;

@@ -24,6 +24,11 @@ class HipEngine : public Backend {
     virtual size_t deviceBytes() const = 0;
     // Run one forward eagerly with a per-kernel-class timing breakdown (ms) printed to stdout.
     virtual void profileForward(int n, const int *tokens, const int *positions, const int *slots) = 0;
+    // Tensor parallel: whether the partial-sum exchange runs fused in the wo / w2 GEMV tails (it is
+    // switched off when a launch's grid would not be fully co-resident), and the largest grid of
+    // such a launch (checked against the device's occupancy at construction).
+    virtual bool tpFused() const { return false; }
+    virtual int fusedGridMax() const { return 0; }
 };
 
 // comm may be null (single GPU). The engine does not own comm.

@@ -183,6 +183,13 @@ void launchNormF16(const GemvArgs &a, _Float16 *out, int M, hipStream_t s);
 
 // B = batch rows in this launch (1, 2 or 4); q40 = weight format.
 void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_t s);
+// Co-residency of one GEMV launch on the current device: its grid and the most workgroups of that
+// kernel (at its LDS size) the device holds at once (occupancy per CU x CUs). A kernel whose
+// workgroups spin on peers (EPI_STORE_TP) is deadlock-free only if grid <= maxResident.
+struct GemvResidency {
+    int grid = 0, maxResident = 0;
+};
+GemvResidency gemvResidency(const GemvArgs &a, int B, int pro, int epi, bool q40);
 // Rows handled by one lane group (2 at batch 1: the activation loads are shared by 2 rows).
 __host__ __device__ constexpr int gemvRowGroup(int B, bool q40) { return q40 ? 2 : 1; }
 // Lanes cooperating on one weight row for a given input width, row count and batch.

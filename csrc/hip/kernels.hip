@@ -15,6 +15,7 @@
 // * Cross-workgroup hand-offs (attention split combine, argmax) follow the agent-scope
 //   release/acquire counter recipe (cdna_hip_programming.md §5 "In-launch split-K reduction").
 #include "../core/common.h"
+#include "device_comm.h"
 #include "device_common.h"
 #include "kernels.h"
 
@@ -1059,18 +1060,13 @@ static void allowLds(const void *fn, size_t bytes) {
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
+// Kernel instance of one GEMV launch configuration (null: unsupported combination).
 template <int L, int B, bool Q40>
-static void gemvDispatchPE(const GemvArgs &a, int pro, int epi, size_t lds, int grid, hipStream_t s) {
-#define DL_GEMV_CASE(P, E)                                                                          \
-    if (pro == P && epi == E) {                                                                     \
-        if constexpr (Q40) {                                                                        \
-            if (lds > 65536) allowLds((const void *)gemvQ40Kernel<L, B, P, E>, lds);                 \
-            hipLaunchKernelGGL((gemvQ40Kernel<L, B, P, E>), dim3(grid), dim3(kThreads), lds, s, a); \
-        } else {                                                                                    \
-            if (lds > 65536) allowLds((const void *)gemvKernel<L, B, P, E, false>, lds);             \
-            hipLaunchKernelGGL((gemvKernel<L, B, P, E, false>), dim3(grid), dim3(kThreads), lds, s, a); \
-        }                                                                                           \
-        return;                                                                                     \
+static const void *gemvFnPE(int pro, int epi) {
+#define DL_GEMV_CASE(P, E)                                                     \
+    if (pro == P && epi == E) {                                                \
+        if constexpr (Q40) return (const void *)gemvQ40Kernel<L, B, P, E>;     \
+        else return (const void *)gemvKernel<L, B, P, E, false>;               \
     }
     DL_GEMV_CASE(PRO_GLOBAL, EPI_STORE)
     DL_GEMV_CASE(PRO_RESNORM, EPI_STORE)
@@ -1082,40 +1078,63 @@ static void gemvDispatchPE(const GemvArgs &a, int pro, int epi, size_t lds, int 
         DL_GEMV_CASE(PRO_RESNORM, EPI_STORE_TP)
     }
 #undef DL_GEMV_CASE
+    return nullptr;
 }
 
 template <int L, bool Q40>
-static void gemvDispatchB(const GemvArgs &a, int B, int pro, int epi, size_t lds, int grid, hipStream_t s) {
+static const void *gemvFnB(int B, int pro, int epi) {
     switch (B) {
-        case 1: gemvDispatchPE<L, 1, Q40>(a, pro, epi, lds, grid, s); break;
-        case 2: gemvDispatchPE<L, 2, Q40>(a, pro, epi, lds, grid, s); break;
-        case 4: gemvDispatchPE<L, 4, Q40>(a, pro, epi, lds, grid, s); break;
-        default: break;
+        case 1: return gemvFnPE<L, 1, Q40>(pro, epi);
+        case 2: return gemvFnPE<L, 2, Q40>(pro, epi);
+        case 4: return gemvFnPE<L, 4, Q40>(pro, epi);
+        default: return nullptr;
     }
 }
 
-void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_t s) {
+// Launch geometry of one GEMV (shared by the launcher and the co-residency check).
+struct GemvLaunch {
+    const void *fn = nullptr;
+    int grid = 0;
+    size_t lds = 0;
+};
+static GemvLaunch gemvLaunchOf(const GemvArgs &a, int B, int pro, int epi, bool q40) {
+    GemvLaunch g;
     const int L = a.lanes > 0 ? a.lanes : gemvLanesPerRow(a.n, a.rows, B, q40);
     const int R = (kThreads / L) * gemvRowGroup(B, q40) * a.passes;
-    const int grid = (a.rows + R - 1) / R;
-    size_t lds = gemvLdsBytes(a.n, B, q40, R, pro);
+    g.grid = (a.rows + R - 1) / R;
+    g.lds = gemvLdsBytes(a.n, B, q40, R, pro);
     if (q40 && epi == EPI_STORE_TP && a.tp.q80) {  // Q80 exchange staging reuses `act`
         const GemvLds lay = gemvLayout(a.n, B, true, R, PRO_RESNORM);
-        lds = std::max(lds, lay.act + tpQ80Lds(B * R, a.tp.world));
+        g.lds = std::max(g.lds, lay.act + tpQ80Lds(B * R, a.tp.world));
     }
-    if (q40) {
-        switch (L) {
-            case 16: gemvDispatchB<16, true>(a, B, pro, epi, lds, grid, s); break;
-            case 32: gemvDispatchB<32, true>(a, B, pro, epi, lds, grid, s); break;
-            default: gemvDispatchB<64, true>(a, B, pro, epi, lds, grid, s); break;
-        }
-    } else {
-        switch (L) {
-            case 16: gemvDispatchB<16, false>(a, B, pro, epi, lds, grid, s); break;
-            case 32: gemvDispatchB<32, false>(a, B, pro, epi, lds, grid, s); break;
-            default: gemvDispatchB<64, false>(a, B, pro, epi, lds, grid, s); break;
-        }
-    }
+    if (q40)
+        g.fn = L == 16 ? gemvFnB<16, true>(B, pro, epi) : L == 32 ? gemvFnB<32, true>(B, pro, epi) : gemvFnB<64, true>(B, pro, epi);
+    else
+        g.fn = L == 16 ? gemvFnB<16, false>(B, pro, epi) : L == 32 ? gemvFnB<32, false>(B, pro, epi) : gemvFnB<64, false>(B, pro, epi);
+    return g;
+}
+
+void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_t s) {
+    const GemvLaunch g = gemvLaunchOf(a, B, pro, epi, q40);
+    if (!g.fn) throw Error("launchGemv: unsupported prologue / epilogue / batch combination");
+    if (g.lds > 65536) allowLds(g.fn, g.lds);
+    GemvArgs args = a;
+    void *kargs[] = {&args};
+    DL_HIP(hipLaunchKernel(g.fn, dim3(g.grid), dim3(kThreads), kargs, g.lds, s));
+}
+
+GemvResidency gemvResidency(const GemvArgs &a, int B, int pro, int epi, bool q40) {
+    GemvResidency r;
+    const GemvLaunch g = gemvLaunchOf(a, B, pro, epi, q40);
+    if (!g.fn) return r;
+    if (g.lds > 65536) allowLds(g.fn, g.lds);
+    int dev = 0, cus = 0, perCu = 0;
+    DL_HIP(hipGetDevice(&dev));
+    DL_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    DL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCu, g.fn, kThreads, g.lds));
+    r.grid = g.grid;
+    r.maxResident = perCu * cus;
+    return r;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1231,6 +1250,11 @@ __device__ __forceinline__ void glds4(const void *g, void *lds) {
                                          reinterpret_cast<uintptr_t>(lds)), 4, 0, 0);
 }
 
+// EPI_RES hand-off scale (power of two: exact) and the f16 store that saturates instead of
+// overflowing to inf.
+static constexpr float kResXScale = 1.0f / 32.0f;
+__device__ __forceinline__ _Float16 satF16(float v) { return (_Float16)fminf(fmaxf(v, -65504.f), 65504.f); }
+
 // Split-K combine and fused epilogues shared by the batched GEMMs (Q40 and f32): `acc` holds this
 // lane's C fragments (weight row (local) wave*16 + col, token t*16 + h*4 + i); `smem` must hold
 // MP x 64 floats and is free (all K-loop LDS reads retired behind a barrier); `flag` one int.
@@ -1316,7 +1340,7 @@ __device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc
         if (tid < ga.M) {
             float tot = 0.f;
             for (int i = 0; i < TPT; i++) tot += slL[tid * TPT + i];
-            rsL[tid] = 1.0f / sqrtf(tot / (float)a.n + a.eps);
+            rsL[tid] = (1.0f / kResXScale) / sqrtf(tot / (float)a.n + a.eps);
         }
     }
     __syncthreads();
@@ -1336,8 +1360,11 @@ __device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc
                 x1 = ga.resIn[o + 1] + v1;
                 ga.resOut[o] = x0;
                 ga.resOut[o + 1] = x1;
-                ga.resX[o] = (_Float16)(x0 * ga.resW[r0]);
-                ga.resX[o + 1] = (_Float16)(x1 * ga.resW[r0 + 1]);
+                // the un-normalised residual can be large (real checkpoints carry outlier channels
+                // of 1e3-1e4): stored pre-scaled by 2^-5 (exact) and saturated, so f16 never
+                // overflows to inf; the consumer folds 2^5 into its RMS scale
+                ga.resX[o] = satF16(x0 * ga.resW[r0] * kResXScale);
+                ga.resX[o + 1] = satF16(x1 * ga.resW[r0 + 1] * kResXScale);
             }
             const float ssq = groupSum<32>(x0 * x0 + x1 * x1);  // the 32 pairs of token t, in lane order
             if (k == 0) ga.ssOut[(size_t)tileIdx * ga.ldSS + t] = ssq;

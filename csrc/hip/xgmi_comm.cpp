@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -76,6 +77,7 @@ struct XgmiCall {
     long long maxFloats;
     long long n;
     int rank, world, gather;
+    int fenced;                     // system-scope release / acquire fences around the flags
     long long timeoutTicks;         // s_memrealtime ticks (100 MHz)
 };
 
@@ -109,6 +111,10 @@ __global__ __launch_bounds__(kThreads) void xgmiKernel(XgmiCall a) {
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every publish store performed
+    // ranks on different GPUs: a system-scope release before the flag store as well (not needed
+    // for the uncached, atomically accessed buffers on paper; kept until the fence-free protocol
+    // has been validated across separate devices - see fencedDefault())
+    if (a.fenced) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __syncthreads();
     // 2. signal every peer, then wait for every peer's signal (one lane per peer)
     if (tid < a.world) {
@@ -129,6 +135,7 @@ __global__ __launch_bounds__(kThreads) void xgmiKernel(XgmiCall a) {
         }
     }
     __syncthreads();
+    if (a.fenced) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     // 3. reduce (rank order, identical on every rank) or gather
     for (long long c = g; c < nChunks; c += kSlots) {
         const long long i = c * kChunk + tid * 4;
@@ -265,6 +272,14 @@ class XgmiComm : public DeviceComm {
         hipIpcMemHandle_t h;
         DL_HIP(hipIpcGetMemHandle(&h, base_));
         handle_.assign(reinterpret_cast<const char *>(&h), reinterpret_cast<const char *>(&h) + sizeof(h));
+        // the handle travels with this rank's PCI bus id, so every rank knows whether its peers
+        // are other GPUs (cross-device: fenced pull protocol by default) or the same one
+        int dev = 0;
+        DL_HIP(hipGetDevice(&dev));
+        char bus[64] = {0};
+        if (hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, dev) != hipSuccess) std::snprintf(bus, sizeof(bus), "dev%d", dev);
+        busId_ = bus;
+        handle_ += busId_;
     }
     ~XgmiComm() override {
         for (int p = 0; p < world_; p++)
@@ -280,7 +295,9 @@ class XgmiComm : public DeviceComm {
             if (p == rank_) {
                 peerBase_[p] = base_;
             } else {
-                DL_CHECK(handles[p].size() == sizeof(hipIpcMemHandle_t), "xgmi comm: bad handle size");
+                DL_CHECK(handles[p].size() >= sizeof(hipIpcMemHandle_t), "xgmi comm: bad handle size");
+                if (handles[p].substr(sizeof(hipIpcMemHandle_t)) != busId_) crossDevice_ = true;
+                else sameDevice_++;
                 hipIpcMemHandle_t h;
                 std::memcpy(&h, handles[p].data(), sizeof(h));
                 DL_HIP(hipIpcOpenMemHandle(&peerBase_[p], h, hipIpcMemLazyEnablePeerAccess));
@@ -292,7 +309,11 @@ class XgmiComm : public DeviceComm {
             fusedArg_[p] = reinterpret_cast<uint64_t *>(static_cast<char *>(peerBase_[p]) + faOff_);
         }
         connected_ = true;
+        fenced_ = crossDevice_ && fencedDefault();
     }
+    bool crossDevice() const { return crossDevice_; }
+    int ranksOnDevice() const override { return sameDevice_; }
+    bool fenced() const { return fenced_; }
     int rank() const override { return rank_; }
     int size() const override { return world_; }
     std::string name() const override { return "xgmi"; }
@@ -335,6 +356,12 @@ class XgmiComm : public DeviceComm {
     }
 
   private:
+    // DL_XGMI_FENCE=0 runs the pull protocol fence-free across devices too (as on one device);
+    // =1 fences even on one device (comparison runs).
+    static bool fencedDefault() {
+        const char *e = std::getenv("DL_XGMI_FENCE");
+        return !(e && *e == '0');
+    }
     static bool pullOnly() {  // DL_XGMI_LL=0: always the pull protocol (comparison runs)
         static const bool v = [] {
             const char *e = std::getenv("DL_XGMI_LL");
@@ -354,6 +381,8 @@ class XgmiComm : public DeviceComm {
         c.rank = rank_;
         c.world = world_;
         c.gather = gather ? 1 : 0;
+        const char *fe = std::getenv("DL_XGMI_FENCE");
+        c.fenced = fenced_ || (fe && *fe == '1') ? 1 : 0;
         c.timeoutTicks = kTimeoutTicks;
         return c;
     }
@@ -389,8 +418,9 @@ class XgmiComm : public DeviceComm {
     void *peerBase_[kMaxRanks] = {};
     XgmiPeers peers_{};
     int *epochs_ = nullptr, *error_ = nullptr;
-    std::string handle_;
-    bool connected_ = false;
+    std::string handle_, busId_;
+    bool connected_ = false, crossDevice_ = false, fenced_ = false;
+    int sameDevice_ = 1;  // ranks on this GPU, this one included
     bool ll_ = true;
 };
 
@@ -406,5 +436,7 @@ void xgmiConnect(DeviceComm *c, const std::vector<std::string> &handles) {
 bool xgmiTimedOut(DeviceComm *c) { return static_cast<XgmiComm *>(c)->timedOut(); }
 void xgmiSetLowLatency(DeviceComm *c, bool on) { static_cast<XgmiComm *>(c)->setLowLatency(on); }
 void xgmiResetError(DeviceComm *c) { static_cast<XgmiComm *>(c)->resetError(); }
+bool xgmiCrossDevice(DeviceComm *c) { return static_cast<XgmiComm *>(c)->crossDevice(); }
+bool xgmiFenced(DeviceComm *c) { return static_cast<XgmiComm *>(c)->fenced(); }
 
 }  // namespace dl

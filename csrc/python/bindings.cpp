@@ -647,6 +647,8 @@ PYBIND11_MODULE(_C, m) {
         .def("timed_out", [](PyComm &c) { return xgmiTimedOut(c.comm.get()); })
         .def("set_low_latency", [](PyComm &c, bool on) { xgmiSetLowLatency(c.comm.get(), on); })
         .def("reset_error", [](PyComm &c) { xgmiResetError(c.comm.get()); })
+        .def_property_readonly("cross_device", [](PyComm &c) { return xgmiCrossDevice(c.comm.get()); })
+        .def_property_readonly("fenced", [](PyComm &c) { return xgmiFenced(c.comm.get()); })
         // µs per in-graph all-reduce of n floats (iters back-to-back collectives in one hipGraph)
         .def("bench_all_reduce",
              [](PyComm &c, size_t n, int iters) {
@@ -750,6 +752,8 @@ PYBIND11_MODULE(_C, m) {
              py::arg("sync_type") = "f32")
         .def_property_readonly("header", [](const PyHipEngine &e) { return headerToDict(e.engine->header()); })
         .def_property_readonly("device_bytes", [](const PyHipEngine &e) { return e.engine->deviceBytes(); })
+        .def_property_readonly("tp_fused", [](const PyHipEngine &e) { return e.engine->tpFused(); })
+        .def_property_readonly("fused_grid_max", [](const PyHipEngine &e) { return e.engine->fusedGridMax(); })
         .def_property_readonly("load_stats",
                                [](const PyHipEngine &e) {
                                    const Backend::LoadStats l = e.engine->loadStats();

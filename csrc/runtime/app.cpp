@@ -78,6 +78,7 @@ AppArgs AppArgs::parse(int argc, char **argv, bool requireMode) {
         else if (name == "--profile") a.profile = std::atoi(value) != 0;
         else throw Error("Unknown option: " + name);
     }
+    if (a.syncType == FloatType::UNK) a.syncType = a.bufferType == FloatType::Q80 ? FloatType::Q80 : FloatType::F32;
     setLogLevel(a.logLevel);
     return a;
 }

@@ -20,7 +20,9 @@ struct AppArgs {
     std::string mode;
     std::string modelPath, tokenizerPath, prompt;
     FloatType bufferType = FloatType::F32;
-    FloatType syncType = FloatType::F32;  // --sync-type: CPU TP wire format (f32 exact | q80 reference)
+    // --sync-type: tensor-parallel wire format of the partial sums (f32 exact | q80). Unset = the
+    // buffer float type, as in the reference (syncType = bufferFloatType, src/app.cpp:81, llm.cpp:150)
+    FloatType syncType = FloatType::UNK;
     std::vector<std::string> workerHosts;
     std::vector<int> workerPorts;
     int port = 9990;

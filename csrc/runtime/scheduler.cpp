@@ -141,16 +141,21 @@ bool Scheduler::step() {
             r->eos.reset(new EosDetector(eosIds, stops, (int)maxLen, (int)maxLen));
             active_.push_back(r);
         }
-        // requests whose client disconnected give their slot back before the batch is built
-        for (auto &r : active_)
+        // requests whose client disconnected give their slot back before the batch is built; the
+        // flag is read ONCE per request (cancel() runs on HTTP threads without mu_), so a request
+        // is either finished + freed + dropped, or kept - never dropped with its slot still held
+        std::vector<std::shared_ptr<GenRequest>> keep;
+        keep.reserve(active_.size());
+        for (auto &r : active_) {
             if (r->isCancelled()) {
                 r->finish("cancelled");
                 freeSlots_.push_back(r->slot);
                 stats_.cancelled++;
+            } else {
+                keep.push_back(r);
             }
-        active_.erase(std::remove_if(active_.begin(), active_.end(),
-                                     [](const std::shared_ptr<GenRequest> &x) { return x->isCancelled(); }),
-                      active_.end());
+        }
+        active_.swap(keep);
         stats_.active = (int)active_.size();
     }
     if (active_.empty()) return false;

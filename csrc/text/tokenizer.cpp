@@ -191,8 +191,7 @@ std::vector<int> Tokenizer::encode(const std::string &text, bool addBos, bool ad
     while (true) {
         float bestScore = -1e10f;
         int bestId = -1, bestIdx = -1;
-        const size_t start = addBos ? 0 : 0;
-        for (size_t i = start; i + 1 < tokens.size(); i++) {
+        for (size_t i = 0; i + 1 < tokens.size(); i++) {  // every pair, BOS included (reference order)
             buf.assign(vocab_[tokens[i]]);
             buf.append(vocab_[tokens[i + 1]]);
             const int id = findRegular(buf);

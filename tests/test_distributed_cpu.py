@@ -77,7 +77,8 @@ def test_tensor_parallel_matches_single(kv4, n_workers):
     assert rc == 0, ref
     procs, addrs = _workers(n_workers)
     try:
-        rc, out = _inference(assets, addrs)
+        # exact f32 exchange: TP=N keeps TP=1's arithmetic (the q80 default rounds the partials)
+        rc, out = _inference(assets, addrs, extra=("--sync-type", "f32"))
         assert rc == 0, out
         assert _preds(out) == _preds(ref)
         # the workers got the stop signal and went back to listening
@@ -102,7 +103,7 @@ def test_workers_without_model_file_get_streamed_slices(kv4, tmp_path):
     assert rc == 0, ref
     procs, addrs = _workers(3, ("--stream-weights", "1", "--weights-cache", str(tmp_path)))
     try:
-        rc, out = _inference(kv4, addrs)
+        rc, out = _inference(kv4, addrs, extra=("--sync-type", "f32"))
         assert rc == 0, out
         assert _preds(out) == _preds(ref)
         # the workers process the stop signal asynchronously: let them end the session
@@ -207,15 +208,18 @@ def _sync_kb(out):
 
 
 def test_q80_sync_type_reference_wire_format(kv4):
-    """--sync-type q80: partial sums cross the wire as Q80 blocks (the reference's SYNC_NODE_SLICES
-    format, 34 B per 32 values instead of 128 B) and every rank merges the same quantized parts, so
-    the greedy continuation stays (almost) that of the exact f32 exchange."""
+    """--buffer-float-type q80 without --sync-type: partial sums cross the wire as Q80 blocks (the
+    reference's SYNC_NODE_SLICES format, syncType = bufferFloatType, app.cpp:81; 34 B per 32 values
+    instead of 128 B) and every rank merges the same quantized parts, so the greedy continuation
+    stays (almost) that of the exact f32 exchange (--sync-type f32)."""
     procs, addrs = _workers(1)
     try:
-        rc, f32 = _inference(kv4, addrs, steps=24)
+        rc, f32 = _inference(kv4, addrs, steps=24, extra=("--sync-type", "f32"))
         assert rc == 0, f32
-        rc, q80 = _inference(kv4, addrs, steps=24, extra=("--sync-type", "q80"))
+        rc, q80 = _inference(kv4, addrs, steps=24)
         assert rc == 0, q80
+        rc, q80x = _inference(kv4, addrs, steps=24, extra=("--sync-type", "q80"))
+        assert rc == 0 and _preds(q80x) == _preds(q80), q80x
     finally:
         for p in procs:
             p.kill()

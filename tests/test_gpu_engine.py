@@ -26,6 +26,16 @@ def _seq(be, tokens, slot=0):
     return np.stack([be.forward([t], [p], [slot])[0] for p, t in enumerate(tokens)])
 
 
+def _assert_replays_equal(be, tokens, first):
+    """The same forward again (same rows and positions: the KV rows are rewritten with the same
+    values): the 2nd use of a shape is captured into a hipGraph and the 3rd replays it; both must
+    equal the eager 1st run bitwise (graphs=False: three eager runs, deterministic kernels)."""
+    n = len(tokens)
+    for _ in range(2):
+        again = be.forward(tokens, list(range(n)), [0] * n)
+        assert np.array_equal(again, first)
+
+
 @pytest.mark.parametrize("kind,kv_bf16", [("q40", True), ("q40", False), ("f32", False), ("f32", True)])
 def test_engine_matches_cpu(C, assets, kind, kv_bf16):
     buf = "q80" if kind == "q40" else "f32"
@@ -36,7 +46,11 @@ def test_engine_matches_cpu(C, assets, kind, kv_bf16):
     got = _seq(gpu, tokens)
     tol = 3e-2 if kind == "q40" else (2e-2 if kv_bf16 else 1e-4)
     assert _rel(got, ref) < tol
-    assert (got.argmax(-1) == ref.argmax(-1)).mean() >= 0.8
+    # every row's argmax agrees unless the CPU's own logits are a near-tie between the two picks
+    for r in range(len(tokens)):
+        a, b = int(got[r].argmax()), int(ref[r].argmax())
+        if a != b:
+            assert ref[r][b] - ref[r][a] <= tol * float(np.abs(ref[r]).max()), (r, a, b)
 
 
 def _first_divergence(got, ref):
@@ -98,6 +112,7 @@ def test_engine_batched_prefill_gemv_chunks(C, assets, graphs, monkeypatch):
     seq = _seq(a, tokens)
     bat = b.forward(tokens, list(range(7)), [0] * 7)
     assert _rel(bat, seq) < 1e-4
+    _assert_replays_equal(b, tokens, bat)
 
 
 @pytest.mark.parametrize("graphs", [True, False])
@@ -116,6 +131,7 @@ def test_engine_batched_prefill_mfma(C, assets, graphs, n, monkeypatch):
     bat = b.forward(tokens, list(range(n)), [0] * n)
     assert _rel(bat, seq) < 2e-2
     assert (bat.argmax(-1) == seq.argmax(-1)).mean() >= 0.85
+    _assert_replays_equal(b, tokens, bat)
     cpu = C.cpu_backend(assets["q40"], "q80", 2, max_batch=128)
     ref = cpu.forward(tokens, list(range(n)), [0] * n)
     assert _rel(bat, ref) < 3e-2
@@ -250,3 +266,28 @@ def test_engine_prefill_mfma_attention(C, medium, n, monkeypatch):
     bat = np.concatenate([first, second])
     assert _rel(bat, seq) < 3e-2
     assert (bat.argmax(-1) == seq.argmax(-1)).mean() >= 0.85
+
+
+def test_batched_path_outlier_residuals(C, tmp_path):
+    """Real checkpoints carry "massive activation" channels in the residual stream (|x| of 1e3-1e4
+    and more). The batched path hands x' * normW between GEMMs in f16 (EPI_RES): with outlier
+    channels of 1.5e5 (x normW ~ 1.6e5 > the f16 maximum) it must stay finite and match the CPU
+    reference (pre-scaled, saturating hand-off), like the per-row GEMV path."""
+    import os
+    from distributed_llama_multiusers_amd.models.synthetic import make_spec, random_tensors, make_tokenizer
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType, write_model
+    spec = make_spec("tiny", FloatType.Q40, 128, dim=512, n_heads=8, n_kv_heads=4, hidden_dim=1024)
+    t = random_tensors(spec, 21)
+    emb = t[("embedding", -1)]
+    emb[:, 7] = 1.5e5   # outlier channels on every token
+    emb[:, 300] = -9e4
+    m = os.path.join(str(tmp_path), "outlier.m")
+    write_model(m, spec, t)
+    cpu = C.cpu_backend(m, "q80", 4, max_batch=64)
+    gpu = C.HipEngine(m, "q80", kv_bf16=False, max_batch=64)
+    rng = np.random.default_rng(2)
+    tokens = [int(x) for x in rng.integers(0, spec.vocab_size, 40)]
+    ref = cpu.forward(tokens, list(range(40)), [0] * 40)
+    got = gpu.forward(tokens, list(range(40)), [0] * 40)
+    assert np.isfinite(got).all()
+    assert _rel(got, ref) < 3e-2

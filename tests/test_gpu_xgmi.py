@@ -92,6 +92,29 @@ def _engine_tp(rank, world, port, model, tokens, q, sync_type="f32", steps=4):
         q.put((rank, repr(e)))
 
 
+def _engine_tp_batched(rank, world, port, model, tokens, q, sync_type="f32", env=None):
+    """Batched (MFMA GEMM) forwards of 32 and 64 prompt rows on a TP engine: rank 0's logits and
+    every rank's argmax ids (the batched path exchanges partial sums with separate all-reduces)."""
+    try:
+        os.environ.update(env or {})
+        C, comm, dist = _setup(rank, world, port, 1 << 16)
+        eng = C.HipEngine(model, "q80", kv_bf16=True, rank=rank, world=world, comm=comm, sync_type=sync_type,
+                          max_batch=64, n_slots=1)
+        n0 = 32
+        lg = [eng.forward(tokens[:n0], list(range(n0)), [0] * n0),
+              eng.forward(tokens[n0:], list(range(n0, len(tokens))), [0] * (len(tokens) - n0))]
+        ids = [list(eng.forward_argmax(tokens[:n0], list(range(n0)), [0] * n0)),
+               list(eng.forward_argmax(tokens[n0:], list(range(n0, len(tokens))), [0] * (len(tokens) - n0)))]
+        _, dec = eng.decode_greedy(6, [ids[1][-1]], [len(tokens)], [0])  # decode rows: fused exchange if on
+        if comm.timed_out():
+            raise AssertionError("a flag wait timed out")
+        fused = bool(eng.tp_fused)
+        dist.barrier()
+        q.put((rank, (np.concatenate(lg) if rank == 0 else None, ids, fused, list(dec))))
+    except Exception as e:
+        q.put((rank, repr(e)))
+
+
 def _run(target, world, *args, timeout=240, kwargs=None):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
@@ -148,6 +171,50 @@ def test_xgmi_engine_tp_matches_single(C, tmp_path, world, sync_type):
     assert agree >= steps - 2 and res[0][1][:4] == list(ref_toks[:4]), (res[0][1], ref_toks)
 
 
+@pytest.mark.parametrize("world,sync_type", [(2, "f32"), (4, "f32"), (2, "q80"), (4, "q80")])
+def test_xgmi_engine_tp_batched_matches_single(C, tmp_path, world, sync_type):
+    """Prefill-sized forwards (32 and 64 rows: MFMA GEMMs, MFMA prefill attention, partial sums
+    all-reduced by separate kernels over xGMI) at TP=2/4 vs TP=1 on the same model: logits within
+    tolerance, argmax ids bitwise identical on every rank."""
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=11, dim=512, n_heads=8,
+                               n_kv_heads=4, hidden_dim=1024, vocab_size=1024)
+    rng = np.random.default_rng(3)
+    tokens = [int(t) for t in rng.integers(0, 1024, 96)]
+    single = C.HipEngine(m, "q80", kv_bf16=True, max_batch=64, n_slots=1)
+    ref = np.concatenate([single.forward(tokens[:32], list(range(32)), [0] * 32),
+                          single.forward(tokens[32:], list(range(32, 96)), [0] * 64)])
+    del single
+    res = _run(_engine_tp_batched, world, m, tokens, kwargs=dict(sync_type=sync_type))
+    assert all(isinstance(v, tuple) for v in res.values()), res
+    got = res[0][0]
+    assert got.shape == ref.shape
+    rel = np.abs(got - ref).max() / np.abs(ref).max()
+    assert rel < (3e-2 if sync_type == "f32" else 6e-2), rel
+    assert (got.argmax(-1) == ref.argmax(-1)).mean() >= 0.95
+    for r in range(1, world):
+        assert res[r][1] == res[0][1] and res[r][3] == res[0][3], r
+    assert res[0][2], "fused exchange expected on for the decode rows"
+
+
+def test_fused_exchange_residency_guard(C, tmp_path):
+    """A fused-exchange GEMV whose grid is not fully co-resident could deadlock (its workgroups
+    spin on peers): the engine checks occupancy x CUs at construction and otherwise falls back to
+    separate all-reduce kernels - forced here with DL_FUSED_RESIDENT=1 - with the same results."""
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=11, dim=512, n_heads=8,
+                               n_kv_heads=4, hidden_dim=1024, vocab_size=1024)
+    tokens = [int(t) for t in np.random.default_rng(4).integers(0, 1024, 96)]
+    a = _run(_engine_tp_batched, 2, m, tokens, kwargs=dict(env={"DL_FUSED_RESIDENT": "1"}))
+    b = _run(_engine_tp_batched, 2, m, tokens)
+    assert all(isinstance(v, tuple) for v in list(a.values()) + list(b.values())), (a, b)
+    assert a[0][2] is False and b[0][2] is True
+    assert np.array_equal(a[0][0], b[0][0]) and a[0][1] == b[0][1]
+    assert a[0][3][:4] == b[0][3][:4] and a[1][3] == a[0][3] and b[1][3] == b[0][3]
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_xgmi_q80_tp_matches_cpu_q80_tp(C, tmp_path, world):
     """GPU TP with the Q80 exchange (fused GEMV-tail exchange of Q80-quantized partials) vs the CPU
@@ -184,7 +251,7 @@ def test_cli_root_workers_over_xgmi(tmp_path, n_workers):
     m, t, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=7, dim=512, n_heads=8,
                                n_kv_heads=4, hidden_dim=1024)
     base = [dllama, "inference", "--model", m, "--tokenizer", t, "--buffer-float-type", "q80", "--prompt",
-            "hello world the", "--steps", "24", "--temperature", "0", "--gpu-index", "0"]
+            "hello world the", "--steps", "24", "--temperature", "0", "--gpu-index", "0", "--sync-type", "f32"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", DL_TP_COMM="xgmi", **_same_gpu_env(n_workers + 1))
     ref = subprocess.run(base, capture_output=True, timeout=120, env=env)
     assert ref.returncode == 0, ref.stdout.decode(errors="replace")
