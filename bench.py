@@ -304,7 +304,7 @@ def main() -> int:
     tpf32_ms = None
     if world > 1 and args.sync_type != "f32":  # the exact f32 exchange next to the Q80 wire format
         del eng
-        eng = make_engine(sync="f32")
+        eng = make_engine(max(seq_len, pos0 + 48), sync="f32")
         eng.decode_greedy(4, tokens, [pos0] * B, list(range(B)))
         barrier()
         torch.cuda.synchronize()
