@@ -1,0 +1,576 @@
+// Batched (prefill / multi-user decode) matmuls on MFMA for gfx950: Q40 and F32 weights, the
+// split-K combine and fused epilogues, and the residual + RMS norm -> f16 staging kernel.
+#include "decode_dev.h"
+
+#include <cstdlib>
+
+namespace dl {
+namespace hipk {
+
+// ------------------------------------------------------------------------------------------------
+// Batched GEMM design notes (measured, profiles/r2_gemm_designs.md): two alternatives were built
+// and measured slower than this kernel on every shape - (v2) weights HBM -> VGPR ring with the
+// activations refilled through a 4-deep LDS ring (shared vmcnt capped the weight stream at 3 steps
+// in flight), (v3) activations resident in LDS with a deep weight ring and 4 or 8 waves (1.4-1.7
+// TB/s on w13, issue-stall bound per PMC: SQ_WAIT_INST_ANY 46 % of wave cycles). This v1 stays.
+// Batched Q40 matmul on MFMA (prefill / multi-user decode, 2..32 tokens per launch).
+//   out[t][row] = sum_k W[row][k] * x[t][k], W Q40 (the GEMV's tiled layout), x f16.
+// Each workgroup owns 64 weight rows (4 waves x 16) and one K split, streamed in chunks of 16
+// Q40 blocks. Both operands are copied HBM/L2 -> LDS with global_load_lds_dwordx4 (no VGPR
+// staging; one 16-B unit per lane, contiguous 256-B+ runs per wave instruction), multi-buffered
+// with counted vmcnt waits and raw barriers (kGemmStages buffers), into XOR-swizzled images so the fragment reads are
+// bank-conflict free. Per block a lane dequantizes 8 nibbles of its row ((1024+q) - 1032 exact in
+// f16, times d) into the B fragment of v_mfma_f32_16x16x32_f16; A fragments are read as is.
+// Split-K partials are combined in split order by the last-arriving workgroup (agent-scope
+// release/acquire counter: deterministic), which runs the fused epilogues (store / SwiGLU /
+// SwiGLU -> f16 / SwiGLU -> Q80 / RoPE + KV append).
+// ------------------------------------------------------------------------------------------------
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+static constexpr int kGemmRows = 64;
+static constexpr int kGemmCh = 8;  // Q40 blocks per pipeline stage (~25 KB at 32 tokens)
+
+// Split-K degree: grow S until the grid reaches the workgroup target (DL_GEMM_WG, read once) or
+// a split would get fewer than kGemmCh blocks. The target is sized so every CU holds its 3
+// resident workgroups: with one chunk in flight per workgroup, bytes in flight per CU (and so
+// HBM bandwidth) scale with resident workgroups, not with tiles.
+static int gemmWgTarget() {
+    static const int v = [] {
+        const char *e = std::getenv("DL_GEMM_WG");
+        return e ? std::max(1, std::atoi(e)) : 256;
+    }();
+    return v;
+}
+static int gemmMaxSplits() {
+    static const int v = [] {
+        const char *e = std::getenv("DL_GEMM_MAXS");
+        return e ? std::max(1, std::atoi(e)) : 8;
+    }();
+    return v;
+}
+
+GemmPlan gemmPlan(int rows, int n, int M) {
+    GemmPlan p;
+    p.rt = 1;
+    p.tiles = (rows + kGemmRows - 1) / kGemmRows;
+    p.splits = gemmSplits(rows, n, M);
+    return p;
+}
+
+bool gemmSupported(int n) { return n % 32 == 0; }
+
+int gemmSplits(int rows, int n, int M) {
+    (void)M;
+    const int tiles = (rows + kGemmRows - 1) / kGemmRows, nb = n / 32;
+    const int target = gemmWgTarget(), maxS = gemmMaxSplits();
+    int S = 1;
+    while (2 * S <= maxS && tiles * S < target && nb % (2 * S) == 0 && nb / (2 * S) >= kGemmCh) S *= 2;
+    // deep K (w2: 4096 x 14336): keep splitting up to two workgroups per CU while every split
+    // still streams >= 4 chunks (measured w2 M=8 23.9 -> 19.6 us; shallower matrices lose)
+    while (2 * S <= maxS && tiles * 2 * S <= 2 * target && nb % (2 * S) == 0 && nb / (2 * S) >= 4 * kGemmCh) S *= 2;
+    return S;
+}
+
+int gemmTokenPad(int M) { return M <= 16 ? 16 : M <= 32 ? 32 : 64; }
+
+size_t gemmPartFloats(int rows, int n, int maxTokens) {
+    const int tiles = (rows + kGemmRows - 1) / kGemmRows, S = gemmSplits(rows, n, maxTokens);
+    const int mp = gemmTokenPad(maxTokens);
+    return S > 1 ? (size_t)S * tiles * mp * kGemmRows : 0;
+}
+
+// stage layout (bytes): weights [64 rows][8 units] x 16 B | scales [32 pairs][8] u32 | x [MP][32 units] x 16 B
+static constexpr int kStW = kGemmRows * kGemmCh * 16, kStD = (kGemmRows / 2) * kGemmCh * 4;
+__host__ __device__ static constexpr int gemmStageBytes(int MT) { return kStW + kStD + MT * 16 * kGemmCh * 64; }
+#ifndef DL_GEMM_STAGES
+#define DL_GEMM_STAGES 2  // 3 stages (2 WGs/CU) measured slower: batch-32 8.1k vs 8.8k tok/s
+#endif
+static constexpr int kGemmStages = DL_GEMM_STAGES;  // stage buffers (kGemmStages-1 chunks in flight)
+static size_t gemmLds(int MT, int stages) { return stages * (size_t)gemmStageBytes(MT) + 16 + 320 * 4; }  // + flag, row scales
+
+// 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d via the 0x6400 | q magic (1024 + q)
+__device__ __forceinline__ half8 dequantQ40x8(u32x2 wv, int nibHi, uint32_t d16) {
+    const uint32_t lo = nibHi ? (wv.x >> 4) & 0x0F0F0F0Fu : wv.x & 0x0F0F0F0Fu;
+    const uint32_t hi = nibHi ? (wv.y >> 4) & 0x0F0F0F0Fu : wv.y & 0x0F0F0F0Fu;
+    const uint32_t p0 = __builtin_amdgcn_perm(0x64646464u, lo, 0x07010700u);
+    const uint32_t p1 = __builtin_amdgcn_perm(0x64646464u, lo, 0x07030702u);
+    const uint32_t p2 = __builtin_amdgcn_perm(0x64646464u, hi, 0x07010700u);
+    const uint32_t p3 = __builtin_amdgcn_perm(0x64646464u, hi, 0x07030702u);
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const _Float16 d = __builtin_bit_cast(_Float16, (uint16_t)d16);
+    // (1024 + q) - 1032 = q - 8 is exact in f16; one rounding in the multiply by d
+    const h2 dd = {d, d};
+    const h2 off = {(_Float16)-1032.0f, (_Float16)-1032.0f};
+    const h2 r0 = (__builtin_bit_cast(h2, p0) + off) * dd;
+    const h2 r1 = (__builtin_bit_cast(h2, p1) + off) * dd;
+    const h2 r2 = (__builtin_bit_cast(h2, p2) + off) * dd;
+    const h2 r3 = (__builtin_bit_cast(h2, p3) + off) * dd;
+    half8 out;
+    out[0] = r0[0]; out[1] = r0[1]; out[2] = r1[0]; out[3] = r1[1];
+    out[4] = r2[0]; out[5] = r2[1]; out[6] = r3[0]; out[7] = r3[1];
+    return out;
+}
+
+// one 16-B global -> LDS copy per lane; `lds` = this wave's base (lane l lands at lds + 16 l)
+__device__ __forceinline__ void glds16(const void *g, void *lds) {
+    __builtin_amdgcn_global_load_lds(const_cast<void *>(g), reinterpret_cast<__attribute__((address_space(3))) void *>(
+                                         reinterpret_cast<uintptr_t>(lds)), 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void *g, void *lds) {
+    __builtin_amdgcn_global_load_lds(const_cast<void *>(g), reinterpret_cast<__attribute__((address_space(3))) void *>(
+                                         reinterpret_cast<uintptr_t>(lds)), 4, 0, 0);
+}
+
+// EPI_RES hand-off scale (power of two: exact) and the f16 store that saturates instead of
+// overflowing to inf.
+static constexpr float kResXScale = 1.0f / 32.0f;
+__device__ __forceinline__ _Float16 satF16(float v) { return (_Float16)fminf(fmaxf(v, -65504.f), 65504.f); }
+
+// Split-K combine and fused epilogues shared by the batched GEMMs (Q40 and f32): `acc` holds this
+// lane's C fragments (weight row (local) wave*16 + col, token t*16 + h*4 + i); `smem` must hold
+// MP x 64 floats and is free (all K-loop LDS reads retired behind a barrier); `flag` one int.
+// tileIdx / tiles: this 64-row tile and the launch's tile count (split-K partial slots, counters).
+template <int MT, int EPI>
+__device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc)[MT], char *smem, int *flag,
+                                           int tileIdx, int tiles) {
+    const GemvArgs &a = ga.e;
+    constexpr int MP = MT * 16;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int col = lane & 15, h = lane >> 4, rl = wave * 16 + col;
+    const int sp = blockIdx.y, S = ga.splits;
+    const int R0 = tileIdx * kGemmRows;
+    float *tile = reinterpret_cast<float *>(smem);  // [MP][64], stages are free now
+    // C layout: weight row (local) wave*16 + col, token t*16 + h*4 + i
+    if (S == 1) {
+#pragma unroll
+        for (int t = 0; t < MT; t++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) tile[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
+    } else {
+        // Partials are written and read with agent-scope atomic accesses (global_store / load sc1:
+        // performed at the coherence point, never held in or served from one XCD's L2), so the
+        // hand-off needs no fence: an agent-scope release / acquire fence is a whole-L2 writeback
+        // (buffer_wbl2) / invalidate (buffer_inv) on gfx950, which measured ~28 us per split level
+        // on w13 (448 -> 896 workgroups) and evicted the other workgroups' cached activations.
+        // vmcnt(0) before the arrival count: every partial store has been performed.
+        float *part = ga.part + ((size_t)sp * tiles + tileIdx) * MP * kGemmRows;
+#pragma unroll
+        for (int t = 0; t < MT; t++)
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                __hip_atomic_store(part + (t * 16 + h * 4 + i) * kGemmRows + rl, acc[t][i], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            const int old = __hip_atomic_fetch_add(ga.counters + tileIdx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            flag[0] = old == S - 1;
+        }
+        __syncthreads();
+        if (!flag[0]) return;
+        if (tid == 0) __hip_atomic_store(ga.counters + tileIdx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // combine in split order (deterministic), all of a thread's splits in flight at once: this
+        // tail runs on one workgroup per tile after the others finished
+        const float *P = ga.part + (size_t)tileIdx * MP * kGemmRows;
+        const size_t stp = (size_t)tiles * MP * kGemmRows;
+        auto ld = [](const float *q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+        for (int i = tid; i < MP * kGemmRows / 4; i += kThreads) {
+            f32x4 v[8];
+#pragma unroll
+            for (int s2 = 0; s2 < 8; s2++)
+                if (s2 < S) {
+                    const float *q = P + s2 * stp + 4 * i;
+                    v[s2] = f32x4{ld(q), ld(q + 1), ld(q + 2), ld(q + 3)};
+                }
+            f32x4 r = v[0];
+#pragma unroll
+            for (int s2 = 1; s2 < 8; s2++)
+                if (s2 < S) r += v[s2];
+            for (int s2 = 8; s2 < S; s2++) {
+                const float *q = P + s2 * stp + 4 * i;
+                r += f32x4{ld(q), ld(q + 1), ld(q + 2), ld(q + 3)};
+            }
+            reinterpret_cast<f32x4 *>(tile)[i] = r;
+        }
+    }
+    // consumer of a fused residual + norm: per-token RMS scale from the producer's tile partials
+    float *rsL = reinterpret_cast<float *>(flag + 4);  // [64]
+    if (ga.ssIn) {
+        // TPT threads per token each sum a strided slice of the tile partials (independent loads
+        // in flight), then one thread per token adds the TPT slices in order (deterministic)
+        float *slL = rsL + 64;  // [256]
+        constexpr int TPT = kThreads / MP;
+        const int t = tid / TPT, q = tid % TPT;
+        float ssum = 0.f;
+        if (t < ga.M) {
+#pragma unroll 8
+            for (int j = q; j < ga.ssTiles; j += TPT) ssum += ga.ssIn[(size_t)j * ga.ldSS + t];
+        }
+        slL[tid] = ssum;
+        __syncthreads();
+        if (tid < ga.M) {
+            float tot = 0.f;
+            for (int i = 0; i < TPT; i++) tot += slL[tid * TPT + i];
+            rsL[tid] = (1.0f / kResXScale) / sqrtf(tot / (float)a.n + a.eps);
+        }
+    }
+    __syncthreads();
+    // fused epilogues on row pairs (2k, 2k+1) of the tile, 32 pairs per token
+    for (int i = tid; i < ga.M * 32; i += kThreads) {
+        const int t = i >> 5, k = i & 31, r0 = R0 + 2 * k;
+        float v0 = tile[t * kGemmRows + 2 * k], v1 = tile[t * kGemmRows + 2 * k + 1];
+        if (ga.ssIn) {
+            v0 *= rsL[t];
+            v1 *= rsL[t];
+        }
+        if constexpr (EPI == EPI_RES) {
+            float x0 = 0.f, x1 = 0.f;
+            if (r0 < a.rows) {  // a.rows even: whole pairs
+                const size_t o = (size_t)t * a.ldOut + r0;
+                x0 = ga.resIn[o] + v0;
+                x1 = ga.resIn[o + 1] + v1;
+                ga.resOut[o] = x0;
+                ga.resOut[o + 1] = x1;
+                // the un-normalised residual can be large (real checkpoints carry outlier channels
+                // of 1e3-1e4): stored pre-scaled by 2^-5 (exact) and saturated, so f16 never
+                // overflows to inf; the consumer folds 2^5 into its RMS scale
+                ga.resX[o] = satF16(x0 * ga.resW[r0] * kResXScale);
+                ga.resX[o + 1] = satF16(x1 * ga.resW[r0 + 1] * kResXScale);
+            }
+            const float ssq = groupSum<32>(x0 * x0 + x1 * x1);  // the 32 pairs of token t, in lane order
+            if (k == 0) ga.ssOut[(size_t)tileIdx * ga.ldSS + t] = ssq;
+        } else if constexpr (EPI == EPI_STORE) {
+            if (r0 < a.rows) a.out[(size_t)t * a.ldOut + r0] = v0;
+            if (r0 + 1 < a.rows) a.out[(size_t)t * a.ldOut + r0 + 1] = v1;
+        } else if constexpr (EPI == EPI_ACT) {
+            if (r0 < a.rows) a.out[(size_t)t * a.ldOut + (r0 >> 1)] = gateAct(a, v0) * v1;
+        } else if constexpr (EPI == EPI_ACT_F16) {
+            if (r0 < a.rows) ga.outH[(size_t)t * a.ldOut + (r0 >> 1)] = (_Float16)(gateAct(a, v0) * v1);
+        } else if constexpr (EPI == EPI_ACT_Q80) {
+            const int hBase = R0 >> 1;
+            if (hBase >= (a.rows >> 1)) continue;  // whole 32-unit block: uniform per lane group
+            const float hv = gateAct(a, v0) * v1;
+            const float amax = groupMax<32>(fabsf(hv));
+            const float d = amax / 127.0f;
+            const float id = d != 0.f ? 1.0f / d : 0.f;
+            int q = (int)rintf(hv * id);
+            q = q > 127 ? 127 : (q < -127 ? -127 : q);
+            a.oq[(size_t)t * a.ldOut + hBase + k] = (int8_t)q;
+            const float qsum = groupSum<32>((float)q);
+            if (k == 0) a.os[(size_t)t * (a.ldOut >> 5) + (hBase >> 5)] = make_float2(roundF16(d), qsum);
+        } else {
+            if (r0 < a.rows)
+                qkvPairStore(a, r0, v0, v1, a.rope + (size_t)a.pos[t] * (a.hs >> 1), a.pos[t], a.slot[t],
+                             a.out + (size_t)t * a.ldOut);
+        }
+    }
+}
+
+// STG = stage buffers: 2 double-buffers the chunk stream inside a workgroup; 1 (the 64-token
+// tile) drops that to fit 3 workgroups per CU, which then overlap each other's loads.
+template <int MT, int EPI, int STG>
+__global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
+    const GemvArgs &a = ga.e;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int SB = gemmStageBytes(MT);
+    constexpr int NW = kGemmRows * kGemmCh / kThreads, NX = MT * 16 * kGemmCh * 4 / kThreads;
+    constexpr int NLD = NW + 1 + NX;  // glds instructions per thread per stage
+    int *flag = reinterpret_cast<int *>(smem + STG * SB);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int col = lane & 15, h = lane >> 4;
+    const int n = a.n, nb = n >> 5, L = a.lanes, NG = kThreads / L, KS = (nb + L - 1) / L;
+    const int lgL = 31 - __builtin_clz(L);
+    const int tileIdx = blockIdx.x, sp = blockIdx.y, S = ga.splits;
+    const int R0 = tileIdx * kGemmRows;
+    const int bps = nb / S, j0 = sp * bps, j1 = j0 + bps;
+    const int nch = (bps + kGemmCh - 1) / kGemmCh;
+    const uint8_t *qs = a.qs;
+    const uint32_t *wd2 = reinterpret_cast<const uint32_t *>(a.wd);
+    auto unitOf = [&](int row, int j) -> size_t {  // tiled 16-B unit of (row, block j), clamped
+        row = min(row, a.rows - 1);
+        j = min(j, j1 - 1);
+        const int g = row / (2 * NG), rem = row % (2 * NG), gi = rem >> 1, rpar = rem & 1;
+        const int k = j >> lgL, li = j & (L - 1);
+        return (((size_t)g * KS + k) * 2 + rpar) * kThreads + gi * L + li;
+    };
+    auto scaleIdx = [&](int pairRow, int j) -> size_t {  // tiled u32 pair scale of (row pair, block j)
+        const int row = min(pairRow, a.rows - 1);
+        j = min(j, j1 - 1);
+        const int g = row / (2 * NG), rem = row % (2 * NG), gi = rem >> 1;
+        const int k = j >> lgL, li = j & (L - 1);
+        return ((size_t)g * KS + k) * kThreads + gi * L + li;
+    };
+    // issue the copies of chunk c into stage buffer b
+    auto issue = [&](int c, int b) {
+        char *st = smem + b * SB;
+        const int c0 = j0 + c * kGemmCh;
+        // weights: unit u = s*256 + tid -> (row_l = u/8, position p = u%8) holds block p ^ ((row_l>>1)&7)
+#pragma unroll
+        for (int s = 0; s < NW; s++) {
+            const int u = s * kThreads + tid, rl = u / kGemmCh, pp = u % kGemmCh;
+            const size_t unit = unitOf(R0 + rl, c0 + (pp ^ ((rl >> 1) & (kGemmCh - 1))));
+            glds16(qs + unit * 16, st + (size_t)(s * kThreads + wave * 64) * 16);
+        }
+        // pair scales: u = tid -> (pair_l = u/8, block u%8), 4 B each
+        {
+            const int pl = tid / kGemmCh, jj = tid % kGemmCh;
+            glds4(wd2 + scaleIdx(R0 + 2 * pl, c0 + jj), st + kStW + (size_t)(wave * 64) * 4);
+        }
+        // activations: token row t = 4*kGemmCh units of 8 f16; position p holds unit p ^ (t&15)
+#pragma unroll
+        for (int s = 0; s < NX; s++) {
+            const int u = s * kThreads + tid, t = u / (4 * kGemmCh), pp = u % (4 * kGemmCh);
+            const int uu = pp ^ (t & 15);
+            const int cb = min(c0 + (uu >> 2), j1 - 1);  // block of this unit (clamped)
+            const _Float16 *src = ga.x + (size_t)t * n + (size_t)cb * 32 + (uu & 3) * 8;
+            glds16(src, st + kStW + kStD + (size_t)(s * kThreads + wave * 64) * 16);
+        }
+    };
+
+    f32x4 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int rl = wave * 16 + col;  // this lane's weight row (local)
+    const int byteHalf = h & 1, nibHi = h >> 1;
+
+    constexpr int PF = STG - 1;  // chunks in flight ahead of the one consumed
+    for (int c = 0; c < PF && c < nch; c++) issue(c, c);
+    for (int c = 0; c < nch; c++) {
+        if (c + PF < nch) issue(c + PF, (c + PF) % STG);
+        // wait until chunk c landed (this thread): the chunks issued after it may stay in flight
+        const int after = min(nch - 1, c + PF) - c;
+        if (after >= 3)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * NLD) : "memory");
+        else if (after == 2)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * NLD) : "memory");
+        else if (after == 1)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NLD) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // ... and for every thread
+        const char *st = smem + (c % STG) * SB;
+        const int cn = min(kGemmCh, bps - c * kGemmCh);
+#pragma unroll
+        for (int jj = 0; jj < kGemmCh; jj++) {
+            // swizzle key (rl >> 1) & 7: the 16 rows of a wave's ds_read_b64 (two 8-B halves per
+            // 16-B unit) land on 32 distinct bank pairs (rows 128 B apart alias every other row;
+            // the old key rl & 7 left 2-way conflicts: SQ_LDS_BANK_CONFLICT 25 % of LDS cycles)
+            const int pp = jj ^ ((rl >> 1) & (kGemmCh - 1));
+            const u32x2 wv = *reinterpret_cast<const u32x2 *>(st + (size_t)(rl * kGemmCh + pp) * 16 + byteHalf * 8);
+            const uint32_t dw = *reinterpret_cast<const uint32_t *>(st + kStW + (size_t)((rl >> 1) * kGemmCh + jj) * 4);
+            const uint32_t d16 = jj < cn ? ((rl & 1) ? dw >> 16 : dw & 0xFFFFu) : 0u;
+            const half8 b = dequantQ40x8(wv, nibHi, d16);
+#pragma unroll
+            for (int t = 0; t < MT; t++) {
+                const int tok = t * 16 + col, up = (jj * 4 + h) ^ (tok & 15);
+                const half8 av = *reinterpret_cast<const half8 *>(st + kStW + kStD + (size_t)(tok * 4 * kGemmCh + up) * 16);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b, acc[t], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // stage c % STG is refilled at iteration c + 1
+    }
+
+    gemmFinish<MT, EPI>(ga, acc, smem, flag, blockIdx.x, gridDim.x);
+}
+
+static int gemmStages4() {  // stage buffers of the 64-token tile (DL_GEMM_STG4, read once)
+    static const int v = [] {
+        const char *e = std::getenv("DL_GEMM_STG4");
+        return e && std::atoi(e) == 2 ? 2 : 1;
+    }();
+    return v;
+}
+
+static int gemmStages2() {  // stage buffers of the 32-token tile (DL_GEMM_STG2, read once)
+    static const int v = [] {
+        const char *e = std::getenv("DL_GEMM_STG2");
+        const int k = e ? std::atoi(e) : kGemmStages;
+        return k >= 1 && k <= 3 ? k : kGemmStages;
+    }();
+    return v;
+}
+
+static int gemmStages1() {  // stage buffers of the 16-token tile (DL_GEMM_STG1 = 2..4, read once)
+    static const int v = [] {
+        const char *e = std::getenv("DL_GEMM_STG1");
+        const int k = e ? std::atoi(e) : kGemmStages;
+        return k >= 2 && k <= 4 ? k : kGemmStages;
+    }();
+    return v;
+}
+
+void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
+    const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
+    const int MT = gemmTokenPad(ga.M) / 16;
+    const int stg = MT == 4 ? gemmStages4() : MT == 2 ? gemmStages2() : gemmStages1();
+    const dim3 grid(tiles, ga.splits);
+    const size_t lds = gemmLds(MT, stg);
+#define DL_GEMM_CASE(M_, E, G)                                                                    \
+    if (MT == M_ && epi == E && stg == G) {                                                       \
+        if (lds > 65536) allowLds((const void *)gemmQ40Kernel<M_, E, G>, lds); /* per device */  \
+        hipLaunchKernelGGL((gemmQ40Kernel<M_, E, G>), grid, dim3(kThreads), lds, s, ga);         \
+        return;                                                                                   \
+    }
+#define DL_GEMM_CASES(M_, G)                                                                      \
+    DL_GEMM_CASE(M_, EPI_STORE, G) DL_GEMM_CASE(M_, EPI_ACT, G) DL_GEMM_CASE(M_, EPI_ACT_Q80, G)  \
+    DL_GEMM_CASE(M_, EPI_QKV, G) DL_GEMM_CASE(M_, EPI_ACT_F16, G) DL_GEMM_CASE(M_, EPI_RES, G)
+    DL_GEMM_CASES(1, kGemmStages) DL_GEMM_CASES(1, 3) DL_GEMM_CASES(1, 4) DL_GEMM_CASES(2, kGemmStages) DL_GEMM_CASES(2, 1) DL_GEMM_CASES(2, 3) DL_GEMM_CASES(4, 1) DL_GEMM_CASES(4, 2)
+#undef DL_GEMM_CASES
+#undef DL_GEMM_CASE
+}
+
+// Batched matmul for F32 weights on MFMA (the reference runs F32 batches through
+// llamafile_sgemm, nn-cpu-ops.cpp:1018-1037): out[t][row] = sum_k W[row][k] x[t][k], W f32
+// row-major [rows][n] (exact: v_mfma_f32_16x16x4_f32), x f16 as on the Q40 path (the only
+// rounding). A wave owns 16 rows; per 32-k step lane (col, h) streams 32 B of its row col
+// (k = 8h .. 8h+7: 4 lanes cover a 128-B line) straight into VGPRs - no LDS for the weights,
+// which are read once - and the matching 16 B of f16 activations per token tile (L2-resident,
+// shared by the workgroup's waves). Element e of those 8 feeds MFMA e on both operands (k = 8h+e,
+// a permutation of k). 4 steps are issued per iteration so 4 x 32 B per lane stay in flight.
+// Split-K, the deterministic combine and the fused epilogues are the Q40 GEMM's (gemmFinish).
+template <int MT, int EPI>
+__global__ __launch_bounds__(kThreads) void gemmF32Kernel(GemmArgs ga) {
+    const GemvArgs &a = ga.e;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    int *flag = reinterpret_cast<int *>(smem + MT * 16 * kGemmRows * 4);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, col = lane & 15, h = lane >> 4;
+    const int n = a.n, kps = n / ga.splits, k0 = blockIdx.y * kps;
+    const int row = min(blockIdx.x * kGemmRows + wave * 16 + col, a.rows - 1);  // clamped: outputs dropped
+    const float *wp = a.wf + (size_t)row * n + k0 + 8 * h;
+    const _Float16 *xp = ga.x + (size_t)col * n + k0 + 8 * h;
+    f32x4 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int U = 4;
+    int k = 0;
+    for (; k + 32 * U <= kps; k += 32 * U) {
+        f32x4 w[U][2];
+        half8 xv[U][MT];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            w[u][0] = *reinterpret_cast<const f32x4 *>(wp + k + 32 * u);
+            w[u][1] = *reinterpret_cast<const f32x4 *>(wp + k + 32 * u + 4);
+#pragma unroll
+            for (int t = 0; t < MT; t++) xv[u][t] = *reinterpret_cast<const half8 *>(xp + (size_t)t * 16 * n + k + 32 * u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int e = 0; e < 8; e++)
+#pragma unroll
+                for (int t = 0; t < MT; t++)
+                    acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)xv[u][t][e], w[u][e >> 2][e & 3], acc[t], 0, 0, 0);
+    }
+    for (; k < kps; k += 32) {  // remainder steps (kps is a multiple of 32)
+        const f32x4 w0 = *reinterpret_cast<const f32x4 *>(wp + k), w1 = *reinterpret_cast<const f32x4 *>(wp + k + 4);
+#pragma unroll
+        for (int t = 0; t < MT; t++) {
+            const half8 xv = *reinterpret_cast<const half8 *>(xp + (size_t)t * 16 * n + k);
+#pragma unroll
+            for (int e = 0; e < 8; e++)
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32((float)xv[e], e < 4 ? w0[e] : w1[e - 4], acc[t], 0, 0, 0);
+        }
+    }
+    gemmFinish<MT, EPI>(ga, acc, smem, flag, blockIdx.x, gridDim.x);
+}
+
+void launchGemmF32(const GemmArgs &ga, int epi, hipStream_t s) {
+    const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
+    const int MT = gemmTokenPad(ga.M) / 16;
+    const dim3 grid(tiles, ga.splits);
+    const size_t lds = (size_t)MT * 16 * kGemmRows * 4 + 16 + 320 * 4;  // + flag, row scales
+#define DL_GEMMF_CASE(M_, E)                                                              \
+    if (MT == M_ && epi == E) {                                                           \
+        if (lds > 65536) allowLds((const void *)gemmF32Kernel<M_, E>, lds);               \
+        hipLaunchKernelGGL((gemmF32Kernel<M_, E>), grid, dim3(kThreads), lds, s, ga);     \
+        return;                                                                           \
+    }
+#define DL_GEMMF_CASES(M_)                                                                \
+    DL_GEMMF_CASE(M_, EPI_STORE) DL_GEMMF_CASE(M_, EPI_ACT) DL_GEMMF_CASE(M_, EPI_QKV)    \
+    DL_GEMMF_CASE(M_, EPI_ACT_F16) DL_GEMMF_CASE(M_, EPI_RES)
+    DL_GEMMF_CASES(1) DL_GEMMF_CASES(2) DL_GEMMF_CASES(4)
+#undef DL_GEMMF_CASES
+#undef DL_GEMMF_CASE
+    throw Error("launchGemmF32: unsupported epilogue");
+}
+
+// Residual add + RMS norm (optional) of M rows -> f16 (one workgroup per row): the batched
+// path's replacement for the GEMV's per-workgroup norm prologue.
+__global__ __launch_bounds__(kThreads) void normF16Kernel(GemvArgs a, _Float16 *out) {
+    __shared__ float scratch[64];
+    constexpr int PV = 8;  // float4 per thread kept in registers (n <= 8192 in one pass)
+    const int b = blockIdx.x, n = a.n, tid = threadIdx.x;
+    const float *x = a.in + (size_t)b * a.ldIn;
+    const float *y = a.addIn ? a.addIn + (size_t)b * a.ldIn : nullptr;
+    float *xo = a.xNext ? a.xNext + (size_t)b * a.ldIn : nullptr;
+    _Float16 *o = out + (size_t)b * n;
+    const bool inReg = n <= kThreads * 4 * PV;
+    float4 v[PV], gw[PV];
+    float ss = 0.f;
+    if (inReg) {
+        // every load (x, the residual delta and the norm weights) is issued before any is used:
+        // one memory round trip before the reduction instead of three
+        float4 w[PV];
+#pragma unroll
+        for (int k = 0; k < PV; k++) {
+            const int i = min((tid + k * kThreads) * 4, n - 4);
+            v[k] = ld4(x + i);
+            w[k] = y ? ld4(y + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+            gw[k] = a.normW ? ld4(a.normW + i) : make_float4(1.f, 1.f, 1.f, 1.f);
+        }
+#pragma unroll
+        for (int k = 0; k < PV; k++) {
+            const int i = (tid + k * kThreads) * 4;
+            if (i < n) {
+                v[k].x += w[k].x; v[k].y += w[k].y; v[k].z += w[k].z; v[k].w += w[k].w;
+                if (xo) st4(xo + i, v[k]);
+                ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+            }
+        }
+    } else {
+        for (int i = tid * 4; i < n; i += kThreads * 4) {
+            float4 u = ld4(x + i);
+            if (y) {
+                const float4 w = ld4(y + i);
+                u.x += w.x; u.y += w.y; u.z += w.z; u.w += w.w;
+            }
+            if (xo) st4(xo + i, u);
+            ss += u.x * u.x + u.y * u.y + u.z * u.z + u.w * u.w;
+        }
+    }
+    float inv = 1.0f;
+    if (a.normW) {
+        ss = blockSum<kThreads>(ss, scratch);
+        inv = 1.0f / sqrtf(ss / (float)n + a.eps);
+    }
+    auto emit = [&](int i, float4 u, const float4 *gp) {
+        const float4 g = gp ? *gp : (a.normW ? ld4(a.normW + i) : make_float4(1.f, 1.f, 1.f, 1.f));
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        const h4 r = {(_Float16)(g.x * (inv * u.x)), (_Float16)(g.y * (inv * u.y)), (_Float16)(g.z * (inv * u.z)),
+                      (_Float16)(g.w * (inv * u.w))};
+        *reinterpret_cast<h4 *>(o + i) = r;
+    };
+    if (inReg) {
+#pragma unroll
+        for (int k = 0; k < PV; k++) {
+            const int i = (tid + k * kThreads) * 4;
+            if (i < n) emit(i, v[k], &gw[k]);
+        }
+    } else {
+        for (int i = tid * 4; i < n; i += kThreads * 4) {
+            float4 u = xo ? ld4(xo + i) : ld4(x + i);
+            if (!xo && y) {
+                const float4 w = ld4(y + i);
+                u.x += w.x; u.y += w.y; u.z += w.z; u.w += w.w;
+            }
+            emit(i, u, nullptr);
+        }
+    }
+}
+
+void launchNormF16(const GemvArgs &a, _Float16 *out, int M, hipStream_t s) {
+    hipLaunchKernelGGL(normF16Kernel, dim3(M), dim3(kThreads), 0, s, a, out);
+}
+
+}  // namespace hipk
+}  // namespace dl
