@@ -1,0 +1,8 @@
+// Fused attention block instances: qkv 64 lanes per row, wo 16, head size 128 (attn_block_inst.h).
+#include "attn_block_inst.h"
+
+namespace dl {
+namespace hipk {
+const void *attnBlockFn_64_16_128(int hg, bool bf16, bool tp) { return attnBlockFnT<64, 16, 128>(hg, bf16, tp); }
+}  // namespace hipk
+}  // namespace dl

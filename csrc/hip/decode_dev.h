@@ -232,8 +232,35 @@ __device__ __forceinline__ float gateAct(const GemvArgs &a, float v) {
     return 0.5f * v * (1.0f + tanhf(0.79788456080286535588f * v * (1.0f + 0.044715f * v * v)));
 }
 
+// Write-through (agent-scope, sc1) stores / loads for data handed to other workgroups INSIDE one
+// launch (cdna_hip_programming.md Guideline 16: L2s are per XCD and not coherent, so a plain store
+// may sit in the writer's L2 and a plain load may hit a stale line): the producer's stores are
+// performed at the coherence point, the consumer's loads bypass its caches. WT = false: plain.
+template <bool WT>
+__device__ __forceinline__ void st32(void *p, uint32_t v) {
+    if constexpr (WT) __hip_atomic_store(reinterpret_cast<uint32_t *>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *reinterpret_cast<uint32_t *>(p) = v;
+}
+template <bool WT>
+__device__ __forceinline__ void st64(void *p, uint64_t v) {
+    if constexpr (WT) __hip_atomic_store(reinterpret_cast<uint64_t *>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *reinterpret_cast<uint64_t *>(p) = v;
+}
+template <bool WT>
+__device__ __forceinline__ void stF2(float *p, float a, float b) {
+    st64<WT>(p, (uint64_t)__float_as_uint(a) | ((uint64_t)__float_as_uint(b) << 32));
+}
+__device__ __forceinline__ uint32_t ldWT32(const void *p) {
+    return __hip_atomic_load(reinterpret_cast<const uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ldWT64(const void *p) {
+    return __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Rows [0, q0) are Q, [q0, q0+kv0) K, then V. Q and K pairs are rotated (RoPE at this row's
-// position); K and V are appended to the KV cache at [slot][pos].
+// position); K and V are appended to the KV cache at [slot][pos]. WT: write-through (the fused
+// attention block's attention workgroups read them in the same launch).
+template <bool WT = false>
 __device__ __forceinline__ void qkvPairStore(const GemvArgs &a, int r0, float v0, float v1, const float2 *ropeRow,
                                              int p, int sl, float *qRow) {
     if (r0 < a.q0 + a.kv0) {
@@ -241,23 +268,23 @@ __device__ __forceinline__ void qkvPairStore(const GemvArgs &a, int r0, float v0
         const float o0 = v0 * cs.x - v1 * cs.y;
         const float o1 = v0 * cs.y + v1 * cs.x;
         if (r0 < a.q0) {
-            *reinterpret_cast<float2 *>(qRow + r0) = make_float2(o0, o1);
+            stF2<WT>(qRow + r0, o0, o1);
         } else {
             const size_t off = ((size_t)sl * a.seqLen + p) * a.kv0 + (r0 - a.q0);
             if (a.kvBf16) {
                 const uint32_t pk = (uint32_t)f32ToBf16(o0) | ((uint32_t)f32ToBf16(o1) << 16);
-                *reinterpret_cast<uint32_t *>(reinterpret_cast<uint16_t *>(a.kcache) + off) = pk;
+                st32<WT>(reinterpret_cast<uint16_t *>(a.kcache) + off, pk);
             } else {
-                *reinterpret_cast<float2 *>(reinterpret_cast<float *>(a.kcache) + off) = make_float2(o0, o1);
+                stF2<WT>(reinterpret_cast<float *>(a.kcache) + off, o0, o1);
             }
         }
     } else {
         const size_t off = ((size_t)sl * a.seqLen + p) * a.kv0 + (r0 - a.q0 - a.kv0);
         if (a.kvBf16) {
             const uint32_t pk = (uint32_t)f32ToBf16(v0) | ((uint32_t)f32ToBf16(v1) << 16);
-            *reinterpret_cast<uint32_t *>(reinterpret_cast<uint16_t *>(a.vcache) + off) = pk;
+            st32<WT>(reinterpret_cast<uint16_t *>(a.vcache) + off, pk);
         } else {
-            *reinterpret_cast<float2 *>(reinterpret_cast<float *>(a.vcache) + off) = make_float2(v0, v1);
+            stF2<WT>(reinterpret_cast<float *>(a.vcache) + off, v0, v1);
         }
     }
 }
@@ -281,15 +308,24 @@ __device__ __forceinline__ void storeHiddenQ80(const GemvArgs &a, const float *h
 }
 
 // Copy B rows of Q80 activations (n int8 + n/32 scale pairs) from global into the LDS image.
-template <int B>
+// WT: the rows were produced in this launch (write-through loads).
+template <int B, bool WT = false>
 __device__ __forceinline__ void stageQ80(const GemvArgs &a, int8_t *sq, float2 *ssc) {
     const int n = a.n, nb = n >> 5;
 #pragma unroll
     for (int b = 0; b < B; b++) {
-        const int4 *src = reinterpret_cast<const int4 *>(a.aq + (size_t)b * n);
-        int4 *dst = reinterpret_cast<int4 *>(sq + (size_t)b * n);
-        for (int i = threadIdx.x; i < (n >> 4); i += kThreads) dst[i] = src[i];
-        for (int i = threadIdx.x; i < nb; i += kThreads) ssc[b * nb + i] = a.as[(size_t)b * nb + i];
+        if constexpr (WT) {
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(a.aq + (size_t)b * n);
+            uint32_t *dst = reinterpret_cast<uint32_t *>(sq + (size_t)b * n);
+            for (int i = threadIdx.x; i < (n >> 2); i += kThreads) dst[i] = ldWT32(src + i);
+            const uint64_t *ss = reinterpret_cast<const uint64_t *>(a.as + (size_t)b * nb);
+            for (int i = threadIdx.x; i < nb; i += kThreads) reinterpret_cast<uint64_t *>(ssc)[b * nb + i] = ldWT64(ss + i);
+        } else {
+            const int4 *src = reinterpret_cast<const int4 *>(a.aq + (size_t)b * n);
+            int4 *dst = reinterpret_cast<int4 *>(sq + (size_t)b * n);
+            for (int i = threadIdx.x; i < (n >> 4); i += kThreads) dst[i] = src[i];
+            for (int i = threadIdx.x; i < nb; i += kThreads) ssc[b * nb + i] = a.as[(size_t)b * nb + i];
+        }
     }
     __syncthreads();
 }
@@ -469,14 +505,59 @@ static constexpr int kEarlySlots = DL_GEMV_KE;  // ring slots issued before the 
 enum GemvMode : int { GEMV_PLAIN = 0, GEMV_PRODUCER = 1, GEMV_CONSUMER = 2 };
 
 // In-launch hand-off state of the fused attention block (decode_block.hip).
+// Counters are monotonic across layers and forwards (never reset): after the s-th layer step
+// (s = (forward epoch - 1) * nLayers + layer + 1) KV group g's counter has been incremented
+// s * qkvExpect[g] times and the attention counter s * (head groups) times, so a waiter compares
+// against a target computed from s in wrapping u32 arithmetic ((int)(cnt - target) >= 0).
 struct BlockSync {
-    unsigned *qkvCnt = nullptr;   // [kv heads] arrivals of qkv workgroups per KV group
-    unsigned *attnCnt = nullptr;  // [1] arrivals of attention head groups
-    unsigned qkvTarget0 = 0;      // per-group target = qkvTarget0 * expected(group) (wrapping u32)
-    unsigned attnTarget = 0;
-    int *error = nullptr;
+    unsigned *qkvCnt = nullptr;          // [kv groups] arrivals of qkv workgroups per KV group
+    const unsigned *qkvExpect = nullptr; // [kv groups] qkv workgroups touching each group
+    unsigned *attnCnt = nullptr;         // [1] arrivals of attention head groups (final outputs)
+    unsigned step = 0;                   // s (see above)
+    unsigned attnTarget = 0;             // s * head groups
+    int *error = nullptr;                // set when a wait gave up (the engine raises)
     long long timeoutTicks = 0;
 };
+
+// One lane waits (relaxed agent-scope polls + s_sleep, bounded: a wait that gives up sets the
+// error word and every later wait fails fast), then the workgroup's barrier releases the others.
+__device__ __forceinline__ void blockWait(const unsigned *cnt, unsigned target, const BlockSync &bs) {
+    if (threadIdx.x == 0) {
+        if (__hip_atomic_load(bs.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            while ((int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+                __builtin_amdgcn_s_sleep(1);
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > bs.timeoutTicks) {
+                    __hip_atomic_store(bs.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// After write-through stores: every wave drains its stores, the barrier, then one lane signals.
+__device__ __forceinline__ void blockDrain() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+// KV groups touched by qkv rows [r0, r1) (Q rows of the group's kvMul heads, its K and V rows):
+// a bit mask (<= 64 groups). Shared by the producers and the host's expected counts.
+__host__ __device__ inline unsigned long long qkvGroupMask(int r0, int r1, int q0, int kv0, int hs, int kvMul) {
+    unsigned long long m = 0;
+    auto span = [&](int lo, int hi, int base, int per) {  // rows [lo, hi) of a part starting at base
+        if (lo >= hi) return;
+        for (int g = (lo - base) / per; g <= (hi - 1 - base) / per; g++) m |= 1ull << g;
+    };
+    auto mx = [](int x, int y) { return x > y ? x : y; };
+    auto mn = [](int x, int y) { return x < y ? x : y; };
+    span(mx(r0, 0), mn(r1, q0), 0, kvMul * hs);
+    span(mx(r0, q0), mn(r1, q0 + kv0), q0, hs);
+    span(mx(r0, q0 + kv0), mn(r1, q0 + 2 * kv0), q0 + kv0, hs);
+    return m;
+}
 
 template <int L, int B, int PRO, int EPI, int MODE = GEMV_PLAIN>
 __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, char *smem, const BlockSync *bs = nullptr) {
@@ -693,7 +774,12 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
                 sRope[b * (kMaxHeadSize / 2) + i % h2] = a.rope[(size_t)a.pos[b] * h2 + i % h2];
             }
         }
-        if constexpr (PRO == PRO_RESNORM)
+        if constexpr (MODE == GEMV_CONSUMER) {
+            // the activations are produced in this launch: wait for every producer (the ring's
+            // weight loads are already in flight), then read them write-through
+            blockWait(bs->attnCnt, bs->attnTarget, *bs);
+            stageQ80<B, true>(a, sq, ssc);
+        } else if constexpr (PRO == PRO_RESNORM)
             resNormPrologue<B, true>(a, scratch, sq, ssc, nullptr);
         else
             stageQ80<B>(a, sq, ssc);
@@ -744,7 +830,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
                 } else if constexpr (EPI == EPI_ACT_Q80) {
                     hbuf[b * (R >> 1) + ((r0 - rowBase) >> 1)] = gateAct(a, v0) * v1;
                 } else {
-                    qkvPairStore(a, r0, v0, v1, sRope + b * (kMaxHeadSize / 2), posB[b], slotB[b],
+                    qkvPairStore<MODE == GEMV_PRODUCER>(a, r0, v0, v1, sRope + b * (kMaxHeadSize / 2), posB[b], slotB[b],
                                  a.out + (size_t)b * a.ldOut);
                 }
             }
@@ -786,7 +872,11 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
 
     const int unitsPerThread = PRO == PRO_RESNORM ? (n + 8 * kThreads - 1) / (8 * kThreads)
                                                   : (n + 16 * kThreads - 1) / (16 * kThreads);
-    if (B == 1 && unitsPerThread <= 1) {
+    static_assert(MODE != GEMV_CONSUMER || PRO == PRO_GLOBAL, "a consumer GEMV reads Q80 activations");
+    if constexpr (MODE == GEMV_CONSUMER) {
+        latePath();
+        mainLoop();
+    } else if (B == 1 && unitsPerThread <= 1) {
         earlyPath(std::integral_constant<int, 1>{});
         mainLoop();
     } else if (B == 1 && unitsPerThread <= 2) {
@@ -802,6 +892,17 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
     if constexpr (EPI == EPI_ACT_Q80) {
         __syncthreads();
         storeHiddenQ80<B>(a, hbuf, R >> 1, rowBase >> 1);
+    }
+    if constexpr (MODE == GEMV_PRODUCER) {  // rows published write-through: drain, then count in
+        blockDrain();
+        if (tid == 0) {
+            unsigned long long m = qkvGroupMask(rowBase, min(rowBase + R, a.rows), a.q0, a.kv0, a.hs, a.kvMul);
+            while (m) {
+                const int g = __builtin_ctzll(m);
+                m &= m - 1;
+                __hip_atomic_fetch_add(bs->qkvCnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     }
     if constexpr (tpx) {  // all-reduce the partial rows over the TP ranks, then store (sq is free now)
         __syncthreads();
@@ -858,7 +959,9 @@ __device__ __forceinline__ void loadKv(const void *base, size_t off, float (&v)[
 }
 
 // Final output of HG heads from LDS fin[HG][HS] -> f32 or Q80 (32-element blocks) in global.
-template <int HG, int HS, int AT>
+// WT: write-through (the fused attention block's wo workgroups read the Q80 output in the same
+// launch): 4 int8 per 32-bit store, the scale pair as one 64-bit store.
+template <int HG, int HS, int AT, bool WT = false>
 __device__ __forceinline__ void attnWriteOut(const AttnArgs &a, int b, int head0, const float *fin) {
     const int tid = threadIdx.x;
     if (a.outQ) {
@@ -870,9 +973,19 @@ __device__ __forceinline__ void attnWriteOut(const AttnArgs &a, int b, int head0
             int q = (int)rintf(v * id);
             q = q > 127 ? 127 : (q < -127 ? -127 : q);
             const int col = head0 * HS + i;
-            a.outQ[(size_t)b * a.ldOut + col] = (int8_t)q;
+            if constexpr (WT) {
+                const int q1 = __shfl_down(q, 1), q2 = __shfl_down(q, 2), q3 = __shfl_down(q, 3);
+                if ((i & 3) == 0)
+                    st32<true>(a.outQ + (size_t)b * a.ldOut + col, (uint32_t)(q & 0xFF) | ((uint32_t)(q1 & 0xFF) << 8) |
+                                                                       ((uint32_t)(q2 & 0xFF) << 16) | ((uint32_t)q3 << 24));
+            } else {
+                a.outQ[(size_t)b * a.ldOut + col] = (int8_t)q;
+            }
             const float qs = groupSum<32>((float)q);
-            if ((i & 31) == 0) a.outS[(size_t)b * (a.ldOut >> 5) + (col >> 5)] = make_float2(roundF16(d), qs);
+            if ((i & 31) == 0) {
+                float *sp = reinterpret_cast<float *>(a.outS + (size_t)b * (a.ldOut >> 5) + (col >> 5));
+                stF2<WT>(sp, roundF16(d), qs);
+            }
         }
     } else if (a.outH) {
         for (int i = tid; i < HG * HS; i += AT) a.outH[(size_t)b * a.ldOut + head0 * HS + i] = (_Float16)fin[i];
@@ -901,14 +1014,14 @@ static constexpr int kAttnThreads = 512;  // 8 waves = 32 groups of 16 lanes, on
 // chunk's (max, sum) in LDS (`scratch`, >= 2 * HG * splitGrid floats) with one load per thread and
 // keeps 8 partial-output loads in flight per thread: a serial loop over the chunks costs one
 // cross-XCD round trip per chunk (~30 us at 32 chunks).
-template <int HG, int HS, int AT>
+template <int HG, int HS, int AT, bool WT = false>
 __device__ __forceinline__ bool attnFinish(const AttnArgs &a, int b, int hgIdx, int c, int nSplit, float *redL,
                                            float *mlL, int *flagL, float *scratch) {
     const int tid = threadIdx.x, head0 = hgIdx * HG;
     if (nSplit == 1) {
         for (int i = tid; i < HG * HS; i += AT) redL[i] = redL[i] / mlL[(i / HS) * 2 + 1];
         __syncthreads();
-        attnWriteOut<HG, HS, AT>(a, b, head0, redL);
+        attnWriteOut<HG, HS, AT, WT>(a, b, head0, redL);
         return true;
     }
     const int G = a.splitGrid;
@@ -975,15 +1088,18 @@ __device__ __forceinline__ bool attnFinish(const AttnArgs &a, int b, int hgIdx, 
         redL[i] = acc / mlL[h * 2 + 1];
     }
     __syncthreads();
-    attnWriteOut<HG, HS, AT>(a, b, head0, redL);
+    attnWriteOut<HG, HS, AT, WT>(a, b, head0, redL);
     return true;
 }
 
 // One attention task: query heads [hgIdx*HG, +HG) of row b over sequence chunk c, AT threads.
 // Returns true when this call wrote the head group's final output (single chunk, or the last
 // chunk to arrive combined all of them).
-template <int HG, int HS, bool BF16, int AT>
-__device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, int c, char *smem) {
+// SYNC (fused attention block): q and the current position's K / V rows are produced by the qkv
+// workgroups of the same launch - wait for this KV group's producers, read those write-through.
+template <int HG, int HS, bool BF16, int AT, bool SYNC = false>
+__device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, int c, char *smem,
+                                         const BlockSync *bs = nullptr) {
     constexpr int NW = AT / 64, NG = AT / 16;
     constexpr int DPL = HS / 16;           // dims per lane: 16 lanes cover one position's head vector
     constexpr int TU = BF16 ? 8 : 4;       // keys per group loaded before any is consumed
@@ -1007,6 +1123,7 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
     float *mlL = redL + HG * HS;                    // [HG][2]
     int *flagL = reinterpret_cast<int *>(mlL + 2 * HG);
 
+    if constexpr (SYNC) blockWait(bs->qkvCnt + kvh, bs->step * bs->qkvExpect[kvh], *bs);
     // this lane's slice of the HG query heads (pre-scaled), vector loads
     const float scale = 1.0f / sqrtf((float)HS);
     float qr[HG][DPL];
@@ -1015,7 +1132,14 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
         const float *qp = a.q + (size_t)b * a.ldq + (head0 + h) * HS + l16 * DPL;
 #pragma unroll
         for (int i = 0; i < DPL; i += 4) {
-            const float4 v = ld4(qp + i);
+            float4 v;
+            if constexpr (SYNC) {
+                const uint64_t lo = ldWT64(qp + i), hi = ldWT64(qp + i + 2);
+                v = make_float4(__uint_as_float((uint32_t)lo), __uint_as_float((uint32_t)(lo >> 32)),
+                                __uint_as_float((uint32_t)hi), __uint_as_float((uint32_t)(hi >> 32)));
+            } else {
+                v = ld4(qp + i);
+            }
             qr[h][i] = v.x * scale;
             qr[h][i + 1] = v.y * scale;
             qr[h][i + 2] = v.z * scale;
@@ -1045,7 +1169,16 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
             const uint32_t *vp = reinterpret_cast<const uint32_t *>(
                 BF16 ? (const void *)(reinterpret_cast<const uint16_t *>(a.vcache) + off)
                      : (const void *)(reinterpret_cast<const float *>(a.vcache) + off));
-            if constexpr (RW == 4) {
+            if (SYNC && t == pos) {  // appended by this launch's qkv workgroups: write-through loads
+#pragma unroll
+                for (int w = 0; w < RW; w += 2) {
+                    const uint64_t kk = ldWT64(kp + w), vv = ldWT64(vp + w);
+                    kr[u][w] = (uint32_t)kk;
+                    kr[u][w + 1] = (uint32_t)(kk >> 32);
+                    vr[u][w] = (uint32_t)vv;
+                    vr[u][w + 1] = (uint32_t)(vv >> 32);
+                }
+            } else if constexpr (RW == 4) {
                 const uint4 k4 = *reinterpret_cast<const uint4 *>(kp), v4 = *reinterpret_cast<const uint4 *>(vp);
                 kr[u][0] = k4.x; kr[u][1] = k4.y; kr[u][2] = k4.z; kr[u][3] = k4.w;
                 vr[u][0] = v4.x; vr[u][1] = v4.y; vr[u][2] = v4.z; vr[u][3] = v4.w;
@@ -1139,7 +1272,7 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
     }
     __syncthreads();
 
-    return attnFinish<HG, HS, AT>(a, b, hgIdx, c, nSplit, redL, mlL, flagL, oW);
+    return attnFinish<HG, HS, AT, SYNC>(a, b, hgIdx, c, nSplit, redL, mlL, flagL, oW);
 }
 
 

@@ -99,6 +99,7 @@ class HipEngineImpl : public HipEngine {
             loadFromFile();
         uploadRope();
         DL_HIP(hipStreamSynchronize(stream_));
+        setupAttnBlock();
         load_.ms = timer.elapsedMs();
         load_.deviceBytes = deviceBytes_;
     }
@@ -182,6 +183,7 @@ class HipEngineImpl : public HipEngine {
 
   public:
     bool tpFused() const override { return tpFused_; }
+    bool attnBlock() const override { return blockOn_; }
     int fusedGridMax() const override { return fusedGridMax_; }
 
     ~HipEngineImpl() override {
@@ -305,7 +307,13 @@ class HipEngineImpl : public HipEngine {
     void syncAndCheckComm() {
         const int *flag = comm_ ? comm_->deviceErrorFlag() : nullptr;
         if (flag) DL_HIP(hipMemcpyAsync(hErr_, flag, sizeof(int), hipMemcpyDeviceToHost, stream_));
+        if (blockOn_) DL_HIP(hipMemcpyAsync(hErr_ + 1, dBlockErr_, sizeof(int), hipMemcpyDeviceToHost, stream_));
         DL_HIP(hipStreamSynchronize(stream_));
+        if (blockOn_ && hErr_[1] != 0) {
+            hErr_[1] = 0;
+            resetAttnBlockState();
+            throw Error("fused attention block: a workgroup wait timed out (not all workgroups resident?)");
+        }
         if (flag && *hErr_ != 0)
             throw Error("tensor-parallel collective timed out: a peer rank did not arrive within 2 s (worker lost?)");
         if (comm_) {
@@ -348,8 +356,8 @@ class HipEngineImpl : public HipEngine {
         dHist_ = dalloc<int>((size_t)MB * h_.seqLen);
         hIn_ = halloc<int>(7 * MB);
         hIds_ = halloc<int>(MB);
-        hErr_ = halloc<int>(1);
-        *hErr_ = 0;
+        hErr_ = halloc<int>(2);
+        hErr_[0] = hErr_[1] = 0;
         hLogits_ = halloc<float>((size_t)MB * h_.vocabSize);
         dX_[0] = dalloc<float>((size_t)MB * h_.dim);
         dX_[1] = dalloc<float>((size_t)MB * h_.dim);
@@ -384,6 +392,16 @@ class HipEngineImpl : public HipEngine {
             // per token, the partial sum of squares
             dSS_ = dalloc<float>((size_t)((h_.dim + 63) / 64) * MB);
             DL_HIP(hipMemsetAsync(dGemmCnt_, 0, sizeof(int) * maxTiles, stream_));
+        }
+        {  // fused attention block: epoch, monotonic counters, expected counts, timeout flag
+            dEpoch_ = dalloc<unsigned>(4);
+            dBlockCnt_ = dalloc<unsigned>(kMaxKvGroups + 4);
+            dBlockExpect_ = dalloc<unsigned>(kMaxKvGroups);
+            dBlockErr_ = dalloc<int>(4);
+            DL_HIP(hipMemsetAsync(dEpoch_, 0, 4 * sizeof(unsigned), stream_));
+            DL_HIP(hipMemsetAsync(dBlockCnt_, 0, (kMaxKvGroups + 4) * sizeof(unsigned), stream_));
+            DL_HIP(hipMemsetAsync(dBlockExpect_, 0, kMaxKvGroups * sizeof(unsigned), stream_));
+            DL_HIP(hipMemsetAsync(dBlockErr_, 0, 4 * sizeof(int), stream_));
         }
         dAttCnt_ = dalloc<int>((size_t)MB * p.nHeads0);
         DL_HIP(hipMemsetAsync(dAttCnt_, 0, sizeof(int) * (size_t)MB * p.nHeads0, stream_));
@@ -764,6 +782,50 @@ class HipEngineImpl : public HipEngine {
 
     // Launch a GEMV over all n rows, in batch chunks of <= 4. tp: all-reduce the EPI_STORE output
     // over the tensor-parallel ranks in the kernel tail (fused exchange).
+    // Arguments of one GEMV launch over rows [c0, c0 + bc) of the batch (see gemv()).
+    hipk::GemvArgs gemvArgs(const DevMat &m, int c0, int bc, int epi, const float *in, int ldIn, const float *add,
+                            float *xNext, const float *normW, float *out, int ldOut, const DevLayer *L,
+                            const int8_t *aq, const float2 *as, int8_t *oq, float2 *os, bool tp) const {
+        hipk::GemvArgs a;
+        a.qs = m.qs;
+        a.wd = m.d;
+        a.wf = m.f;
+        a.rows = m.rows;
+        a.n = m.n;
+        a.passes = tp ? tpPasses(m, bc) : passesFor(m, epi, bc);
+        a.lanes = m.lanes;
+        if (tp) a.tp = tpVec_;
+        a.in = in ? in + (size_t)c0 * ldIn : nullptr;
+        a.aq = aq ? aq + (size_t)c0 * m.n : nullptr;
+        a.as = as ? as + (size_t)c0 * (m.n / 32) : nullptr;
+        a.oq = oq ? oq + (size_t)c0 * ldOut : nullptr;
+        a.os = os ? os + (size_t)c0 * (ldOut / 32) : nullptr;
+        a.ldIn = ldIn;
+        a.addIn = add ? add + (size_t)c0 * ldIn : nullptr;
+        a.xNext = xNext ? xNext + (size_t)c0 * ldIn : nullptr;
+        a.normW = normW;
+        a.eps = h_.normEpsilon;
+        a.out = out ? out + (size_t)c0 * ldOut : nullptr;
+        a.ldOut = ldOut;
+        a.act = h_.hiddenAct == HiddenAct::GELU ? 0 : 1;
+        if (L) {
+            a.q0 = plan_.q0;
+            a.kv0 = plan_.kv0;
+            a.hs = plan_.headSize;
+            a.kvMul = plan_.kvMul;
+            a.seqLen = h_.seqLen;
+            a.rope = dRope_;
+            a.pos = dPos_ + c0;
+            a.slot = dSlot_ + c0;
+            a.kcache = L->k;
+            a.vcache = L->v;
+            a.kvBf16 = kvBf16_ ? 1 : 0;
+        }
+        return a;
+    }
+
+    // Launch a GEMV over all n rows, in batch chunks of <= 4. tp: all-reduce the EPI_STORE output
+    // over the tensor-parallel ranks in the kernel tail (fused exchange).
     void gemv(const DevMat &m, int n, int pro, int epi, const float *in, int ldIn, const float *add, float *xNext,
               const float *normW, float *out, int ldOut, const DevLayer *L, const int8_t *aq = nullptr,
               const float2 *as = nullptr, int8_t *oq = nullptr, float2 *os = nullptr, bool tp = false) {
@@ -773,43 +835,94 @@ class HipEngineImpl : public HipEngine {
             int bc = n - c0;
             if (bc > bcMax) bc = bcMax;
             if (bc == 3) bc = 2;
-            hipk::GemvArgs a;
-            a.qs = m.qs;
-            a.wd = m.d;
-            a.wf = m.f;
-            a.rows = m.rows;
-            a.n = m.n;
-            a.passes = tp ? tpPasses(m, bc) : passesFor(m, epi, bc);
-            a.lanes = m.lanes;
-            if (tp) a.tp = tpVec_;
-            a.in = in ? in + (size_t)c0 * ldIn : nullptr;
-            a.aq = aq ? aq + (size_t)c0 * m.n : nullptr;
-            a.as = as ? as + (size_t)c0 * (m.n / 32) : nullptr;
-            a.oq = oq ? oq + (size_t)c0 * ldOut : nullptr;
-            a.os = os ? os + (size_t)c0 * (ldOut / 32) : nullptr;
-            a.ldIn = ldIn;
-            a.addIn = add ? add + (size_t)c0 * ldIn : nullptr;
-            a.xNext = xNext ? xNext + (size_t)c0 * ldIn : nullptr;
-            a.normW = normW;
-            a.eps = h_.normEpsilon;
-            a.out = out ? out + (size_t)c0 * ldOut : nullptr;
-            a.ldOut = ldOut;
-            a.act = h_.hiddenAct == HiddenAct::GELU ? 0 : 1;
-            if (L) {
-                a.q0 = plan_.q0;
-                a.kv0 = plan_.kv0;
-                a.hs = plan_.headSize;
-                a.seqLen = h_.seqLen;
-                a.rope = dRope_;
-                a.pos = dPos_ + c0;
-                a.slot = dSlot_ + c0;
-                a.kcache = L->k;
-                a.vcache = L->v;
-                a.kvBf16 = kvBf16_ ? 1 : 0;
-            }
+            const hipk::GemvArgs a = gemvArgs(m, c0, bc, epi, in, ldIn, add, xNext, normW, out, ldOut, L, aq, as, oq, os, tp);
             hipk::launchGemv(a, bc, pro, epi, q40_, stream_);
             c0 += bc;
         }
+    }
+
+    // Decode attention of this layer (rows 0..n of the forward).
+    hipk::AttnArgs attnArgs(const DevLayer &L, bool bat) const {
+        const ShardPlan &p = plan_;
+        hipk::AttnArgs a;
+        a.q = dQ_;
+        a.ldq = p.q0;
+        a.kcache = L.k;
+        a.vcache = L.v;
+        a.pos = dPos_;
+        a.slot = dSlot_;
+        a.nHeads0 = p.nHeads0;
+        a.kvMul = p.kvMul;
+        a.hs = p.headSize;
+        a.kv0 = p.kv0;
+        a.seqLen = h_.seqLen;
+        a.splitGrid = splitGrid_;
+        a.chunkMax = chunkMax_;
+        a.partO = dPartO_;
+        a.partML = dPartML_;
+        a.out = dAtt_;
+        a.outQ = q40_ && !bat ? dAttQ_ : nullptr;
+        a.outS = q40_ && !bat ? dAttS_ : nullptr;
+        a.outH = bat ? dAttH_ : nullptr;
+        a.ldOut = p.q0;
+        a.kvBf16 = kvBf16_ ? 1 : 0;
+        a.counters = dAttCnt_;
+        return a;
+    }
+
+    // The fused attention block of a single decode row (kernels.h AttnBlockArgs): qkv GEMV +
+    // attention + wo GEMV in one launch. Layer l, residual input dX_[cur].
+    hipk::AttnBlockArgs attnBlockArgs(const DevLayer &L, u32 l, int cur) const {
+        const ShardPlan &p = plan_;
+        const bool hasDelta = l > 0;
+        hipk::AttnBlockArgs b;
+        b.qkv = gemvArgs(L.qkv, 0, 1, hipk::EPI_QKV, dX_[cur], h_.dim, hasDelta ? dY_ : nullptr,
+                         hasDelta ? dX_[cur ^ 1] : nullptr, L.rmsAtt, dQ_, p.q0, &L, nullptr, nullptr, nullptr, nullptr,
+                         false);
+        b.at = attnArgs(L, false);
+        const bool tp = fusedTp(false);
+        b.wo = gemvArgs(L.wo, 0, 1, tp ? hipk::EPI_STORE_TP : hipk::EPI_STORE, nullptr, p.q0, nullptr, nullptr, nullptr,
+                        dY_, h_.dim, nullptr, dAttQ_, dAttS_, nullptr, nullptr, tp);
+        b.hg = hipk::attnBlockHG(b.at);
+        b.layer = (int)l;
+        b.nLayers = (int)h_.nLayers;
+        b.epoch = dEpoch_;
+        b.qkvCnt = dBlockCnt_;
+        b.attnCnt = dBlockCnt_ + kMaxKvGroups;
+        b.qkvExpect = dBlockExpect_;
+        b.error = dBlockErr_;
+        return b;
+    }
+
+    // Decide once whether decode rows run the fused attention block: Q40 weights, a compiled
+    // instance for this shape, <= 64 KV groups, and the whole grid co-resident (shared with the
+    // other ranks on this GPU). DL_ATTN_BLOCK=0 keeps the three separate launches.
+    void setupAttnBlock() {
+        const char *e = std::getenv("DL_ATTN_BLOCK");
+        if ((e && *e == '0') || !q40_ || plan_.nKvHeads0 > kMaxKvGroups) return;
+        const hipk::AttnBlockArgs b = attnBlockArgs(layers_[0], 0, 0);
+        if (!hipk::attnBlockPlan(b, fusedTp(false)).fn) return;
+        const hipk::GemvResidency r = hipk::attnBlockResidency(b, fusedTp(false));
+        const int share = comm_ ? std::max(1, comm_->ranksOnDevice()) : 1;
+        if (r.maxResident <= 0 || r.grid > r.maxResident / share) {
+            std::fprintf(stderr, "ℹ️  fused attention block off: grid %d > %d co-resident workgroups per rank\n", r.grid,
+                         r.maxResident / share);
+            return;
+        }
+        std::vector<unsigned> expect(kMaxKvGroups, 0);
+        hipk::attnBlockExpect(b.qkv, (int)plan_.nKvHeads0, expect.data());
+        DL_HIP(hipMemcpy(dBlockExpect_, expect.data(), expect.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+        blockGrid_ = r.grid;
+        blockOn_ = true;
+    }
+
+    // A fused-block wait gave up (a workgroup of the launch never arrived): reset the monotonic
+    // counters and the epoch so the engine stays usable, then raise.
+    void resetAttnBlockState() {
+        DL_HIP(hipMemsetAsync(dBlockCnt_, 0, sizeof(unsigned) * (kMaxKvGroups + 1), stream_));
+        DL_HIP(hipMemsetAsync(dEpoch_, 0, sizeof(unsigned), stream_));
+        DL_HIP(hipMemsetAsync(dBlockErr_, 0, sizeof(int), stream_));
+        DL_HIP(hipStreamSynchronize(stream_));
     }
 
     // rows per forward from which the MFMA GEMM replaces the GEMV (DL_GEMM_MIN, read at construction)
@@ -930,15 +1043,22 @@ class HipEngineImpl : public HipEngine {
         const ShardPlan &p = plan_;
         const int dim = h_.dim;
         int cur = 0;
-        {
-            ProfScope ps(this, "embedding");
-            hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_);
-        }
         const bool bat = batchedPath(n);  // MFMA GEMMs on f16 activations instead of GEMVs
         const bool fz = bat && fuseNorm();  // residual + norm carried by the GEMM epilogues
+        const bool blk = blockOn_ && n == 1 && !bat;  // fused attention block per layer
+        {
+            ProfScope ps(this, "embedding");
+            // the epoch counts the forwards that run the fused block (its counters' targets)
+            hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_, blk ? dEpoch_ : nullptr);
+        }
         for (u32 l = 0; l < h_.nLayers; l++) {
             DevLayer &L = layers_[l];
             const bool hasDelta = l > 0;
+            if (blk) {
+                ProfScope ps(this, "attn_block");
+                hipk::launchAttnBlock(attnBlockArgs(L, l, cur), fusedTp(false), stream_);
+                if (hasDelta) cur ^= 1;
+            } else {
             {
                 ProfScope ps(this, "gemv_qkv");
                 if (fz && hasDelta)
@@ -955,29 +1075,7 @@ class HipEngineImpl : public HipEngine {
             const bool pf = mallPrefetch() && q40_ && !profile_;
             {
                 ProfScope ps(this, "attention");
-                hipk::AttnArgs a;
-                a.q = dQ_;
-                a.ldq = p.q0;
-                a.kcache = L.k;
-                a.vcache = L.v;
-                a.pos = dPos_;
-                a.slot = dSlot_;
-                a.nHeads0 = p.nHeads0;
-                a.kvMul = p.kvMul;
-                a.hs = p.headSize;
-                a.kv0 = p.kv0;
-                a.seqLen = h_.seqLen;
-                a.splitGrid = splitGrid_;
-                a.chunkMax = chunkMax_;
-                a.partO = dPartO_;
-                a.partML = dPartML_;
-                a.out = dAtt_;
-                a.outQ = q40_ && !bat ? dAttQ_ : nullptr;
-                a.outS = q40_ && !bat ? dAttS_ : nullptr;
-                a.outH = bat ? dAttH_ : nullptr;
-                a.ldOut = p.q0;
-                a.kvBf16 = kvBf16_ ? 1 : 0;
-                a.counters = dAttCnt_;
+                hipk::AttnArgs a = attnArgs(L, bat);
                 if (pf) {
                     // attention keeps a handful of CUs busy for several µs while HBM idles: extra
                     // workgroups of the same launch pull wo and the head of w13 into the MALL
@@ -1006,6 +1104,7 @@ class HipEngineImpl : public HipEngine {
                 else
                     gemv(L.wo, n, hipk::PRO_GLOBAL, hipk::EPI_STORE, q40_ ? nullptr : dAtt_, p.q0, nullptr, nullptr,
                          nullptr, dY_, dim, nullptr, dAttQ_, dAttS_, nullptr, nullptr, fusedTp(bat));
+            }
             }
             if (!fusedTp(bat)) allReduce(dY_, (size_t)n * dim);
             // Q80 hand-off of h needs one workgroup per 32 hidden units; for skinny TP shards the
@@ -1118,6 +1217,11 @@ class HipEngineImpl : public HipEngine {
     ShardPlan plan_;
     bool q40_ = true, kvBf16_ = true, syncQ80_ = false, tpFused_ = false;
     int fusedGridMax_ = 0;  // largest grid of a fused-exchange GEMV launch (checked co-resident)
+    static constexpr int kMaxKvGroups = 64;
+    unsigned *dEpoch_ = nullptr, *dBlockCnt_ = nullptr, *dBlockExpect_ = nullptr;
+    int *dBlockErr_ = nullptr;
+    bool blockOn_ = false;  // decode rows run the fused attention block (setupAttnBlock)
+    int blockGrid_ = 0;
     int gemmMin_ = 3;       // DL_GEMM_MIN: rows per forward from which the batched MFMA path runs
     bool fuseNormEnv_ = true;  // DL_GEMM_FUSE_NORM
     hipk::TpXchg tpVec_, tpArg_;

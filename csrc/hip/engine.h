@@ -28,6 +28,8 @@ class HipEngine : public Backend {
     // switched off when a launch's grid would not be fully co-resident), and the largest grid of
     // such a launch (checked against the device's occupancy at construction).
     virtual bool tpFused() const { return false; }
+    // Single decode rows run the fused attention block (qkv + attention + wo in one launch).
+    virtual bool attnBlock() const { return false; }
     virtual int fusedGridMax() const { return 0; }
 };
 

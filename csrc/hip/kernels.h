@@ -121,6 +121,7 @@ struct GemvArgs {
     float2 *os = nullptr;
     // EPI_QKV
     int q0 = 0, kv0 = 0, hs = 0, seqLen = 0;
+    int kvMul = 1;                // query heads per KV head (fused attention block: KV groups of the rows)
     const float2 *rope = nullptr; // [seqLen][hs/2] (cos, sin)
     const int *pos = nullptr;     // per batch row
     const int *slot = nullptr;
@@ -205,6 +206,40 @@ size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg, int pro);
 int gemvDefaultPasses(int n, int rows, int B, bool q40, int epi);
 
 void launchAttention(const AttnArgs &a, int B, hipStream_t s);
+
+// Fused attention block of one decode row (B = 1): the qkv GEMV (norm prologue, RoPE + KV append),
+// the decode attention and the wo GEMV in ONE launch, as three workgroup roles
+//   [0, gq) qkv rows | [gq, gq + ga) attention tasks | [gq + ga, gq + ga + gw) wo rows,
+// handing off in-launch through write-through stores and monotonic arrival counters (decode_dev.h
+// BlockSync): attention tasks wait for their KV group's qkv workgroups, wo workgroups issue their
+// weight ring first and then wait for every head group's output. Removes two kernel boundaries
+// and the attention / wo start-up latency per layer. Requires the whole grid co-resident
+// (attnBlockResidency) - every wait is bounded and raises `error` instead of hanging.
+struct AttnBlockArgs {
+    GemvArgs qkv;                 // PRO_RESNORM + EPI_QKV (lanes = the qkv tiling's L, kvMul set)
+    AttnArgs at;                  // one row; outQ / outS = the wo input
+    GemvArgs wo;                  // PRO_GLOBAL + EPI_STORE (or EPI_STORE_TP: wo.tp set)
+    int hg = 1;                   // query heads per attention workgroup (attnBlockHG)
+    int layer = 0, nLayers = 1;
+    const unsigned *epoch = nullptr;  // per-forward epoch (1, 2, ...), incremented by launchEmbedding
+    unsigned *qkvCnt = nullptr;       // [kv groups] monotonic counters (zeroed once)
+    const unsigned *qkvExpect = nullptr;  // [kv groups] qkv workgroups per group (attnBlockExpect)
+    unsigned *attnCnt = nullptr;      // [1] monotonic counter (zeroed once)
+    int *error = nullptr;             // wait timeout flag (zeroed once)
+    long long timeoutTicks = 200LL * 1000 * 1000;  // 2 s of s_memrealtime (100 MHz)
+};
+int attnBlockHG(const AttnArgs &a);  // query heads per attention workgroup (256 threads, one row)
+// Launch geometry; fn == null when (qkv lanes, wo lanes, head size, HG) has no compiled instance.
+struct AttnBlockPlan {
+    const void *fn = nullptr;
+    int gq = 0, ga = 0, gw = 0;
+    size_t lds = 0;
+};
+AttnBlockPlan attnBlockPlan(const AttnBlockArgs &a, bool tp);
+// qkv workgroups touching each KV group (host side of the counters' targets): out[g], g < nKv.
+void attnBlockExpect(const GemvArgs &qkv, int nKv, unsigned *out);
+GemvResidency attnBlockResidency(const AttnBlockArgs &a, bool tp);
+void launchAttnBlock(const AttnBlockArgs &a, bool tp, hipStream_t s);
 // Prefill rows on MFMA (bf16 caches): blocks of attnPrefillRowsPerBlock(kvMul) consecutive rows
 // must share one slot (positions arbitrary, causal per row); counters >= blocks x KV heads.
 void launchAttentionPrefill(const AttnArgs &a, int nRows, hipStream_t s);
@@ -213,7 +248,9 @@ bool attnPrefillSupported(int hs, int kvMul, bool kvBf16);
 int attnSplitGrid(int seqLen);
 int attnChunkMax(int seqLen, int splitGrid);
 
-void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s);
+// epoch (optional): one thread increments it - the per-forward epoch of the fused attention block.
+void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s,
+                     unsigned *epoch = nullptr);
 // Parallel argmax over [B][vocab]; partials need B*256 floats + ints, counters B ints (zeroed).
 // When `tokens` is non-null the result is also fed back (tokens[b] = id; hist[b][pos] = id; pos += 1).
 struct ArgmaxArgs {

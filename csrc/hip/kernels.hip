@@ -504,8 +504,9 @@ void launchAttentionPrefill(const AttnArgs &a, int nRows, hipStream_t s) {
 // ------------------------------------------------------------------------------------------------
 // Small kernels
 // ------------------------------------------------------------------------------------------------
-__global__ void embeddingKernel(const float *table, const int *tokens, float *x, int dim) {
+__global__ void embeddingKernel(const float *table, const int *tokens, float *x, int dim, unsigned *epoch) {
     const int b = blockIdx.x;
+    if (epoch && b == 0 && threadIdx.x == 0) *epoch += 1;  // read by later kernels of this forward
     const float *src = table + (size_t)tokens[b] * dim;
     float *dst = x + (size_t)b * dim;
     // all of a thread's row loads in flight before the first store (one HBM round trip, not four)
@@ -525,8 +526,8 @@ __global__ void embeddingKernel(const float *table, const int *tokens, float *x,
     }
 }
 
-void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s) {
-    hipLaunchKernelGGL(embeddingKernel, dim3(B), dim3(256), 0, s, table, tokens, x, dim);
+void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s, unsigned *epoch) {
+    hipLaunchKernelGGL(embeddingKernel, dim3(B), dim3(256), 0, s, table, tokens, x, dim, epoch);
 }
 
 __device__ __forceinline__ void argBetter(float &bv, int &bi, float ov, int oi) {

@@ -753,6 +753,7 @@ PYBIND11_MODULE(_C, m) {
         .def_property_readonly("header", [](const PyHipEngine &e) { return headerToDict(e.engine->header()); })
         .def_property_readonly("device_bytes", [](const PyHipEngine &e) { return e.engine->deviceBytes(); })
         .def_property_readonly("tp_fused", [](const PyHipEngine &e) { return e.engine->tpFused(); })
+        .def_property_readonly("attn_block", [](const PyHipEngine &e) { return e.engine->attnBlock(); })
         .def_property_readonly("fused_grid_max", [](const PyHipEngine &e) { return e.engine->fusedGridMax(); })
         .def_property_readonly("load_stats",
                                [](const PyHipEngine &e) {

@@ -291,3 +291,26 @@ def test_batched_path_outlier_residuals(C, tmp_path):
     got = gpu.forward(tokens, list(range(40)), [0] * 40)
     assert np.isfinite(got).all()
     assert _rel(got, ref) < 3e-2
+
+
+@pytest.mark.parametrize("kv_bf16", [True, False])
+def test_attn_block_matches_separate_kernels(C, assets, medium, monkeypatch, kv_bf16):
+    """Single decode rows run the fused attention block (qkv GEMV + attention + wo GEMV as one
+    launch with in-launch write-through hand-offs): same logits as the three separate launches
+    (attention reduces in another order: tolerance), same greedy chain, over many forwards (the
+    block's monotonic counters across layers, forwards and graph replays)."""
+    for model in (assets["q40"], medium):
+        monkeypatch.setenv("DL_ATTN_BLOCK", "0")
+        ref = C.HipEngine(model, "q80", kv_bf16=kv_bf16, max_batch=8)
+        monkeypatch.delenv("DL_ATTN_BLOCK")
+        got = C.HipEngine(model, "q80", kv_bf16=kv_bf16, max_batch=8)
+        assert got.attn_block and not ref.attn_block
+        toks = [3, 17, 101, 7, 250, 9]
+        a, b = _seq(ref, toks), _seq(got, toks)
+        assert _rel(b, a) < 1e-3
+        # a batched forward in between (no block; the block's epoch must not advance)
+        ref.forward([5, 6, 7], [6, 7, 8], [0, 0, 0])
+        got.forward([5, 6, 7], [6, 7, 8], [0, 0, 0])
+        _, ca = ref.decode_greedy(24, [int(a[-1].argmax())], [9], [0])
+        _, cb = got.decode_greedy(24, [int(b[-1].argmax())], [9], [0])
+        assert list(ca) == list(cb)
