@@ -86,6 +86,10 @@ void launchAttnBlock(const AttnBlockArgs &a, bool tp, hipStream_t s) {
     if (!p.fn) throw Error("launchAttnBlock: no kernel instance for this shape");
     if (p.lds > 65536) allowLds(p.fn, p.lds);
     AttnBlockArgs args = a;
+    if (a.trace) {  // per-role trace slots: qkv [0, gq), attention [gq, gq + ga), wo after them
+        args.qkv.trace = a.trace;
+        args.wo.trace = a.trace + 8 * (size_t)(p.gq + p.ga);
+    }
     void *kargs[] = {&args};
     DL_HIP(hipLaunchKernel(p.fn, dim3(p.gq + p.ga + p.gw), dim3(kThreads), kargs, p.lds, s));
 }

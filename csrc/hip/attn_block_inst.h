@@ -16,8 +16,10 @@ __global__ __launch_bounds__(kThreads) void attnBlockKernel(AttnBlockArgs ba) {
     bs.qkvCnt = ba.qkvCnt;
     bs.qkvExpect = ba.qkvExpect;
     bs.attnCnt = ba.attnCnt;
+    bs.attnFlag = ba.attnFlag;
     bs.step = (*ba.epoch - 1u) * (unsigned)ba.nLayers + (unsigned)ba.layer + 1u;
     bs.attnTarget = bs.step * (unsigned)nHG;
+    bs.nKv = ba.at.nHeads0 / ba.at.kvMul;
     bs.error = ba.error;
     bs.timeoutTicks = ba.timeoutTicks;
     int x = blockIdx.x;
@@ -27,9 +29,23 @@ __global__ __launch_bounds__(kThreads) void attnBlockKernel(AttnBlockArgs ba) {
     }
     x -= gq;
     if (x < ga) {
-        if (attnTask<HG, HS, BF16, kThreads, true>(ba.at, 0, x % nHG, x / nHG, smem, &bs)) {
-            blockDrain();  // this head group's final output is stored write-through: count it in
-            if (threadIdx.x == 0) __hip_atomic_fetch_add(bs.attnCnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned long long *tr = ba.trace ? ba.trace + 8 * (size_t)blockIdx.x : nullptr;
+        const unsigned long long t0 = tr ? wall_clock64() : 0ull;
+        const bool fin = attnTask<HG, HS, BF16, kThreads, true>(ba.at, 0, x % nHG, x / nHG, smem, &bs, tr);
+        if (fin) {
+            blockDrain();  // this head group's final output is stored write-through: count it in;
+            // the last head group to arrive raises the step's per-XCD ready flags for the wo role
+            if (threadIdx.x == 0 &&
+                __hip_atomic_fetch_add(bs.attnCnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == bs.attnTarget) {
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    __hip_atomic_store(bs.attnFlag + k * kCntStride, bs.step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (tr && threadIdx.x == 0) {
+            tr[0] = t0;
+            tr[3] = wall_clock64();
+            tr[7] = 1u | (fin ? 16u : 0u);
         }
         return;
     }

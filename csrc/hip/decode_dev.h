@@ -509,19 +509,27 @@ enum GemvMode : int { GEMV_PLAIN = 0, GEMV_PRODUCER = 1, GEMV_CONSUMER = 2 };
 // (s = (forward epoch - 1) * nLayers + layer + 1) KV group g's counter has been incremented
 // s * qkvExpect[g] times and the attention counter s * (head groups) times, so a waiter compares
 // against a target computed from s in wrapping u32 arithmetic ((int)(cnt - target) >= 0).
+// Every polled word sits on its own 256-byte line (kCntStride u32): 192 qkv workgroups adding into
+// one line serialised their atomics (~4 us per layer, traced); the attention -> wo "ready" flag is
+// replicated per XCD so 256 pollers do not hammer one line.
+constexpr int kCntStride = 64;
 struct BlockSync {
-    unsigned *qkvCnt = nullptr;          // [kv groups] arrivals of qkv workgroups per KV group
+    unsigned *qkvCnt = nullptr;          // [kv groups * kCntStride] arrivals of qkv workgroups per group
     const unsigned *qkvExpect = nullptr; // [kv groups] qkv workgroups touching each group
     unsigned *attnCnt = nullptr;         // [1] arrivals of attention head groups (final outputs)
+    unsigned *attnFlag = nullptr;        // [8 * kCntStride] per-XCD copies of the last step all heads finished
     unsigned step = 0;                   // s (see above)
+    int nKv = 0;                         // KV groups
     unsigned attnTarget = 0;             // s * head groups
     int *error = nullptr;                // set when a wait gave up (the engine raises)
     long long timeoutTicks = 0;
 };
+__device__ __forceinline__ int xccId() { return (int)(__builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u); }
 
 // One lane waits (relaxed agent-scope polls + s_sleep, bounded: a wait that gives up sets the
 // error word and every later wait fails fast), then the workgroup's barrier releases the others.
-__device__ __forceinline__ void blockWait(const unsigned *cnt, unsigned target, const BlockSync &bs) {
+__device__ __forceinline__ unsigned long long blockWait(const unsigned *cnt, unsigned target, const BlockSync &bs) {
+    unsigned long long stamp = 0ull;
     if (threadIdx.x == 0) {
         if (__hip_atomic_load(bs.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
             const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
@@ -532,6 +540,30 @@ __device__ __forceinline__ void blockWait(const unsigned *cnt, unsigned target, 
                     break;
                 }
             }
+        }
+        stamp = wall_clock64();
+    }
+    __syncthreads();
+    return stamp;
+}
+
+// Wait until every KV group's qkv workgroups of this step arrived (thread 0 polls each group).
+__device__ __forceinline__ void blockWaitQkv(const BlockSync &bs, int nKv) {
+    if (threadIdx.x == 0 && __hip_atomic_load(bs.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        for (int g = 0; g < nKv; g++) {
+            const unsigned target = bs.step * bs.qkvExpect[g];
+            bool ok = true;
+            while ((int)(__hip_atomic_load(bs.qkvCnt + g * kCntStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                         target) < 0) {
+                __builtin_amdgcn_s_sleep(2);
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > bs.timeoutTicks) {
+                    __hip_atomic_store(bs.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = false;
+                    break;
+                }
+            }
+            if (!ok) break;
         }
     }
     __syncthreads();
@@ -575,7 +607,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
     const int rowBase = blk * R;
     // timestamps stay in SGPRs until the end: a store here would join the ring's vmcnt accounting
     const unsigned long long tEntry = a.trace ? wall_clock64() : 0ull;
-    unsigned long long tReady = 0ull, tLoaded = 0ull, tFirst = 0ull;
+    unsigned long long tReady = 0ull, tLoaded = 0ull, tFirst = 0ull, tWaited = 0ull;
 
     // slot = 2 rows x 16 B of nibbles + the pair's two f16 scales in one 32-bit word
     u32x4 w[D][RG];
@@ -760,6 +792,9 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
         }
     };
     auto latePath = [&]() {
+        // consumer: the weight ring is issued once the qkv phase of the launch is done, so it streams
+        // while HBM would idle during attention instead of competing with the qkv weights
+        if constexpr (MODE == GEMV_CONSUMER) blockWaitQkv(*bs, bs->nKv);
         // sched_barrier keeps issue order == slot order, so each step waits for exactly its own
         // slot (vmcnt = loads of the other kRing-1 slots) instead of the scheduler batching the ring.
 #pragma unroll
@@ -777,7 +812,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
         if constexpr (MODE == GEMV_CONSUMER) {
             // the activations are produced in this launch: wait for every producer (the ring's
             // weight loads are already in flight), then read them write-through
-            blockWait(bs->attnCnt, bs->attnTarget, *bs);
+            tWaited = blockWait(bs->attnFlag + xccId() * kCntStride, bs->step, *bs);
             stageQ80<B, true>(a, sq, ssc);
         } else if constexpr (PRO == PRO_RESNORM)
             resNormPrologue<B, true>(a, scratch, sq, ssc, nullptr);
@@ -900,7 +935,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
             while (m) {
                 const int g = __builtin_ctzll(m);
                 m &= m - 1;
-                __hip_atomic_fetch_add(bs->qkvCnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_add(bs->qkvCnt + g * kCntStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }
@@ -922,6 +957,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
             t[3] = ((unsigned long long)hw << 32) | xcc;
             t[4] = tLoaded;
             t[5] = tFirst;
+            t[6] = tWaited;
         }
     }
 }
@@ -1099,7 +1135,7 @@ __device__ __forceinline__ bool attnFinish(const AttnArgs &a, int b, int hgIdx, 
 // workgroups of the same launch - wait for this KV group's producers, read those write-through.
 template <int HG, int HS, bool BF16, int AT, bool SYNC = false>
 __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, int c, char *smem,
-                                         const BlockSync *bs = nullptr) {
+                                         const BlockSync *bs = nullptr, unsigned long long *trace = nullptr) {
     constexpr int NW = AT / 64, NG = AT / 16;
     constexpr int DPL = HS / 16;           // dims per lane: 16 lanes cover one position's head vector
     constexpr int TU = BF16 ? 8 : 4;       // keys per group loaded before any is consumed
@@ -1123,7 +1159,62 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
     float *mlL = redL + HG * HS;                    // [HG][2]
     int *flagL = reinterpret_cast<int *>(mlL + 2 * HG);
 
-    if constexpr (SYNC) blockWait(bs->qkvCnt + kvh, bs->step * bs->qkvExpect[kvh], *bs);
+    // SYNC: the first round's keys written by earlier forwards are loaded before the wait (their
+    // latency overlaps the qkv workgroups); the current position's row after it, write-through
+    const size_t slotBase = (size_t)sl * a.seqLen;
+    uint32_t kr[TU][RW], vr[TU][RW];
+    // phase 0: every key (the current one write-through under SYNC); 1: all but the current one;
+    // 2: only the current one
+    auto loadRound = [&](int tb, int phase) {
+#pragma unroll
+        for (int u = 0; u < TU; u++) {
+            const int t = min(tb + u * NG, t1 - 1);  // clamped: no divergent loads
+            const bool cur = SYNC && t == pos;
+            if ((phase == 1 && cur) || (phase == 2 && !cur)) continue;
+            const size_t off = (slotBase + t) * a.kv0 + kvh * HS + l16 * DPL;
+            const uint32_t *kp = reinterpret_cast<const uint32_t *>(
+                BF16 ? (const void *)(reinterpret_cast<const uint16_t *>(a.kcache) + off)
+                     : (const void *)(reinterpret_cast<const float *>(a.kcache) + off));
+            const uint32_t *vp = reinterpret_cast<const uint32_t *>(
+                BF16 ? (const void *)(reinterpret_cast<const uint16_t *>(a.vcache) + off)
+                     : (const void *)(reinterpret_cast<const float *>(a.vcache) + off));
+            if (cur) {  // appended by this launch's qkv workgroups: write-through loads
+#pragma unroll
+                for (int w = 0; w < RW; w += 2) {
+                    const uint64_t kk = ldWT64(kp + w), vv = ldWT64(vp + w);
+                    kr[u][w] = (uint32_t)kk;
+                    kr[u][w + 1] = (uint32_t)(kk >> 32);
+                    vr[u][w] = (uint32_t)vv;
+                    vr[u][w + 1] = (uint32_t)(vv >> 32);
+                }
+            } else if constexpr (RW == 4) {
+                const uint4 k4 = *reinterpret_cast<const uint4 *>(kp), v4 = *reinterpret_cast<const uint4 *>(vp);
+                kr[u][0] = k4.x; kr[u][1] = k4.y; kr[u][2] = k4.z; kr[u][3] = k4.w;
+                vr[u][0] = v4.x; vr[u][1] = v4.y; vr[u][2] = v4.z; vr[u][3] = v4.w;
+            } else if constexpr (RW == 8) {
+                const uint4 k0 = reinterpret_cast<const uint4 *>(kp)[0], k1 = reinterpret_cast<const uint4 *>(kp)[1];
+                const uint4 v0 = reinterpret_cast<const uint4 *>(vp)[0], v1 = reinterpret_cast<const uint4 *>(vp)[1];
+                kr[u][0] = k0.x; kr[u][1] = k0.y; kr[u][2] = k0.z; kr[u][3] = k0.w;
+                kr[u][4] = k1.x; kr[u][5] = k1.y; kr[u][6] = k1.z; kr[u][7] = k1.w;
+                vr[u][0] = v0.x; vr[u][1] = v0.y; vr[u][2] = v0.z; vr[u][3] = v0.w;
+                vr[u][4] = v1.x; vr[u][5] = v1.y; vr[u][6] = v1.z; vr[u][7] = v1.w;
+            } else {
+                const uint2 k2 = *reinterpret_cast<const uint2 *>(kp), v2 = *reinterpret_cast<const uint2 *>(vp);
+                kr[u][0] = k2.x; kr[u][1] = k2.y;
+                vr[u][0] = v2.x; vr[u][1] = v2.y;
+            }
+        }
+    };
+    int tb = t0 + g16;
+    bool prefetched = false;
+    unsigned long long tWaited = 0ull;
+    if constexpr (SYNC) {
+        if (tb < t1) {
+            loadRound(tb, 1);
+            prefetched = true;
+        }
+        tWaited = blockWait(bs->qkvCnt + kvh * kCntStride, bs->step * bs->qkvExpect[kvh], *bs);
+    }
     // this lane's slice of the HG query heads (pre-scaled), vector loads
     const float scale = 1.0f / sqrtf((float)HS);
     float qr[HG][DPL];
@@ -1156,45 +1247,9 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
     }
     // each 16-lane group walks keys g16, g16+NG, ... with a running softmax; TU keys per group are
     // in flight at once (NG*TU = 256 keys per memory round trip for bf16 caches)
-    const size_t slotBase = (size_t)sl * a.seqLen;
-    for (int tb = t0 + g16; tb < t1; tb += TU * NG) {
-        uint32_t kr[TU][RW], vr[TU][RW];
-#pragma unroll
-        for (int u = 0; u < TU; u++) {
-            const int t = min(tb + u * NG, t1 - 1);  // clamped: no divergent loads
-            const size_t off = (slotBase + t) * a.kv0 + kvh * HS + l16 * DPL;
-            const uint32_t *kp = reinterpret_cast<const uint32_t *>(
-                BF16 ? (const void *)(reinterpret_cast<const uint16_t *>(a.kcache) + off)
-                     : (const void *)(reinterpret_cast<const float *>(a.kcache) + off));
-            const uint32_t *vp = reinterpret_cast<const uint32_t *>(
-                BF16 ? (const void *)(reinterpret_cast<const uint16_t *>(a.vcache) + off)
-                     : (const void *)(reinterpret_cast<const float *>(a.vcache) + off));
-            if (SYNC && t == pos) {  // appended by this launch's qkv workgroups: write-through loads
-#pragma unroll
-                for (int w = 0; w < RW; w += 2) {
-                    const uint64_t kk = ldWT64(kp + w), vv = ldWT64(vp + w);
-                    kr[u][w] = (uint32_t)kk;
-                    kr[u][w + 1] = (uint32_t)(kk >> 32);
-                    vr[u][w] = (uint32_t)vv;
-                    vr[u][w + 1] = (uint32_t)(vv >> 32);
-                }
-            } else if constexpr (RW == 4) {
-                const uint4 k4 = *reinterpret_cast<const uint4 *>(kp), v4 = *reinterpret_cast<const uint4 *>(vp);
-                kr[u][0] = k4.x; kr[u][1] = k4.y; kr[u][2] = k4.z; kr[u][3] = k4.w;
-                vr[u][0] = v4.x; vr[u][1] = v4.y; vr[u][2] = v4.z; vr[u][3] = v4.w;
-            } else if constexpr (RW == 8) {
-                const uint4 k0 = reinterpret_cast<const uint4 *>(kp)[0], k1 = reinterpret_cast<const uint4 *>(kp)[1];
-                const uint4 v0 = reinterpret_cast<const uint4 *>(vp)[0], v1 = reinterpret_cast<const uint4 *>(vp)[1];
-                kr[u][0] = k0.x; kr[u][1] = k0.y; kr[u][2] = k0.z; kr[u][3] = k0.w;
-                kr[u][4] = k1.x; kr[u][5] = k1.y; kr[u][6] = k1.z; kr[u][7] = k1.w;
-                vr[u][0] = v0.x; vr[u][1] = v0.y; vr[u][2] = v0.z; vr[u][3] = v0.w;
-                vr[u][4] = v1.x; vr[u][5] = v1.y; vr[u][6] = v1.z; vr[u][7] = v1.w;
-            } else {
-                const uint2 k2 = *reinterpret_cast<const uint2 *>(kp), v2 = *reinterpret_cast<const uint2 *>(vp);
-                kr[u][0] = k2.x; kr[u][1] = k2.y;
-                vr[u][0] = v2.x; vr[u][1] = v2.y;
-            }
-        }
+    for (; tb < t1; tb += TU * NG) {
+        loadRound(tb, prefetched ? 2 : 0);
+        prefetched = false;
 #pragma unroll
         for (int u = 0; u < TU; u++) {
             if (tb + u * NG >= t1) break;  // uniform within the 16-lane group
@@ -1272,6 +1327,10 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
     }
     __syncthreads();
 
+    if (trace && threadIdx.x == 0) {
+        trace[1] = tWaited;
+        trace[2] = wall_clock64();
+    }
     return attnFinish<HG, HS, AT, SYNC>(a, b, hgIdx, c, nSplit, redL, mlL, flagL, oW);
 }
 

@@ -184,6 +184,26 @@ class HipEngineImpl : public HipEngine {
   public:
     bool tpFused() const override { return tpFused_; }
     bool attnBlock() const override { return blockOn_; }
+    std::vector<unsigned long long> traceAttnBlock(int token, int pos, int slot, int layer) override {
+        if (!blockOn_) return {};
+        const hipk::AttnBlockPlan pl = hipk::attnBlockPlan(attnBlockArgs(layers_[0], 0, 0), fusedTp(false));
+        const size_t words = 8 * (size_t)(pl.gq + pl.ga + pl.gw);
+        traceBuf_ = dalloc<unsigned long long>(words);
+        DL_HIP(hipMemsetAsync(traceBuf_, 0, words * 8, stream_));
+        traceLayer_ = layer;
+        setInputs(1, &token, &pos, &slot);
+        enqueueForward(1, GraphKind::LOGITS);
+        syncAndCheckComm();
+        inputsInFlight_ = false;
+        std::vector<unsigned long long> out(3 + words);
+        out[0] = pl.gq;
+        out[1] = pl.ga;
+        out[2] = pl.gw;
+        DL_HIP(hipMemcpy(out.data() + 3, traceBuf_, words * 8, hipMemcpyDeviceToHost));
+        traceLayer_ = -1;
+        traceBuf_ = nullptr;  // (one small buffer per call, released with the engine)
+        return out;
+    }
     int fusedGridMax() const override { return fusedGridMax_; }
 
     ~HipEngineImpl() override {
@@ -395,11 +415,11 @@ class HipEngineImpl : public HipEngine {
         }
         {  // fused attention block: epoch, monotonic counters, expected counts, timeout flag
             dEpoch_ = dalloc<unsigned>(4);
-            dBlockCnt_ = dalloc<unsigned>(kMaxKvGroups + 4);
+            dBlockCnt_ = dalloc<unsigned>(kBlockCntWords);
             dBlockExpect_ = dalloc<unsigned>(kMaxKvGroups);
             dBlockErr_ = dalloc<int>(4);
             DL_HIP(hipMemsetAsync(dEpoch_, 0, 4 * sizeof(unsigned), stream_));
-            DL_HIP(hipMemsetAsync(dBlockCnt_, 0, (kMaxKvGroups + 4) * sizeof(unsigned), stream_));
+            DL_HIP(hipMemsetAsync(dBlockCnt_, 0, kBlockCntWords * sizeof(unsigned), stream_));
             DL_HIP(hipMemsetAsync(dBlockExpect_, 0, kMaxKvGroups * sizeof(unsigned), stream_));
             DL_HIP(hipMemsetAsync(dBlockErr_, 0, 4 * sizeof(int), stream_));
         }
@@ -888,7 +908,8 @@ class HipEngineImpl : public HipEngine {
         b.nLayers = (int)h_.nLayers;
         b.epoch = dEpoch_;
         b.qkvCnt = dBlockCnt_;
-        b.attnCnt = dBlockCnt_ + kMaxKvGroups;
+        b.attnCnt = dBlockCnt_ + kMaxKvGroups * 64;
+        b.attnFlag = dBlockCnt_ + kMaxKvGroups * 64 + 64;
         b.qkvExpect = dBlockExpect_;
         b.error = dBlockErr_;
         return b;
@@ -919,7 +940,7 @@ class HipEngineImpl : public HipEngine {
     // A fused-block wait gave up (a workgroup of the launch never arrived): reset the monotonic
     // counters and the epoch so the engine stays usable, then raise.
     void resetAttnBlockState() {
-        DL_HIP(hipMemsetAsync(dBlockCnt_, 0, sizeof(unsigned) * (kMaxKvGroups + 1), stream_));
+        DL_HIP(hipMemsetAsync(dBlockCnt_, 0, sizeof(unsigned) * kBlockCntWords, stream_));
         DL_HIP(hipMemsetAsync(dEpoch_, 0, sizeof(unsigned), stream_));
         DL_HIP(hipMemsetAsync(dBlockErr_, 0, sizeof(int), stream_));
         DL_HIP(hipStreamSynchronize(stream_));
@@ -1056,7 +1077,9 @@ class HipEngineImpl : public HipEngine {
             const bool hasDelta = l > 0;
             if (blk) {
                 ProfScope ps(this, "attn_block");
-                hipk::launchAttnBlock(attnBlockArgs(L, l, cur), fusedTp(false), stream_);
+                hipk::AttnBlockArgs ba = attnBlockArgs(L, l, cur);
+                if ((int)l == traceLayer_) ba.trace = traceBuf_;
+                hipk::launchAttnBlock(ba, fusedTp(false), stream_);
                 if (hasDelta) cur ^= 1;
             } else {
             {
@@ -1218,9 +1241,13 @@ class HipEngineImpl : public HipEngine {
     bool q40_ = true, kvBf16_ = true, syncQ80_ = false, tpFused_ = false;
     int fusedGridMax_ = 0;  // largest grid of a fused-exchange GEMV launch (checked co-resident)
     static constexpr int kMaxKvGroups = 64;
+    // counters: [64 groups x 64 words] qkv arrivals, [64] attention arrivals, [8 x 64] ready flags
+    static constexpr int kBlockCntWords = kMaxKvGroups * 64 + 64 + 8 * 64;
     unsigned *dEpoch_ = nullptr, *dBlockCnt_ = nullptr, *dBlockExpect_ = nullptr;
     int *dBlockErr_ = nullptr;
     bool blockOn_ = false;  // decode rows run the fused attention block (setupAttnBlock)
+    int traceLayer_ = -1;   // traceAttnBlock: the layer whose block launch is traced
+    unsigned long long *traceBuf_ = nullptr;
     int blockGrid_ = 0;
     int gemmMin_ = 3;       // DL_GEMM_MIN: rows per forward from which the batched MFMA path runs
     bool fuseNormEnv_ = true;  // DL_GEMM_FUSE_NORM

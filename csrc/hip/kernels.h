@@ -222,11 +222,15 @@ struct AttnBlockArgs {
     int hg = 1;                   // query heads per attention workgroup (attnBlockHG)
     int layer = 0, nLayers = 1;
     const unsigned *epoch = nullptr;  // per-forward epoch (1, 2, ...), incremented by launchEmbedding
-    unsigned *qkvCnt = nullptr;       // [kv groups] monotonic counters (zeroed once)
+    unsigned *qkvCnt = nullptr;       // [kv groups * 64] monotonic counters, one per 256-B line (zeroed once)
     const unsigned *qkvExpect = nullptr;  // [kv groups] qkv workgroups per group (attnBlockExpect)
     unsigned *attnCnt = nullptr;      // [1] monotonic counter (zeroed once)
+    unsigned *attnFlag = nullptr;     // [8 * 64] per-XCD step-done flags (zeroed once)
     int *error = nullptr;             // wait timeout flag (zeroed once)
     long long timeoutTicks = 200LL * 1000 * 1000;  // 2 s of s_memrealtime (100 MHz)
+    // diagnostics: 8 u64 per workgroup (qkv / wo: GemvArgs::trace layout + [6] wait done; attention:
+    // [0] entry, [1] wait done, [2] compute done, [3] exit, [7] role 1 | 16 if it wrote the output)
+    unsigned long long *trace = nullptr;
 };
 int attnBlockHG(const AttnArgs &a);  // query heads per attention workgroup (256 threads, one row)
 // Launch geometry; fn == null when (qkv lanes, wo lanes, head size, HG) has no compiled instance.
