@@ -20,6 +20,9 @@ __global__ __launch_bounds__(kThreads) void attnBlockKernel(AttnBlockArgs ba) {
     bs.step = (*ba.epoch - 1u) * (unsigned)ba.nLayers + (unsigned)ba.layer + 1u;
     bs.attnTarget = bs.step * (unsigned)nHG;
     bs.nKv = ba.at.nHeads0 / ba.at.kvMul;
+    bs.qkvAll = ba.attnFlag + 8 * kCntStride;   // layout: engine.cpp kBlockCntWords
+    bs.qkvFlag = ba.attnFlag + 9 * kCntStride;
+    bs.qkvAllTarget = bs.step * (unsigned)gq;
     bs.error = ba.error;
     bs.timeoutTicks = ba.timeoutTicks;
     int x = blockIdx.x;
@@ -37,9 +40,7 @@ __global__ __launch_bounds__(kThreads) void attnBlockKernel(AttnBlockArgs ba) {
             // the last head group to arrive raises the step's per-XCD ready flags for the wo role
             if (threadIdx.x == 0 &&
                 __hip_atomic_fetch_add(bs.attnCnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == bs.attnTarget) {
-#pragma unroll
-                for (int k = 0; k < 8; k++)
-                    __hip_atomic_store(bs.attnFlag + k * kCntStride, bs.step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                raiseFlags(bs.attnFlag, bs.step);
             }
         }
         if (tr && threadIdx.x == 0) {

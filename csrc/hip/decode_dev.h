@@ -518,6 +518,9 @@ struct BlockSync {
     const unsigned *qkvExpect = nullptr; // [kv groups] qkv workgroups touching each group
     unsigned *attnCnt = nullptr;         // [1] arrivals of attention head groups (final outputs)
     unsigned *attnFlag = nullptr;        // [8 * kCntStride] per-XCD copies of the last step all heads finished
+    unsigned *qkvAll = nullptr;          // [1] arrivals of every qkv workgroup
+    unsigned *qkvFlag = nullptr;         // [8 * kCntStride] per-XCD copies of the last step the qkv phase finished
+    unsigned qkvAllTarget = 0;           // s * qkv workgroups
     unsigned step = 0;                   // s (see above)
     int nKv = 0;                         // KV groups
     unsigned attnTarget = 0;             // s * head groups
@@ -528,7 +531,8 @@ __device__ __forceinline__ int xccId() { return (int)(__builtin_amdgcn_s_getreg(
 
 // One lane waits (relaxed agent-scope polls + s_sleep, bounded: a wait that gives up sets the
 // error word and every later wait fails fast), then the workgroup's barrier releases the others.
-__device__ __forceinline__ unsigned long long blockWait(const unsigned *cnt, unsigned target, const BlockSync &bs) {
+__device__ __forceinline__ unsigned long long blockWait(const unsigned *cnt, unsigned target, const BlockSync &bs,
+                                                        int code = 1) {
     unsigned long long stamp = 0ull;
     if (threadIdx.x == 0) {
         if (__hip_atomic_load(bs.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
@@ -536,7 +540,7 @@ __device__ __forceinline__ unsigned long long blockWait(const unsigned *cnt, uns
             while ((int)(__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
                 __builtin_amdgcn_s_sleep(1);
                 if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > bs.timeoutTicks) {
-                    __hip_atomic_store(bs.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(bs.error, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
             }
@@ -547,26 +551,10 @@ __device__ __forceinline__ unsigned long long blockWait(const unsigned *cnt, uns
     return stamp;
 }
 
-// Wait until every KV group's qkv workgroups of this step arrived (thread 0 polls each group).
-__device__ __forceinline__ void blockWaitQkv(const BlockSync &bs, int nKv) {
-    if (threadIdx.x == 0 && __hip_atomic_load(bs.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-        for (int g = 0; g < nKv; g++) {
-            const unsigned target = bs.step * bs.qkvExpect[g];
-            bool ok = true;
-            while ((int)(__hip_atomic_load(bs.qkvCnt + g * kCntStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
-                         target) < 0) {
-                __builtin_amdgcn_s_sleep(2);
-                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > bs.timeoutTicks) {
-                    __hip_atomic_store(bs.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = false;
-                    break;
-                }
-            }
-            if (!ok) break;
-        }
-    }
-    __syncthreads();
+// Raise the per-XCD copies of a "step done" flag (the last arriver of a phase).
+__device__ __forceinline__ void raiseFlags(unsigned *flag, unsigned step) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) __hip_atomic_store(flag + k * kCntStride, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // After write-through stores: every wave drains its stores, the barrier, then one lane signals.
@@ -794,7 +782,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
     auto latePath = [&]() {
         // consumer: the weight ring is issued once the qkv phase of the launch is done, so it streams
         // while HBM would idle during attention instead of competing with the qkv weights
-        if constexpr (MODE == GEMV_CONSUMER) blockWaitQkv(*bs, bs->nKv);
+        if constexpr (MODE == GEMV_CONSUMER) blockWait(bs->qkvFlag + xccId() * kCntStride, bs->step, *bs, 4);
         // sched_barrier keeps issue order == slot order, so each step waits for exactly its own
         // slot (vmcnt = loads of the other kRing-1 slots) instead of the scheduler batching the ring.
 #pragma unroll
@@ -812,7 +800,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
         if constexpr (MODE == GEMV_CONSUMER) {
             // the activations are produced in this launch: wait for every producer (the ring's
             // weight loads are already in flight), then read them write-through
-            tWaited = blockWait(bs->attnFlag + xccId() * kCntStride, bs->step, *bs);
+            tWaited = blockWait(bs->attnFlag + xccId() * kCntStride, bs->step, *bs, 3);
             stageQ80<B, true>(a, sq, ssc);
         } else if constexpr (PRO == PRO_RESNORM)
             resNormPrologue<B, true>(a, scratch, sq, ssc, nullptr);
@@ -937,6 +925,10 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
                 m &= m - 1;
                 __hip_atomic_fetch_add(bs->qkvCnt + g * kCntStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            // the last qkv workgroup of the step tells the wo role (per-XCD flags) to start its weight
+            // ring, so the wo weights stream while attention runs instead of competing with qkv's
+            if (__hip_atomic_fetch_add(bs->qkvAll, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == bs->qkvAllTarget)
+                raiseFlags(bs->qkvFlag, bs->step);
         }
     }
     if constexpr (tpx) {  // all-reduce the partial rows over the TP ranks, then store (sq is free now)
@@ -1213,7 +1205,7 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
             loadRound(tb, 1);
             prefetched = true;
         }
-        tWaited = blockWait(bs->qkvCnt + kvh * kCntStride, bs->step * bs->qkvExpect[kvh], *bs);
+        tWaited = blockWait(bs->qkvCnt + kvh * kCntStride, bs->step * bs->qkvExpect[kvh], *bs, 2);
     }
     // this lane's slice of the HG query heads (pre-scaled), vector loads
     const float scale = 1.0f / sqrtf((float)HS);

@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <string>
 #include <unordered_set>
 #include <vector>
 
@@ -330,9 +331,11 @@ class HipEngineImpl : public HipEngine {
         if (blockOn_) DL_HIP(hipMemcpyAsync(hErr_ + 1, dBlockErr_, sizeof(int), hipMemcpyDeviceToHost, stream_));
         DL_HIP(hipStreamSynchronize(stream_));
         if (blockOn_ && hErr_[1] != 0) {
+            const int code = hErr_[1];
             hErr_[1] = 0;
             resetAttnBlockState();
-            throw Error("fused attention block: a workgroup wait timed out (not all workgroups resident?)");
+            throw Error("fused attention block: a hand-off wait timed out (code " + std::to_string(code) +
+                        ": 2 qkv->attention, 3 attention->wo, 4 qkv phase; not all workgroups resident?)");
         }
         if (flag && *hErr_ != 0)
             throw Error("tensor-parallel collective timed out: a peer rank did not arrive within 2 s (worker lost?)");
@@ -1242,7 +1245,8 @@ class HipEngineImpl : public HipEngine {
     int fusedGridMax_ = 0;  // largest grid of a fused-exchange GEMV launch (checked co-resident)
     static constexpr int kMaxKvGroups = 64;
     // counters: [64 groups x 64 words] qkv arrivals, [64] attention arrivals, [8 x 64] ready flags
-    static constexpr int kBlockCntWords = kMaxKvGroups * 64 + 64 + 8 * 64;
+    // + [64] qkv arrivals, [8 x 64] qkv-done flags (attn_block_inst.h carves them after attnFlag)
+    static constexpr int kBlockCntWords = kMaxKvGroups * 64 + 64 + 8 * 64 + 64 + 8 * 64 + 64;
     unsigned *dEpoch_ = nullptr, *dBlockCnt_ = nullptr, *dBlockExpect_ = nullptr;
     int *dBlockErr_ = nullptr;
     bool blockOn_ = false;  // decode rows run the fused attention block (setupAttnBlock)
