@@ -152,6 +152,8 @@ def main() -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-f32kv", action="store_true", help="skip the f32 KV-cache decode point")
     ap.add_argument("--no-prefill4k", action="store_true", help="skip the 4096-token prompt-eval point")
+    ap.add_argument("--prefill-chunk", type=int, default=256,
+                    help="rows per forward of the second 4096-token prompt point (the first uses the reference's 32)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -314,31 +316,46 @@ def main() -> int:
         tpf32_ms = (time.perf_counter() - tt) * 1000.0 / 32
         barrier()
 
-    p4k_ms = None
+    p4k_ms = p4k_big_ms = None
     if not args.no_prefill4k:  # a 4096-token prompt evaluated in 32-token chunks (attention grows with it)
         del eng
         eng = make_engine(4096 + 8)
         p4k = [(i * 7919 + 13) % 128000 for i in range(4096)]
-        for _ in range(2):  # eager first use, then graph capture - both outside the timing
-            eng.forward_argmax(p4k[:32], list(range(32)), [0] * 32)
-        barrier()
-        torch.cuda.synchronize()
-        tp4 = time.perf_counter()
-        for s0 in range(0, 4096, 32):
-            eng.forward_argmax(p4k[s0:s0 + 32], list(range(s0, s0 + 32)), [0] * 32)
-        torch.cuda.synchronize()
-        p4k_ms = (time.perf_counter() - tp4) * 1000.0 / 4096
-        barrier()
+
+        def prefill(e, chunk):
+            for _ in range(2):  # eager first use, then graph capture - both outside the timing
+                e.forward_argmax(p4k[:chunk], list(range(chunk)), [0] * chunk)
+            barrier()
+            torch.cuda.synchronize()
+            tp4 = time.perf_counter()
+            for s0 in range(0, 4096, chunk):
+                e.forward_argmax(p4k[s0:s0 + chunk], list(range(s0, s0 + chunk)), [0] * chunk)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - tp4) * 1000.0 / 4096
+            barrier()
+            return ms
+
+        p4k_ms = prefill(eng, 32)
+        # the same prompt in chunks of `--prefill-chunk` rows (dllama --max-batch / the API's prefill):
+        # each matrix's 64-row GEMM launches follow each other, the repeats read it from the MALL
+        if args.prefill_chunk > 32:
+            del eng
+            eng = C.HipEngine(args.model, "q80", max_seq_len=4096 + 8, max_batch=args.prefill_chunk, n_slots=1,
+                              kv_bf16=True, gpu_index=local, use_graphs=not args.no_graphs,
+                              synthetic=None if args.model else dict(shape, seq_len=4096 + 8), seed=1234, rank=rank,
+                              world=world, uid=uid, comm=comm, sync_type=args.sync_type)
+            p4k_big_ms = prefill(eng, args.prefill_chunk)
 
     if dist is not None:
-        t = torch.tensor([elapsed, eval_s, long_ms or 0.0, f32kv_ms or 0.0, p4k_ms or 0.0, tpf32_ms or 0.0],
-                         dtype=torch.float64)
+        t = torch.tensor([elapsed, eval_s, long_ms or 0.0, f32kv_ms or 0.0, p4k_ms or 0.0, tpf32_ms or 0.0,
+                          p4k_big_ms or 0.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, eval_s = float(t[0]), float(t[1])
         long_ms = float(t[2]) if long_ms is not None else None
         f32kv_ms = float(t[3]) if f32kv_ms is not None else None
         p4k_ms = float(t[4]) if p4k_ms is not None else None
         tpf32_ms = float(t[5]) if tpf32_ms is not None else None
+        p4k_big_ms = float(t[6]) if p4k_big_ms is not None else None
 
     ms_per_step = elapsed * 1000.0 / args.steps
     pred_ms_tok = ms_per_step / B
@@ -385,6 +402,8 @@ def main() -> int:
             "long_ctx_pred_ms_per_token": round(long_ms / B, 4) if long_ms is not None else None,
             "f32_kv_pred_ms_per_token": round(f32kv_ms / B, 4) if f32kv_ms is not None else None,
             "prompt_4k_eval_ms_per_token": round(p4k_ms, 4) if p4k_ms is not None else None,
+            "prompt_4k_chunk": args.prefill_chunk if p4k_big_ms is not None else None,
+            "prompt_4k_eval_big_chunk_ms_per_token": round(p4k_big_ms, 4) if p4k_big_ms is not None else None,
             "load_s": round(load_s, 2),
             "hip_graphs": not args.no_graphs,
             "tp_ranks": world,
