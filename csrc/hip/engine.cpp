@@ -261,6 +261,26 @@ class HipEngineImpl : public HipEngine {
         stats_.computeMs = t.elapsedMs();
     }
 
+    // Pipelined serving: the forward and the D2H copy of its ids are enqueued; the host returns at
+    // once (inputs are staged in pinned memory: the previous forward was collected before).
+    void launchIds(int n, const int *tokens, const int *positions, const int *slots, const SampleSpec *specs) override {
+        DL_CHECK(pendingN_ == 0, "launchIds: the previous forward was not collected");
+        Timer t;
+        setInputs(n, tokens, positions, slots, specs);
+        runGraph(n, specs ? GraphKind::SAMPLE : GraphKind::ARGMAX);
+        DL_HIP(hipMemcpyAsync(hIds_, dIds_, n * sizeof(int), hipMemcpyDeviceToHost, stream_));
+        pendingN_ = n;
+        stats_.computeMs = t.elapsedMs();
+    }
+    void collectIds(int *out) override {
+        DL_CHECK(pendingN_ > 0, "collectIds: nothing launched");
+        const int n = pendingN_;
+        pendingN_ = 0;
+        syncAndCheckComm();
+        inputsInFlight_ = false;
+        std::memcpy(out, hIds_, n * sizeof(int));
+    }
+
     double decodeGreedy(int steps, int token, int pos, int slot, int *outTokens) override {
         return decodeGreedyBatch(steps, 1, &token, &pos, &slot, outTokens);
     }
@@ -1282,6 +1302,7 @@ class HipEngineImpl : public HipEngine {
     bool profile_ = false;
     bool graphsBroken_ = false;
     bool inputsInFlight_ = false;  // an H2D copy from hIn_ may still be pending
+    int pendingN_ = 0;             // rows of a launchIds forward not collected yet
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> profTimes_;
 };
 

@@ -275,6 +275,24 @@ void InferenceSession::forwardSample(int n, const int *tokens, const int *positi
     recordMetrics("forward_sample", n, t.elapsedMs());
 }
 
+void InferenceSession::launchIds(int n, const int *tokens, const int *positions, const int *slots,
+                                 const SampleSpec *specs) {
+    launchTimer_.reset();
+    if (specs) {
+        sendControl(Cmd::FORWARD_SAMPLE, n, tokens, positions, slots);
+        for (auto &s : workers_) s.sendAll(specs, n * sizeof(SampleSpec));
+    } else {
+        sendControl(Cmd::FORWARD_ARGMAX, n, tokens, positions, slots);
+    }
+    backend_->launchIds(n, tokens, positions, slots, specs);
+    launchedSample_ = specs != nullptr;
+}
+
+void InferenceSession::collectIds(int n, int *out) {
+    backend_->collectIds(out);
+    recordMetrics(launchedSample_ ? "forward_sample" : "forward_argmax", n, launchTimer_.elapsedMs());
+}
+
 void InferenceSession::recordMetrics(const char *kind, int n, double ms) {
     MetricsSink &m = MetricsSink::global();
     if (!m.enabled()) return;

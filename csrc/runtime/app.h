@@ -72,6 +72,9 @@ class InferenceSession {
     // per-row sampling on the backend (device sampler on GPUs: only token ids leave the device)
     void forwardSample(int n, const int *tokens, const int *positions, const int *slots, const SampleSpec *specs,
                        int *out);
+    // Pipelined serving (Backend::launchIds / collectIds; workers run the forward in lockstep).
+    void launchIds(int n, const int *tokens, const int *positions, const int *slots, const SampleSpec *specs);
+    void collectIds(int n, int *out);
     ForwardStats lastStats();
     void finish();  // stop workers (they return to listening)
     // GPU only: one eager forward of these rows with a per-kernel-class device-time table.
@@ -92,6 +95,8 @@ class InferenceSession {
     std::unique_ptr<Sampler> sampler_;
     bool finished_ = false;
     unsigned long long mSent_ = 0, mRecv_ = 0;  // control-plane bytes at the previous metrics record
+    Timer launchTimer_;                          // launchIds -> collectIds (metrics)
+    bool launchedSample_ = false;
 };
 
 // `dllama worker`: serve forever; a root disconnect returns to listening.

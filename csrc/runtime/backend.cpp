@@ -2,6 +2,8 @@
 // device sampler (csrc/hip/kernels.hip sampleKernel).
 #include "backend.h"
 
+#include <algorithm>
+
 #include <vector>
 
 #include "../text/tokenizer.h"
@@ -25,6 +27,19 @@ void Backend::forwardSample(int n, const int *tokens, const int *positions, cons
     std::vector<float> logits((size_t)n * vocab);
     forward(n, tokens, positions, slots, logits.data());
     for (int i = 0; i < n; i++) out[i] = sampleHost(&logits[(size_t)i * vocab], vocab, specs[i]);
+}
+
+void Backend::launchIds(int n, const int *tokens, const int *positions, const int *slots, const SampleSpec *specs) {
+    pendingIds_.assign(n, -1);
+    if (specs)
+        forwardSample(n, tokens, positions, slots, specs, pendingIds_.data());
+    else
+        forwardArgmax(n, tokens, positions, slots, pendingIds_.data());
+}
+
+void Backend::collectIds(int *out) {
+    std::copy(pendingIds_.begin(), pendingIds_.end(), out);
+    pendingIds_.clear();
 }
 
 }  // namespace dl

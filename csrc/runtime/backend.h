@@ -9,6 +9,7 @@
 
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "../core/model_file.h"
 #include "../core/plan.h"
@@ -66,6 +67,12 @@ class Backend {
     // Default: full logits to the root, host draw, ids shared through forwardArgmax's channel.
     virtual void forwardSample(int n, const int *tokens, const int *positions, const int *slots,
                                const SampleSpec *specs, int *out);
+    // Pipelined serving (scheduler.cpp): launchIds enqueues a forward whose result is one token id
+    // per row (argmax when specs is null, else per-row sampling) and may return before it ran;
+    // collectIds waits for it and writes the ids. At most one launch is outstanding. The default
+    // runs the forward synchronously inside launchIds (host backends: no overlap).
+    virtual void launchIds(int n, const int *tokens, const int *positions, const int *slots, const SampleSpec *specs);
+    virtual void collectIds(int *out);
     virtual ForwardStats lastStats() const { return stats_; }
     // Weight residency: time to load (file read + repack + upload, or on-device init), bytes read
     // from the model file by this rank, bytes resident on its device (0 for host backends).
@@ -78,6 +85,7 @@ class Backend {
 
   protected:
     ForwardStats stats_;
+    std::vector<int> pendingIds_;  // default launchIds / collectIds
 };
 
 // Host data plane used by the CPU backend for tensor parallelism.

@@ -86,28 +86,87 @@ void Scheduler::loop() {
     while (true) {
         {
             std::unique_lock<std::mutex> lk(mu_);
-            cv_.wait(lk, [&] { return stop_ || !queue_.empty() || !active_.empty(); });
-            if (stop_) return;
+            cv_.wait(lk, [&] { return stop_ || !queue_.empty() || !active_.empty() || inflight_; });
+            if (stop_) break;
         }
         try {
             step();
         } catch (const std::exception &e) {
             // a failed forward poisons every in-flight request; the session stays usable
-            std::lock_guard<std::mutex> lk(mu_);
-            for (auto &r : active_) {
-                r->error = e.what();
-                r->finish("error");
-                freeSlots_.push_back(r->slot);
-            }
-            active_.clear();
+            failAll(e.what());
         }
     }
+    if (inflight_) {  // leave no forward running on the backend
+        try {
+            std::vector<int> ids(flight_.n);
+            sess_.collectIds(flight_.n, ids.data());
+        } catch (const std::exception &) {
+        }
+        inflight_ = false;
+    }
+}
+
+void Scheduler::failAll(const std::string &what) {
+    std::lock_guard<std::mutex> lk(mu_);
+    inflight_ = false;
+    flight_.picks.clear();
+    for (auto &r : active_) {
+        r->error = what;
+        r->finished = true;
+        r->finish("error");
+        freeSlots_.push_back(r->slot);
+    }
+    for (auto &r : draining_) freeSlots_.push_back(r->slot);
+    active_.clear();
+    draining_.clear();
+}
+
+// Under mu_. Finished requests leave active_; their KV slot is reused only once no forward in
+// flight still writes it (rows launched before the host saw the EOS are dropped at collection).
+void Scheduler::finishRequest(const std::shared_ptr<GenRequest> &r, const char *reason) {
+    r->finished = true;
+    r->finish(reason);
+    bool inFlight = false;
+    if (inflight_)
+        for (auto &p : flight_.picks)
+            if (p.r == r) inFlight = true;
+    if (inFlight)
+        draining_.push_back(r);
+    else
+        freeSlots_.push_back(r->slot);
+    active_.erase(std::remove(active_.begin(), active_.end(), r), active_.end());
 }
 
 bool Scheduler::step() {
     const u32 seqLen = sess_.header().seqLen;
     const int vocab = (int)sess_.header().vocabSize;
-    // 1) admission: one free KV slot per request
+
+    // 0) collect the forward in flight: token ids and prompt progress only (cheap); the text work
+    //    for these tokens runs after the next forward has been launched (step 4)
+    std::vector<Pick> done;
+    std::vector<int> ids;
+    int doneRows = 0, doneDecode = 0;
+    double doneMs = 0;
+    if (inflight_) {
+        ids.resize(flight_.n);
+        sess_.collectIds(flight_.n, ids.data());
+        doneMs = flight_.t.elapsedMs();
+        doneRows = flight_.n;
+        doneDecode = flight_.nDecode;
+        for (auto &p : flight_.picks) {
+            GenRequest *r = p.r.get();
+            if (r->finished) continue;  // finished while its row was in flight: dropped
+            r->prefilled += p.prefill;
+            if (p.sample) r->generated.push_back(ids[p.row]);
+        }
+        done.swap(flight_.picks);
+        inflight_ = false;
+        std::lock_guard<std::mutex> lk(mu_);
+        for (auto &r : draining_) freeSlots_.push_back(r->slot);  // their last rows have completed
+        draining_.clear();
+    }
+
+    // 1) admission: one free KV slot per request; cancelled requests give their slot back
     {
         std::lock_guard<std::mutex> lk(mu_);
         while (!queue_.empty() && !freeSlots_.empty()) {
@@ -141,46 +200,36 @@ bool Scheduler::step() {
             r->eos.reset(new EosDetector(eosIds, stops, (int)maxLen, (int)maxLen));
             active_.push_back(r);
         }
-        // requests whose client disconnected give their slot back before the batch is built; the
-        // flag is read ONCE per request (cancel() runs on HTTP threads without mu_), so a request
-        // is either finished + freed + dropped, or kept - never dropped with its slot still held
-        std::vector<std::shared_ptr<GenRequest>> keep;
-        keep.reserve(active_.size());
-        for (auto &r : active_) {
-            if (r->isCancelled()) {
-                r->finish("cancelled");
-                freeSlots_.push_back(r->slot);
-                stats_.cancelled++;
-            } else {
-                keep.push_back(r);
-            }
+        // the cancel flag is read ONCE per request (cancel() runs on HTTP threads without mu_)
+        std::vector<std::shared_ptr<GenRequest>> cancelled;
+        for (auto &r : active_)
+            if (r->isCancelled()) cancelled.push_back(r);
+        for (auto &r : cancelled) {
+            finishRequest(r, "cancelled");
+            stats_.cancelled++;
         }
-        active_.swap(keep);
         stats_.active = (int)active_.size();
     }
-    if (active_.empty()) return false;
 
-    // 2) build the batch: decode rows first (latency), then prefill chunks with the remaining budget
+    // 2) build the next batch: decode rows first (latency), then prefill chunks with the remaining
+    //    budget. A decode row is launched before the host has decoded the previous token: a request
+    //    whose last token turns out to end it (EOS / stop string) wastes one row, dropped at collection.
     const int maxRows = sess_.maxBatch();
     std::vector<int> tokens, positions, slots;
-    struct Pick {
-        GenRequest *r;
-        int row;       // batch row whose logits are sampled
-        bool sample;
-        int prefill;   // prompt tokens consumed this step
-    };
-    std::vector<Pick> picks;
+    Flight next;
     for (auto &rp : active_) {
         GenRequest *r = rp.get();
         if (r->prefilled < r->prompt.size()) continue;
         if ((int)tokens.size() >= maxRows) break;
         const int pos = (int)(r->prompt.size() + r->generated.size()) - 1;
+        if ((r->params.maxTokens > 0 && (int)r->generated.size() >= r->params.maxTokens) || (u32)(pos + 1) >= seqLen)
+            continue;  // ends at this step's text work (length)
         tokens.push_back(r->generated.back());
         positions.push_back(pos);
         slots.push_back(r->slot);
-        picks.push_back({r, (int)tokens.size() - 1, true, 0});
+        next.picks.push_back({rp, (int)tokens.size() - 1, true, 0});
     }
-    const int nDecode = (int)tokens.size();
+    next.nDecode = (int)tokens.size();
     for (auto &rp : active_) {
         GenRequest *r = rp.get();
         if (r->prefilled >= r->prompt.size()) continue;
@@ -193,44 +242,52 @@ bool Scheduler::step() {
             slots.push_back(r->slot);
         }
         const bool completes = r->prefilled + take == r->prompt.size();
-        picks.push_back({r, (int)tokens.size() - 1, completes, take});
+        next.picks.push_back({rp, (int)tokens.size() - 1, completes, take});
     }
-    const int n = (int)tokens.size();
-    if (n == 0) return false;
+    next.n = (int)tokens.size();
 
-    // 3) forward: device argmax when every sampled row is greedy; otherwise per-row draws on the
+    // 3) launch: device argmax when every sampled row is greedy; otherwise per-row draws on the
     //    backend (the device sampler on GPUs) with each request's own temperature / top-p and the
     //    coin its own seeded generator yields, so only token ids come back
-    bool allGreedy = true;
-    for (auto &p : picks)
-        if (p.sample && p.r->params.temperature != 0.0f) allGreedy = false;
-    Timer t;
-    std::vector<int> ids(n);
-    if (allGreedy) {
-        sess_.forwardArgmax(n, tokens.data(), positions.data(), slots.data(), ids.data());
-    } else {
-        std::vector<SampleSpec> specs(n);
-        for (auto &sp : specs) sp.temperature = -1.f;  // rows that are not sampled
-        for (auto &p : picks) {
-            if (!p.sample) continue;
-            SampleSpec &sp = specs[p.row];
-            sp.temperature = p.r->params.temperature;
-            sp.topp = p.r->params.topp;
-            sp.coin = p.r->sampler->drawCoin();
+    if (next.n > 0) {
+        bool allGreedy = true;
+        for (auto &p : next.picks)
+            if (p.sample && p.r->params.temperature != 0.0f) allGreedy = false;
+        next.t.reset();
+        if (allGreedy) {
+            sess_.launchIds(next.n, tokens.data(), positions.data(), slots.data(), nullptr);
+        } else {
+            std::vector<SampleSpec> specs(next.n);
+            for (auto &sp : specs) sp.temperature = -1.f;  // rows that are not sampled
+            for (auto &p : next.picks) {
+                if (!p.sample) continue;
+                SampleSpec &sp = specs[p.row];
+                sp.temperature = p.r->params.temperature;
+                sp.topp = p.r->params.topp;
+                sp.coin = p.r->sampler->drawCoin();
+            }
+            sess_.launchIds(next.n, tokens.data(), positions.data(), slots.data(), specs.data());
         }
-        sess_.forwardSample(n, tokens.data(), positions.data(), slots.data(), specs.data(), ids.data());
+        std::lock_guard<std::mutex> lk(mu_);
+        flight_ = std::move(next);
+        inflight_ = true;
     }
-    (void)vocab;
-    const double ms = t.elapsedMs();
 
-    // 4) sample, detect stops, stream deltas
-    std::vector<GenRequest *> finished;
-    for (auto &p : picks) {
-        GenRequest *r = p.r;
-        r->prefilled += p.prefill;
-        if (!p.sample) continue;
+    // 4) text work of the collected forward (overlaps the forward just launched): decode, detect
+    //    stops, stream deltas, finish
+    std::lock_guard<std::mutex> lk(mu_);
+    if (doneRows > 0) {
+        stats_.forwards++;
+        stats_.rows += doneRows;
+        stats_.decodeRows += doneDecode;
+        stats_.prefillRows += doneRows - doneDecode;
+        stats_.busyMs += doneMs;
+    }
+    for (auto &p : done) {
+        const std::shared_ptr<GenRequest> &rp = p.r;
+        GenRequest *r = rp.get();
+        if (!p.sample || r->finished) continue;
         const int token = ids[p.row];
-        r->generated.push_back(token);
         r->completionTokens = (int)r->generated.size();
         std::string piece, delta;
         const bool has = r->decoder->decode(token, piece);
@@ -240,32 +297,19 @@ bool Scheduler::step() {
             r->eos->reset();
         }
         const int nextPos = (int)(r->prompt.size() + r->generated.size());
-        if (er == EosResult::EOS) {
-            r->finish("stop");
-            finished.push_back(r);
-        } else if ((r->params.maxTokens > 0 && (int)r->generated.size() >= r->params.maxTokens) ||
-                   (u32)nextPos >= seqLen) {
-            r->finish("length");
-            finished.push_back(r);
+        const char *reason = nullptr;
+        if (er == EosResult::EOS)
+            reason = "stop";
+        else if ((r->params.maxTokens > 0 && (int)r->generated.size() >= r->params.maxTokens) || (u32)nextPos >= seqLen)
+            reason = "length";
+        if (reason) {
+            stats_.completed++;
+            stats_.generatedTokens += r->generated.size();
+            finishRequest(rp, reason);
         }
     }
-
-    std::lock_guard<std::mutex> lk(mu_);
-    stats_.forwards++;
-    stats_.rows += n;
-    stats_.decodeRows += nDecode;
-    stats_.prefillRows += n - nDecode;
-    stats_.busyMs += ms;
-    for (GenRequest *r : finished) {
-        stats_.completed++;
-        stats_.generatedTokens += r->generated.size();
-        freeSlots_.push_back(r->slot);
-        active_.erase(std::remove_if(active_.begin(), active_.end(),
-                                     [r](const std::shared_ptr<GenRequest> &x) { return x.get() == r; }),
-                      active_.end());
-    }
     stats_.active = (int)active_.size();
-    return true;
+    return next.n > 0 || doneRows > 0;
 }
 
 }  // namespace dl

@@ -58,6 +58,7 @@ class GenRequest {
   private:
     friend class Scheduler;
     std::atomic<bool> cancelled{false};
+    bool finished = false;  // scheduler thread only: finish() ran (rows still in flight are dropped)
     int slot = -1;
     size_t prefilled = 0;
     std::vector<int> generated;
@@ -83,8 +84,23 @@ class Scheduler {
     SchedulerStats stats();
 
   private:
+    // One batched forward in flight (pipelined serving): while the device runs it, the host
+    // decodes, EOS-checks and streams the previous forward's tokens.
+    struct Pick {
+        std::shared_ptr<GenRequest> r;
+        int row;      // batch row whose id belongs to the request
+        bool sample;  // the row yields the request's next token
+        int prefill;  // prompt tokens consumed by this forward
+    };
+    struct Flight {
+        std::vector<Pick> picks;
+        int n = 0, nDecode = 0;
+        Timer t;
+    };
     void loop();
-    bool step();  // one batched forward; false when idle
+    bool step();  // collect the forward in flight, launch the next, post-process the collected one
+    void finishRequest(const std::shared_ptr<GenRequest> &r, const char *reason);
+    void failAll(const std::string &what);
 
     InferenceSession &sess_;
     Tokenizer &tok_;
@@ -92,7 +108,10 @@ class Scheduler {
     std::condition_variable cv_;
     std::deque<std::shared_ptr<GenRequest>> queue_;
     std::vector<std::shared_ptr<GenRequest>> active_;
+    std::vector<std::shared_ptr<GenRequest>> draining_;  // finished, rows still in the forward in flight
     std::vector<int> freeSlots_;
+    Flight flight_;
+    bool inflight_ = false;
     bool stop_ = false;
     u64 nextId_ = 1;
     SchedulerStats stats_;

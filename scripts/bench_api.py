@@ -92,9 +92,21 @@ def main():
         _round(port, args.n, 8, 0.0, 0)      # untimed: graph capture for the batch sizes
         _round(port, args.n, 8, 0.8, 100)
         res = {}
+
+        def health():
+            c = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+            c.request("GET", "/health")
+            return json.loads(c.getresponse().read())
+
         for name, temp, seed in (("greedy", 0.0, 0), ("sampled", 0.8, 1000)):
+            h0 = health()
             toks, dt = _round(port, args.n, args.max_tokens, temp, seed)
-            res[name] = {"completion_tokens": toks, "s": round(dt, 3), "tok_s": round(toks / dt, 1)}
+            h1 = health()
+            d = {k: h1[k] - h0[k] for k in ("forwards", "rows", "prefill_rows", "decode_rows", "busy_ms") if k in h1}
+            res[name] = {"completion_tokens": toks, "s": round(dt, 3), "tok_s": round(toks / dt, 1),
+                         "forwards": d.get("forwards"), "rows": d.get("rows"), "prefill_rows": d.get("prefill_rows"),
+                         "forward_ms": round(d.get("busy_ms", 0.0), 1),
+                         "host_ms": round(dt * 1000 - d.get("busy_ms", 0.0), 1)}
             print(name, res[name], flush=True)
         res["sampled_vs_greedy"] = round(res["sampled"]["tok_s"] / res["greedy"]["tok_s"], 3)
         res["concurrent_requests"] = args.n
