@@ -25,6 +25,12 @@ class DeviceComm {
     virtual int size() const = 0;
     virtual void allReduceSum(float *buf, size_t n, hipStream_t s) = 0;
     virtual void allGather(const float *send, float *recv, size_t nPerRank, hipStream_t s) = 0;
+    // Rank 0 receives every rank's nPerRank floats in rank order (the reference gathers the logits
+    // slices to the root only: SYNC_NODE_SLICES_EXCEPT_ROOT, llm.cpp:432); recv is only written on
+    // rank 0. Default: an all-gather.
+    virtual void gatherToRoot(const float *send, float *recv, size_t nPerRank, hipStream_t s) {
+        allGather(send, recv, nPerRank, s);
+    }
     virtual void broadcastInts(int *buf, size_t n, int root, hipStream_t s) = 0;
     virtual std::string name() const = 0;
     // Health reporting: device int set non-zero when a collective stopped waiting

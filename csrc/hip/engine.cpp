@@ -1205,13 +1205,21 @@ class HipEngineImpl : public HipEngine {
         // (value, index) winners cross the links (reference: logits gathered to the root,
         // llm.cpp:432); the full logits are gathered only when the host samples them
         const bool distArgmax = tpFused_ && (kind == GraphKind::ARGMAX || kind == GraphKind::CHAIN);
+        // logits for the host (LOGITS) and sampled rows (SAMPLE) are needed on the root only: the
+        // vocab slices are gathered to rank 0 (the reference's SYNC_NODE_SLICES_EXCEPT_ROOT), the
+        // other ranks publish theirs and skip the unshard and the draw (the root's ids are used)
+        const bool rootOnly = kind == GraphKind::LOGITS || kind == GraphKind::SAMPLE;
         if (p.nRanks > 1 && !distArgmax) {
             ProfScope ps(this, "allgather");
-            comm_->allGather(dLogits_, dLogitsAll_, (size_t)n * p.vocab0, stream_);
-            hipk::launchUnshardLogits(dLogitsAll_, dLogitsFull_, p.nRanks, n, p.vocab0, stream_);
+            if (rootOnly)
+                comm_->gatherToRoot(dLogits_, dLogitsAll_, (size_t)n * p.vocab0, stream_);
+            else
+                comm_->allGather(dLogits_, dLogitsAll_, (size_t)n * p.vocab0, stream_);
+            if (!rootOnly || rank() == 0)
+                hipk::launchUnshardLogits(dLogitsAll_, dLogitsFull_, p.nRanks, n, p.vocab0, stream_);
             full = dLogitsFull_;
         }
-        if (kind == GraphKind::SAMPLE) {
+        if (kind == GraphKind::SAMPLE && (p.nRanks == 1 || rank() == 0)) {
             ProfScope ps(this, "sample");
             hipk::SampleArgs g;
             g.logits = full;

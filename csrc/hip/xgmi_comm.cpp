@@ -76,7 +76,7 @@ struct XgmiCall {
     float *out;                     // local output (n floats for reduce, W*n for gather)
     long long maxFloats;
     long long n;
-    int rank, world, gather;
+    int rank, world, gather;        // gather: 0 all-reduce, 1 all-gather, 2 gather to rank 0
     int fenced;                     // system-scope release / acquire fences around the flags
     long long timeoutTicks;         // s_memrealtime ticks (100 MHz)
 };
@@ -136,7 +136,12 @@ __global__ __launch_bounds__(kThreads) void xgmiKernel(XgmiCall a) {
     }
     __syncthreads();
     if (a.fenced) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    // 3. reduce (rank order, identical on every rank) or gather
+    // 3. reduce (rank order, identical on every rank) or gather (gather to rank 0: the other
+    //    ranks only publish and take part in the flag protocol, which keeps the double buffer safe)
+    if (a.gather == 2 && a.rank != 0) {
+        if (tid == 0) a.epochs[g] = e;
+        return;
+    }
     for (long long c = g; c < nChunks; c += kSlots) {
         const long long i = c * kChunk + tid * 4;
         const long long cnt = i + 3 < a.n ? 4 : (i < a.n ? a.n - i : 0);
@@ -321,10 +326,13 @@ class XgmiComm : public DeviceComm {
         if (ll_ && n <= (size_t)kLLMax && !pullOnly() && (world_ == 2 || world_ == 4 || world_ == 8))
             launchLL(buf, n, s);
         else
-            launch(buf, buf, n, false, s);
+            launch(buf, buf, n, 0, s);
     }
     void allGather(const float *send, float *recv, size_t nPerRank, hipStream_t s) override {
-        launch(send, recv, nPerRank, true, s);
+        launch(send, recv, nPerRank, 1, s);
+    }
+    void gatherToRoot(const float *send, float *recv, size_t nPerRank, hipStream_t s) override {
+        launch(send, recv, nPerRank, 2, s);
     }
     void broadcastInts(int *, size_t, int, hipStream_t) override {
         throw Error("xgmi comm: broadcastInts is not used on the device data plane");
@@ -369,7 +377,7 @@ class XgmiComm : public DeviceComm {
         }();
         return v;
     }
-    XgmiCall call(const float *in, float *out, size_t n, bool gather) const {
+    XgmiCall call(const float *in, float *out, size_t n, int gather) const {
         XgmiCall c;
         c.peers = peers_;
         c.epochs = epochs_;
@@ -380,7 +388,7 @@ class XgmiComm : public DeviceComm {
         c.n = (long long)n;
         c.rank = rank_;
         c.world = world_;
-        c.gather = gather ? 1 : 0;
+        c.gather = gather;
         const char *fe = std::getenv("DL_XGMI_FENCE");
         c.fenced = fenced_ || (fe && *fe == '1') ? 1 : 0;
         c.timeoutTicks = kTimeoutTicks;
@@ -390,7 +398,7 @@ class XgmiComm : public DeviceComm {
         DL_CHECK(connected_, "xgmi comm: connect() was not called");
         const int grid = (int)((n + kChunk - 1) / kChunk);
         if (grid == 0) return;
-        const XgmiCall c = call(buf, buf, n, false);
+        const XgmiCall c = call(buf, buf, n, 0);
         switch (world_) {
             case 2: hipLaunchKernelGGL(xgmiLLKernel<2>, dim3(grid), dim3(kThreads), 0, s, c, llEpochs_); break;
             case 4: hipLaunchKernelGGL(xgmiLLKernel<4>, dim3(grid), dim3(kThreads), 0, s, c, llEpochs_); break;
@@ -398,7 +406,7 @@ class XgmiComm : public DeviceComm {
         }
         DL_HIP(hipGetLastError());
     }
-    void launch(const float *in, float *out, size_t n, bool gather, hipStream_t s) {
+    void launch(const float *in, float *out, size_t n, int gather, hipStream_t s) {
         DL_CHECK(connected_, "xgmi comm: connect() was not called");
         DL_CHECK(n <= maxFloats_, "xgmi comm: message larger than the published buffer");
         const XgmiCall c = call(in, out, n, gather);

@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--n", type=int, default=64)
     ap.add_argument("--max-tokens", type=int, default=64)
     ap.add_argument("--port", type=int, default=0)
+    ap.add_argument("--max-batch", type=int, default=0,
+                    help="rows per forward (default 4 x --n: prompts prefill in big chunks, MALL-resident weights)")
     args = ap.parse_args()
     from distributed_llama_multiusers_amd.models.synthetic import make_tokenizer
     tmp = tempfile.mkdtemp()
@@ -73,7 +75,7 @@ def main():
     make_tokenizer(tok, 128256)
     port = args.port or _port()
     cmd = [os.path.join(REPO, "build", "dllama-api"), "--synthetic", "llama3_1_8b", "--tokenizer", tok,
-           "--gpu-index", "0", "--port", str(port), "--slots", str(args.n), "--max-batch", str(args.n),
+           "--gpu-index", "0", "--port", str(port), "--slots", str(args.n), "--max-batch", str(args.max_batch or 4 * args.n),
            "--max-seq-len", str(64 + args.max_tokens + 32), "--buffer-float-type", "q80"]
     log = open(os.path.join(tmp, "api.log"), "w")
     srv = subprocess.Popen(cmd, stdout=log, stderr=subprocess.STDOUT)
@@ -110,6 +112,7 @@ def main():
             print(name, res[name], flush=True)
         res["sampled_vs_greedy"] = round(res["sampled"]["tok_s"] / res["greedy"]["tok_s"], 3)
         res["concurrent_requests"] = args.n
+        res["max_batch"] = args.max_batch or 4 * args.n
         res["max_tokens"] = args.max_tokens
         print(json.dumps(res), flush=True)
     finally:

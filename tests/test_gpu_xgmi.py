@@ -115,6 +115,24 @@ def _engine_tp_batched(rank, world, port, model, tokens, q, sync_type="f32", env
         q.put((rank, repr(e)))
 
 
+def _engine_tp_sample(rank, world, port, model, tokens, temps, topps, coins, q):
+    """Sampled rows on a TP engine: the vocab slices are gathered to rank 0 only, which unshards
+    and draws (the other ranks publish their slices and skip the draw)."""
+    try:
+        C, comm, dist = _setup(rank, world, port, 1 << 16)
+        eng = C.HipEngine(model, "q80", kv_bf16=False, rank=rank, world=world, comm=comm, sync_type="f32",
+                          max_batch=8, n_slots=1)
+        n = len(tokens)
+        got = [list(eng.forward_sample(tokens, list(range(n)), [0] * n, temps, topps, coins)) for _ in range(3)]
+        lg = eng.forward(tokens, list(range(n)), [0] * n)  # LOGITS kind: also gathered to the root
+        if comm.timed_out():
+            raise AssertionError("a flag wait timed out")
+        dist.barrier()
+        q.put((rank, (got, lg if rank == 0 else None)))
+    except Exception as e:
+        q.put((rank, repr(e)))
+
+
 def _run(target, world, *args, timeout=240, kwargs=None):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
@@ -196,6 +214,33 @@ def test_xgmi_engine_tp_batched_matches_single(C, tmp_path, world, sync_type):
     for r in range(1, world):
         assert res[r][1] == res[0][1] and res[r][3] == res[0][3], r
     assert res[0][2], "fused exchange expected on for the decode rows"
+
+
+def test_xgmi_engine_tp_sampled_rows_on_root(C, tmp_path):
+    """Sampled rows at TP=2 (logits gathered to rank 0 only, like the reference's
+    SYNC_NODE_SLICES_EXCEPT_ROOT): rank 0's draws == the TP=1 engine's draws with the same coins
+    (random model: allow one near-tie flip), stable over graph replays; logits within tolerance."""
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=9, dim=512, n_heads=8,
+                               n_kv_heads=4, hidden_dim=1024, vocab_size=1024)
+    tokens = [5, 99, 300, 7, 1000, 2, 17, 400]
+    temps = [0.0, 0.7, 1.0, -1.0, 0.9, 1.2, 0.5, 0.8]
+    topps = [0.9, 0.9, 1.0, 0.9, 0.5, 0.95, 0.9, 0.0]
+    coins = [0.1, 0.35, 0.6, 0.2, 0.85, 0.5, 0.05, 0.7]
+    single = C.HipEngine(m, "q80", kv_bf16=False, max_batch=8, n_slots=1)
+    n = len(tokens)
+    ref = list(single.forward_sample(tokens, list(range(n)), [0] * n, temps, topps, coins))
+    ref_lg = single.forward(tokens, list(range(n)), [0] * n)
+    del single
+    res = _run(_engine_tp_sample, 2, m, tokens, temps, topps, coins)
+    assert all(isinstance(v, tuple) for v in res.values()), res
+    got, lg = res[0]
+    assert got[0] == got[1] == got[2], got
+    rows = [i for i in range(n) if temps[i] >= 0]
+    assert sum(got[0][i] == ref[i] for i in rows) >= len(rows) - 1, (got[0], ref)
+    rel = np.abs(lg - ref_lg).max() / np.abs(ref_lg).max()
+    assert rel < 3e-2, rel
 
 
 def test_fused_exchange_residency_guard(C, tmp_path):
