@@ -290,7 +290,9 @@ __device__ __forceinline__ void qkvPairStore(const GemvArgs &a, int r0, float v0
 }
 
 // Quantize a workgroup's `halfR` hidden units (multiple of 32, in LDS) to Q80 blocks in global.
-template <int B>
+// WT: the hidden rows are consumed in this launch (fused FFN block): 4 lanes' bytes packed into one
+// write-through 32-bit store, the scale pair one write-through 64-bit store.
+template <int B, bool WT = false>
 __device__ __forceinline__ void storeHiddenQ80(const GemvArgs &a, const float *hbuf, int halfR, int hBase) {
     for (int i = threadIdx.x; i < B * halfR; i += kThreads) {  // 32-lane groups = one block
         const int b = i / halfR, k = i % halfR;
@@ -301,9 +303,18 @@ __device__ __forceinline__ void storeHiddenQ80(const GemvArgs &a, const float *h
         const float id = d != 0.f ? 1.0f / d : 0.f;
         int q = (int)rintf(h * id);
         q = q > 127 ? 127 : (q < -127 ? -127 : q);
-        a.oq[(size_t)b * a.ldOut + hBase + k] = (int8_t)q;
+        int8_t *dst = a.oq + (size_t)b * a.ldOut + hBase + k;
+        if constexpr (WT) {
+            const uint32_t u = (uint32_t)(uint8_t)q;
+            const uint32_t w = u | ((uint32_t)__shfl_down((int)u, 1, 32) << 8) |
+                               ((uint32_t)__shfl_down((int)u, 2, 32) << 16) | ((uint32_t)__shfl_down((int)u, 3, 32) << 24);
+            if ((k & 3) == 0) st32<true>(dst, w);
+        } else {
+            *dst = (int8_t)q;
+        }
         const float qs = groupSum<32>((float)q);
-        if ((k & 31) == 0) a.os[(size_t)b * (a.ldOut >> 5) + ((hBase + k) >> 5)] = make_float2(roundF16(d), qs);
+        if ((k & 31) == 0) stF2<WT>(reinterpret_cast<float *>(a.os + (size_t)b * (a.ldOut >> 5) + ((hBase + k) >> 5)),
+                                    roundF16(d), qs);
     }
 }
 
@@ -526,6 +537,8 @@ struct BlockSync {
     unsigned attnTarget = 0;             // s * head groups
     int *error = nullptr;                // set when a wait gave up (the engine raises)
     long long timeoutTicks = 0;
+    int codeBase = 0;                    // added to the GEMV waits' error codes (3 data, 4 ring start)
+    bool ringEarly = false;              // consumer: issue the weight ring at entry (no ring-start wait)
 };
 __device__ __forceinline__ int xccId() { return (int)(__builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u); }
 
@@ -782,7 +795,8 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
     auto latePath = [&]() {
         // consumer: the weight ring is issued once the qkv phase of the launch is done, so it streams
         // while HBM would idle during attention instead of competing with the qkv weights
-        if constexpr (MODE == GEMV_CONSUMER) blockWait(bs->qkvFlag + xccId() * kCntStride, bs->step, *bs, 4);
+        if constexpr (MODE == GEMV_CONSUMER)
+            if (!bs->ringEarly) blockWait(bs->qkvFlag + xccId() * kCntStride, bs->step, *bs, bs->codeBase + 4);
         // sched_barrier keeps issue order == slot order, so each step waits for exactly its own
         // slot (vmcnt = loads of the other kRing-1 slots) instead of the scheduler batching the ring.
 #pragma unroll
@@ -800,7 +814,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
         if constexpr (MODE == GEMV_CONSUMER) {
             // the activations are produced in this launch: wait for every producer (the ring's
             // weight loads are already in flight), then read them write-through
-            tWaited = blockWait(bs->attnFlag + xccId() * kCntStride, bs->step, *bs, 3);
+            tWaited = blockWait(bs->attnFlag + xccId() * kCntStride, bs->step, *bs, bs->codeBase + 3);
             stageQ80<B, true>(a, sq, ssc);
         } else if constexpr (PRO == PRO_RESNORM)
             resNormPrologue<B, true>(a, scratch, sq, ssc, nullptr);
@@ -914,19 +928,22 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
     }
     if constexpr (EPI == EPI_ACT_Q80) {
         __syncthreads();
-        storeHiddenQ80<B>(a, hbuf, R >> 1, rowBase >> 1);
+        storeHiddenQ80<B, MODE == GEMV_PRODUCER>(a, hbuf, R >> 1, rowBase >> 1);
     }
     if constexpr (MODE == GEMV_PRODUCER) {  // rows published write-through: drain, then count in
         blockDrain();
         if (tid == 0) {
-            unsigned long long m = qkvGroupMask(rowBase, min(rowBase + R, a.rows), a.q0, a.kv0, a.hs, a.kvMul);
-            while (m) {
-                const int g = __builtin_ctzll(m);
-                m &= m - 1;
-                __hip_atomic_fetch_add(bs->qkvCnt + g * kCntStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if constexpr (EPI == EPI_QKV) {  // attention block: per KV group arrivals
+                unsigned long long m = qkvGroupMask(rowBase, min(rowBase + R, a.rows), a.q0, a.kv0, a.hs, a.kvMul);
+                while (m) {
+                    const int g = __builtin_ctzll(m);
+                    m &= m - 1;
+                    __hip_atomic_fetch_add(bs->qkvCnt + g * kCntStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
-            // the last qkv workgroup of the step tells the wo role (per-XCD flags) to start its weight
-            // ring, so the wo weights stream while attention runs instead of competing with qkv's
+            // the last producer workgroup of the step raises the per-XCD "phase done" flags: the
+            // attention block's wo role starts its weight ring (so the wo weights stream while
+            // attention runs instead of competing with qkv's), the FFN block's w2 role its ring + reads
             if (__hip_atomic_fetch_add(bs->qkvAll, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == bs->qkvAllTarget)
                 raiseFlags(bs->qkvFlag, bs->step);
         }

@@ -101,6 +101,7 @@ class HipEngineImpl : public HipEngine {
         uploadRope();
         DL_HIP(hipStreamSynchronize(stream_));
         setupAttnBlock();
+        setupFfnBlock();
         load_.ms = timer.elapsedMs();
         load_.deviceBytes = deviceBytes_;
     }
@@ -185,23 +186,34 @@ class HipEngineImpl : public HipEngine {
   public:
     bool tpFused() const override { return tpFused_; }
     bool attnBlock() const override { return blockOn_; }
-    std::vector<unsigned long long> traceAttnBlock(int token, int pos, int slot, int layer) override {
-        if (!blockOn_) return {};
-        const hipk::AttnBlockPlan pl = hipk::attnBlockPlan(attnBlockArgs(layers_[0], 0, 0), fusedTp(false));
-        const size_t words = 8 * (size_t)(pl.gq + pl.ga + pl.gw);
+    bool ffnBlock() const override { return ffnOn_; }
+    std::vector<unsigned long long> traceAttnBlock(int token, int pos, int slot, int layer, bool ffn) override {
+        if (ffn ? !ffnOn_ : !blockOn_) return {};
+        int g[3] = {0, 0, 0};
+        if (ffn) {
+            const hipk::FfnBlockPlan pl = hipk::ffnBlockPlan(ffnBlockArgs(layers_[0], 0, 0), fusedTp(false));
+            g[0] = pl.g13;
+            g[2] = pl.g2;
+        } else {
+            const hipk::AttnBlockPlan pl = hipk::attnBlockPlan(attnBlockArgs(layers_[0], 0, 0), fusedTp(false));
+            g[0] = pl.gq;
+            g[1] = pl.ga;
+            g[2] = pl.gw;
+        }
+        const size_t words = 8 * (size_t)(g[0] + g[1] + g[2]);
         traceBuf_ = dalloc<unsigned long long>(words);
         DL_HIP(hipMemsetAsync(traceBuf_, 0, words * 8, stream_));
         traceLayer_ = layer;
+        traceFfn_ = ffn;
         setInputs(1, &token, &pos, &slot);
         enqueueForward(1, GraphKind::LOGITS);
         syncAndCheckComm();
         inputsInFlight_ = false;
         std::vector<unsigned long long> out(3 + words);
-        out[0] = pl.gq;
-        out[1] = pl.ga;
-        out[2] = pl.gw;
+        for (int i = 0; i < 3; i++) out[i] = (unsigned long long)g[i];
         DL_HIP(hipMemcpy(out.data() + 3, traceBuf_, words * 8, hipMemcpyDeviceToHost));
         traceLayer_ = -1;
+        traceFfn_ = false;
         traceBuf_ = nullptr;  // (one small buffer per call, released with the engine)
         return out;
     }
@@ -348,14 +360,16 @@ class HipEngineImpl : public HipEngine {
     void syncAndCheckComm() {
         const int *flag = comm_ ? comm_->deviceErrorFlag() : nullptr;
         if (flag) DL_HIP(hipMemcpyAsync(hErr_, flag, sizeof(int), hipMemcpyDeviceToHost, stream_));
-        if (blockOn_) DL_HIP(hipMemcpyAsync(hErr_ + 1, dBlockErr_, sizeof(int), hipMemcpyDeviceToHost, stream_));
+        const bool anyBlock = blockOn_ || ffnOn_;
+        if (anyBlock) DL_HIP(hipMemcpyAsync(hErr_ + 1, dBlockErr_, sizeof(int), hipMemcpyDeviceToHost, stream_));
         DL_HIP(hipStreamSynchronize(stream_));
-        if (blockOn_ && hErr_[1] != 0) {
+        if (anyBlock && hErr_[1] != 0) {
             const int code = hErr_[1];
             hErr_[1] = 0;
             resetAttnBlockState();
-            throw Error("fused attention block: a hand-off wait timed out (code " + std::to_string(code) +
-                        ": 2 qkv->attention, 3 attention->wo, 4 qkv phase; not all workgroups resident?)");
+            throw Error("fused layer block: a hand-off wait timed out (code " + std::to_string(code) +
+                        ": 2 qkv->attention, 3 attention->wo, 4 qkv phase, 13 w13->w2, 14 w13 phase; not all "
+                        "workgroups resident?)");
         }
         if (flag && *hErr_ != 0)
             throw Error("tensor-parallel collective timed out: a peer rank did not arrive within 2 s (worker lost?)");
@@ -960,6 +974,58 @@ class HipEngineImpl : public HipEngine {
         blockOn_ = true;
     }
 
+    // The fused FFN block of a single decode row (kernels.h FfnBlockArgs): w13 GEMV (SwiGLU -> Q80
+    // hidden, write-through) + w2 GEMV in one launch. Layer l, residual input dX_[cur] + dY_.
+    hipk::FfnBlockArgs ffnBlockArgs(const DevLayer &L, u32 l, int cur) const {
+        const ShardPlan &p = plan_;
+        const bool tp = fusedTp(false);
+        hipk::FfnBlockArgs b;
+        b.w13 = gemvArgs(L.w13, 0, 1, hipk::EPI_ACT_Q80, dX_[cur], h_.dim, dY_, dX_[cur ^ 1], L.rmsFfn, dH_, p.hidden0,
+                         nullptr, nullptr, nullptr, dHQ_, dHS_, false);
+        b.w13.passes *= ffnW13PassMul_;
+        b.w2 = gemvArgs(L.w2, 0, 1, tp ? hipk::EPI_STORE_TP : hipk::EPI_STORE, nullptr, p.hidden0, nullptr, nullptr,
+                        nullptr, dY_, h_.dim, nullptr, dHQ_, dHS_, nullptr, nullptr, tp);
+        b.layer = (int)l;
+        b.nLayers = (int)h_.nLayers;
+        b.epoch = dEpoch_;
+        b.cnt = dBlockCnt_ + kFfnCntOff;
+        b.flag = dBlockCnt_ + kFfnCntOff + 64;
+        b.error = dBlockErr_;
+        b.ringEarly = ffnRingEarly_;
+        return b;
+    }
+
+    // Decide once whether decode rows run the fused FFN block: Q40 weights with the Q80 hidden
+    // hand-off, a compiled instance for the (w13, w2) lane counts, and the whole grid co-resident
+    // (shared with the other ranks on this GPU); w13's passes are doubled (fewer, longer
+    // workgroups) until it fits. DL_FFN_BLOCK=1 enables it (default: the two launches); DL_FFN_RING_EARLY=1 issues
+    // w2's weight ring at entry instead of after the w13 phase; DL_FFN_W13_PASSES sets w13's
+    // passes multiplier.
+    void setupFfnBlock() {
+        const char *e = std::getenv("DL_FFN_BLOCK");  // opt-in: measured slower so far (profiles/r3_attn_block.md)
+        if (!(e && *e == '1') || !q40_ || plan_.hidden0 / 32 < 192) return;
+        const char *re = std::getenv("DL_FFN_RING_EARLY");
+        ffnRingEarly_ = re && *re == '1' ? 1 : 0;
+        const char *pm = std::getenv("DL_FFN_W13_PASSES");
+        const int share = comm_ ? std::max(1, comm_->ranksOnDevice()) : 1;
+        for (int mul = pm && *pm ? std::max(1, std::atoi(pm)) : 1; mul <= 8; mul *= 2) {
+            ffnW13PassMul_ = mul;
+            const hipk::FfnBlockArgs b = ffnBlockArgs(layers_[0], 0, 0);
+            if (!hipk::ffnBlockPlan(b, fusedTp(false)).fn) break;
+            const hipk::GemvResidency r = hipk::ffnBlockResidency(b, fusedTp(false));
+            if (r.maxResident > 0 && r.grid <= r.maxResident / share) {
+                ffnOn_ = true;
+                return;
+            }
+            if (pm && *pm) {
+                std::fprintf(stderr, "ℹ️  fused FFN block off: grid %d > %d co-resident workgroups per rank\n", r.grid,
+                             r.maxResident / share);
+                break;
+            }
+        }
+        ffnW13PassMul_ = 1;
+    }
+
     // A fused-block wait gave up (a workgroup of the launch never arrived): reset the monotonic
     // counters and the epoch so the engine stays usable, then raise.
     void resetAttnBlockState() {
@@ -1006,8 +1072,9 @@ class HipEngineImpl : public HipEngine {
     void gemmBatched(const DevMat &m, int n, int epi, const float *in, int ldIn, const float *add, float *xNext,
                      const float *normW, const _Float16 *xh, float *out, int ldOut, _Float16 *outH,
                      const DevLayer *L, const ResFuse *rf = nullptr, bool ssIn = false) {
-        for (int c0 = 0; c0 < n; c0 += kGemmMaxTokens) {
-            const int bc = std::min(kGemmMaxTokens, n - c0);
+        const int chunk = q40_ ? kGemmMaxTokens : hipk::kGemmF32MaxTokens;  // tokens per weight pass
+        for (int c0 = 0; c0 < n; c0 += chunk) {
+            const int bc = std::min(chunk, n - c0);
             hipk::GemmArgs g;
             hipk::GemvArgs &a = g.e;
             a.qs = m.qs;
@@ -1090,10 +1157,11 @@ class HipEngineImpl : public HipEngine {
         const bool bat = batchedPath(n);  // MFMA GEMMs on f16 activations instead of GEMVs
         const bool fz = bat && fuseNorm();  // residual + norm carried by the GEMM epilogues
         const bool blk = blockOn_ && n == 1 && !bat;  // fused attention block per layer
+        const bool fb = ffnOn_ && n == 1 && !bat;     // fused FFN block per layer
         {
             ProfScope ps(this, "embedding");
-            // the epoch counts the forwards that run the fused block (its counters' targets)
-            hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_, blk ? dEpoch_ : nullptr);
+            // the epoch counts the forwards that run a fused block (its counters' targets)
+            hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_, blk || fb ? dEpoch_ : nullptr);
         }
         for (u32 l = 0; l < h_.nLayers; l++) {
             DevLayer &L = layers_[l];
@@ -1101,7 +1169,7 @@ class HipEngineImpl : public HipEngine {
             if (blk) {
                 ProfScope ps(this, "attn_block");
                 hipk::AttnBlockArgs ba = attnBlockArgs(L, l, cur);
-                if ((int)l == traceLayer_) ba.trace = traceBuf_;
+                if ((int)l == traceLayer_ && !traceFfn_) ba.trace = traceBuf_;
                 hipk::launchAttnBlock(ba, fusedTp(false), stream_);
                 if (hasDelta) cur ^= 1;
             } else {
@@ -1156,6 +1224,13 @@ class HipEngineImpl : public HipEngine {
             // Q80 hand-off of h needs one workgroup per 32 hidden units; for skinny TP shards the
             // w13 epilogue emits f32 and w2 quantizes in its prologue instead.
             const bool hQ80 = q40_ && p.hidden0 / 32 >= 192;
+            if (fb) {
+                ProfScope ps(this, "ffn_block");
+                hipk::FfnBlockArgs fa = ffnBlockArgs(L, l, cur);
+                if ((int)l == traceLayer_ && traceFfn_) fa.trace = traceBuf_;
+                hipk::launchFfnBlock(fa, fusedTp(false), stream_);
+                cur ^= 1;
+            } else {
             {
                 ProfScope ps(this, "gemv_w13");
                 if (fz)
@@ -1185,6 +1260,7 @@ class HipEngineImpl : public HipEngine {
                 else
                     gemv(L.w2, n, hipk::PRO_RESNORM, hipk::EPI_STORE, dH_, p.hidden0, nullptr, nullptr, nullptr, dY_,
                          dim, nullptr, nullptr, nullptr, nullptr, nullptr, fusedTp(bat));
+            }
             }
             if (!fusedTp(bat)) allReduce(dY_, (size_t)n * dim);
         }
@@ -1274,10 +1350,16 @@ class HipEngineImpl : public HipEngine {
     static constexpr int kMaxKvGroups = 64;
     // counters: [64 groups x 64 words] qkv arrivals, [64] attention arrivals, [8 x 64] ready flags
     // + [64] qkv arrivals, [8 x 64] qkv-done flags (attn_block_inst.h carves them after attnFlag)
-    static constexpr int kBlockCntWords = kMaxKvGroups * 64 + 64 + 8 * 64 + 64 + 8 * 64 + 64;
+    // attention block: qkv counters per KV group | attention counter | 8 flags | qkv counter | 8 flags |
+    // spare line; FFN block: w13 counter | 8 flags (every word on its own 256-B line)
+    static constexpr int kFfnCntOff = kMaxKvGroups * 64 + 64 + 8 * 64 + 64 + 8 * 64 + 64;
+    static constexpr int kBlockCntWords = kFfnCntOff + 64 + 8 * 64;
     unsigned *dEpoch_ = nullptr, *dBlockCnt_ = nullptr, *dBlockExpect_ = nullptr;
     int *dBlockErr_ = nullptr;
     bool blockOn_ = false;  // decode rows run the fused attention block (setupAttnBlock)
+    bool ffnOn_ = false;    // decode rows run the fused FFN block (setupFfnBlock)
+    int ffnRingEarly_ = 0, ffnW13PassMul_ = 1;
+    bool traceFfn_ = false;  // traceAttnBlock(layer, ffn=true) traces the FFN block instead
     int traceLayer_ = -1;   // traceAttnBlock: the layer whose block launch is traced
     unsigned long long *traceBuf_ = nullptr;
     int blockGrid_ = 0;

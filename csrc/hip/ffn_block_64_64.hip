@@ -1,0 +1,8 @@
+// Fused FFN block instance: w13 lanes 64, w2 lanes 64 (ffn_block_inst.h).
+#include "ffn_block_inst.h"
+
+namespace dl {
+namespace hipk {
+const void *ffnBlockFn_64_64(bool tp) { return ffnBlockFnT<64, 64>(tp); }
+}  // namespace hipk
+}  // namespace dl

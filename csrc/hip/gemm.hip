@@ -70,7 +70,7 @@ int gemmSplits(int rows, int n, int M) {
     return S;
 }
 
-int gemmTokenPad(int M) { return M <= 16 ? 16 : M <= 32 ? 32 : 64; }
+int gemmTokenPad(int M) { return M <= 16 ? 16 : M <= 32 ? 32 : M <= 64 ? 64 : 128; }
 
 size_t gemmPartFloats(int rows, int n, int maxTokens) {
     const int tiles = (rows + kGemmRows - 1) / kGemmRows, S = gemmSplits(rows, n, maxTokens);
@@ -85,7 +85,8 @@ __host__ __device__ static constexpr int gemmStageBytes(int MT) { return kStW + 
 #define DL_GEMM_STAGES 2  // 3 stages (2 WGs/CU) measured slower: batch-32 8.1k vs 8.8k tok/s
 #endif
 static constexpr int kGemmStages = DL_GEMM_STAGES;  // stage buffers (kGemmStages-1 chunks in flight)
-static size_t gemmLds(int MT, int stages) { return stages * (size_t)gemmStageBytes(MT) + 16 + 320 * 4; }  // + flag, row scales
+static constexpr int kGemmScaleFloats = 128 + 256;  // gemmFinish: per-token RMS scales + per-thread slices
+static size_t gemmLds(int MT, int stages) { return stages * (size_t)gemmStageBytes(MT) + 16 + kGemmScaleFloats * 4; }  // + flag
 
 // 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d via the 0x6400 | q magic (1024 + q)
 __device__ __forceinline__ half8 dequantQ40x8(u32x2 wv, int nibHi, uint32_t d16) {
@@ -193,11 +194,11 @@ __device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc
         }
     }
     // consumer of a fused residual + norm: per-token RMS scale from the producer's tile partials
-    float *rsL = reinterpret_cast<float *>(flag + 4);  // [64]
+    float *rsL = reinterpret_cast<float *>(flag + 4);  // [128]
     if (ga.ssIn) {
         // TPT threads per token each sum a strided slice of the tile partials (independent loads
         // in flight), then one thread per token adds the TPT slices in order (deterministic)
-        float *slL = rsL + 64;  // [256]
+        float *slL = rsL + 128;  // [256]
         constexpr int TPT = kThreads / MP;
         const int t = tid / TPT, q = tid % TPT;
         float ssum = 0.f;
@@ -373,6 +374,9 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     gemmFinish<MT, EPI>(ga, acc, smem, flag, blockIdx.x, gridDim.x);
 }
 
+// The 128-token tile (prefill chunks): one stage buffer (73 KB), two workgroups per CU; each
+// weight chunk feeds 8 MFMA token tiles, so a 128-token slice streams the weights once instead of
+// twice.
 static int gemmStages4() {  // stage buffers of the 64-token tile (DL_GEMM_STG4, read once)
     static const int v = [] {
         const char *e = std::getenv("DL_GEMM_STG4");
@@ -402,7 +406,7 @@ static int gemmStages1() {  // stage buffers of the 16-token tile (DL_GEMM_STG1 
 void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
     const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
     const int MT = gemmTokenPad(ga.M) / 16;
-    const int stg = MT == 4 ? gemmStages4() : MT == 2 ? gemmStages2() : gemmStages1();
+    const int stg = MT == 8 ? 1 : MT == 4 ? gemmStages4() : MT == 2 ? gemmStages2() : gemmStages1();
     const dim3 grid(tiles, ga.splits);
     const size_t lds = gemmLds(MT, stg);
 #define DL_GEMM_CASE(M_, E, G)                                                                    \
@@ -414,7 +418,7 @@ void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
 #define DL_GEMM_CASES(M_, G)                                                                      \
     DL_GEMM_CASE(M_, EPI_STORE, G) DL_GEMM_CASE(M_, EPI_ACT, G) DL_GEMM_CASE(M_, EPI_ACT_Q80, G)  \
     DL_GEMM_CASE(M_, EPI_QKV, G) DL_GEMM_CASE(M_, EPI_ACT_F16, G) DL_GEMM_CASE(M_, EPI_RES, G)
-    DL_GEMM_CASES(1, kGemmStages) DL_GEMM_CASES(1, 3) DL_GEMM_CASES(1, 4) DL_GEMM_CASES(2, kGemmStages) DL_GEMM_CASES(2, 1) DL_GEMM_CASES(2, 3) DL_GEMM_CASES(4, 1) DL_GEMM_CASES(4, 2)
+    DL_GEMM_CASES(1, kGemmStages) DL_GEMM_CASES(1, 3) DL_GEMM_CASES(1, 4) DL_GEMM_CASES(2, kGemmStages) DL_GEMM_CASES(2, 1) DL_GEMM_CASES(2, 3) DL_GEMM_CASES(4, 1) DL_GEMM_CASES(4, 2) DL_GEMM_CASES(8, 1)
 #undef DL_GEMM_CASES
 #undef DL_GEMM_CASE
 }
@@ -476,9 +480,10 @@ __global__ __launch_bounds__(kThreads) void gemmF32Kernel(GemmArgs ga) {
 
 void launchGemmF32(const GemmArgs &ga, int epi, hipStream_t s) {
     const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
+    if (ga.M > kGemmF32MaxTokens) throw Error("launchGemmF32: more than 64 tokens per launch");
     const int MT = gemmTokenPad(ga.M) / 16;
     const dim3 grid(tiles, ga.splits);
-    const size_t lds = (size_t)MT * 16 * kGemmRows * 4 + 16 + 320 * 4;  // + flag, row scales
+    const size_t lds = (size_t)MT * 16 * kGemmRows * 4 + 16 + kGemmScaleFloats * 4;  // + flag, row scales
 #define DL_GEMMF_CASE(M_, E)                                                              \
     if (MT == M_ && epi == E) {                                                           \
         if (lds > 65536) allowLds((const void *)gemmF32Kernel<M_, E>, lds);               \

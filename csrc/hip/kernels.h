@@ -169,13 +169,14 @@ void launchGemmF32(const GemmArgs &a, int epi, hipStream_t s);
 struct GemmPlan {
     int rt = 1, tiles = 0, splits = 1;
 };
-constexpr int kGemmMaxTokens = 64;  // tokens per GEMM launch (16, 32 or 64 padded)
+constexpr int kGemmMaxTokens = 128;    // tokens per Q40 GEMM launch (16, 32, 64 or 128 padded)
+constexpr int kGemmF32MaxTokens = 64;  // tokens per F32 GEMM launch (16, 32 or 64 padded)
 GemmPlan gemmPlan(int rows, int n, int M);
 bool gemmSupported(int n);  // input width a multiple of 32 (whole Q40 blocks)
 int gemmSplits(int rows, int n, int M);
 // split-K partial floats for any launch of up to maxTokens tokens on this matrix
 size_t gemmPartFloats(int rows, int n, int maxTokens);
-// token rows one GEMM launch of M (1..64) tokens reads from its f16 activation operand (16/32/64)
+// token rows one GEMM launch of M (1..128) tokens reads from its f16 activation operand (16/32/64/128)
 int gemmTokenPad(int M);
 // Residual add + RMS norm (normW may be null: no norm) of M rows -> f16:
 // in/addIn/xNext [M][ldIn] f32 -> out [M][n] f16 (xNext = in + addIn when set).
@@ -244,6 +245,35 @@ AttnBlockPlan attnBlockPlan(const AttnBlockArgs &a, bool tp);
 void attnBlockExpect(const GemvArgs &qkv, int nKv, unsigned *out);
 GemvResidency attnBlockResidency(const AttnBlockArgs &a, bool tp);
 void launchAttnBlock(const AttnBlockArgs &a, bool tp, hipStream_t s);
+
+// Fused FFN block of one decode row (B = 1, Q40, Q80 hidden hand-off): the w13 GEMV (residual + RMS
+// norm prologue, SwiGLU -> Q80 epilogue stored write-through) and the w2 GEMV in ONE launch, roles
+//   [0, g13) w13 rows | [g13, g13 + g2) w2 rows.
+// The last w13 workgroup of a step raises per-XCD "w13 done" flags (monotonic arrival counter, the
+// step numbering of AttnBlockArgs); w2 workgroups issue their weight ring after that flag (or at
+// entry: ringEarly), then read the hidden vector write-through. Removes one kernel boundary and the
+// w2 start-up latency per layer. Requires the whole grid co-resident (ffnBlockResidency); every
+// wait is bounded and raises `error` (codes 13 data, 14 ring start).
+struct FfnBlockArgs {
+    GemvArgs w13;                     // PRO_RESNORM + EPI_ACT_Q80 (oq / os = the w2 input)
+    GemvArgs w2;                      // PRO_GLOBAL + EPI_STORE (or EPI_STORE_TP: w2.tp set)
+    int layer = 0, nLayers = 1;
+    const unsigned *epoch = nullptr;  // per-forward epoch, as AttnBlockArgs
+    unsigned *cnt = nullptr;          // [1] monotonic arrivals of w13 workgroups (own 256-B line)
+    unsigned *flag = nullptr;         // [8 * 64] per-XCD w13-done flags
+    int *error = nullptr;
+    long long timeoutTicks = 200LL * 1000 * 1000;
+    int ringEarly = 0;
+    unsigned long long *trace = nullptr;  // GemvArgs::trace layout, w13 workgroups then w2
+};
+struct FfnBlockPlan {
+    const void *fn = nullptr;
+    int g13 = 0, g2 = 0;
+    size_t lds = 0;
+};
+FfnBlockPlan ffnBlockPlan(const FfnBlockArgs &a, bool tp);
+GemvResidency ffnBlockResidency(const FfnBlockArgs &a, bool tp);
+void launchFfnBlock(const FfnBlockArgs &a, bool tp, hipStream_t s);
 // Prefill rows on MFMA (bf16 caches): blocks of attnPrefillRowsPerBlock(kvMul) consecutive rows
 // must share one slot (positions arbitrary, causal per row); counters >= blocks x KV heads.
 void launchAttentionPrefill(const AttnArgs &a, int nRows, hipStream_t s);

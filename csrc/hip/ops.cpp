@@ -168,7 +168,7 @@ std::vector<float> gemvQ40Q80In(const std::vector<uint8_t> &blocks, int rows, in
 
 std::vector<float> gemmQ40(const std::vector<uint8_t> &blocks, int rows, int n, const std::vector<float> &in,
                            const std::vector<float> &residual, const std::vector<float> &normW, float eps, int M) {
-    DL_CHECK(M >= 1 && M <= 64, "gemm tokens must be 1..64");
+    DL_CHECK(M >= 1 && M <= 256, "gemm tokens must be 1..256");
     DL_CHECK(in.size() == (size_t)M * n, "gemm input size");
     DL_CHECK(hipk::gemmSupported(n), "gemm input width must be a multiple of 32");
     checkRows(residual, (size_t)M * n, "residual");
@@ -190,7 +190,7 @@ std::vector<float> gemmQ40(const std::vector<uint8_t> &blocks, int rows, int n, 
     const size_t part = hipk::gemmPartFloats(rows, n, M);
     float *partBuf = part ? sc.alloc<float>(part) : nullptr;
     int *counters = sc.alloc<int>((size_t)(rows + 63) / 64 + 1);
-    // one launch per <= 32 tokens (the engine's chunking)
+    // one launch per <= 128 tokens (the engine's chunking)
     for (int c0 = 0; c0 < M; c0 += hipk::kGemmMaxTokens) {
         const int bc = std::min(hipk::kGemmMaxTokens, M - c0);
         hipk::GemmArgs g;
@@ -226,7 +226,7 @@ std::vector<float> gemmF32(const std::vector<float> &w, int rows, int n, const s
     nq.ldIn = n;
     nq.normW = sc.upload(normW);
     nq.eps = eps;
-    const int rowsPad = (M + hipk::kGemmMaxTokens - 1) / hipk::kGemmMaxTokens * hipk::kGemmMaxTokens;
+    const int rowsPad = (M + hipk::kGemmF32MaxTokens - 1) / hipk::kGemmF32MaxTokens * hipk::kGemmF32MaxTokens;
     _Float16 *xh = sc.alloc<_Float16>((size_t)rowsPad * n);
     hipk::launchNormF16(nq, xh, M, sc.s);
     const float *wd = sc.upload(w);
@@ -234,8 +234,8 @@ std::vector<float> gemmF32(const std::vector<float> &w, int rows, int n, const s
     const size_t part = hipk::gemmPartFloats(rows, n, M);
     float *partBuf = part ? sc.alloc<float>(part) : nullptr;
     int *counters = sc.alloc<int>((size_t)(rows + 63) / 64 + 1);
-    for (int c0 = 0; c0 < M; c0 += hipk::kGemmMaxTokens) {
-        const int bc = std::min(hipk::kGemmMaxTokens, M - c0);
+    for (int c0 = 0; c0 < M; c0 += hipk::kGemmF32MaxTokens) {
+        const int bc = std::min(hipk::kGemmF32MaxTokens, M - c0);
         hipk::GemmArgs g;
         g.e.wf = wd;
         g.e.rows = rows;

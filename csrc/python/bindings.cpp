@@ -754,12 +754,13 @@ PYBIND11_MODULE(_C, m) {
         .def_property_readonly("device_bytes", [](const PyHipEngine &e) { return e.engine->deviceBytes(); })
         .def_property_readonly("tp_fused", [](const PyHipEngine &e) { return e.engine->tpFused(); })
         .def_property_readonly("attn_block", [](const PyHipEngine &e) { return e.engine->attnBlock(); })
+        .def_property_readonly("ffn_block", [](const PyHipEngine &e) { return e.engine->ffnBlock(); })
         .def("trace_attn_block",
-             [](PyHipEngine &e, int token, int pos, int slot, int layer) {
+             [](PyHipEngine &e, int token, int pos, int slot, int layer, bool ffn) {
                  py::gil_scoped_release rel;
-                 return e.engine->traceAttnBlock(token, pos, slot, layer);
+                 return e.engine->traceAttnBlock(token, pos, slot, layer, ffn);
              },
-             py::arg("token"), py::arg("pos"), py::arg("slot") = 0, py::arg("layer") = 1)
+             py::arg("token"), py::arg("pos"), py::arg("slot") = 0, py::arg("layer") = 1, py::arg("ffn") = false)
         .def_property_readonly("fused_grid_max", [](const PyHipEngine &e) { return e.engine->fusedGridMax(); })
         .def_property_readonly("load_stats",
                                [](const PyHipEngine &e) {

@@ -314,3 +314,30 @@ def test_attn_block_matches_separate_kernels(C, assets, medium, monkeypatch, kv_
         _, ca = ref.decode_greedy(24, [int(a[-1].argmax())], [9], [0])
         _, cb = got.decode_greedy(24, [int(b[-1].argmax())], [9], [0])
         assert list(ca) == list(cb)
+
+
+@pytest.mark.parametrize("ring_early", ["0", "1"])
+def test_ffn_block_matches_separate_kernels(C, medium, monkeypatch, ring_early):
+    """Single decode rows run the fused FFN block (w13 GEMV with the SwiGLU -> Q80 hidden stored
+    write-through + the w2 GEMV as one launch): bitwise the same logits as the two separate
+    launches (same kernels, same reduction order), over many forwards and graph replays (monotonic
+    counters), with and without the attention block, w2's weight ring issued at entry or after the
+    w13 phase."""
+    monkeypatch.setenv("DL_FFN_RING_EARLY", ring_early)
+    for attn in ("0", "1"):
+        monkeypatch.setenv("DL_ATTN_BLOCK", attn)
+        monkeypatch.setenv("DL_FFN_BLOCK", "0")
+        ref = C.HipEngine(medium, "q80", kv_bf16=True, max_batch=8)
+        monkeypatch.setenv("DL_FFN_BLOCK", "1")
+        got = C.HipEngine(medium, "q80", kv_bf16=True, max_batch=8)
+        assert got.ffn_block and not ref.ffn_block and got.attn_block == (attn == "1")
+        toks = [3, 17, 101, 7, 250, 9]
+        a, b = _seq(ref, toks), _seq(got, toks)
+        assert np.array_equal(a, b)
+        ref.forward([5, 6, 7], [6, 7, 8], [0, 0, 0])  # batched forward between: the epoch must not advance
+        got.forward([5, 6, 7], [6, 7, 8], [0, 0, 0])
+        _, ca = ref.decode_greedy(24, [int(a[-1].argmax())], [9], [0])
+        _, cb = got.decode_greedy(24, [int(b[-1].argmax())], [9], [0])
+        assert list(ca) == list(cb)
+        tr = got.trace_attn_block(7, 40, 0, 1, ffn=True)
+        assert tr[0] > 0 and tr[2] > 0 and len(tr) == 3 + 8 * (tr[0] + tr[2])

@@ -67,7 +67,7 @@ def test_gemv_q40_on_q80_activations(ops, B):
     assert rel(out, x @ w.T) < 0.12
 
 
-@pytest.mark.parametrize("M", [2, 7, 32, 40, 64])
+@pytest.mark.parametrize("M", [2, 7, 32, 40, 64, 100, 128, 200])
 def test_gemm_q40_mfma(ops, M):
     rows, n = 768, 2048
     w = make_w(rows, n, 7)
