@@ -1,0 +1,266 @@
+// Decode attention on MFMA for bf16 KV caches (separate-kernel decode rows: serving batches, long
+// contexts; reference: the per-row attention of src/nn/nn-cpu-ops.cpp:749-784 / :1135-1161).
+//
+// The VALU kernel (attnTask) spends 16 lanes and a cross-lane reduction per key and a serial
+// online-softmax chain per 16-lane group: at long context it is latency-bound (21.9 us at pos 8000,
+// profiles/r1_attention.md) while the KV stream alone takes ~6 us. Here one workgroup owns one
+// (row, KV head, key chunk) and its 4 waves split the chunk's 32-key tiles (wave w: tiles w, w+4,
+// ...). Per tile a wave
+//   * copies K and V (32 keys x HS bf16 each) HBM -> its own LDS buffers with global_load_lds
+//     (double-buffered, the next tile in flight; no barrier: only the issuing wave reads them),
+//   * S^T = K . Q^T on v_mfma_f32_16x16x32_bf16 (A = 16 keys x 32 dims read row-wise from LDS,
+//     B = the row's kvMul query heads as the MFMA columns, pre-scaled, in registers),
+//   * one online-softmax step per column over the 32 keys (max / sum over the lane's 8 scores
+//     and 2 cross-lane shuffles, instead of per key),
+//   * O^T += V^T . P^T (B = P^T straight from the S^T accumulators; A = V^T read from the
+//     row-major V tile with ds_read_b64_tr_b16, the hardware transpose read: no transposed cache).
+// The LDS tile image is the 256-B-row layout (b) of cdna_hip_programming.md T10 (chunk ch of row r
+// at 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3)))), written by the DMA as a permutation of each
+// 1-KB wave-instruction image. The 4 waves' (max, sum, O) merge in LDS; chunks of one head group
+// combine through attnFinish (fence-free last arriver, decode_dev.h) like the VALU kernel, with
+// the same split plan (attnSplit), so both kernels share the engine's partial buffers.
+#include "decode_dev.h"
+
+#include <cstdlib>
+
+namespace dl {
+namespace hipk {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+static constexpr int kAmThreads = 256, kAmWaves = 4, kAmTile = 32, kAmHS = 128;
+static constexpr int kAmTileBytes = kAmTile * kAmHS * 2;     // one K or V tile: 8 KB
+static constexpr int kAmWaveBytes = 2 * 2 * kAmTileBytes;    // double-buffered K + V per wave
+static constexpr size_t kAmLds = (size_t)kAmWaves * kAmWaveBytes + 64;
+
+__device__ __forceinline__ int amSwz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+// TR: V^T fragments by the hardware transpose read (default); false: 8 scalar 16-bit LDS reads per
+// fragment (DL_ATTN_TR=0, a cross-check of the transposed-read addressing).
+template <int KM, bool TR>
+__global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
+    constexpr int HS = kAmHS, DS = HS / 32, NT = HS / 16;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int g = blockIdx.x, c = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, col = lane & 15, h = lane >> 4;
+    const int pos = a.pos[b], sl = a.slot[b], len = pos + 1;
+    int nSplit, ch;
+    attnSplit(len, a.splitGrid, nSplit, ch);
+    if (c >= nSplit) return;
+    const int t0 = c * ch, t1 = min(t0 + ch, len);
+    const int nTiles = (t1 - t0 + kAmTile - 1) / kAmTile;
+
+    // this lane's column: query head g * KM + col (columns >= KM are zero and discarded)
+    const float scale = 1.0f / sqrtf((float)HS);
+    bf16x8 qf[DS];
+#pragma unroll
+    for (int s = 0; s < DS; s++) {
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (col < KM) {
+            const float *qp = a.q + (size_t)b * a.ldq + (size_t)(g * KM + col) * HS + 32 * s + 8 * h;
+            const float4 x0 = ld4(qp), x1 = ld4(qp + 4);
+            v[0] = x0.x * scale; v[1] = x0.y * scale; v[2] = x0.z * scale; v[3] = x0.w * scale;
+            v[4] = x1.x * scale; v[5] = x1.y * scale; v[6] = x1.z * scale; v[7] = x1.w * scale;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) qf[s][j] = (__bf16)v[j];
+    }
+
+    char *wbuf = smem + wave * kAmWaveBytes;  // [2 buffers][K tile | V tile]
+    const uint16_t *kc = reinterpret_cast<const uint16_t *>(a.kcache);
+    const uint16_t *vc = reinterpret_cast<const uint16_t *>(a.vcache);
+    const size_t kvBase = (size_t)g * HS;
+    // DMA of tile i (keys t0 + 32 i ...) into buffer bf: 8 + 8 wave-instructions of 4 rows x 256 B
+    auto issue = [&](int i, int bf) {
+        char *kb = wbuf + bf * 2 * kAmTileBytes, *vb = kb + kAmTileBytes;
+#pragma unroll
+        for (int j = 0; j < kAmTile / 4; j++) {
+            const int r = 4 * j + (lane >> 4), p = lane & 15;
+            const int key = min(t0 + kAmTile * i + r, t1 - 1);  // past the chunk: masked below
+            const size_t off = kvBase + kvRow(a.kvMap, a.seqLen, sl, key) * a.kv0 + (size_t)(p ^ amSwz(r)) * 8;
+            __builtin_amdgcn_global_load_lds(const_cast<uint16_t *>(kc + off),
+                                             reinterpret_cast<__attribute__((address_space(3))) void *>(
+                                                 reinterpret_cast<uintptr_t>(kb + j * 1024)), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(const_cast<uint16_t *>(vc + off),
+                                             reinterpret_cast<__attribute__((address_space(3))) void *>(
+                                                 reinterpret_cast<uintptr_t>(vb + j * 1024)), 16, 0, 0);
+        }
+    };
+
+    f32x4 o[NT];
+#pragma unroll
+    for (int n = 0; n < NT; n++) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, lsum = 0.f;
+    // transposed-read address pieces of this lane (lane 4q + p of its 16-lane group h)
+    const int tq = col >> 2, tp = col & 3;
+    int k = 0;
+    if (wave < nTiles) issue(wave, 0);
+    if (wave + kAmWaves < nTiles) issue(wave + kAmWaves, 1);
+    for (int i = wave; i < nTiles; i += kAmWaves, k++) {
+        if (i + kAmWaves < nTiles)
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile i landed, tile i + 4 in flight
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const char *kb = wbuf + (k & 1) * 2 * kAmTileBytes, *vb = kb + kAmTileBytes;
+        const int tb = t0 + kAmTile * i;
+        f32x4 st[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            st[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const int r = 16 * u + col;
+#pragma unroll
+            for (int s = 0; s < DS; s++) {
+                const bf16x8 kf = *reinterpret_cast<const bf16x8 *>(kb + r * 256 + 16 * ((4 * s + h) ^ amSwz(r)));
+                st[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], st[u], 0, 0, 0);
+            }
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                if (tb + 16 * u + 4 * h + e >= t1) st[u][e] = -INFINITY;
+                mx = fmaxf(mx, st[u][e]);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float mn = fmaxf(m, mx);
+        const float corr = m == -INFINITY ? 0.f : __expf(m - mn);
+        bf16x8 pf;
+        float ps = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const float p = st[u][e] == -INFINITY ? 0.f : __expf(st[u][e] - mn);
+                ps += p;
+                pf[4 * u + e] = (__bf16)p;
+            }
+        lsum = lsum * corr + ps;
+        m = mn;
+#pragma unroll
+        for (int n = 0; n < NT; n++) {
+            // A = V^T (16 dims x 32 keys): elements 0-3 keys 4h..4h+3, 4-7 keys 16+4h.., the
+            // order of P^T's registers; lane 4q+p of group h addresses row r0 + q, dims 16n+4p..
+            s16x4 vv[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                if constexpr (TR) {
+                    const int r = 16 * u + 4 * h + tq;
+                    const char *ad = vb + r * 256 + 16 * ((2 * n + (tp >> 1)) ^ amSwz(r)) + 8 * (tp & 1);
+                    vv[u] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        reinterpret_cast<__attribute__((address_space(3))) s16x4 *>(reinterpret_cast<uintptr_t>(ad)));
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        const int r = 16 * u + 4 * h + e;
+                        vv[u][e] = *reinterpret_cast<const short *>(vb + r * 256 + 16 * ((2 * n + (col >> 3)) ^ amSwz(r)) +
+                                                                    2 * (col & 7));
+                    }
+                }
+            }
+            bf16x8 vf;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                vf[e] = __builtin_bit_cast(__bf16, vv[0][e]);
+                vf[4 + e] = __builtin_bit_cast(__bf16, vv[1][e]);
+            }
+            o[n] *= corr;
+            o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[n], 0, 0, 0);
+        }
+        // this buffer's reads retire before the DMA of tile i + 8 overwrites it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (i + 2 * kAmWaves < nTiles) issue(i + 2 * kAmWaves, k & 1);
+    }
+    lsum += __shfl_xor(lsum, 16);
+    lsum += __shfl_xor(lsum, 32);
+
+    // merge the waves (LDS: the tile buffers are free once every wave is past its loop)
+    __syncthreads();
+    float *oW = reinterpret_cast<float *>(smem);  // [4 waves][KM][HS]
+    float *mW = oW + kAmWaves * KM * HS;          // [4][KM]
+    float *lW = mW + kAmWaves * KM;               // [4][KM]
+    float *redL = lW + kAmWaves * KM;             // [KM][HS]
+    float *mlL = redL + KM * HS;                  // [KM][2]
+    int *flagL = reinterpret_cast<int *>(mlL + 2 * KM);
+    float *scratch = reinterpret_cast<float *>(flagL + 4);  // attnFinish: 2 * KM * splitGrid
+    if (col < KM) {
+        if (h == 0) {
+            mW[wave * KM + col] = wave < nTiles ? m : -INFINITY;
+            lW[wave * KM + col] = wave < nTiles ? lsum : 0.f;
+        }
+#pragma unroll
+        for (int n = 0; n < NT; n++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) oW[(wave * KM + col) * HS + 16 * n + 4 * h + e] = o[n][e];
+    }
+    __syncthreads();
+    for (int i = tid; i < KM * HS; i += kAmThreads) {
+        const int hh = i / HS;
+        float M = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < kAmWaves; w++) M = fmaxf(M, mW[w * KM + hh]);
+        float acc = 0.f, Ls = 0.f;
+#pragma unroll
+        for (int w = 0; w < kAmWaves; w++) {
+            const float e = mW[w * KM + hh] == -INFINITY ? 0.f : __expf(mW[w * KM + hh] - M);
+            acc += e * oW[(w * KM + hh) * HS + (i % HS)];
+            Ls += e * lW[w * KM + hh];
+        }
+        redL[i] = acc;
+        if (i % HS == 0) {
+            mlL[hh * 2] = M;
+            mlL[hh * 2 + 1] = Ls;
+        }
+    }
+    __syncthreads();
+    attnFinish<KM, HS, kAmThreads>(a, b, g, c, nSplit, redL, mlL, flagL, scratch);
+}
+
+bool attnMfmaSupported(const AttnArgs &a) {
+    return a.kvBf16 && a.hs == kAmHS && (a.kvMul == 1 || a.kvMul == 2 || a.kvMul == 4 || a.kvMul == 8) &&
+           a.nHeads0 % a.kvMul == 0 && a.pfBlocks == 0;
+}
+
+// DL_ATTN_MFMA: 0 = the VALU kernel everywhere, 1 = this kernel for every supported launch,
+// default (-1) = this kernel when the cache is long enough for it to matter (seqLen >= 1024).
+static int attnMfmaMode() {
+    static const int v = [] {
+        const char *e = std::getenv("DL_ATTN_MFMA");
+        return e ? std::atoi(e) : -1;
+    }();
+    return v;
+}
+
+bool attnUsesMfma(const AttnArgs &a) {
+    const int mode = attnMfmaMode();
+    if (mode == 0 || !attnMfmaSupported(a)) return false;
+    return mode == 1 || a.seqLen >= 1024;
+}
+
+static bool attnTrRead() {
+    static const bool v = [] {
+        const char *e = std::getenv("DL_ATTN_TR");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
+
+void launchAttentionMfma(const AttnArgs &a, int B, hipStream_t s) {
+    const dim3 grid(a.nHeads0 / a.kvMul, a.splitGrid, B);
+    if (2 * a.kvMul * a.splitGrid * 4 + 4096 > (int)kAmLds) throw Error("attention split grid too large");
+#define DL_AM_CASE(K, T)                                                                          \
+    if (a.kvMul == K && attnTrRead() == T) {                                                      \
+        allowLds((const void *)attnDecodeMfmaKernel<K, T>, kAmLds);                               \
+        hipLaunchKernelGGL((attnDecodeMfmaKernel<K, T>), grid, dim3(kAmThreads), kAmLds, s, a);   \
+        return;                                                                                   \
+    }
+    DL_AM_CASE(1, true) DL_AM_CASE(2, true) DL_AM_CASE(4, true) DL_AM_CASE(8, true)
+    DL_AM_CASE(1, false) DL_AM_CASE(2, false) DL_AM_CASE(4, false) DL_AM_CASE(8, false)
+#undef DL_AM_CASE
+    throw Error("launchAttentionMfma: unsupported kvMul");
+}
+
+}  // namespace hipk
+}  // namespace dl

@@ -270,7 +270,7 @@ __device__ __forceinline__ void qkvPairStore(const GemvArgs &a, int r0, float v0
         if (r0 < a.q0) {
             stF2<WT>(qRow + r0, o0, o1);
         } else {
-            const size_t off = ((size_t)sl * a.seqLen + p) * a.kv0 + (r0 - a.q0);
+            const size_t off = kvRow(a.kvMap, a.seqLen, sl, p) * a.kv0 + (r0 - a.q0);
             if (a.kvBf16) {
                 const uint32_t pk = (uint32_t)f32ToBf16(o0) | ((uint32_t)f32ToBf16(o1) << 16);
                 st32<WT>(reinterpret_cast<uint16_t *>(a.kcache) + off, pk);
@@ -279,7 +279,7 @@ __device__ __forceinline__ void qkvPairStore(const GemvArgs &a, int r0, float v0
             }
         }
     } else {
-        const size_t off = ((size_t)sl * a.seqLen + p) * a.kv0 + (r0 - a.q0 - a.kv0);
+        const size_t off = kvRow(a.kvMap, a.seqLen, sl, p) * a.kv0 + (r0 - a.q0 - a.kv0);
         if (a.kvBf16) {
             const uint32_t pk = (uint32_t)f32ToBf16(v0) | ((uint32_t)f32ToBf16(v1) << 16);
             st32<WT>(reinterpret_cast<uint16_t *>(a.vcache) + off, pk);
@@ -1170,7 +1170,7 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
 
     // SYNC: the first round's keys written by earlier forwards are loaded before the wait (their
     // latency overlaps the qkv workgroups); the current position's row after it, write-through
-    const size_t slotBase = (size_t)sl * a.seqLen;
+
     uint32_t kr[TU][RW], vr[TU][RW];
     // phase 0: every key (the current one write-through under SYNC); 1: all but the current one;
     // 2: only the current one
@@ -1180,7 +1180,7 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
             const int t = min(tb + u * NG, t1 - 1);  // clamped: no divergent loads
             const bool cur = SYNC && t == pos;
             if ((phase == 1 && cur) || (phase == 2 && !cur)) continue;
-            const size_t off = (slotBase + t) * a.kv0 + kvh * HS + l16 * DPL;
+            const size_t off = kvRow(a.kvMap, a.seqLen, sl, t) * a.kv0 + kvh * HS + l16 * DPL;
             const uint32_t *kp = reinterpret_cast<const uint32_t *>(
                 BF16 ? (const void *)(reinterpret_cast<const uint16_t *>(a.kcache) + off)
                      : (const void *)(reinterpret_cast<const float *>(a.kcache) + off));

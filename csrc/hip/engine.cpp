@@ -108,6 +108,82 @@ class HipEngineImpl : public HipEngine {
 
     LoadStats loadStats() const override { return load_; }
 
+    // ---------------------------------------------------------------- paged KV cache
+    // With cfg.kvPages > 0 each layer's K / V cache is a pool of kvPages pages of kvPageSize
+    // positions and a page table maps (slot, pos) to a pool row (kernels.h KvMap): a slot holds only
+    // the pages its sequence reached, so many slots can share HBM sized for the tokens actually in
+    // flight instead of nSlots x seqLen. Pages are mapped at setInputs for every position a forward
+    // (or a decode chain) writes and released when a slot restarts at position 0: the same
+    // deterministic rule on every tensor-parallel rank, so no page messages are exchanged.
+    size_t kvPoolRows() const {
+        return cfg_.kvPages ? (size_t)cfg_.kvPages * cfg_.kvPageSize : (size_t)cfg_.nSlots * h_.seqLen;
+    }
+    bool paged() const { return cfg_.kvPages > 0; }
+    int kvPagesFree() const override { return paged() ? (int)freePages_.size() : -1; }
+    int kvPageSize() const override { return paged() ? (int)cfg_.kvPageSize : 0; }
+    void setupPages() {
+        if (!paged()) return;
+        const u32 P = cfg_.kvPageSize;
+        DL_CHECK(P >= 32 && (P & (P - 1)) == 0, "--kv-page-size must be a power of two >= 32");
+        pageShift_ = 0;
+        while ((1u << pageShift_) < P) pageShift_++;
+        pagesPerSlot_ = (int)((h_.seqLen + P - 1) / P);
+        const size_t entries = (size_t)cfg_.nSlots * pagesPerSlot_;
+        hostTable_.assign(entries, -1);
+        slotPages_.assign(cfg_.nSlots, 0);
+        for (int pg = (int)cfg_.kvPages - 1; pg >= 0; pg--) freePages_.push_back(pg);
+        dKvTable_ = dalloc<int>(entries);
+        // unmapped entries read page 0 (valid memory, masked out): never a stray address
+        DL_HIP(hipMemsetAsync(dKvTable_, 0, entries * sizeof(int), stream_));
+        for (int i = 0; i < 2; i++) hTableStage_[i] = halloc<int>(entries);
+    }
+    hipk::KvMap kvMap() const {
+        hipk::KvMap m;
+        if (paged()) {
+            m.table = dKvTable_;
+            m.pageShift = pageShift_;
+            m.pagesPerSlot = pagesPerSlot_;
+        }
+        return m;
+    }
+    // Map the pages every row's positions [pos, pos + ahead] need; a row at position 0 starts a new
+    // sequence in its slot and releases the slot's old pages first. Uploads the table if it changed
+    // (stream-ordered before the forward that reads it).
+    void mapPages(int n, const int *positions, const int *slots, int ahead) {
+        if (!paged()) return;
+        bool dirty = false;
+        auto release = [&](int s) {
+            for (int i = 0; i < slotPages_[s]; i++) {
+                int &e = hostTable_[(size_t)s * pagesPerSlot_ + i];
+                freePages_.push_back(e);
+                e = -1;
+            }
+            if (slotPages_[s]) dirty = true;
+            slotPages_[s] = 0;
+        };
+        for (int b = 0; b < n; b++)
+            if (positions[b] == 0) release(slots[b]);
+        for (int b = 0; b < n; b++) {
+            const int s = slots[b];
+            const int need = std::min(pagesPerSlot_, ((positions[b] + ahead) >> pageShift_) + 1);
+            while (slotPages_[s] < need) {
+                if (freePages_.empty())
+                    throw Error("KV page pool exhausted: " + std::to_string(cfg_.kvPages) + " pages of " +
+                                std::to_string(cfg_.kvPageSize) + " positions are all mapped; raise --kv-pages " +
+                                "or lower the concurrent context");
+                hostTable_[(size_t)s * pagesPerSlot_ + slotPages_[s]++] = freePages_.back();
+                freePages_.pop_back();
+                dirty = true;
+            }
+        }
+        if (!dirty) return;
+        // a pinned copy per upload, alternating: the previous upload may still be reading the other
+        int *st = hTableStage_[tableFlip_ ^= 1];
+        if (inputsInFlight_) DL_HIP(hipStreamSynchronize(stream_));
+        for (size_t i = 0; i < hostTable_.size(); i++) st[i] = hostTable_[i] < 0 ? 0 : hostTable_[i];
+        DL_HIP(hipMemcpyAsync(dKvTable_, st, hostTable_.size() * sizeof(int), hipMemcpyHostToDevice, stream_));
+    }
+
     // Refuse a configuration whose weights + KV cache cannot be resident, with the numbers, before
     // allocating anything (KV is preallocated as nSlots x seqLen per layer).
     void checkFits() {
@@ -115,7 +191,7 @@ class HipEngineImpl : public HipEngine {
         DL_HIP(hipMemGetInfo(&freeB, &totalB));
         const ShardPlan &p = plan_;
         const double GB = 1e9;
-        const size_t kv = (size_t)h_.nLayers * 2 * cfg_.nSlots * h_.seqLen * p.kv0 * (kvBf16_ ? 2 : 4);
+        const size_t kv = (size_t)h_.nLayers * 2 * kvPoolRows() * p.kv0 * (kvBf16_ ? 2 : 4);
         size_t w = (size_t)h_.nLayers * (matStageBytes(p.q0 + 2 * p.kv0, h_.dim) + matStageBytes(h_.dim, p.q0) +
                                          matStageBytes(2 * p.hidden0, h_.dim) + matStageBytes(h_.dim, p.hidden0));
         w += matStageBytes(p.vocab0, h_.dim) + (size_t)h_.vocabSize * h_.dim * 4;
@@ -301,7 +377,7 @@ class HipEngineImpl : public HipEngine {
                              int *outTokens) override {
         DL_CHECK(nSeq >= 1 && (u32)nSeq <= cfg_.maxBatch, "nSeq");
         for (int b = 0; b < nSeq; b++) DL_CHECK((u32)(pos[b] + steps) <= h_.seqLen, "decode exceeds seqLen");
-        setInputs(nSeq, tokens, pos, slots);
+        setInputs(nSeq, tokens, pos, slots, nullptr, steps - 1);
         DL_HIP(hipMemsetAsync(dHist_, 0xff, sizeof(int) * (size_t)cfg_.maxBatch * h_.seqLen, stream_));
         hipEvent_t e0, e1;
         DL_HIP(hipEventCreate(&e0));
@@ -434,16 +510,20 @@ class HipEngineImpl : public HipEngine {
             DL_HIP(hipMemsetAsync(dXh_, 0, rowsH * h_.dim * 2, stream_));
             DL_HIP(hipMemsetAsync(dAttH_, 0, rowsH * p.q0 * 2, stream_));
             DL_HIP(hipMemsetAsync(dHh_, 0, rowsH * p.hidden0 * 2, stream_));
-            const int mt = std::min((int)MB, kGemmMaxTokens);
+            const int mt = (int)MB;
             size_t part = 0;
-            auto acc = [&](int rows, int n) { part = std::max(part, hipk::gemmPartFloats(rows, n, mt)); };
+            int cnt = 0;
+            auto acc = [&](int rows, int n) {
+                part = std::max(part, hipk::gemmPartFloats(rows, n, mt));
+                cnt = std::max(cnt, hipk::gemmCounterInts(rows, mt));
+            };
             acc(p.q0 + 2 * p.kv0, h_.dim);
             acc(h_.dim, p.q0);
             acc(2 * p.hidden0, h_.dim);
             acc(h_.dim, p.hidden0);
             acc(p.vocab0, h_.dim);
             if (part) dPart_ = dalloc<float>(part);
-            const int maxTiles = (std::max<int>({(int)(p.q0 + 2 * p.kv0), (int)h_.dim, (int)(2 * p.hidden0), (int)p.vocab0}) + 63) / 64;
+            const int maxTiles = cnt;
             dGemmCnt_ = dalloc<int>(maxTiles);
             // fused residual + norm hand-off between batched GEMMs (TP1): per 64-row tile of dim,
             // per token, the partial sum of squares
@@ -482,7 +562,8 @@ class HipEngineImpl : public HipEngine {
         dPartML_ = dalloc<float>((size_t)MB * p.nHeads0 * splitGrid_ * 2);
         dRope_ = dalloc<float2>((size_t)h_.seqLen * (p.headSize / 2));
         layers_.resize(h_.nLayers);
-        const size_t kvElems = (size_t)cfg_.nSlots * h_.seqLen * p.kv0;
+        const size_t kvElems = kvPoolRows() * p.kv0;
+        setupPages();
         for (auto &L : layers_) {
             if (kvBf16_) {
                 L.k = dalloc<uint16_t>(kvElems);
@@ -718,13 +799,15 @@ class HipEngineImpl : public HipEngine {
     }
 
     // ---------------------------------------------------------------- forward schedule
-    void setInputs(int n, const int *tokens, const int *positions, const int *slots, const SampleSpec *specs = nullptr) {
+    void setInputs(int n, const int *tokens, const int *positions, const int *slots, const SampleSpec *specs = nullptr,
+                   int ahead = 0) {
         DL_CHECK(n >= 1 && (u32)n <= cfg_.maxBatch, "batch size out of range");
         for (int b = 0; b < n; b++) {
             DL_CHECK(tokens[b] >= 0 && (u32)tokens[b] < h_.vocabSize, "token out of range");
             DL_CHECK(positions[b] >= 0 && (u32)positions[b] < h_.seqLen, "position out of range");
             DL_CHECK(slots[b] >= 0 && (u32)slots[b] < cfg_.nSlots, "slot out of range");
         }
+        mapPages(n, positions, slots, ahead);
         const u32 MB = cfg_.maxBatch;
         // keep the pinned staging buffer stable while a previous copy may still read it (every
         // public entry point ends with a stream sync, so this only waits after an async path)
@@ -875,6 +958,7 @@ class HipEngineImpl : public HipEngine {
             a.pos = dPos_ + c0;
             a.slot = dSlot_ + c0;
             a.kcache = L->k;
+            a.kvMap = kvMap();
             a.vcache = L->v;
             a.kvBf16 = kvBf16_ ? 1 : 0;
         }
@@ -905,6 +989,7 @@ class HipEngineImpl : public HipEngine {
         a.q = dQ_;
         a.ldq = p.q0;
         a.kcache = L.k;
+        a.kvMap = kvMap();
         a.vcache = L.v;
         a.pos = dPos_;
         a.slot = dSlot_;
@@ -992,6 +1077,7 @@ class HipEngineImpl : public HipEngine {
         b.flag = dBlockCnt_ + kFfnCntOff + 64;
         b.error = dBlockErr_;
         b.ringEarly = ffnRingEarly_;
+        b.sameWg = ffnSameWg_;
         return b;
     }
 
@@ -1002,8 +1088,11 @@ class HipEngineImpl : public HipEngine {
     // w2's weight ring at entry instead of after the w13 phase; DL_FFN_W13_PASSES sets w13's
     // passes multiplier.
     void setupFfnBlock() {
-        const char *e = std::getenv("DL_FFN_BLOCK");  // opt-in: measured slower so far (profiles/r3_attn_block.md)
-        if (!(e && *e == '1') || !q40_ || plan_.hidden0 / 32 < 192) return;
+        // opt-in: 1 = producer / consumer workgroups (measured slower, profiles/r3_attn_block.md),
+        // 2 = the same workgroups run w13 then w2
+        const char *e = std::getenv("DL_FFN_BLOCK");
+        if (!(e && (*e == '1' || *e == '2')) || !q40_ || plan_.hidden0 / 32 < 192) return;
+        ffnSameWg_ = *e == '2' ? 1 : 0;
         const char *re = std::getenv("DL_FFN_RING_EARLY");
         ffnRingEarly_ = re && *re == '1' ? 1 : 0;
         const char *pm = std::getenv("DL_FFN_W13_PASSES");
@@ -1072,7 +1161,9 @@ class HipEngineImpl : public HipEngine {
     void gemmBatched(const DevMat &m, int n, int epi, const float *in, int ldIn, const float *add, float *xNext,
                      const float *normW, const _Float16 *xh, float *out, int ldOut, _Float16 *outH,
                      const DevLayer *L, const ResFuse *rf = nullptr, bool ssIn = false) {
-        const int chunk = q40_ ? kGemmMaxTokens : hipk::kGemmF32MaxTokens;  // tokens per weight pass
+        // tokens per launch: the wide Q40 kernel takes the whole forward in one launch (one weight
+        // pass per token tile, all tiles of a row tile on one XCD), the narrow one <= 128
+        const int chunk = q40_ ? (hipk::gemmUsesWide(n) ? n : kGemmMaxTokens) : hipk::kGemmF32MaxTokens;
         for (int c0 = 0; c0 < n; c0 += chunk) {
             const int bc = std::min(chunk, n - c0);
             hipk::GemmArgs g;
@@ -1116,6 +1207,7 @@ class HipEngineImpl : public HipEngine {
                 a.pos = dPos_ + c0;
                 a.slot = dSlot_ + c0;
                 a.kcache = L->k;
+                a.kvMap = kvMap();
                 a.vcache = L->v;
                 a.kvBf16 = kvBf16_ ? 1 : 0;
             }
@@ -1357,7 +1449,13 @@ class HipEngineImpl : public HipEngine {
     unsigned *dEpoch_ = nullptr, *dBlockCnt_ = nullptr, *dBlockExpect_ = nullptr;
     int *dBlockErr_ = nullptr;
     bool blockOn_ = false;  // decode rows run the fused attention block (setupAttnBlock)
-    bool ffnOn_ = false;    // decode rows run the fused FFN block (setupFfnBlock)
+    bool ffnOn_ = false;
+    // paged KV cache (setupPages / mapPages)
+    int *dKvTable_ = nullptr;
+    int *hTableStage_[2] = {nullptr, nullptr};
+    int tableFlip_ = 0, pageShift_ = 0, pagesPerSlot_ = 0;
+    std::vector<int> hostTable_, slotPages_, freePages_;
+    int ffnSameWg_ = 0;     // DL_FFN_BLOCK=2: w13 and w2 rows on the same workgroups    // decode rows run the fused FFN block (setupFfnBlock)
     int ffnRingEarly_ = 0, ffnW13PassMul_ = 1;
     bool traceFfn_ = false;  // traceAttnBlock(layer, ffn=true) traces the FFN block instead
     int traceLayer_ = -1;   // traceAttnBlock: the layer whose block launch is traced

@@ -47,7 +47,7 @@ GemvResidency ffnBlockResidency(const FfnBlockArgs &a, bool tp) {
     DL_HIP(hipGetDevice(&dev));
     DL_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     DL_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCu, p.fn, kThreads, p.lds));
-    r.grid = p.g13 + p.g2;
+    r.grid = a.sameWg ? std::max(p.g13, p.g2) : p.g13 + p.g2;
     // one workgroup per CU of margin, as the attention block (DL_FFN_MARGIN=0: none, diagnostics)
     static const int margin = [] {
         const char *e = std::getenv("DL_FFN_MARGIN");
@@ -67,7 +67,7 @@ void launchFfnBlock(const FfnBlockArgs &a, bool tp, hipStream_t s) {
         args.w2.trace = a.trace + 8 * (size_t)p.g13;
     }
     void *kargs[] = {&args};
-    DL_HIP(hipLaunchKernel(p.fn, dim3(p.g13 + p.g2), dim3(kThreads), kargs, p.lds, s));
+    DL_HIP(hipLaunchKernel(p.fn, dim3(a.sameWg ? std::max(p.g13, p.g2) : p.g13 + p.g2), dim3(kThreads), kargs, p.lds, s));
 }
 
 }  // namespace hipk

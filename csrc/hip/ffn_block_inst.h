@@ -21,6 +21,18 @@ __global__ __launch_bounds__(kThreads) void ffnBlockKernel(FfnBlockArgs fa) {
     bs.timeoutTicks = fa.timeoutTicks;
     bs.codeBase = 10;
     bs.ringEarly = fa.ringEarly != 0;
+    if (fa.sameWg) {
+        const int r2 = (kThreads / L2) * 2 * fa.w2.passes;
+        const int g2 = (fa.w2.rows + r2 - 1) / r2;
+        if ((int)blockIdx.x < g13)
+            gemvQ40Body<L13, 1, PRO_RESNORM, EPI_ACT_Q80, GEMV_PRODUCER>(fa.w13, blockIdx.x, smem, &bs);
+        if ((int)blockIdx.x < g2) {
+            __syncthreads();  // the w13 body's LDS is reused
+            bs.ringEarly = true;
+            gemvQ40Body<L2, 1, PRO_GLOBAL, TP ? EPI_STORE_TP : EPI_STORE, GEMV_CONSUMER>(fa.w2, blockIdx.x, smem, &bs);
+        }
+        return;
+    }
     if ((int)blockIdx.x < g13) {  // producers first: dispatched ahead of the role that waits on them
         gemvQ40Body<L13, 1, PRO_RESNORM, EPI_ACT_Q80, GEMV_PRODUCER>(fa.w13, blockIdx.x, smem, &bs);
         return;

@@ -1,6 +1,6 @@
 // Batched (prefill / multi-user decode) matmuls on MFMA for gfx950: Q40 and F32 weights, the
 // split-K combine and fused epilogues, and the residual + RMS norm -> f16 staging kernel.
-#include "decode_dev.h"
+#include "gemm_dev.h"
 
 #include <cstdlib>
 
@@ -25,7 +25,6 @@ namespace hipk {
 // release/acquire counter: deterministic), which runs the fused epilogues (store / SwiGLU /
 // SwiGLU -> f16 / SwiGLU -> Q80 / RoPE + KV append).
 // ------------------------------------------------------------------------------------------------
-typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 static constexpr int kGemmRows = 64;
 static constexpr int kGemmCh = 8;  // Q40 blocks per pipeline stage (~25 KB at 32 tokens)
 
@@ -59,7 +58,7 @@ GemmPlan gemmPlan(int rows, int n, int M) {
 bool gemmSupported(int n) { return n % 32 == 0; }
 
 int gemmSplits(int rows, int n, int M) {
-    (void)M;
+    if (gemmUsesWide(M)) return gemmWideSplits(rows, n, M);
     const int tiles = (rows + kGemmRows - 1) / kGemmRows, nb = n / 32;
     const int target = gemmWgTarget(), maxS = gemmMaxSplits();
     int S = 1;
@@ -73,9 +72,22 @@ int gemmSplits(int rows, int n, int M) {
 int gemmTokenPad(int M) { return M <= 16 ? 16 : M <= 32 ? 32 : M <= 64 ? 64 : 128; }
 
 size_t gemmPartFloats(int rows, int n, int maxTokens) {
-    const int tiles = (rows + kGemmRows - 1) / kGemmRows, S = gemmSplits(rows, n, maxTokens);
-    const int mp = gemmTokenPad(maxTokens);
-    return S > 1 ? (size_t)S * tiles * mp * kGemmRows : 0;
+    // narrow launches carry <= 128 tokens (the wide kernel takes the larger ones when enabled)
+    const int mt = std::min(maxTokens, kGemmMaxTokens);
+    const int tiles = (rows + kGemmRows - 1) / kGemmRows;
+    size_t best = 0;
+    for (int m = 16; m <= gemmTokenPad(mt); m *= 2) {
+        if (gemmUsesWide(m)) break;
+        const int S = gemmSplits(rows, n, m);
+        if (S > 1) best = std::max(best, (size_t)S * tiles * m * kGemmRows);
+    }
+    if (gemmUsesWide(maxTokens)) best = std::max(best, gemmWidePartFloats(rows, n, maxTokens));
+    return best;
+}
+
+int gemmCounterInts(int rows, int maxTokens) {
+    const int narrow = (rows + kGemmRows - 1) / kGemmRows;
+    return std::max(narrow, gemmUsesWide(maxTokens) ? gemmWideCounters(rows, maxTokens) : 0);
 }
 
 // stage layout (bytes): weights [64 rows][8 units] x 16 B | scales [32 pairs][8] u32 | x [MP][32 units] x 16 B
@@ -88,44 +100,6 @@ static constexpr int kGemmStages = DL_GEMM_STAGES;  // stage buffers (kGemmStage
 static constexpr int kGemmScaleFloats = 128 + 256;  // gemmFinish: per-token RMS scales + per-thread slices
 static size_t gemmLds(int MT, int stages) { return stages * (size_t)gemmStageBytes(MT) + 16 + kGemmScaleFloats * 4; }  // + flag
 
-// 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d via the 0x6400 | q magic (1024 + q)
-__device__ __forceinline__ half8 dequantQ40x8(u32x2 wv, int nibHi, uint32_t d16) {
-    const uint32_t lo = nibHi ? (wv.x >> 4) & 0x0F0F0F0Fu : wv.x & 0x0F0F0F0Fu;
-    const uint32_t hi = nibHi ? (wv.y >> 4) & 0x0F0F0F0Fu : wv.y & 0x0F0F0F0Fu;
-    const uint32_t p0 = __builtin_amdgcn_perm(0x64646464u, lo, 0x07010700u);
-    const uint32_t p1 = __builtin_amdgcn_perm(0x64646464u, lo, 0x07030702u);
-    const uint32_t p2 = __builtin_amdgcn_perm(0x64646464u, hi, 0x07010700u);
-    const uint32_t p3 = __builtin_amdgcn_perm(0x64646464u, hi, 0x07030702u);
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-    const _Float16 d = __builtin_bit_cast(_Float16, (uint16_t)d16);
-    // (1024 + q) - 1032 = q - 8 is exact in f16; one rounding in the multiply by d
-    const h2 dd = {d, d};
-    const h2 off = {(_Float16)-1032.0f, (_Float16)-1032.0f};
-    const h2 r0 = (__builtin_bit_cast(h2, p0) + off) * dd;
-    const h2 r1 = (__builtin_bit_cast(h2, p1) + off) * dd;
-    const h2 r2 = (__builtin_bit_cast(h2, p2) + off) * dd;
-    const h2 r3 = (__builtin_bit_cast(h2, p3) + off) * dd;
-    half8 out;
-    out[0] = r0[0]; out[1] = r0[1]; out[2] = r1[0]; out[3] = r1[1];
-    out[4] = r2[0]; out[5] = r2[1]; out[6] = r3[0]; out[7] = r3[1];
-    return out;
-}
-
-// one 16-B global -> LDS copy per lane; `lds` = this wave's base (lane l lands at lds + 16 l)
-__device__ __forceinline__ void glds16(const void *g, void *lds) {
-    __builtin_amdgcn_global_load_lds(const_cast<void *>(g), reinterpret_cast<__attribute__((address_space(3))) void *>(
-                                         reinterpret_cast<uintptr_t>(lds)), 16, 0, 0);
-}
-__device__ __forceinline__ void glds4(const void *g, void *lds) {
-    __builtin_amdgcn_global_load_lds(const_cast<void *>(g), reinterpret_cast<__attribute__((address_space(3))) void *>(
-                                         reinterpret_cast<uintptr_t>(lds)), 4, 0, 0);
-}
-
-// EPI_RES hand-off scale (power of two: exact) and the f16 store that saturates instead of
-// overflowing to inf.
-static constexpr float kResXScale = 1.0f / 32.0f;
-__device__ __forceinline__ _Float16 satF16(float v) { return (_Float16)fminf(fmaxf(v, -65504.f), 65504.f); }
-
 // Split-K combine and fused epilogues shared by the batched GEMMs (Q40 and f32): `acc` holds this
 // lane's C fragments (weight row (local) wave*16 + col, token t*16 + h*4 + i); `smem` must hold
 // MP x 64 floats and is free (all K-loop LDS reads retired behind a barrier); `flag` one int.
@@ -133,7 +107,6 @@ __device__ __forceinline__ _Float16 satF16(float v) { return (_Float16)fminf(fma
 template <int MT, int EPI>
 __device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc)[MT], char *smem, int *flag,
                                            int tileIdx, int tiles) {
-    const GemvArgs &a = ga.e;
     constexpr int MP = MT * 16;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int col = lane & 15, h = lane >> 4, rl = wave * 16 + col;
@@ -157,113 +130,18 @@ __device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc
 #pragma unroll
         for (int t = 0; t < MT; t++)
 #pragma unroll
-            for (int i = 0; i < 4; i++)
-                __hip_atomic_store(part + (t * 16 + h * 4 + i) * kGemmRows + rl, acc[t][i], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            const int old = __hip_atomic_fetch_add(ga.counters + tileIdx, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            flag[0] = old == S - 1;
-        }
-        __syncthreads();
-        if (!flag[0]) return;
-        if (tid == 0) __hip_atomic_store(ga.counters + tileIdx, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // combine in split order (deterministic), all of a thread's splits in flight at once: this
-        // tail runs on one workgroup per tile after the others finished
-        const float *P = ga.part + (size_t)tileIdx * MP * kGemmRows;
-        const size_t stp = (size_t)tiles * MP * kGemmRows;
-        auto ld = [](const float *q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-        for (int i = tid; i < MP * kGemmRows / 4; i += kThreads) {
-            f32x4 v[8];
-#pragma unroll
-            for (int s2 = 0; s2 < 8; s2++)
-                if (s2 < S) {
-                    const float *q = P + s2 * stp + 4 * i;
-                    v[s2] = f32x4{ld(q), ld(q + 1), ld(q + 2), ld(q + 3)};
-                }
-            f32x4 r = v[0];
-#pragma unroll
-            for (int s2 = 1; s2 < 8; s2++)
-                if (s2 < S) r += v[s2];
-            for (int s2 = 8; s2 < S; s2++) {
-                const float *q = P + s2 * stp + 4 * i;
-                r += f32x4{ld(q), ld(q + 1), ld(q + 2), ld(q + 3)};
-            }
-            reinterpret_cast<f32x4 *>(tile)[i] = r;
-        }
+            for (int i = 0; i < 4; i++) wtStore(part + (t * 16 + h * 4 + i) * kGemmRows + rl, acc[t][i]);
+        if (!splitArrive(ga.counters + tileIdx, S, flag)) return;
+        // combine in split order (deterministic): this tail runs on one workgroup per tile after
+        // the others finished
+        splitCombine(ga.part + (size_t)tileIdx * MP * kGemmRows, (size_t)tiles * MP * kGemmRows, S,
+                     MP * kGemmRows / 4, reinterpret_cast<f32x4 *>(tile));
     }
     // consumer of a fused residual + norm: per-token RMS scale from the producer's tile partials
-    float *rsL = reinterpret_cast<float *>(flag + 4);  // [128]
-    if (ga.ssIn) {
-        // TPT threads per token each sum a strided slice of the tile partials (independent loads
-        // in flight), then one thread per token adds the TPT slices in order (deterministic)
-        float *slL = rsL + 128;  // [256]
-        constexpr int TPT = kThreads / MP;
-        const int t = tid / TPT, q = tid % TPT;
-        float ssum = 0.f;
-        if (t < ga.M) {
-#pragma unroll 8
-            for (int j = q; j < ga.ssTiles; j += TPT) ssum += ga.ssIn[(size_t)j * ga.ldSS + t];
-        }
-        slL[tid] = ssum;
-        __syncthreads();
-        if (tid < ga.M) {
-            float tot = 0.f;
-            for (int i = 0; i < TPT; i++) tot += slL[tid * TPT + i];
-            rsL[tid] = (1.0f / kResXScale) / sqrtf(tot / (float)a.n + a.eps);
-        }
-    }
+    float *rsL = reinterpret_cast<float *>(flag + 4);  // [128] + [256] scratch
+    if (ga.ssIn) gemmRowScales(ga, 0, MP, rsL, rsL + 128);
     __syncthreads();
-    // fused epilogues on row pairs (2k, 2k+1) of the tile, 32 pairs per token
-    for (int i = tid; i < ga.M * 32; i += kThreads) {
-        const int t = i >> 5, k = i & 31, r0 = R0 + 2 * k;
-        float v0 = tile[t * kGemmRows + 2 * k], v1 = tile[t * kGemmRows + 2 * k + 1];
-        if (ga.ssIn) {
-            v0 *= rsL[t];
-            v1 *= rsL[t];
-        }
-        if constexpr (EPI == EPI_RES) {
-            float x0 = 0.f, x1 = 0.f;
-            if (r0 < a.rows) {  // a.rows even: whole pairs
-                const size_t o = (size_t)t * a.ldOut + r0;
-                x0 = ga.resIn[o] + v0;
-                x1 = ga.resIn[o + 1] + v1;
-                ga.resOut[o] = x0;
-                ga.resOut[o + 1] = x1;
-                // the un-normalised residual can be large (real checkpoints carry outlier channels
-                // of 1e3-1e4): stored pre-scaled by 2^-5 (exact) and saturated, so f16 never
-                // overflows to inf; the consumer folds 2^5 into its RMS scale
-                ga.resX[o] = satF16(x0 * ga.resW[r0] * kResXScale);
-                ga.resX[o + 1] = satF16(x1 * ga.resW[r0 + 1] * kResXScale);
-            }
-            const float ssq = groupSum<32>(x0 * x0 + x1 * x1);  // the 32 pairs of token t, in lane order
-            if (k == 0) ga.ssOut[(size_t)tileIdx * ga.ldSS + t] = ssq;
-        } else if constexpr (EPI == EPI_STORE) {
-            if (r0 < a.rows) a.out[(size_t)t * a.ldOut + r0] = v0;
-            if (r0 + 1 < a.rows) a.out[(size_t)t * a.ldOut + r0 + 1] = v1;
-        } else if constexpr (EPI == EPI_ACT) {
-            if (r0 < a.rows) a.out[(size_t)t * a.ldOut + (r0 >> 1)] = gateAct(a, v0) * v1;
-        } else if constexpr (EPI == EPI_ACT_F16) {
-            if (r0 < a.rows) ga.outH[(size_t)t * a.ldOut + (r0 >> 1)] = (_Float16)(gateAct(a, v0) * v1);
-        } else if constexpr (EPI == EPI_ACT_Q80) {
-            const int hBase = R0 >> 1;
-            if (hBase >= (a.rows >> 1)) continue;  // whole 32-unit block: uniform per lane group
-            const float hv = gateAct(a, v0) * v1;
-            const float amax = groupMax<32>(fabsf(hv));
-            const float d = amax / 127.0f;
-            const float id = d != 0.f ? 1.0f / d : 0.f;
-            int q = (int)rintf(hv * id);
-            q = q > 127 ? 127 : (q < -127 ? -127 : q);
-            a.oq[(size_t)t * a.ldOut + hBase + k] = (int8_t)q;
-            const float qsum = groupSum<32>((float)q);
-            if (k == 0) a.os[(size_t)t * (a.ldOut >> 5) + (hBase >> 5)] = make_float2(roundF16(d), qsum);
-        } else {
-            if (r0 < a.rows)
-                qkvPairStore(a, r0, v0, v1, a.rope + (size_t)a.pos[t] * (a.hs >> 1), a.pos[t], a.slot[t],
-                             a.out + (size_t)t * a.ldOut);
-        }
-    }
+    gemmEpilogue<EPI, 32>(ga, tile, kGemmRows, 0, ga.M, 0, R0, tileIdx, ga.ssIn ? rsL : nullptr);
 }
 
 // STG = stage buffers: 2 double-buffers the chunk stream inside a workgroup; 1 (the 64-token
@@ -404,6 +282,11 @@ static int gemmStages1() {  // stage buffers of the 16-token tile (DL_GEMM_STG1 
 }
 
 void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
+    if (gemmUsesWide(ga.M)) {
+        launchGemmWide(ga, epi, s);
+        return;
+    }
+    if (ga.M > kGemmMaxTokens) throw Error("launchGemmQ40: more than 128 tokens per narrow launch");
     const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
     const int MT = gemmTokenPad(ga.M) / 16;
     const int stg = MT == 8 ? 1 : MT == 4 ? gemmStages4() : MT == 2 ? gemmStages2() : gemmStages1();

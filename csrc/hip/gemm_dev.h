@@ -1,0 +1,192 @@
+// Device building blocks shared by the batched MFMA GEMMs (gemm.hip: 16..128-token tiles of 64
+// rows; gemm_wide.hip: 128 x 128 tiles for prefill chunks): Q40 nibble dequantization to f16,
+// global -> LDS copies, the range-safe f16 hand-off of EPI_RES and the fused epilogues.
+#pragma once
+
+#include "decode_dev.h"
+
+namespace dl {
+namespace hipk {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+// 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d via the 0x6400 | q magic (1024 + q)
+__device__ __forceinline__ half8 dequantQ40x8(u32x2 wv, int nibHi, uint32_t d16) {
+    const uint32_t lo = nibHi ? (wv.x >> 4) & 0x0F0F0F0Fu : wv.x & 0x0F0F0F0Fu;
+    const uint32_t hi = nibHi ? (wv.y >> 4) & 0x0F0F0F0Fu : wv.y & 0x0F0F0F0Fu;
+    const uint32_t p0 = __builtin_amdgcn_perm(0x64646464u, lo, 0x07010700u);
+    const uint32_t p1 = __builtin_amdgcn_perm(0x64646464u, lo, 0x07030702u);
+    const uint32_t p2 = __builtin_amdgcn_perm(0x64646464u, hi, 0x07010700u);
+    const uint32_t p3 = __builtin_amdgcn_perm(0x64646464u, hi, 0x07030702u);
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const _Float16 d = __builtin_bit_cast(_Float16, (uint16_t)d16);
+    // (1024 + q) - 1032 = q - 8 is exact in f16; one rounding in the multiply by d
+    const h2 dd = {d, d};
+    const h2 off = {(_Float16)-1032.0f, (_Float16)-1032.0f};
+    const h2 r0 = (__builtin_bit_cast(h2, p0) + off) * dd;
+    const h2 r1 = (__builtin_bit_cast(h2, p1) + off) * dd;
+    const h2 r2 = (__builtin_bit_cast(h2, p2) + off) * dd;
+    const h2 r3 = (__builtin_bit_cast(h2, p3) + off) * dd;
+    half8 out;
+    out[0] = r0[0]; out[1] = r0[1]; out[2] = r1[0]; out[3] = r1[1];
+    out[4] = r2[0]; out[5] = r2[1]; out[6] = r3[0]; out[7] = r3[1];
+    return out;
+}
+
+// one 16-B global -> LDS copy per lane; `lds` = this wave's base (lane l lands at lds + 16 l)
+__device__ __forceinline__ void glds16(const void *g, void *lds) {
+    __builtin_amdgcn_global_load_lds(const_cast<void *>(g), reinterpret_cast<__attribute__((address_space(3))) void *>(
+                                         reinterpret_cast<uintptr_t>(lds)), 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void *g, void *lds) {
+    __builtin_amdgcn_global_load_lds(const_cast<void *>(g), reinterpret_cast<__attribute__((address_space(3))) void *>(
+                                         reinterpret_cast<uintptr_t>(lds)), 4, 0, 0);
+}
+
+// EPI_RES hand-off scale (power of two: exact) and the f16 store that saturates instead of
+// overflowing to inf.
+static constexpr float kResXScale = 1.0f / 32.0f;
+__device__ __forceinline__ _Float16 satF16(float v) { return (_Float16)fminf(fmaxf(v, -65504.f), 65504.f); }
+
+// Fence-free cross-workgroup hand-off (split-K partials), one place for the pattern:
+// * producer: every handed-off value stored with wtStore (agent-scope relaxed atomic store =
+//   global_store ... sc1, performed at the device coherence point, never left dirty in one XCD's
+//   L2), then splitArrive: s_waitcnt vmcnt(0) (all of this wave's stores performed), a workgroup
+//   barrier, one relaxed agent-scope fetch_add on the tile counter;
+// * consumer (the last arriver): loads with wtLoad (global_load ... sc1, served from the coherence
+//   point, never from a stale L1/L2 line).
+// This is the "Valid forms" alternative to a release/acquire pair in MI355X_MICROARCH.md
+// (Correctness boundaries: inter-workgroup visibility). The release/acquire fences compile to a
+// whole-L2 writeback / invalidate (buffer_wbl2 sc1 / buffer_inv sc1) on gfx950, ~28 us per split
+// level on w13 (profiles/r2_splitk_fences.md). The asm vmcnt(0) carries a "memory" clobber so the
+// compiler cannot move the stores below it; tests/test_gpu_ops.py::test_gemm_split_determinism
+// pins the result of many splits across XCDs bitwise against one split.
+__device__ __forceinline__ void wtStore(float *p, float v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float wtLoad(const float *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// All S workgroups of a tile call this after their wtStores; true in the last arriver only (which
+// also re-arms the counter for the next launch). flag: one int of LDS.
+__device__ __forceinline__ bool splitArrive(int *counter, int S, int *flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int old = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flag[0] = old == S - 1;
+    }
+    __syncthreads();
+    const bool last = flag[0] != 0;
+    if (last && threadIdx.x == 0) __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return last;
+}
+// Sum S partials (P + s * stride, f32x4 units [0, n4)) in split order into dst (LDS; unit i lands
+// at dst[(i / rowU) * ldU + i % rowU], a padded row stride): every split's load of a unit is in
+// flight before the adds.
+__device__ __forceinline__ void splitCombine(const float *P, size_t stride, int S, int n4, f32x4 *dst, int rowU = 1,
+                                             int ldU = 1) {
+    for (int i = threadIdx.x; i < n4; i += kThreads) {
+        f32x4 v[8];
+#pragma unroll
+        for (int s2 = 0; s2 < 8; s2++)
+            if (s2 < S) {
+                const float *q = P + s2 * stride + 4 * i;
+                v[s2] = f32x4{wtLoad(q), wtLoad(q + 1), wtLoad(q + 2), wtLoad(q + 3)};
+            }
+        f32x4 r = v[0];
+#pragma unroll
+        for (int s2 = 1; s2 < 8; s2++)
+            if (s2 < S) r += v[s2];
+        for (int s2 = 8; s2 < S; s2++) {
+            const float *q = P + s2 * stride + 4 * i;
+            r += f32x4{wtLoad(q), wtLoad(q + 1), wtLoad(q + 2), wtLoad(q + 3)};
+        }
+        dst[(i / rowU) * ldU + i % rowU] = r;
+    }
+}
+
+// Consumer of a fused residual + norm (ga.ssIn): per-token RMS scale of tokens [t0, t0 + nt) of the
+// launch (nt <= 128) from the producer's 64-row tile partials, into rsL[0, nt). TPT threads per
+// token each sum a strided slice (independent loads in flight), then one thread per token adds the
+// slices in order (deterministic). slL: kThreads floats of scratch. Ends with a barrier.
+__device__ __forceinline__ void gemmRowScales(const GemmArgs &ga, int t0, int nt, float *rsL, float *slL) {
+    const int tid = threadIdx.x;
+    const int TPT = nt <= 16 ? 16 : nt <= 32 ? 8 : nt <= 64 ? 4 : 2;
+    const int t = tid / TPT, q = tid % TPT;
+    float ssum = 0.f;
+    if (t < nt && t0 + t < ga.M) {
+#pragma unroll 8
+        for (int j = q; j < ga.ssTiles; j += TPT) ssum += ga.ssIn[(size_t)j * ga.ldSS + t0 + t];
+    }
+    slL[tid] = ssum;
+    __syncthreads();
+    if (tid < nt) {
+        float tot = 0.f;
+        for (int i = 0; i < TPT; i++) tot += slL[tid * TPT + i];
+        rsL[tid] = (1.0f / kResXScale) / sqrtf(tot / (float)ga.e.n + ga.e.eps);
+    }
+    __syncthreads();
+}
+
+// Fused epilogues of an output tile in LDS: tile[tl * ldT + r] holds tokens tl in [tl0, tl1) (local
+// to the tile; launch token = tokBase + tl) and the tile's rows r in [0, 2 * PAIRS) (global row
+// R0 + r), processed as row pairs (2k, 2k+1). rsL (indexed tl - tl0): per-token RMS scales of an
+// ssIn consumer, else null. EPI_RES writes one sum of squares per 64 rows (32 pairs) and token to
+// ssOut[(ssSlot0 + k / 32) * ldSS + t].
+template <int EPI, int PAIRS>
+__device__ __forceinline__ void gemmEpilogue(const GemmArgs &ga, const float *tile, int ldT, int tl0, int tl1,
+                                             int tokBase, int R0, int ssSlot0, const float *rsL) {
+    const GemvArgs &a = ga.e;
+    for (int i = threadIdx.x; i < (tl1 - tl0) * PAIRS; i += kThreads) {
+        const int tl = tl0 + i / PAIRS, k = i % PAIRS, r0 = R0 + 2 * k, t = tokBase + tl;
+        float v0 = tile[tl * ldT + 2 * k], v1 = tile[tl * ldT + 2 * k + 1];
+        if (rsL) {
+            v0 *= rsL[tl - tl0];
+            v1 *= rsL[tl - tl0];
+        }
+        if constexpr (EPI == EPI_RES) {
+            float x0 = 0.f, x1 = 0.f;
+            if (r0 < a.rows) {  // a.rows even: whole pairs
+                const size_t o = (size_t)t * a.ldOut + r0;
+                x0 = ga.resIn[o] + v0;
+                x1 = ga.resIn[o + 1] + v1;
+                ga.resOut[o] = x0;
+                ga.resOut[o + 1] = x1;
+                // the un-normalised residual can be large (real checkpoints carry outlier channels
+                // of 1e3-1e4): stored pre-scaled by 2^-5 (exact) and saturated, so f16 never
+                // overflows to inf; the consumer folds 2^5 into its RMS scale
+                ga.resX[o] = satF16(x0 * ga.resW[r0] * kResXScale);
+                ga.resX[o + 1] = satF16(x1 * ga.resW[r0 + 1] * kResXScale);
+            }
+            const float ssq = groupSum<32>(x0 * x0 + x1 * x1);  // 32 pairs = 64 rows of token t, in lane order
+            if ((k & 31) == 0 && R0 + 2 * k < a.rows) ga.ssOut[(size_t)(ssSlot0 + (k >> 5)) * ga.ldSS + t] = ssq;
+        } else if constexpr (EPI == EPI_STORE) {
+            if (r0 < a.rows) a.out[(size_t)t * a.ldOut + r0] = v0;
+            if (r0 + 1 < a.rows) a.out[(size_t)t * a.ldOut + r0 + 1] = v1;
+        } else if constexpr (EPI == EPI_ACT) {
+            if (r0 < a.rows) a.out[(size_t)t * a.ldOut + (r0 >> 1)] = gateAct(a, v0) * v1;
+        } else if constexpr (EPI == EPI_ACT_F16) {
+            if (r0 < a.rows) ga.outH[(size_t)t * a.ldOut + (r0 >> 1)] = (_Float16)(gateAct(a, v0) * v1);
+        } else if constexpr (EPI == EPI_ACT_Q80) {
+            const int hBase = (R0 >> 1) + (k & ~31);
+            if (hBase >= (a.rows >> 1)) continue;  // whole 32-unit block: uniform per lane group
+            const float hv = gateAct(a, v0) * v1;
+            const float amax = groupMax<32>(fabsf(hv));
+            const float d = amax / 127.0f;
+            const float id = d != 0.f ? 1.0f / d : 0.f;
+            int q = (int)rintf(hv * id);
+            q = q > 127 ? 127 : (q < -127 ? -127 : q);
+            a.oq[(size_t)t * a.ldOut + hBase + (k & 31)] = (int8_t)q;
+            const float qsum = groupSum<32>((float)q);
+            if ((k & 31) == 0) a.os[(size_t)t * (a.ldOut >> 5) + (hBase >> 5)] = make_float2(roundF16(d), qsum);
+        } else {
+            if (r0 < a.rows)
+                qkvPairStore(a, r0, v0, v1, a.rope + (size_t)a.pos[t] * (a.hs >> 1), a.pos[t], a.slot[t],
+                             a.out + (size_t)t * a.ldOut);
+        }
+    }
+}
+
+}  // namespace hipk
+}  // namespace dl

@@ -50,10 +50,27 @@ void tileQ40(const uint8_t *qs, const uint16_t *d, int rows, int n, int L, uint8
 // at row r's first block of the column slice being tiled.
 void tileQ40AoS(const uint8_t *const *rowBlocks, int rows, int n, int L, uint8_t *qsOut, uint32_t *dOut);
 
+// Paged KV cache: with a page table the cache rows of (slot, pos) live at row
+// table[slot * pagesPerSlot + (pos >> pageShift)] * 2^pageShift + (pos & (2^pageShift - 1)) of a
+// per-layer pool of pages, so slots hold only the pages their sequences reached; without one the
+// cache is contiguous [slot][seqLen]. Pages are >= 32 positions (a 32-key attention tile never
+// crosses a page).
+struct KvMap {
+    const int *table = nullptr;  // [slots][pagesPerSlot] page ids (null: contiguous)
+    int pageShift = 0;
+    int pagesPerSlot = 0;
+};
+__host__ __device__ inline size_t kvRow(const KvMap &m, int seqLen, int slot, int pos) {
+    if (!m.table) return (size_t)slot * seqLen + pos;
+    const int pg = m.table[slot * m.pagesPerSlot + (pos >> m.pageShift)];
+    return ((size_t)pg << m.pageShift) + (size_t)(pos & ((1 << m.pageShift) - 1));
+}
+
 struct AttnArgs {
     const float *q = nullptr;   // [B][ldq], rotated queries
     int ldq = 0;
-    const void *kcache = nullptr, *vcache = nullptr;  // layer base [slot][seqLen][kv0]
+    const void *kcache = nullptr, *vcache = nullptr;  // layer base [slot][seqLen][kv0] (or a page pool)
+    KvMap kvMap;
     const int *pos = nullptr, *slot = nullptr;
     int nHeads0 = 0, kvMul = 1, hs = 0, kv0 = 0, seqLen = 0;
     int splitGrid = 1;          // max sequence splits (grid.y)
@@ -125,8 +142,9 @@ struct GemvArgs {
     const float2 *rope = nullptr; // [seqLen][hs/2] (cos, sin)
     const int *pos = nullptr;     // per batch row
     const int *slot = nullptr;
-    void *kcache = nullptr;       // layer base: [slot][seqLen][kv0]
+    void *kcache = nullptr;       // layer base: [slot][seqLen][kv0] (or a page pool: kvMap)
     void *vcache = nullptr;
+    KvMap kvMap;
     int kvBf16 = 1;
     // EPI_STORE_TP (Q40 GEMV): the partial rows are all-reduced over the tensor-parallel ranks in
     // the kernel tail before `out` is written (exchange element = b * ldOut + row)
@@ -169,7 +187,19 @@ void launchGemmF32(const GemmArgs &a, int epi, hipStream_t s);
 struct GemmPlan {
     int rt = 1, tiles = 0, splits = 1;
 };
-constexpr int kGemmMaxTokens = 128;    // tokens per Q40 GEMM launch (16, 32, 64 or 128 padded)
+constexpr int kGemmMaxTokens = 128;    // tokens per narrow Q40 GEMM launch (16, 32, 64 or 128 padded)
+// Wide Q40 GEMM (gemm_wide.hip): launches of >= gemmWideMin() tokens (default 65; DL_GEMM_WIDE=0
+// disables) run 128 x 128 tiles over every token tile of the launch; any token count per launch
+// (activation operand padded to whole 128-token tiles).
+bool gemmWideOn();
+int gemmWideMin();
+bool gemmUsesWide(int M);
+int gemmWideSplits(int rows, int n, int M);
+size_t gemmWidePartFloats(int rows, int n, int maxTokens);
+int gemmWideCounters(int rows, int maxTokens);
+void launchGemmWide(const GemmArgs &a, int epi, hipStream_t s);
+// split-K counter ints for any launch of up to maxTokens tokens on a matrix of `rows`
+int gemmCounterInts(int rows, int maxTokens);
 constexpr int kGemmF32MaxTokens = 64;  // tokens per F32 GEMM launch (16, 32 or 64 padded)
 GemmPlan gemmPlan(int rows, int n, int M);
 bool gemmSupported(int n);  // input width a multiple of 32 (whole Q40 blocks)
@@ -207,6 +237,12 @@ size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg, int pro);
 int gemvDefaultPasses(int n, int rows, int B, bool q40, int epi);
 
 void launchAttention(const AttnArgs &a, int B, hipStream_t s);
+// MFMA decode attention (attn_mfma.hip): bf16 cache, head size 128, kvMul 1/2/4/8; launchAttention
+// takes it for caches of >= 1024 positions (DL_ATTN_MFMA=1: always, 0: never).
+bool attnMfmaSupported(const AttnArgs &a);
+bool attnUsesMfma(const AttnArgs &a);
+void launchAttentionMfma(const AttnArgs &a, int B, hipStream_t s);
+void launchAttentionValu(const AttnArgs &a, int B, hipStream_t s);  // the VALU kernel (attnTask)
 
 // Fused attention block of one decode row (B = 1): the qkv GEMV (norm prologue, RoPE + KV append),
 // the decode attention and the wo GEMV in ONE launch, as three workgroup roles
@@ -264,6 +300,10 @@ struct FfnBlockArgs {
     int *error = nullptr;
     long long timeoutTicks = 200LL * 1000 * 1000;
     int ringEarly = 0;
+    // 0: w13 producers and w2 consumers are different workgroups (grid g13 + g2); 1: every
+    // workgroup runs its w13 rows, then issues its w2 weight ring at once and waits for the w13
+    // phase (grid max(g13, g2)): the w2 ramp overlaps the w13 stragglers and the flag latency
+    int sameWg = 0;
     unsigned long long *trace = nullptr;  // GemvArgs::trace layout, w13 workgroups then w2
 };
 struct FfnBlockPlan {

@@ -230,6 +230,13 @@ static void attnDispatchHG(const AttnArgs &a, int B, int HG, hipStream_t s) {
 }
 
 void launchAttention(const AttnArgs &a, int B, hipStream_t s) {
+    if (attnUsesMfma(a))  // bf16 cache, long context: MFMA kernel (attn_mfma.hip)
+        launchAttentionMfma(a, B, s);
+    else
+        launchAttentionValu(a, B, s);
+}
+
+void launchAttentionValu(const AttnArgs &a, int B, hipStream_t s) {
     static const int hgOverride = [] {  // experiments: DL_ATTN_HG forces query heads per workgroup
         const char *e = getenv("DL_ATTN_HG");
         return e ? atoi(e) : 0;
@@ -324,14 +331,14 @@ __global__ __launch_bounds__(kPfThreads) void attnPrefillKernel(AttnArgs a, int 
     }
     const uint16_t *kc = reinterpret_cast<const uint16_t *>(a.kcache);
     const uint16_t *vc = reinterpret_cast<const uint16_t *>(a.vcache);
-    const size_t kvBase = (size_t)sl * a.seqLen * a.kv0 + (size_t)g * HS;
+    const size_t kvBase = (size_t)g * HS;
     u32x4 kr[PER], vr[PER];
     auto gload = [&](int t0) {
 #pragma unroll
         for (int u = 0; u < PER; u++) {
             const int e = tid + u * kPfThreads;
-            const int key = min(t0 + e / U8, a.seqLen - 1);  // past the range: masked in compute
-            const size_t off = kvBase + (size_t)key * a.kv0 + (e % U8) * 8;
+            const int key = min(t0 + e / U8, k1 - 1);  // past the range: masked in compute (and mapped)
+            const size_t off = kvBase + kvRow(a.kvMap, a.seqLen, sl, key) * a.kv0 + (e % U8) * 8;
             kr[u] = *reinterpret_cast<const u32x4 *>(kc + off);
             vr[u] = *reinterpret_cast<const u32x4 *>(vc + off);
         }

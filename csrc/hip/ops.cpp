@@ -167,8 +167,10 @@ std::vector<float> gemvQ40Q80In(const std::vector<uint8_t> &blocks, int rows, in
 }
 
 std::vector<float> gemmQ40(const std::vector<uint8_t> &blocks, int rows, int n, const std::vector<float> &in,
-                           const std::vector<float> &residual, const std::vector<float> &normW, float eps, int M) {
-    DL_CHECK(M >= 1 && M <= 256, "gemm tokens must be 1..256");
+                           const std::vector<float> &residual, const std::vector<float> &normW, float eps, int M,
+                           int splits) {
+    DL_CHECK(splits == 0 || (splits > 0 && (n / 32) % splits == 0), "gemm splits must divide n / 32");
+    DL_CHECK(M >= 1 && M <= 2048, "gemm tokens must be 1..2048");
     DL_CHECK(in.size() == (size_t)M * n, "gemm input size");
     DL_CHECK(hipk::gemmSupported(n), "gemm input width must be a multiple of 32");
     checkRows(residual, (size_t)M * n, "residual");
@@ -187,12 +189,14 @@ std::vector<float> gemmQ40(const std::vector<uint8_t> &blocks, int rows, int n, 
     _Float16 *xh = sc.alloc<_Float16>((size_t)rowsPad * n);
     hipk::launchNormF16(nq, xh, M, sc.s);
     float *out = sc.alloc<float>((size_t)M * rows);
-    const size_t part = hipk::gemmPartFloats(rows, n, M);
+    size_t part = hipk::gemmPartFloats(rows, n, M);
+    if (splits > 0) part = std::max(part, (size_t)splits * ((rows + 127) / 128) * (size_t)rowsPad * 128);
     float *partBuf = part ? sc.alloc<float>(part) : nullptr;
-    int *counters = sc.alloc<int>((size_t)(rows + 63) / 64 + 1);
-    // one launch per <= 128 tokens (the engine's chunking)
-    for (int c0 = 0; c0 < M; c0 += hipk::kGemmMaxTokens) {
-        const int bc = std::min(hipk::kGemmMaxTokens, M - c0);
+    int *counters = sc.alloc<int>((size_t)hipk::gemmCounterInts(rows, M) + (size_t)(rows + 63) / 64 * (M / 128 + 1) + 1);
+    // the engine's chunking: one wide launch, or <= 128 tokens per narrow launch
+    const int chunk = hipk::gemmUsesWide(M) ? M : hipk::kGemmMaxTokens;
+    for (int c0 = 0; c0 < M; c0 += chunk) {
+        const int bc = std::min(chunk, M - c0);
         hipk::GemmArgs g;
         g.e.qs = w.qs;
         g.e.wd = w.d;
@@ -203,7 +207,7 @@ std::vector<float> gemmQ40(const std::vector<uint8_t> &blocks, int rows, int n, 
         g.e.ldOut = rows;
         g.x = xh + (size_t)c0 * n;
         g.M = bc;
-        g.splits = hipk::gemmSplits(rows, n, bc);
+        g.splits = splits > 0 ? splits : hipk::gemmSplits(rows, n, bc);
         g.part = partBuf;
         g.counters = counters;
         hipk::launchGemmQ40(g, hipk::EPI_STORE, sc.s);
@@ -326,10 +330,10 @@ std::vector<float> qkvRope(const std::vector<uint8_t> &blocks, int q0, int kv0, 
 
 std::vector<float> attention(const std::vector<float> &q, const std::vector<float> &k, const std::vector<float> &v,
                              int nSlots, int seqLen, int nHeads0, int kvMul, int hs, const std::vector<int> &pos,
-                             const std::vector<int> &slot, bool kvBf16, bool prefill) {
+                             const std::vector<int> &slot, bool kvBf16, int impl) {
     const int B = (int)pos.size();
     DL_CHECK(B >= 1 && slot.size() == pos.size(), "attention rows");
-    if (prefill) {
+    if (impl == 1) {
         DL_CHECK(hipk::attnPrefillSupported(hs, kvMul, kvBf16), "prefill attention needs a bf16 cache");
         const int rpb = hipk::attnPrefillRowsPerBlock(kvMul);
         for (int b = 0; b < B; b++) DL_CHECK(slot[b] == slot[b - b % rpb], "prefill row blocks must share a slot");
@@ -372,9 +376,14 @@ std::vector<float> attention(const std::vector<float> &q, const std::vector<floa
     a.kvBf16 = kvBf16 ? 1 : 0;
     a.counters = sc.alloc<int>((size_t)B * nHeads0);
     DL_HIP(hipMemsetAsync(a.counters, 0, sizeof(int) * (size_t)B * nHeads0, sc.s));
-    if (prefill)
+    if (impl == 1)
         hipk::launchAttentionPrefill(a, B, sc.s);
-    else
+    else if (impl == 2)
+        hipk::launchAttentionValu(a, B, sc.s);
+    else if (impl == 3) {
+        DL_CHECK(hipk::attnMfmaSupported(a), "MFMA decode attention: bf16 cache, head size 128, kvMul 1/2/4/8");
+        hipk::launchAttentionMfma(a, B, sc.s);
+    } else
         hipk::launchAttention(a, B, sc.s);
     sc.sync();
     return sc.download(a.out, (size_t)B * q0);

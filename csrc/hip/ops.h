@@ -25,12 +25,13 @@ std::vector<float> gemvQ40(const std::vector<uint8_t> &blocks, int rows, int n, 
 std::vector<float> gemvQ40Q80In(const std::vector<uint8_t> &blocks, int rows, int n, const std::vector<float> &in,
                                 int B);
 
-// Batched Q40 matmul on MFMA (M = 2..32 tokens): norm kernel (in + residual -> RMS norm -> f16)
-// then the MFMA GEMM with the plain store epilogue.
+// Batched F32 matmul on MFMA: norm kernel -> f16 -> gemmF32Kernel (store epilogue).
 std::vector<float> gemmF32(const std::vector<float> &w, int rows, int n, const std::vector<float> &in,
                            const std::vector<float> &normW, float eps, int M);
 std::vector<float> gemmQ40(const std::vector<uint8_t> &blocks, int rows, int n, const std::vector<float> &in,
-                           const std::vector<float> &residual, const std::vector<float> &normW, float eps, int M);
+                           const std::vector<float> &residual, const std::vector<float> &normW, float eps, int M,
+                           int splits = 0);  // Batched Q40 matmul on MFMA (narrow <= 64 tokens, wide above);
+                                             // splits > 0 forces the K split (must divide n / 32)
 
 // QKV GEMV with the RoPE + KV-append epilogue (rows = q0 + 2*kv0, head size hs): returns rotated q
 // [B][q0]; kOut/vOut receive the appended cache rows [B][kv0] (f32 view of the bf16 or f32 cache).
@@ -44,7 +45,9 @@ std::vector<float> qkvRope(const std::vector<uint8_t> &blocks, int q0, int kv0, 
 // q [B][nHeads0*hs] (already rotated), row b at position pos[b] in slot slot[b]. Returns f32 [B][q0].
 std::vector<float> attention(const std::vector<float> &q, const std::vector<float> &k, const std::vector<float> &v,
                              int nSlots, int seqLen, int nHeads0, int kvMul, int hs, const std::vector<int> &pos,
-                             const std::vector<int> &slot, bool kvBf16, bool prefill = false);
+                             const std::vector<int> &slot, bool kvBf16, int impl = 0);
+// attention impl: 0 = launchAttention's choice, 1 = MFMA prefill kernel, 2 = VALU decode kernel,
+// 3 = MFMA decode kernel
 
 // Parallel argmax over [B][vocab] (ties -> lowest index).
 std::vector<int> argmax(const std::vector<float> &logits, int B, int vocab);

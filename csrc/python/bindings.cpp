@@ -196,19 +196,20 @@ void bindOps(py::module_ &m) {
           },
           py::arg("blocks"), py::arg("rows"), py::arg("n"), py::arg("x"));
     o.def("gemm_q40",
-          [](py::object blocks, int rows, int n, py::object x, py::object residual, py::object normW, float eps) {
+          [](py::object blocks, int rows, int n, py::object x, py::object residual, py::object normW, float eps,
+             int splits) {
               const std::vector<uint8_t> w = vec<uint8_t>(blocks);
               const std::vector<float> in = vec<float>(x), res = vec<float>(residual), nw = vec<float>(normW);
               const int M = (int)(in.size() / n);
               std::vector<float> out;
               {
                   py::gil_scoped_release rel;
-                  out = ops::gemmQ40(w, rows, n, in, res, nw, eps, M);
+                  out = ops::gemmQ40(w, rows, n, in, res, nw, eps, M, splits);
               }
               return arr(out, {M, rows});
           },
           py::arg("blocks"), py::arg("rows"), py::arg("n"), py::arg("x"), py::arg("residual") = py::none(),
-          py::arg("norm_w") = py::none(), py::arg("eps") = 1e-5f);
+          py::arg("norm_w") = py::none(), py::arg("eps") = 1e-5f, py::arg("splits") = 0);
     o.def("gemm_f32",
           [](py::object wts, int rows, int n, py::object x, py::object normW, float eps) {
               const std::vector<float> w = vec<float>(wts), in = vec<float>(x), nw = vec<float>(normW);
@@ -239,18 +240,18 @@ void bindOps(py::module_ &m) {
           py::arg("norm_w"), py::arg("eps"), py::arg("rope"), py::arg("seq_len"), py::arg("pos"), py::arg("kv_bf16") = true);
     o.def("attention",
           [](py::object q, py::object k, py::object v, int nSlots, int seqLen, int nHeads0, int kvMul, int hs,
-             std::vector<int> pos, std::vector<int> slot, bool kvBf16, bool prefill) {
+             std::vector<int> pos, std::vector<int> slot, bool kvBf16, int impl) {
               const std::vector<float> qv = vec<float>(q), kv = vec<float>(k), vv = vec<float>(v);
               std::vector<float> out;
               {
                   py::gil_scoped_release rel;
-                  out = ops::attention(qv, kv, vv, nSlots, seqLen, nHeads0, kvMul, hs, pos, slot, kvBf16, prefill);
+                  out = ops::attention(qv, kv, vv, nSlots, seqLen, nHeads0, kvMul, hs, pos, slot, kvBf16, impl);
               }
               return arr(out, {(py::ssize_t)pos.size(), (py::ssize_t)nHeads0 * hs});
           },
           py::arg("q"), py::arg("k"), py::arg("v"), py::arg("n_slots"), py::arg("seq_len"), py::arg("n_heads0"),
           py::arg("kv_mul"), py::arg("head_size"), py::arg("pos"), py::arg("slot"), py::arg("kv_bf16") = true,
-          py::arg("prefill") = false);
+          py::arg("impl") = 0);
     o.def("sample",
           [](py::object logits, int B, py::object specs) {
               const std::vector<float> l = vec<float>(logits), sp = vec<float>(specs);
@@ -725,10 +726,13 @@ PYBIND11_MODULE(_C, m) {
     py::class_<PyHipEngine>(m, "HipEngine")
         .def(py::init([](const std::string &model, const std::string &bufferType, u32 maxSeqLen, u32 maxBatch,
                          u32 nSlots, int gpuIndex, bool useGraphs, bool kvBf16, py::object synthetic, u64 seed,
-                         int rank, int world, py::object uid, py::object comm, const std::string &syncType) {
+                         int rank, int world, py::object uid, py::object comm, const std::string &syncType,
+                         u32 kvPages, u32 kvPageSize) {
                  EngineConfig c = makeConfig(model, bufferType, 1, maxSeqLen, maxBatch, nSlots, gpuIndex, useGraphs,
                                              kvBf16, synthetic, seed);
                  c.syncType = parseFloatType(syncType);
+                 c.kvPages = kvPages;
+                 c.kvPageSize = kvPageSize;
                  auto *e = new PyHipEngine();
                  if (!comm.is_none()) e->comm = comm.cast<PyComm &>().comm;
                  py::gil_scoped_release rel;
@@ -749,7 +753,7 @@ PYBIND11_MODULE(_C, m) {
              py::arg("max_batch") = 32, py::arg("n_slots") = 1, py::arg("gpu_index") = 0, py::arg("use_graphs") = true,
              py::arg("kv_bf16") = true, py::arg("synthetic") = py::none(), py::arg("seed") = 1234, py::arg("rank") = 0,
              py::arg("world") = 1, py::arg("uid") = py::none(), py::arg("comm") = py::none(),
-             py::arg("sync_type") = "f32")
+             py::arg("sync_type") = "f32", py::arg("kv_pages") = 0, py::arg("kv_page_size") = 256)
         .def_property_readonly("header", [](const PyHipEngine &e) { return headerToDict(e.engine->header()); })
         .def_property_readonly("device_bytes", [](const PyHipEngine &e) { return e.engine->deviceBytes(); })
         .def_property_readonly("tp_fused", [](const PyHipEngine &e) { return e.engine->tpFused(); })
@@ -762,6 +766,7 @@ PYBIND11_MODULE(_C, m) {
              },
              py::arg("token"), py::arg("pos"), py::arg("slot") = 0, py::arg("layer") = 1, py::arg("ffn") = false)
         .def_property_readonly("fused_grid_max", [](const PyHipEngine &e) { return e.engine->fusedGridMax(); })
+        .def_property_readonly("kv_pages_free", [](const PyHipEngine &e) { return e.engine->kvPagesFree(); })
         .def_property_readonly("load_stats",
                                [](const PyHipEngine &e) {
                                    const Backend::LoadStats l = e.engine->loadStats();

@@ -67,7 +67,9 @@ AppArgs AppArgs::parse(int argc, char **argv, bool requireMode) {
             if (v == "bf16") a.kvBf16 = true;
             else if (v == "f32") a.kvBf16 = false;
             else throw Error("Invalid --kv-dtype (bf16|f32): " + v);
-        } else if (name == "--graph") a.graphs = std::atoi(value) != 0;
+        } else if (name == "--kv-pages") a.kvPages = std::atoi(value);
+        else if (name == "--kv-page-size") a.kvPageSize = std::atoi(value);
+        else if (name == "--graph") a.graphs = std::atoi(value) != 0;
         else if (name == "--log-level") a.logLevel = std::atoi(value);
         else if (name == "--synthetic") a.synthetic = value;
         else if (name == "--web-ui") a.webUi = value;
@@ -117,6 +119,8 @@ static EngineConfig engineConfigFrom(const AppArgs &a, int nSlots) {
     c.gpuIndex = a.gpuIndex;
     c.useGraphs = a.graphs;
     c.kvBf16 = a.kvBf16;
+    c.kvPages = (u32)std::max(0, a.kvPages);
+    c.kvPageSize = (u32)std::max(32, a.kvPageSize);
     if (!a.synthetic.empty()) {
         c.synthetic = true;
         c.syntheticHeader = syntheticHeader(a.synthetic, a.maxSeqLen);

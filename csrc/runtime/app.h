@@ -39,6 +39,8 @@ struct AppArgs {
     int gpuSegmentFrom = -1, gpuSegmentTo = -1;  // accepted for CLI compatibility (no effect)
     int slots = 0;                               // KV slots (0 = 1 for CLI modes, 8 for the API)
     bool kvBf16 = true;
+    int kvPages = 0;       // --kv-pages: paged KV pool pages per layer (0 = contiguous per slot)
+    int kvPageSize = 256;  // --kv-page-size: positions per page
     bool graphs = true;
     int logLevel = 1;
     std::string synthetic;                       // "llama3_1_8b" etc: random-init weights on device
@@ -63,6 +65,9 @@ class InferenceSession {
     Sampler &sampler() { return *sampler_; }
     int nSlots() const { return nSlots_; }
     int maxBatch() const { return maxBatch_; }
+    // paged KV cache of the (root) backend: free pages and positions per page (-1 / 0: contiguous)
+    int kvPagesFree() const { return backend_->kvPagesFree(); }
+    int kvPageSize() const { return backend_->kvPageSize(); }
     bool isGpu() const { return gpu_; }
     int nNodes() const { return 1 + (int)workers_.size(); }
 

@@ -29,6 +29,9 @@ struct EngineConfig {
     int gpuIndex = -1;              // HIP device ordinal (-1 = CPU backend)
     bool useGraphs = true;          // capture per-batch-size hipGraphs
     bool kvBf16 = true;             // GPU KV cache dtype (bf16 default, f32 when false)
+    u32 kvPages = 0;                // GPU paged KV cache: pool pages per layer (0 = contiguous
+                                    // nSlots x seqLen, no page table)
+    u32 kvPageSize = 256;           // positions per page (power of two, >= 32)
     bool synthetic = false;         // random-init weights of the header's shape (no file)
     ModelHeader syntheticHeader;    // used when synthetic
     u64 seed = 1234;                // synthetic weight seed
@@ -81,6 +84,10 @@ class Backend {
         u64 fileBytes = 0, deviceBytes = 0;
     };
     virtual LoadStats loadStats() const { return {}; }
+    // Paged KV cache (GPU, EngineConfig::kvPages > 0): free pages of the pool and positions per page
+    // (the scheduler admits requests by pages); -1 / 0 when the cache is contiguous per slot.
+    virtual int kvPagesFree() const { return -1; }
+    virtual int kvPageSize() const { return 0; }
     virtual std::string name() const = 0;
 
   protected:

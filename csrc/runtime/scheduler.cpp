@@ -39,6 +39,9 @@ void GenRequest::finish(const std::string &reason) {
 
 Scheduler::Scheduler(InferenceSession &sess) : sess_(sess), tok_(sess.tokenizer()) {
     for (int s = sess.nSlots() - 1; s >= 0; s--) freeSlots_.push_back(s);
+    pagesTotal_ = sess.kvPagesFree();
+    pageSize_ = sess.kvPageSize();
+    slotPages_.assign(sess.nSlots(), 0);
     thread_ = std::thread([this] { loop(); });
 }
 
@@ -166,23 +169,42 @@ bool Scheduler::step() {
         draining_.clear();
     }
 
-    // 1) admission: one free KV slot per request; cancelled requests give their slot back
+    // 1) admission: one free KV slot per request (and, with a paged KV cache, the pages its prompt +
+    //    max_tokens can reach; FIFO: the head waits until enough pages are free); cancelled requests
+    //    give their slot back
     {
         std::lock_guard<std::mutex> lk(mu_);
         while (!queue_.empty() && !freeSlots_.empty()) {
             auto r = queue_.front();
-            queue_.pop_front();
             if (r->isCancelled()) {
+                queue_.pop_front();
                 r->finish("cancelled");
                 stats_.cancelled++;
                 continue;
             }
             if (r->prompt.empty() || r->prompt.size() >= seqLen) {
+                queue_.pop_front();
                 r->error = r->prompt.empty() ? "empty prompt" : "prompt longer than the context";
                 r->finish("error");
                 continue;
             }
-            r->slot = freeSlots_.back();
+            const int slot = freeSlots_.back();
+            if (pagesTotal_ >= 0) {
+                const u64 span = r->params.maxTokens > 0 ? (u64)r->prompt.size() + (u64)r->params.maxTokens + 1 : seqLen;
+                const int need = (int)((std::min<u64>(span, seqLen) + pageSize_ - 1) / pageSize_);
+                int held = 0;
+                for (int p : slotPages_) held += p;
+                if (need > pagesTotal_) {
+                    queue_.pop_front();
+                    r->error = "request needs more KV pages than the pool holds";
+                    r->finish("error");
+                    continue;
+                }
+                if (need > pagesTotal_ - held + slotPages_[slot]) break;  // wait for pages
+                slotPages_[slot] = need;
+            }
+            queue_.pop_front();
+            r->slot = slot;
             freeSlots_.pop_back();
             r->prefilled = 0;
             r->sampler.reset(new Sampler(vocab, r->params.temperature, r->params.topp, r->params.seed));

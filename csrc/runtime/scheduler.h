@@ -110,6 +110,10 @@ class Scheduler {
     std::vector<std::shared_ptr<GenRequest>> active_;
     std::vector<std::shared_ptr<GenRequest>> draining_;  // finished, rows still in the forward in flight
     std::vector<int> freeSlots_;
+    // paged KV cache: pages the engine may hold for each slot's current / last request (released by
+    // the engine when the slot's next request starts at position 0); admission needs enough pages
+    int pagesTotal_ = -1, pageSize_ = 0;
+    std::vector<int> slotPages_;
     Flight flight_;
     bool inflight_ = false;
     bool stop_ = false;

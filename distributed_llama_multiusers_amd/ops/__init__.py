@@ -57,10 +57,13 @@ def gemv_q40_q80_in(blocks, rows: int, n: int, x) -> torch.Tensor:
     return torch.from_numpy(native().ops.gemv_q40_q80_in(_np(blocks, np.uint8), rows, n, _np(x)))
 
 
-def gemm_q40(blocks, rows: int, n: int, x, residual=None, norm_w=None, eps: float = 1e-5) -> torch.Tensor:
-    """Batched (MFMA) matmul for 1..32 tokens: (x + residual) -> RMS norm -> f16 -> W.x (f32 accumulate)."""
+def gemm_q40(blocks, rows: int, n: int, x, residual=None, norm_w=None, eps: float = 1e-5,
+             splits: int = 0) -> torch.Tensor:
+    """Batched (MFMA) matmul for 1..2048 tokens: (x + residual) -> RMS norm -> f16 -> W.x (f32
+    accumulate); narrow 64-row tiles up to 64 tokens, 128 x 128 wide tiles above. `splits` > 0
+    forces the K split (a divisor of n / 32)."""
     return torch.from_numpy(native().ops.gemm_q40(_np(blocks, np.uint8), rows, n, _np(x), _np(residual),
-                                                  _np(norm_w), eps))
+                                                  _np(norm_w), eps, splits))
 
 
 def gemm_f32(w, x, norm_w=None, eps: float = 1e-5) -> torch.Tensor:
@@ -79,13 +82,16 @@ def qkv_rope(blocks, q0: int, kv0: int, head_size: int, n: int, x, norm_w, eps: 
 
 
 def attention(q, k_cache, v_cache, n_heads0: int, kv_mul: int, head_size: int, pos, slot,
-              kv_bf16: bool = True, prefill: bool = False) -> torch.Tensor:
+              kv_bf16: bool = True, prefill: bool = False, impl: str = "auto") -> torch.Tensor:
     """Decode attention. k_cache / v_cache: [slots, seq_len, kv0]; q: [B, n_heads0 * head_size].
-    prefill=True: the MFMA prefill kernel (bf16 cache; row blocks of 64 / kv_mul rows share a slot)."""
+    prefill=True (impl "prefill"): the MFMA prefill kernel (bf16 cache; row blocks of 64 / kv_mul rows
+    share a slot). impl "valu" / "mfma": force the VALU or the MFMA decode kernel ("auto": the
+    engine's choice, MFMA for bf16 caches of >= 1024 positions)."""
     n_slots, seq_len, _ = k_cache.shape
+    code = {"auto": 0, "prefill": 1, "valu": 2, "mfma": 3}["prefill" if prefill else impl]
     return torch.from_numpy(native().ops.attention(_np(q), _np(k_cache), _np(v_cache), n_slots, seq_len, n_heads0,
                                                    kv_mul, head_size, [int(p) for p in pos], [int(s) for s in slot],
-                                                   kv_bf16, prefill))
+                                                   kv_bf16, code))
 
 
 def sample(logits, temperatures, topps, coins) -> list:

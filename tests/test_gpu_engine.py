@@ -1,4 +1,9 @@
 """HIP engine (gfx950 kernels) vs the CPU reference backend / torch oracle."""
+import json
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
@@ -116,25 +121,56 @@ def test_engine_batched_prefill_gemv_chunks(C, assets, graphs, monkeypatch):
 
 
 @pytest.mark.parametrize("graphs", [True, False])
-@pytest.mark.parametrize("n", [2, 7, 16, 23, 40, 64, 72, 100])
+@pytest.mark.parametrize("n", [2, 7, 16, 23, 40, 64, 72, 100, 128])
 def test_engine_batched_prefill_mfma(C, assets, graphs, n, monkeypatch):
     """MFMA GEMM batch path (f16 dequantized Q40 x f16 activations, split-K, fused epilogues) vs
-    sequential int8 GEMV decodes and vs the CPU reference backend. Up to 64 rows are one GEMM
-    launch per matrix; 72 and 100 rows take the multi-launch loop (row offsets into positions,
-    slots and the f16 activation buffers)."""
+    sequential int8 GEMV decodes and vs the CPU reference backend. Up to 64 rows run the narrow
+    64-row tiles; 72, 100 and 128 rows the wide 128 x 128 tiles (split-K on the thin matrices)."""
     monkeypatch.setenv("DL_GEMM_MIN", "2")
     rng = np.random.default_rng(n)
     tokens = [int(t) for t in rng.integers(0, 512, n)]
-    a = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=128, use_graphs=graphs)
-    b = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=128, use_graphs=graphs)
+    a = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=256, use_graphs=graphs)
+    b = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=256, use_graphs=graphs)
     seq = _seq(a, tokens)
     bat = b.forward(tokens, list(range(n)), [0] * n)
     assert _rel(bat, seq) < 2e-2
     assert (bat.argmax(-1) == seq.argmax(-1)).mean() >= 0.85
     _assert_replays_equal(b, tokens, bat)
-    cpu = C.cpu_backend(assets["q40"], "q80", 2, max_batch=128)
+    cpu = C.cpu_backend(assets["q40"], "q80", 2, max_batch=256)
     ref = cpu.forward(tokens, list(range(n)), [0] * n)
     assert _rel(bat, ref) < 3e-2
+
+
+@pytest.mark.parametrize("n", [100, 256])
+def test_engine_wide_gemm_matches_narrow(C, medium, n, monkeypatch):
+    """The wide 128 x 128 GEMM (one launch over all token tiles) and the narrow 64-row kernel
+    (DL_GEMM_WIDE=0: 128-token launches) give the same forward within f32 reassociation, with the
+    bf16 cache's MFMA prefill attention in between."""
+    rng = np.random.default_rng(7 + n)
+    toks = [int(t) for t in rng.integers(0, 2048, n)]
+    monkeypatch.setenv("DL_GEMM_MIN", "2")
+    wide = C.HipEngine(medium, "q80", kv_bf16=True, max_batch=256)
+    got = wide.forward(toks, list(range(n)), [0] * n)
+    monkeypatch.setenv("DL_GEMM_WIDE", "0")
+    env = dict(os.environ, PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    out = subprocess.run([sys.executable, "-c", _NARROW_CHILD, medium, json.dumps(toks)], env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    ref = np.array(json.loads(out.stdout.strip().splitlines()[-1]), dtype=np.float32)
+    assert _rel(got, ref) < 2e-3
+    assert (got.argmax(-1) == ref.argmax(-1)).mean() >= 0.95
+
+
+# the knob is read once per process: the narrow reference runs in a child
+_NARROW_CHILD = """
+import json, sys
+import distributed_llama_multiusers_amd as dl
+C = dl.native()
+toks = json.loads(sys.argv[2])
+n = len(toks)
+e = C.HipEngine(sys.argv[1], "q80", kv_bf16=True, max_batch=256)
+print(json.dumps(e.forward(toks, list(range(n)), [0] * n).tolist()))
+"""
 
 
 @pytest.mark.parametrize("n", [7, 40, 72])
@@ -250,16 +286,17 @@ def test_kv_cache_larger_than_hbm_is_refused(C):
         C.HipEngine("", "q80", synthetic=h, max_seq_len=131072, n_slots=64, max_batch=1)
 
 
-@pytest.mark.parametrize("n", [8, 32, 64])
+@pytest.mark.parametrize("n", [8, 32, 64, 200])
 def test_engine_prefill_mfma_attention(C, medium, n, monkeypatch):
     """Batched forward with a bf16 cache (MFMA prefill attention over the chunk's rows, one slot) ==
     sequential decodes (per-row attention), and a second chunk on top of the first (keys of the
-    earlier chunk + causal keys of its own)."""
+    earlier chunk + causal keys of its own). 200 rows: the wide GEMM over two token tiles in one
+    launch with the fused residual + norm hand-off across them."""
     monkeypatch.setenv("DL_GEMM_MIN", "2")
     rng = np.random.default_rng(n)
     toks = [int(t) for t in rng.integers(0, 2048, 2 * n)]
-    a = C.HipEngine(medium, "q80", kv_bf16=True, max_batch=64)
-    b = C.HipEngine(medium, "q80", kv_bf16=True, max_batch=64)
+    a = C.HipEngine(medium, "q80", kv_bf16=True, max_batch=256)
+    b = C.HipEngine(medium, "q80", kv_bf16=True, max_batch=256)
     seq = _seq(a, toks)
     first = b.forward(toks[:n], list(range(n)), [0] * n)
     second = b.forward(toks[n:], list(range(n, 2 * n)), [0] * n)
@@ -316,19 +353,19 @@ def test_attn_block_matches_separate_kernels(C, assets, medium, monkeypatch, kv_
         assert list(ca) == list(cb)
 
 
-@pytest.mark.parametrize("ring_early", ["0", "1"])
-def test_ffn_block_matches_separate_kernels(C, medium, monkeypatch, ring_early):
+@pytest.mark.parametrize("mode,ring_early", [("1", "0"), ("1", "1"), ("2", "0")])
+def test_ffn_block_matches_separate_kernels(C, medium, monkeypatch, mode, ring_early):
     """Single decode rows run the fused FFN block (w13 GEMV with the SwiGLU -> Q80 hidden stored
     write-through + the w2 GEMV as one launch): bitwise the same logits as the two separate
     launches (same kernels, same reduction order), over many forwards and graph replays (monotonic
     counters), with and without the attention block, w2's weight ring issued at entry or after the
-    w13 phase."""
+    w13 phase; mode 2: the same workgroups run their w13 rows, then their w2 rows."""
     monkeypatch.setenv("DL_FFN_RING_EARLY", ring_early)
     for attn in ("0", "1"):
         monkeypatch.setenv("DL_ATTN_BLOCK", attn)
         monkeypatch.setenv("DL_FFN_BLOCK", "0")
         ref = C.HipEngine(medium, "q80", kv_bf16=True, max_batch=8)
-        monkeypatch.setenv("DL_FFN_BLOCK", "1")
+        monkeypatch.setenv("DL_FFN_BLOCK", mode)
         got = C.HipEngine(medium, "q80", kv_bf16=True, max_batch=8)
         assert got.ffn_block and not ref.ffn_block and got.attn_block == (attn == "1")
         toks = [3, 17, 101, 7, 250, 9]
@@ -341,3 +378,44 @@ def test_ffn_block_matches_separate_kernels(C, medium, monkeypatch, ring_early):
         assert list(ca) == list(cb)
         tr = got.trace_attn_block(7, 40, 0, 1, ffn=True)
         assert tr[0] > 0 and tr[2] > 0 and len(tr) == 3 + 8 * (tr[0] + tr[2])
+
+
+@pytest.mark.parametrize("kv_bf16,page", [(True, 32), (False, 64)])
+def test_paged_kv_cache_matches_contiguous(C, medium, kv_bf16, page):
+    """Paged KV cache (page table per slot over a shared pool): the same forwards as the contiguous
+    cache give bitwise the same logits - interleaved slots, a prefill chunk crossing page edges
+    (MFMA path), single decode rows, a decode chain mapping pages ahead, a slot restarted at
+    position 0 (its pages released and reused by another slot) - and the pool's free count follows."""
+    seq = [int(t) for t in np.random.default_rng(5).integers(0, 2048, 200)]
+    kw = dict(kv_bf16=kv_bf16, max_batch=64, n_slots=3)
+    ref = C.HipEngine(medium, "q80", **kw)
+    pg = C.HipEngine(medium, "q80", kv_pages=12, kv_page_size=page, **kw)
+    assert pg.kv_pages_free == 12 and ref.kv_pages_free == -1
+
+    def both(toks, pos, slots):
+        a, b = ref.forward(toks, pos, slots), pg.forward(toks, pos, slots)
+        assert np.array_equal(a, b)
+
+    both(seq[:40], list(range(40)), [1] * 40)          # slot 1: 40 positions (pages 0..)
+    both(seq[:3], [0, 1, 2], [2] * 3)                   # slot 2
+    for p in range(40, 44):                             # interleaved single rows
+        both([seq[p]], [p], [1])
+        both([seq[p - 37]], [p - 37], [2])
+    _, ca = ref.decode_greedy(20, [seq[44]], [44], [1])
+    _, cb = pg.decode_greedy(20, [seq[44]], [44], [1])
+    assert list(ca) == list(cb)
+    used = 12 - pg.kv_pages_free
+    assert used == -(-64 // page) + -(-7 // page)
+    both(seq[100:110], list(range(10)), [1] * 10)       # slot 1 restarts: its pages are released
+    assert 12 - pg.kv_pages_free == -(-10 // page) + -(-7 // page)
+    both(seq[:64], list(range(64)), [0] * 64)           # slot 0 takes pages slot 1 gave back
+    both([seq[64]], [64], [0])
+
+
+def test_paged_kv_pool_exhaustion_raises(C, medium):
+    """A forward that needs more pages than the pool has left fails with a clear error instead of
+    writing through an unmapped page."""
+    pg = C.HipEngine(medium, "q80", kv_bf16=True, max_batch=64, n_slots=2, kv_pages=2, kv_page_size=32)
+    pg.forward(list(range(1, 41)), list(range(40)), [0] * 40)  # 2 pages
+    with pytest.raises(RuntimeError, match="KV page pool exhausted"):
+        pg.forward([5], [0], [1])

@@ -67,8 +67,10 @@ def test_gemv_q40_on_q80_activations(ops, B):
     assert rel(out, x @ w.T) < 0.12
 
 
-@pytest.mark.parametrize("M", [2, 7, 32, 40, 64, 100, 128, 200])
+@pytest.mark.parametrize("M", [2, 7, 32, 40, 64, 100, 128, 200, 384, 520])
 def test_gemm_q40_mfma(ops, M):
+    """Narrow 64-row tiles up to 64 tokens, 128 x 128 wide tiles above (one launch over all token
+    tiles; 768 rows = 6 row tiles, split-K at few tiles)."""
     rows, n = 768, 2048
     w = make_w(rows, n, 7)
     blocks = ops.quantize_q40(w)
@@ -80,6 +82,23 @@ def test_gemm_q40_mfma(ops, M):
     xh = ops.ref_rmsnorm(x + r, nw).half().float()  # the GEMM's activations are f16
     assert rel(out, xh @ wd.T) < 5e-4  # weights dequantized to f16 in registers
     assert rel(out, ops.ref_rmsnorm(x + r, nw) @ w.T) < 0.12
+
+
+@pytest.mark.parametrize("M,splits", [(16, 2), (16, 8), (48, 4), (100, 2), (256, 4), (300, 2)])
+def test_gemm_split_determinism(ops, M, splits):
+    """Split-K partials handed between workgroups without fences (write-through stores + relaxed
+    counter, gemm_dev.h): many splits spread over the XCDs must give bitwise the same result on every
+    run (a stale or torn partial would not) and match one split within f32 reassociation."""
+    rows, n = 1024, 4096
+    w = make_w(rows, n, 21)
+    blocks = ops.quantize_q40(w)
+    g = torch.Generator().manual_seed(22)
+    x = torch.randn(M, n, generator=g)
+    one = ops.gemm_q40(blocks, rows, n, x, splits=1)
+    runs = [ops.gemm_q40(blocks, rows, n, x, splits=splits) for _ in range(3)]
+    for r in runs[1:]:
+        assert torch.equal(r, runs[0])
+    assert rel(runs[0], one) < 1e-5
 
 
 @pytest.mark.parametrize("M", [5, 16, 33, 64, 100])
@@ -141,9 +160,12 @@ def test_attention_decode(ops, kv_bf16, n_heads0, kv_mul, hs, seq, pos):
     q = torch.randn(B, n_heads0 * hs, generator=g) * 2
     if kv_bf16:
         k, v = k.bfloat16().float(), v.bfloat16().float()
-    out = ops.attention(q, k, v, n_heads0, kv_mul, hs, pos, slots, kv_bf16)
+    out = ops.attention(q, k, v, n_heads0, kv_mul, hs, pos, slots, kv_bf16, impl="valu")
     want = ops.ref_attention(q, k, v, n_heads0, kv_mul, hs, pos, slots)
     assert rel(out, want) < 1e-4  # f32 arithmetic on the (bf16-rounded) cache values
+    if kv_bf16 and hs == 128:  # MFMA decode kernel: bf16 Q and P bound the error
+        got = ops.attention(q, k, v, n_heads0, kv_mul, hs, pos, slots, kv_bf16, impl="mfma")
+        assert rel(got, want) < 1.2e-2, rel(got, want)
 
 
 @pytest.mark.parametrize("n_heads0,kv_mul,hs,seq,p0,rows", [
@@ -186,9 +208,38 @@ def test_attention_split_edges(ops, n_heads0, kv_mul, hs, seq, pos):
     k = torch.randn(B, seq, kv0, generator=g).bfloat16().float()
     v = torch.randn(B, seq, kv0, generator=g).bfloat16().float()
     q = torch.randn(B, n_heads0 * hs, generator=g) * 2
-    out = ops.attention(q, k, v, n_heads0, kv_mul, hs, pos, slots, True)
+    out = ops.attention(q, k, v, n_heads0, kv_mul, hs, pos, slots, True, impl="valu")
     want = ops.ref_attention(q, k, v, n_heads0, kv_mul, hs, pos, slots)
     assert rel(out, want) < 1e-4
+    if hs == 128 and kv_mul <= 8:
+        got = ops.attention(q, k, v, n_heads0, kv_mul, hs, pos, slots, True, impl="mfma")
+        assert rel(got, want) < 1.2e-2, rel(got, want)
+
+
+@pytest.mark.parametrize("kv_mul,n_heads0,pos", [(4, 32, [8000]), (8, 8, [2047, 100, 33, 0]), (1, 4, [1500, 31, 32]),
+                                                 (2, 8, [5000] * 3)])
+def test_attention_decode_mfma(ops, kv_mul, n_heads0, pos):
+    """MFMA decode attention (LDS-DMA K/V tiles, S^T = K.Q^T, one softmax step per 32 keys,
+    O^T = V^T.P^T with hardware-transposed V reads) vs the fp32 reference: tile and split edges
+    (positions 0, 31, 32, ...), several rows sharing a launch, every supported GQA group size."""
+    hs, seq = 128, max(pos) + 64
+    kv0 = n_heads0 // kv_mul * hs
+    g = torch.Generator().manual_seed(31 + kv_mul)
+    B = len(pos)
+    slots = list(range(B))[::-1]
+    k = torch.randn(B, seq, kv0, generator=g).bfloat16().float()
+    v = torch.randn(B, seq, kv0, generator=g).bfloat16().float()
+    q = torch.randn(B, n_heads0 * hs, generator=g) * 2
+    got = ops.attention(q, k, v, n_heads0, kv_mul, hs, pos, slots, True, impl="mfma")
+    want = ops.ref_attention(q, k, v, n_heads0, kv_mul, hs, pos, slots)
+    assert rel(got, want) < 1.2e-2, rel(got, want)
+    # integer-valued small data: bf16-exact operands, so the MFMA path must match closely
+    k2 = torch.randint(-2, 3, k.shape, generator=g).float()
+    v2 = torch.randint(-4, 5, v.shape, generator=g).float()
+    q2 = torch.randint(-1, 2, q.shape, generator=g).float() * (hs ** 0.5) / 8
+    got2 = ops.attention(q2, k2, v2, n_heads0, kv_mul, hs, pos, slots, True, impl="mfma")
+    want2 = ops.ref_attention(q2, k2, v2, n_heads0, kv_mul, hs, pos, slots)
+    assert rel(got2, want2) < 1e-2, rel(got2, want2)
 
 
 def test_argmax_ties_lowest_index(ops):
