@@ -190,6 +190,7 @@ static void usage() {
                  "  --chat-template {llama2|llama3|deepSeek3}\n"
                  "  --max-seq-len <n> --max-batch <n> --slots <n>\n"
                  "  --kv-dtype {bf16|f32} --graph {0|1} --log-level {0|1|2}\n"
+                 "  --kv-pages <n> --kv-page-size <p>   (GPU paged KV cache: pool of n pages of p positions)\n"
                  "  --metrics <file|->                  (JSON line per forward)  --profile 1  (GPU kernel table)\n"
                  "  --synthetic {llama3_2_1b|llama3_1_8b|llama3_3_70b|llama3_1_405b}  (random-init weights)\n"
                  "  --net-turbo {0|1} --gpu-segments <a:b>  (accepted for compatibility)\n");

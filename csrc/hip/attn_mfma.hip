@@ -94,14 +94,20 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
     float m = -INFINITY, lsum = 0.f;
     // transposed-read address pieces of this lane (lane 4q + p of its 16-lane group h)
     const int tq = col >> 2, tp = col & 3;
-    int k = 0;
+    // Rounds of 4 tiles (wave w: tile 4 r + w), the same count on every wave: LDS-DMA data is ordered
+    // for a ds_read only by the issuing wave's counted vmcnt FOLLOWED BY a workgroup barrier
+    // (cdna_hip_programming.md, "Read a staged buffer one phase after the wait that retires it")
+    const int nRounds = (nTiles + kAmWaves - 1) / kAmWaves;
     if (wave < nTiles) issue(wave, 0);
     if (wave + kAmWaves < nTiles) issue(wave + kAmWaves, 1);
-    for (int i = wave; i < nTiles; i += kAmWaves, k++) {
+    for (int k = 0; k < nRounds; k++) {
+        const int i = k * kAmWaves + wave;
         if (i + kAmWaves < nTiles)
             asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile i landed, tile i + 4 in flight
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (i >= nTiles) continue;  // wave-uniform; the barrier above is reached by every wave
         const char *kb = wbuf + (k & 1) * 2 * kAmTileBytes, *vb = kb + kAmTileBytes;
         const int tb = t0 + kAmTile * i;
         f32x4 st[2];
@@ -115,6 +121,11 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
                 st[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], st[u], 0, 0, 0);
             }
         }
+#ifdef DL_AM_DEBUG
+        if (g == 0 && c == 0 && b == 0 && i == 0)
+            for (int u = 0; u < 2; u++)
+                for (int e = 0; e < 4; e++) a.partO[(16 * u + 4 * h + e) * 16 + col] = st[u][e];
+#endif
         float mx = -INFINITY;
 #pragma unroll
         for (int u = 0; u < 2; u++)
@@ -160,12 +171,20 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
                     }
                 }
             }
-            bf16x8 vf;
-#pragma unroll
-            for (int e = 0; e < 4; e++) {
-                vf[e] = __builtin_bit_cast(__bf16, vv[0][e]);
-                vf[4 + e] = __builtin_bit_cast(__bf16, vv[1][e]);
-            }
+            // whole-register bit casts (per-element short -> __bf16 inserts were miscompiled by
+            // ROCm 7.2's hipcc into a broadcast of element 0: scripts/probe_attn.hip)
+            const u32x2 lo = __builtin_bit_cast(u32x2, vv[0]), hi = __builtin_bit_cast(u32x2, vv[1]);
+            const bf16x8 vf = __builtin_bit_cast(bf16x8, u32x4{lo.x, lo.y, hi.x, hi.y});
+#ifdef DL_AM_DEBUG
+            if (g == 0 && c == 0 && b == 0 && i == 0 && n == 0)
+                for (int e = 0; e < 8; e++) {
+                    a.partO[8192 + lane * 8 + e] = (float)vf[e];
+                    a.partO[12288 + lane * 8 + e] = (float)pf[e];
+                }
+            if (g == 0 && c == 0 && b == 0 && i == 0 && n == 0)  // raw V tile rows 0..3, LDS order
+                for (int e = lane; e < 4 * 128; e += 64)
+                    a.partO[16384 + e] = __uint_as_float((uint32_t)reinterpret_cast<const uint16_t *>(vb)[e] << 16);
+#endif
             o[n] *= corr;
             o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[n], 0, 0, 0);
         }
@@ -175,6 +194,14 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
     }
     lsum += __shfl_xor(lsum, 16);
     lsum += __shfl_xor(lsum, 32);
+#ifdef DL_AM_DEBUG
+    if (g == 0 && c == 0 && b == 0 && wave == 0) {
+        for (int n = 0; n < NT; n++)
+            for (int e = 0; e < 4; e++) a.partO[1024 + (16 * n + 4 * h + e) * 16 + col] = o[n][e];
+        a.partO[4096 + lane * 2] = m;
+        a.partO[4096 + lane * 2 + 1] = lsum;
+    }
+#endif
 
     // merge the waves (LDS: the tile buffers are free once every wave is past its loop)
     __syncthreads();
@@ -236,7 +263,8 @@ static int attnMfmaMode() {
 bool attnUsesMfma(const AttnArgs &a) {
     const int mode = attnMfmaMode();
     if (mode == 0 || !attnMfmaSupported(a)) return false;
-    return mode == 1 || a.seqLen >= 1024;
+    if (mode == 1) return true;
+    return a.mfma >= 0 ? a.mfma == 1 : a.seqLen >= 1024;
 }
 
 static bool attnTrRead() {

@@ -1115,22 +1115,40 @@ __device__ __forceinline__ bool attnFinish(const AttnArgs &a, int b, int hgIdx, 
         mlL[tid * 2 + 1] = Ls;
     }
     __syncthreads();
-    constexpr int U = 8;
-    for (int i = tid; i < HG * HS; i += AT) {
-        const int h = i / HS, d = i % HS;
+    // Weighted sum of the chunks' partial outputs: (item = 4 dims of one head) x (part = a strided
+    // subset of the chunks) per thread, the `parts` threads of an item adjacent lanes, every load
+    // of a thread (16-B coherence-point loads, sc1 like the atomic loads above) in flight at once,
+    // then a fixed butterfly over the parts (deterministic). One memory round trip for <= 8 chunks
+    // per thread instead of one per 8 chunks of a head dimension (long contexts: 32 chunks).
+    constexpr int U = 8, ITEMS = HG * (HS / 4), PARTS = ITEMS >= AT ? 1 : AT / ITEMS;
+    for (int base = 0; base < ITEMS * PARTS; base += AT) {
+        const int t = base + tid, item = t / PARTS, part = t % PARTS;
+        const int h = min(item, ITEMS - 1) / (HS / 4), d = (min(item, ITEMS - 1) % (HS / 4)) * 4;
         const float *po = a.partO + (pbase + (size_t)h * G) * HS + d;
         const float *wv = scratch + 2 * h * G;
-        float acc = 0.f;
-        int cc = 0;
-        for (; cc + U <= nSplit; cc += U) {
-            float v[U];
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int c0 = part; c0 < nSplit; c0 += U * PARTS) {
+            f32x4 v[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) v[u] = ld(po + (size_t)(cc + u) * HS);
+            for (int u = 0; u < U; u++) {
+                const int cc = min(c0 + u * PARTS, nSplit - 1);
+                asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v[u]) : "v"(po + (size_t)cc * HS));
+            }
 #pragma unroll
-            for (int u = 0; u < U; u++) acc += wv[2 * (cc + u)] * v[u];
+            for (int u = 0; u < U; u++) {  // each wait pins its own load's registers (no early use)
+                asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v[u]) : "i"(U - 1 - u) : "memory");
+                if (c0 + u * PARTS < nSplit) acc += wv[2 * (c0 + u * PARTS)] * v[u];
+            }
         }
-        for (; cc < nSplit; cc++) acc += wv[2 * cc] * ld(po + (size_t)cc * HS);
-        redL[i] = acc / mlL[h * 2 + 1];
+#pragma unroll
+        for (int off = 1; off < PARTS; off <<= 1)
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[j] += __shfl_xor(acc[j], off);
+        if (part == 0 && item < ITEMS) {
+            const float il = 1.0f / mlL[h * 2 + 1];
+#pragma unroll
+            for (int j = 0; j < 4; j++) redL[h * HS + d + j] = acc[j] * il;
+        }
     }
     __syncthreads();
     attnWriteOut<HG, HS, AT, WT>(a, b, head0, redL);

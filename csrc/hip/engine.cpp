@@ -808,6 +808,12 @@ class HipEngineImpl : public HipEngine {
             DL_CHECK(slots[b] >= 0 && (u32)slots[b] < cfg_.nSlots, "slot out of range");
         }
         mapPages(n, positions, slots, ahead);
+        // decode attention kernel for this forward (part of the graph key): the MFMA kernel once a
+        // row's context reaches kAttnMfmaMinPos keys (measured faster from ~1.5K keys, slower on
+        // short contexts: profiles/r3_prefill_attention.md), else the VALU kernel
+        int maxPos = 0;
+        for (int b = 0; b < n; b++) maxPos = std::max(maxPos, positions[b] + ahead);
+        attnLong_ = maxPos >= kAttnMfmaMinPos;
         const u32 MB = cfg_.maxBatch;
         // keep the pinned staging buffer stable while a previous copy may still read it (every
         // public entry point ends with a stream sync, so this only waits after an async path)
@@ -835,7 +841,7 @@ class HipEngineImpl : public HipEngine {
             enqueueForward(n, kind);
             return;
         }
-        const int key = (n * 4 + (int)kind) * 2 + (prefillOk_ ? 1 : 0);
+        const int key = ((n * 4 + (int)kind) * 2 + (prefillOk_ ? 1 : 0)) * 2 + (attnLong_ ? 1 : 0);
         auto it = graphs_.find(key);
         if (it == graphs_.end()) {
             // capture on the second use of a shape: a one-off row count (the tail chunk of a prompt,
@@ -1008,6 +1014,7 @@ class HipEngineImpl : public HipEngine {
         a.outH = bat ? dAttH_ : nullptr;
         a.ldOut = p.q0;
         a.kvBf16 = kvBf16_ ? 1 : 0;
+        a.mfma = attnLong_ ? 1 : 0;
         a.counters = dAttCnt_;
         return a;
     }
@@ -1450,6 +1457,8 @@ class HipEngineImpl : public HipEngine {
     int *dBlockErr_ = nullptr;
     bool blockOn_ = false;  // decode rows run the fused attention block (setupAttnBlock)
     bool ffnOn_ = false;
+    static constexpr int kAttnMfmaMinPos = 1024;
+    bool attnLong_ = false;  // this forward's decode attention runs the MFMA kernel (setInputs)
     // paged KV cache (setupPages / mapPages)
     int *dKvTable_ = nullptr;
     int *hTableStage_[2] = {nullptr, nullptr};

@@ -83,6 +83,7 @@ struct AttnArgs {
     float2 *outS = nullptr;
     int ldOut = 0;
     int kvBf16 = 1;
+    int mfma = -1;              // decode kernel: 1 MFMA, 0 VALU, -1 by cache length (attnUsesMfma)
     int *counters = nullptr;    // [B][nHeads0/HG] arrival counters (zero-initialised, self-resetting)
     // optional MALL warm-up run by extra workgroups of the same launch (weights of the next GEMVs)
     const void *pf0 = nullptr, *pf1 = nullptr;
