@@ -10,13 +10,14 @@
 //
 // Workgroup: 256 threads = 4 waves in a 2 x 2 arrangement, wave (wr, wt) owning rows
 // [64 wr, 64 wr + 64) x tokens [64 wt, 64 wt + 64) of the tile: 4 x 4 accumulators of
-// v_mfma_f32_16x16x32_f16 (64 VGPRs). K advances one Q40 block (32) per pipeline stage; a stage
-// holds the tile's 128 weight rows (16 B each), their f16 scales (u32 pairs) and the 128 tokens'
-// 32 f16 activations, copied HBM/L2 -> LDS by global_load_lds (3 wave-instructions per thread per
-// stage, 6 stages = 5 blocks in flight, ~54 KB per workgroup). Per block a wave dequantizes its 4
-// weight fragments once (nibbles -> f16, gemm_dev.h) and reuses each for 4 token fragments.
-// LDS images are bank-conflict free: weight rows are 16 B apart (a wave's ds_read_b64 covers 256
-// contiguous bytes), activation units of token t sit at position h ^ ((t >> 1) & 3).
+// v_mfma_f32_16x16x32_f16 (64 VGPRs). K advances two Q40 blocks (64) per pipeline stage; a stage
+// holds the tile's 128 weight rows (2 x 16 B each), their f16 scales (u32 pairs) and the 128
+// tokens' 64 f16 activations, copied HBM/L2 -> LDS by global_load_lds (6 wave-instructions per
+// thread per stage, 3 stages = 2 in flight, ~43 KB per workgroup; one block per stage measured
+// slower: twice the barriers). Per block a wave dequantizes its 4 weight fragments once (nibbles
+// -> f16, gemm_dev.h) and reuses each for 4 token fragments. LDS images are bank-conflict free:
+// a row's two 16-B units swap places for rows 8..15 of each 16 (ds_read_b64 of 16 rows x 2 halves
+// covers all 64 banks), activation unit u of token t sits at position u ^ ((t >> 1) & 7).
 // The grid is mapped XCD-aware: consecutive logical workgroups (the token tiles and K splits of one
 // row tile, which share weights) are dispatched to the same XCD (its L2).
 // Split-K (thin matrices: wo, w2, qkv) stores partials with write-through stores; the last arriving
@@ -29,10 +30,10 @@
 namespace dl {
 namespace hipk {
 
-static constexpr int kWRows = 128, kWTok = 128, kWStages = 6, kWNld = 3;
-static constexpr int kWStW = kWRows * 16;   // [128 rows][16 B]
-static constexpr int kWStD = 2 * 64 * 4;    // [64 row pairs] u32 scales + a dummy copy (wave 3)
-static constexpr int kWStX = kWTok * 64;    // [128 tokens][4 x 16 B], swizzled
+static constexpr int kWRows = 128, kWTok = 128, kWKB = 2, kWStages = 3, kWNld = 6;
+static constexpr int kWStW = kWRows * kWKB * 16;   // [128 rows][2 blocks] x 16 B
+static constexpr int kWStD = 2 * kWKB * 64 * 4;    // [2 blocks][64 row pairs] u32 scales + a dummy copy
+static constexpr int kWStX = kWTok * kWKB * 64;    // [128 tokens][8 x 16 B], swizzled
 static constexpr int kWStage = kWStW + kWStD + kWStX;
 static constexpr int kWTileLd = kWRows + 4;  // padded f32 row stride of the output tile
 static constexpr int kWMain = kWStages * kWStage > kWTok * kWTileLd * 4 ? kWStages * kWStage : kWTok * kWTileLd * 4;
@@ -59,7 +60,7 @@ bool gemmUsesWide(int M) { return gemmWideOn() && M >= gemmWideMin(); }
 int gemmWideSplits(int rows, int n, int M) {
     const int rowTiles = (rows + kWRows - 1) / kWRows, tokTiles = (M + kWTok - 1) / kWTok, nb = n / 32;
     int S = 1;
-    while (S < 4 && rowTiles * tokTiles * S < 256 && nb % (2 * S) == 0 && nb / (2 * S) >= 16) S *= 2;
+    while (S < 4 && rowTiles * tokTiles * S < 256 && nb % (4 * S) == 0 && nb / (2 * S) >= 16) S *= 2;
     return S;
 }
 
@@ -98,24 +99,26 @@ __global__ __launch_bounds__(kThreads) void gemmWideKernel(GemmArgs ga, int rowT
     const uint8_t *qs = a.qs;
     const uint32_t *wd2 = reinterpret_cast<const uint32_t *>(a.wd);
 
-    // global -> LDS copies of block j into stage buffer b (3 wave-instructions per thread)
+    // global -> LDS copies of blocks j, j+1 into stage buffer b (6 wave-instructions per thread)
     auto issue = [&](int j, int b) {
         char *st = smem + b * kWStage;
-        if (wave < 2) {  // weights: lane = row (tiled 16-B unit of (row, j), GEMV layout)
-            const int row = min(R0 + wave * 64 + lane, a.rows - 1);
+        {  // weights: slot s = wave * 64 + lane -> row s / 2, position s & 1 holds block (s & 1) ^ ((row >> 3) & 1)
+            const int sl = wave * 64 + lane, rl = sl >> 1, jb = j + ((sl & 1) ^ ((rl >> 3) & 1));
+            const int row = min(R0 + rl, a.rows - 1);
             const int g = row / (2 * NG), rm = row % (2 * NG), gi = rm >> 1, rpar = rm & 1;
-            const size_t unit = (((size_t)g * KS + (j >> lgL)) * 2 + rpar) * kThreads + gi * Ln + (j & (Ln - 1));
+            const size_t unit = (((size_t)g * KS + (jb >> lgL)) * 2 + rpar) * kThreads + gi * Ln + (jb & (Ln - 1));
             glds16(qs + unit * 16, st + wave * 1024);
-        } else {  // scales: lane = row pair (wave 3 repeats wave 2's copy into a dummy slot)
-            const int row = min(R0 + 2 * lane, a.rows - 1);
+        }
+        {  // scales of block j + (wave & 1): lane = row pair (waves 2, 3 repeat into a dummy copy)
+            const int jb = j + (wave & 1), row = min(R0 + 2 * lane, a.rows - 1);
             const int g = row / (2 * NG), gi = (row % (2 * NG)) >> 1;
-            glds4(wd2 + ((size_t)g * KS + (j >> lgL)) * kThreads + gi * Ln + (j & (Ln - 1)),
-                  st + kWStW + (wave - 2) * 256);
+            glds4(wd2 + ((size_t)g * KS + (jb >> lgL)) * kThreads + gi * Ln + (jb & (Ln - 1)), st + kWStW + wave * 256);
         }
 #pragma unroll
-        for (int q = 0; q < 2; q++) {  // activations: 8 wave-instructions of 64 x 16 B
-            const int k = wave + 4 * q, slot = k * 64 + lane, t = slot >> 2, u = (slot & 3) ^ ((t >> 1) & 3);
-            glds16(ga.x + (size_t)(T0 + t) * n + (size_t)j * 32 + u * 8, st + kWStW + kWStD + k * 1024);
+        for (int q = 0; q < 4; q++) {  // activations: 16 wave-instructions of 64 x 16 B
+            const int k = wave + 4 * q, slot = k * 64 + lane, t = slot >> 3, u = (slot & 7) ^ ((t >> 1) & 7);
+            glds16(ga.x + (size_t)(T0 + t) * n + (size_t)(j + (u >> 2)) * 32 + (u & 3) * 8,
+                   st + kWStW + kWStD + k * 1024);
         }
     };
 
@@ -126,35 +129,36 @@ __global__ __launch_bounds__(kThreads) void gemmWideKernel(GemmArgs ga, int rowT
         for (int t = 0; t < 4; t++) acc[f][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int byteHalf = h & 1, nibHi = h >> 1;
     constexpr int PF = kWStages - 1;
-    for (int c = 0; c < PF && c < bps; c++) issue(j0 + c, c);
-    for (int c = 0; c < bps; c++) {
-        if (c + PF < bps) issue(j0 + c + PF, (c + PF) % kWStages);
-        // block c landed for this thread (the younger blocks may stay in flight), then for all
-        switch (min(bps - 1, c + PF) - c) {
-            case 5: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(5 * kWNld) : "memory"); break;
-            case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(4 * kWNld) : "memory"); break;
-            case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(3 * kWNld) : "memory"); break;
+    const int nch = bps / kWKB;
+    for (int c = 0; c < PF && c < nch; c++) issue(j0 + kWKB * c, c);
+    for (int c = 0; c < nch; c++) {
+        if (c + PF < nch) issue(j0 + kWKB * (c + PF), (c + PF) % kWStages);
+        // chunk c landed for this thread (the younger chunks may stay in flight), then for all
+        switch (min(nch - 1, c + PF) - c) {
             case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * kWNld) : "memory"); break;
             case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kWNld) : "memory"); break;
             default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
         }
         __builtin_amdgcn_s_barrier();
         const char *st = smem + (c % kWStages) * kWStage;
-        half8 b[4];
 #pragma unroll
-        for (int f = 0; f < 4; f++) {
-            const int rl = wr * 64 + f * 16 + col;
-            const u32x2 wv = *reinterpret_cast<const u32x2 *>(st + rl * 16 + byteHalf * 8);
-            const uint32_t dw = *reinterpret_cast<const uint32_t *>(st + kWStW + (rl >> 1) * 4);
-            b[f] = dequantQ40x8(wv, nibHi, (rl & 1) ? dw >> 16 : dw & 0xFFFFu);
-        }
+        for (int kb = 0; kb < kWKB; kb++) {
+            half8 b[4];
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const int tok = wt * 64 + t * 16 + col;
-            const half8 av =
-                *reinterpret_cast<const half8 *>(st + kWStW + kWStD + (tok * 4 + (h ^ ((tok >> 1) & 3))) * 16);
+            for (int f = 0; f < 4; f++) {
+                const int rl = wr * 64 + f * 16 + col;
+                const u32x2 wv = *reinterpret_cast<const u32x2 *>(st + (rl * 2 + (kb ^ ((rl >> 3) & 1))) * 16 + byteHalf * 8);
+                const uint32_t dw = *reinterpret_cast<const uint32_t *>(st + kWStW + (kb * 64 + (rl >> 1)) * 4);
+                b[f] = dequantQ40x8(wv, nibHi, (rl & 1) ? dw >> 16 : dw & 0xFFFFu);
+            }
 #pragma unroll
-            for (int f = 0; f < 4; f++) acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b[f], acc[f][t], 0, 0, 0);
+            for (int t = 0; t < 4; t++) {
+                const int tok = wt * 64 + t * 16 + col;
+                const half8 av = *reinterpret_cast<const half8 *>(st + kWStW + kWStD +
+                                                                 (tok * 8 + ((kb * 4 + h) ^ ((tok >> 1) & 7))) * 16);
+#pragma unroll
+                for (int f = 0; f < 4; f++) acc[f][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b[f], acc[f][t], 0, 0, 0);
+            }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // stage c % kWStages is refilled at iteration c + 1
@@ -193,7 +197,7 @@ __global__ __launch_bounds__(kThreads) void gemmWideKernel(GemmArgs ga, int rowT
 
 void launchGemmWide(const GemmArgs &ga, int epi, hipStream_t s) {
     const int rowTiles = (ga.e.rows + kWRows - 1) / kWRows, tokTiles = (ga.M + kWTok - 1) / kWTok;
-    if (ga.e.n % 32 != 0 || (ga.e.n / 32) % ga.splits != 0) throw Error("launchGemmWide: bad K split");
+    if (ga.e.n % 64 != 0 || (ga.e.n / 32) % (kWKB * ga.splits) != 0) throw Error("launchGemmWide: bad K split");
     if (ga.splits > 1 && (!ga.part || !ga.counters)) throw Error("launchGemmWide: split-K without buffers");
     const dim3 grid(rowTiles * tokTiles * ga.splits);
 #define DL_GEMMW_CASE(E)                                                                              \

@@ -1,12 +1,13 @@
 #!/bin/bash
-# Round-3 iteration: attention tests, VALU vs MFMA decode-attention microbench, long-context bench.
+# Round-3 iteration: wide GEMM (2 blocks per stage) tests and prefill points.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/${1:-r3dbg3}
+O=$R/gpurun_out/${1:-r3dbg4}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest $R/tests/test_gpu_ops.py $R/tests/test_gpu_engine.py -q --timeout 120 --timeout-method thread -k "attention or long_context or decode or greedy or paged" > $O/tests.log 2>&1
-for m in 0 1; do
-  DL_ATTN_MFMA=$m timeout -k 10 200 python -u $R/scripts/bench_attn.py > $O/attn_mfma$m.log 2>&1 || exit $?
+timeout -k 10 400 python -u -m pytest $R/tests/test_gpu_ops.py $R/tests/test_gpu_engine.py -x -q --timeout 120 --timeout-method thread -k "gemm or batched or prefill or wide or outlier or slots or paged" > $O/tests.log 2>&1 || exit $?
+for c in 256 1024; do
+  timeout -k 10 200 python -u $R/bench.py --steps 8 --warmup 2 --no-cli --long-ctx 0 --no-f32kv --prefill-chunk $c > $O/bench_c$c.log 2>&1 || exit $?
 done
-timeout -k 10 300 python -u $R/bench.py --steps 64 --warmup 8 --no-cli --no-f32kv --no-prefill4k > $O/bench.log 2>&1 || exit $?
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof_pf -- python3 $R/bench.py --steps 4 --warmup 1 --no-cli --long-ctx 0 --no-f32kv --prefill-chunk 1024 > $O/prof_pf.log 2>&1 || exit $?
+python3 $R/scripts/prof_summary.py $O/prof_pf > $O/prof_pf.md 2>&1
 exit 0
