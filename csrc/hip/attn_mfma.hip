@@ -245,6 +245,258 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
     attnFinish<KM, HS, kAmThreads>(a, b, g, c, nSplit, redL, mlL, flagL, scratch);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Prefill attention with the same staging (the batched path's rows; reference: the per-row causal
+// attention of nn-cpu-ops.cpp:1135-1161 for every prompt row). A workgroup owns one KV head and a
+// block of 4 x 16 / kvMul rows of one slot: wave w's 16 MFMA columns are (row, query head) pairs, so
+// every S^T / O^T MFMA is fully used, and all 4 waves read every K / V tile of the chunk from LDS.
+// The chunk's tiles are DMA'd in rounds of 4 (wave w copies tile 4 r + w), two rounds in flight
+// (128 KB of LDS); the previous kernel (kernels.hip attnPrefillKernel) staged one 32-key tile ahead
+// through registers with a transposing LDS scatter for V. Causal mask per column (key <= the row's
+// position); chunks of long contexts combine through the last arriver as before.
+// ------------------------------------------------------------------------------------------------
+static constexpr int kApRound = 4;  // tiles per round (one per wave)
+static constexpr size_t kApLds = 2 * kApRound * 2 * kAmTileBytes + 64;
+
+template <int KM>
+__global__ __launch_bounds__(kAmThreads) void attnPrefillDmaKernel(AttnArgs a, int nRows) {
+    constexpr int HS = kAmHS, DS = HS / 32, NT = HS / 16, RPW = 16 / KM, RPB = kAmWaves * RPW;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int nKv = a.nHeads0 / KM;
+    const int g = blockIdx.x % nKv, rb = blockIdx.x / nKv, c = blockIdx.y;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, col = lane & 15, h = lane >> 4;
+    const int b0 = rb * RPB;
+    int maxLen = 0;
+    for (int r = 0; r < RPB && b0 + r < nRows; r++) maxLen = max(maxLen, a.pos[b0 + r] + 1);
+    int nSplit = (maxLen + 255) / 256;
+    nSplit = max(1, min(min(nSplit, a.splitGrid), HS / 2));  // combine weights: 64 columns x nSplit in LDS
+    const int ch = ((maxLen + nSplit - 1) / nSplit + kAmTile - 1) / kAmTile * kAmTile;
+    if (c >= nSplit) return;
+    const int k0 = c * ch, k1 = min(k0 + ch, maxLen);
+    const int sl = a.slot[b0];  // every row of the block (host-checked)
+    const int row = b0 + wave * RPW + col / KM, head = g * KM + col % KM;
+    const bool rowOk = row < nRows;
+    const int myLen = rowOk ? a.pos[row] + 1 : 0;
+    const float scale = 1.0f / sqrtf((float)HS);
+    bf16x8 qf[DS];
+#pragma unroll
+    for (int s = 0; s < DS; s++) {
+        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (rowOk) {
+            const float *qp = a.q + (size_t)row * a.ldq + (size_t)head * HS + 32 * s + 8 * h;
+            const float4 x0 = ld4(qp), x1 = ld4(qp + 4);
+            v[0] = x0.x * scale; v[1] = x0.y * scale; v[2] = x0.z * scale; v[3] = x0.w * scale;
+            v[4] = x1.x * scale; v[5] = x1.y * scale; v[6] = x1.z * scale; v[7] = x1.w * scale;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) qf[s][j] = (__bf16)v[j];
+    }
+    const uint16_t *kc = reinterpret_cast<const uint16_t *>(a.kcache);
+    const uint16_t *vc = reinterpret_cast<const uint16_t *>(a.vcache);
+    const size_t kvBase = (size_t)g * HS;
+    const int nTiles = (k1 - k0 + kAmTile - 1) / kAmTile, nRounds = (nTiles + kApRound - 1) / kApRound;
+    auto tileBuf = [&](int bf, int tt) { return smem + (size_t)(bf * kApRound + tt) * 2 * kAmTileBytes; };
+    // wave w copies tile kApRound * r + w of round r into buffer bf (16 wave-instructions, or none)
+    auto issue = [&](int r, int bf) {
+        const int t = kApRound * r + wave;
+        if (t >= nTiles) return;
+        char *kb = tileBuf(bf, wave), *vb = kb + kAmTileBytes;
+#pragma unroll
+        for (int j = 0; j < kAmTile / 4; j++) {
+            const int rr = 4 * j + (lane >> 4), p = lane & 15;
+            const int key = min(k0 + kAmTile * t + rr, k1 - 1);  // past the chunk: masked below
+            const size_t off = kvBase + kvRow(a.kvMap, a.seqLen, sl, key) * a.kv0 + (size_t)(p ^ amSwz(rr)) * 8;
+            __builtin_amdgcn_global_load_lds(const_cast<uint16_t *>(kc + off),
+                                             reinterpret_cast<__attribute__((address_space(3))) void *>(
+                                                 reinterpret_cast<uintptr_t>(kb + j * 1024)), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(const_cast<uint16_t *>(vc + off),
+                                             reinterpret_cast<__attribute__((address_space(3))) void *>(
+                                                 reinterpret_cast<uintptr_t>(vb + j * 1024)), 16, 0, 0);
+        }
+    };
+    f32x4 o[NT];
+#pragma unroll
+    for (int n = 0; n < NT; n++) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, lsum = 0.f;
+    const int tq = col >> 2, tp = col & 3;
+    issue(0, 0);
+    if (nRounds > 1) issue(1, 1);
+    for (int r = 0; r < nRounds; r++) {
+        // this wave's copy of round r landed (round r + 1's may stay in flight), then every wave's
+        if (r + 1 < nRounds && kApRound * (r + 1) + wave < nTiles)
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        for (int tt = 0; tt < kApRound; tt++) {
+            const int t = kApRound * r + tt;
+            if (t >= nTiles) break;  // uniform over the workgroup
+            const char *kb = tileBuf(r & 1, tt), *vb = kb + kAmTileBytes;
+            const int tb = k0 + kAmTile * t;
+            f32x4 st[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                st[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+                const int rr = 16 * u + col;
+#pragma unroll
+                for (int s = 0; s < DS; s++) {
+                    const bf16x8 kf = *reinterpret_cast<const bf16x8 *>(kb + rr * 256 + 16 * ((4 * s + h) ^ amSwz(rr)));
+                    st[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[s], st[u], 0, 0, 0);
+                }
+            }
+            float mx = -INFINITY;
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int key = tb + 16 * u + 4 * h + e;
+                    if (key >= k1 || key >= myLen) st[u][e] = -INFINITY;
+                    mx = fmaxf(mx, st[u][e]);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 16));
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            const float mn = fmaxf(m, mx);
+            const float corr = m == -INFINITY ? 0.f : __expf(m - mn);
+            bf16x8 pf;
+            float ps = 0.f;
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const float p = st[u][e] == -INFINITY ? 0.f : __expf(st[u][e] - mn);
+                    ps += p;
+                    pf[4 * u + e] = (__bf16)p;
+                }
+            lsum = lsum * corr + ps;
+            m = mn;
+#pragma unroll
+            for (int n = 0; n < NT; n++) {
+                s16x4 vv[2];
+#pragma unroll
+                for (int u = 0; u < 2; u++) {
+                    const int rr = 16 * u + 4 * h + tq;
+                    const char *ad = vb + rr * 256 + 16 * ((2 * n + (tp >> 1)) ^ amSwz(rr)) + 8 * (tp & 1);
+                    vv[u] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        reinterpret_cast<__attribute__((address_space(3))) s16x4 *>(reinterpret_cast<uintptr_t>(ad)));
+                }
+                const u32x2 lo = __builtin_bit_cast(u32x2, vv[0]), hi = __builtin_bit_cast(u32x2, vv[1]);
+                const bf16x8 vf = __builtin_bit_cast(bf16x8, u32x4{lo.x, lo.y, hi.x, hi.y});
+                o[n] *= corr;
+                o[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[n], 0, 0, 0);
+            }
+        }
+        // every wave's reads of buffer r & 1 retired before round r + 2 is copied into it
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (r + 2 < nRounds) issue(r + 2, r & 1);
+    }
+    lsum += __shfl_xor(lsum, 16);
+    lsum += __shfl_xor(lsum, 32);
+    // O^T accumulators: lane holds O[column][dim 16 n + 4 h + e]
+    auto writeOut = [&](int rw, int hd, int d, const float (&v)[4]) {
+        const size_t at = (size_t)rw * a.ldOut + (size_t)hd * HS + d;
+        if (a.outH) {
+            typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<h4 *>(a.outH + at) = h4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+        } else {
+            *reinterpret_cast<float4 *>(a.out + at) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    };
+    if (nSplit == 1) {
+        if (rowOk) {
+            const float il = lsum > 0.f ? 1.0f / lsum : 0.f;
+#pragma unroll
+            for (int n = 0; n < NT; n++) {
+                const float v[4] = {o[n][0] * il, o[n][1] * il, o[n][2] * il, o[n][3] * il};
+                writeOut(row, head, 16 * n + 4 * h, v);
+            }
+        }
+        return;
+    }
+    // several chunks: publish (fence-free, gemm_dev.h pattern: write-through stores, drained, then
+    // the arrival count), the last arriver combines in chunk order
+    const int G = a.splitGrid;
+    if (rowOk) {
+        const size_t pb = ((size_t)row * a.nHeads0 + head) * G + c;
+#pragma unroll
+        for (int n = 0; n < NT; n++)
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+                __hip_atomic_store(a.partO + pb * HS + 16 * n + 4 * h + e, o[n][e], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        if (h == 0) {
+            __hip_atomic_store(a.partML + pb * 2, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.partML + pb * 2 + 1, lsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int *flagL = reinterpret_cast<int *>(smem + 2 * kApRound * 2 * kAmTileBytes);
+    int *cnt = a.counters + (size_t)rb * nKv + g;
+    if (tid == 0) flagL[0] = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nSplit - 1;
+    __syncthreads();
+    if (!flagL[0]) return;
+    if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    auto ld = [](const float *q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    constexpr int nCol = RPB * KM;  // 64 columns
+    float *wts = reinterpret_cast<float *>(smem);  // [nCol][nSplit] (the tiles are free)
+    float *tot = wts + nCol * (HS / 2);            // [nCol]
+    if (tid < nCol) {
+        const int rw = b0 + tid / KM, hd = g * KM + tid % KM;
+        float M = -INFINITY, L = 0.f;
+        if (rw < nRows) {
+            const float *ml = a.partML + ((size_t)rw * a.nHeads0 + hd) * G * 2;
+            for (int cc = 0; cc < nSplit; cc++) M = fmaxf(M, ld(ml + 2 * cc));
+            for (int cc = 0; cc < nSplit; cc++) {
+                const float mc = ld(ml + 2 * cc);
+                const float w = (M == -INFINITY || mc == -INFINITY) ? 0.f : __expf(mc - M);
+                wts[tid * nSplit + cc] = w;
+                L += w * ld(ml + 2 * cc + 1);
+            }
+        }
+        tot[tid] = L;
+    }
+    __syncthreads();
+    for (int i = tid; i < nCol * (HS / 4); i += kAmThreads) {
+        const int cl = i / (HS / 4), d = (i % (HS / 4)) * 4;
+        const int rw = b0 + cl / KM, hd = g * KM + cl % KM;
+        if (rw >= nRows) continue;
+        const float *po = a.partO + ((size_t)rw * a.nHeads0 + hd) * G * HS + d;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int cc = 0; cc < nSplit; cc++) {
+            const float w = wts[cl * nSplit + cc];
+            const float *x = po + (size_t)cc * HS;
+            acc[0] += w * ld(x); acc[1] += w * ld(x + 1); acc[2] += w * ld(x + 2); acc[3] += w * ld(x + 3);
+        }
+        const float il = tot[cl] > 0.f ? 1.0f / tot[cl] : 0.f;
+        const float v[4] = {acc[0] * il, acc[1] * il, acc[2] * il, acc[3] * il};
+        writeOut(rw, hd, d, v);
+    }
+}
+
+bool attnPrefillDmaSupported(const AttnArgs &a) {
+    static const bool on = [] {
+        const char *e = std::getenv("DL_PF_ATTN_DMA");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on && a.kvBf16 && a.hs == kAmHS && (a.kvMul == 1 || a.kvMul == 2 || a.kvMul == 4 || a.kvMul == 8 ||
+                                                a.kvMul == 16);
+}
+
+void launchAttentionPrefillDma(const AttnArgs &a, int nRows, hipStream_t s) {
+    const int nKv = a.nHeads0 / a.kvMul, rpb = kAmWaves * (16 / a.kvMul);
+    const dim3 grid(nKv * ((nRows + rpb - 1) / rpb), a.splitGrid);
+#define DL_AP_CASE(K)                                                                                 \
+    if (a.kvMul == K) {                                                                               \
+        allowLds((const void *)attnPrefillDmaKernel<K>, kApLds);                                      \
+        hipLaunchKernelGGL((attnPrefillDmaKernel<K>), grid, dim3(kAmThreads), kApLds, s, a, nRows);   \
+        return;                                                                                       \
+    }
+    DL_AP_CASE(1) DL_AP_CASE(2) DL_AP_CASE(4) DL_AP_CASE(8) DL_AP_CASE(16)
+#undef DL_AP_CASE
+    throw Error("launchAttentionPrefillDma: unsupported kvMul");
+}
+
 bool attnMfmaSupported(const AttnArgs &a) {
     return a.kvBf16 && a.hs == kAmHS && (a.kvMul == 1 || a.kvMul == 2 || a.kvMul == 4 || a.kvMul == 8) &&
            a.nHeads0 % a.kvMul == 0 && a.pfBlocks == 0;

@@ -244,6 +244,10 @@ bool attnMfmaSupported(const AttnArgs &a);
 bool attnUsesMfma(const AttnArgs &a);
 void launchAttentionMfma(const AttnArgs &a, int B, hipStream_t s);
 void launchAttentionValu(const AttnArgs &a, int B, hipStream_t s);  // the VALU kernel (attnTask)
+// Prefill rows with LDS-DMA staged K / V (attn_mfma.hip; DL_PF_ATTN_DMA=0 keeps the register-staged
+// kernels.hip kernel): bf16 cache, head size 128, kvMul 1..16.
+bool attnPrefillDmaSupported(const AttnArgs &a);
+void launchAttentionPrefillDma(const AttnArgs &a, int nRows, hipStream_t s);
 
 // Fused attention block of one decode row (B = 1): the qkv GEMV (norm prologue, RoPE + KV append),
 // the decode attention and the wo GEMV in ONE launch, as three workgroup roles

@@ -502,6 +502,10 @@ __global__ __launch_bounds__(kPfThreads) void attnPrefillKernel(AttnArgs a, int 
 }
 
 void launchAttentionPrefill(const AttnArgs &a, int nRows, hipStream_t s) {
+    if (attnPrefillDmaSupported(a)) {  // LDS-DMA staged kernel (attn_mfma.hip)
+        launchAttentionPrefillDma(a, nRows, s);
+        return;
+    }
     const int nKv = a.nHeads0 / a.kvMul, rpb = attnPrefillRowsPerBlock(a.kvMul);
     const dim3 grid(nKv * ((nRows + rpb - 1) / rpb), a.splitGrid);
     if (a.hs == 128) hipLaunchKernelGGL(attnPrefillKernel<128>, grid, dim3(kPfThreads), 0, s, a, nRows);
