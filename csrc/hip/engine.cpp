@@ -121,6 +121,16 @@ class HipEngineImpl : public HipEngine {
     bool paged() const { return cfg_.kvPages > 0; }
     int kvPagesFree() const override { return paged() ? (int)freePages_.size() : -1; }
     int kvPageSize() const override { return paged() ? (int)cfg_.kvPageSize : 0; }
+    void releaseSlot(int slot) override {
+        if (!paged() || slot < 0 || (u32)slot >= cfg_.nSlots) return;
+        for (int i = 0; i < slotPages_[slot]; i++) {
+            int &e = hostTable_[(size_t)slot * pagesPerSlot_ + i];
+            freePages_.push_back(e);
+            e = -1;
+        }
+        if (slotPages_[slot]) tableDirty_ = true;  // uploaded with the next forward's mapping
+        slotPages_[slot] = 0;
+    }
     void setupPages() {
         if (!paged()) return;
         const u32 P = cfg_.kvPageSize;
@@ -151,7 +161,8 @@ class HipEngineImpl : public HipEngine {
     // (stream-ordered before the forward that reads it).
     void mapPages(int n, const int *positions, const int *slots, int ahead) {
         if (!paged()) return;
-        bool dirty = false;
+        bool dirty = tableDirty_;
+        tableDirty_ = false;
         auto release = [&](int s) {
             for (int i = 0; i < slotPages_[s]; i++) {
                 int &e = hostTable_[(size_t)s * pagesPerSlot_ + i];
@@ -1463,6 +1474,7 @@ class HipEngineImpl : public HipEngine {
     int *dKvTable_ = nullptr;
     int *hTableStage_[2] = {nullptr, nullptr};
     int tableFlip_ = 0, pageShift_ = 0, pagesPerSlot_ = 0;
+    bool tableDirty_ = false;
     std::vector<int> hostTable_, slotPages_, freePages_;
     int ffnSameWg_ = 0;     // DL_FFN_BLOCK=2: w13 and w2 rows on the same workgroups    // decode rows run the fused FFN block (setupFfnBlock)
     int ffnRingEarly_ = 0, ffnW13PassMul_ = 1;

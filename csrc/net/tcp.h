@@ -97,7 +97,9 @@ constexpr u32 kMeshMagic = 0xD11A3356;   // worker -> worker data-plane connecti
 constexpr u32 kProtoVersion = 1;
 constexpr u32 kAck = 23571114;           // same ACK value as the reference (nn-network.cpp:23)
 
-enum class Cmd : u32 { FORWARD = 1, FORWARD_ARGMAX = 2, STOP = 3, PING = 4, FORWARD_SAMPLE = 5 };
+// RELEASE: the first n ints of the payload are KV slots whose sequences ended (paged KV cache:
+// their pages return to the pool on every rank).
+enum class Cmd : u32 { FORWARD = 1, FORWARD_ARGMAX = 2, STOP = 3, PING = 4, FORWARD_SAMPLE = 5, RELEASE = 6 };
 
 struct ControlHeader {
     u32 cmd;

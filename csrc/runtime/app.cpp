@@ -251,6 +251,12 @@ void InferenceSession::sendControl(Cmd cmd, int n, const int *tokens, const int 
     for (auto &s : workers_) s.sendAll(buf.data(), buf.size() * sizeof(int));
 }
 
+void InferenceSession::releaseSlot(int slot) {
+    const int zero = 0;
+    sendControl(Cmd::RELEASE, 1, &slot, &zero, &zero);
+    backend_->releaseSlot(slot);
+}
+
 void InferenceSession::forward(int n, const int *tokens, const int *positions, const int *slots, float *logits) {
     TraceRange tr("dllama.forward");
     Timer t;
@@ -451,6 +457,8 @@ void runWorker(const AppArgs &args) {
                 } else if (cmd == Cmd::FORWARD_ARGMAX) {
                     ids.resize(n);
                     backend->forwardArgmax(n, &buf[0], &buf[n], &buf[2 * n], ids.data());
+                } else if (cmd == Cmd::RELEASE) {
+                    for (int i = 0; i < n; i++) backend->releaseSlot(buf[i]);
                 } else if (cmd == Cmd::FORWARD_SAMPLE) {
                     ids.resize(n);
                     specs.resize(n);

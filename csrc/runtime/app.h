@@ -67,6 +67,8 @@ class InferenceSession {
     int maxBatch() const { return maxBatch_; }
     // paged KV cache of the (root) backend: free pages and positions per page (-1 / 0: contiguous)
     int kvPagesFree() const { return backend_->kvPagesFree(); }
+    // a sequence ended: its KV slot's pages return to the pool on every rank (no-op when contiguous)
+    void releaseSlot(int slot);
     int kvPageSize() const { return backend_->kvPageSize(); }
     bool isGpu() const { return gpu_; }
     int nNodes() const { return 1 + (int)workers_.size(); }

@@ -88,6 +88,8 @@ class Backend {
     // (the scheduler admits requests by pages); -1 / 0 when the cache is contiguous per slot.
     virtual int kvPagesFree() const { return -1; }
     virtual int kvPageSize() const { return 0; }
+    // The sequence in this slot ended: a paged cache returns its pages to the pool (no-op otherwise).
+    virtual void releaseSlot(int slot) { (void)slot; }
     virtual std::string name() const = 0;
 
   protected:

@@ -109,6 +109,18 @@ void Scheduler::loop() {
     }
 }
 
+// Under mu_. A request's slot becomes free: its KV pages go back to the pool (every rank).
+void Scheduler::returnSlot(int slot) {
+    freeSlots_.push_back(slot);
+    if (pagesTotal_ >= 0 && slotPages_[slot]) {
+        try {
+            sess_.releaseSlot(slot);
+        } catch (const std::exception &) {  // a lost worker surfaces on the next forward
+        }
+        slotPages_[slot] = 0;
+    }
+}
+
 void Scheduler::failAll(const std::string &what) {
     std::lock_guard<std::mutex> lk(mu_);
     inflight_ = false;
@@ -117,9 +129,9 @@ void Scheduler::failAll(const std::string &what) {
         r->error = what;
         r->finished = true;
         r->finish("error");
-        freeSlots_.push_back(r->slot);
+        returnSlot(r->slot);
     }
-    for (auto &r : draining_) freeSlots_.push_back(r->slot);
+    for (auto &r : draining_) returnSlot(r->slot);
     active_.clear();
     draining_.clear();
 }
@@ -136,7 +148,7 @@ void Scheduler::finishRequest(const std::shared_ptr<GenRequest> &r, const char *
     if (inFlight)
         draining_.push_back(r);
     else
-        freeSlots_.push_back(r->slot);
+        returnSlot(r->slot);
     active_.erase(std::remove(active_.begin(), active_.end(), r), active_.end());
 }
 
@@ -165,7 +177,7 @@ bool Scheduler::step() {
         done.swap(flight_.picks);
         inflight_ = false;
         std::lock_guard<std::mutex> lk(mu_);
-        for (auto &r : draining_) freeSlots_.push_back(r->slot);  // their last rows have completed
+        for (auto &r : draining_) returnSlot(r->slot);  // their last rows have completed
         draining_.clear();
     }
 
@@ -192,7 +204,7 @@ bool Scheduler::step() {
             if (pagesTotal_ >= 0) {
                 const u64 span = r->params.maxTokens > 0 ? (u64)r->prompt.size() + (u64)r->params.maxTokens + 1 : seqLen;
                 const int need = (int)((std::min<u64>(span, seqLen) + pageSize_ - 1) / pageSize_);
-                int held = 0;
+                int held = 0;  // pages reserved by the active requests
                 for (int p : slotPages_) held += p;
                 if (need > pagesTotal_) {
                     queue_.pop_front();
@@ -200,7 +212,7 @@ bool Scheduler::step() {
                     r->finish("error");
                     continue;
                 }
-                if (need > pagesTotal_ - held + slotPages_[slot]) break;  // wait for pages
+                if (need > pagesTotal_ - held) break;  // wait for pages
                 slotPages_[slot] = need;
             }
             queue_.pop_front();

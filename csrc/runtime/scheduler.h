@@ -114,6 +114,7 @@ class Scheduler {
     // the engine when the slot's next request starts at position 0); admission needs enough pages
     int pagesTotal_ = -1, pageSize_ = 0;
     std::vector<int> slotPages_;
+    void returnSlot(int slot);
     Flight flight_;
     bool inflight_ = false;
     bool stop_ = false;

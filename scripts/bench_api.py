@@ -68,6 +68,9 @@ def main():
     ap.add_argument("--port", type=int, default=0)
     ap.add_argument("--max-batch", type=int, default=0,
                     help="rows per forward (default 4 x --n: prompts prefill in big chunks, MALL-resident weights)")
+    ap.add_argument("--kv-pages", type=int, default=0,
+                    help="paged KV cache: pool pages per layer (0: contiguous slots x seq_len)")
+    ap.add_argument("--kv-page-size", type=int, default=64)
     args = ap.parse_args()
     from distributed_llama_multiusers_amd.models.synthetic import make_tokenizer
     tmp = tempfile.mkdtemp()
@@ -77,6 +80,8 @@ def main():
     cmd = [os.path.join(REPO, "build", "dllama-api"), "--synthetic", "llama3_1_8b", "--tokenizer", tok,
            "--gpu-index", "0", "--port", str(port), "--slots", str(args.n), "--max-batch", str(args.max_batch or 4 * args.n),
            "--max-seq-len", str(64 + args.max_tokens + 32), "--buffer-float-type", "q80"]
+    if args.kv_pages:
+        cmd += ["--kv-pages", str(args.kv_pages), "--kv-page-size", str(args.kv_page_size)]
     log = open(os.path.join(tmp, "api.log"), "w")
     srv = subprocess.Popen(cmd, stdout=log, stderr=subprocess.STDOUT)
     try:
