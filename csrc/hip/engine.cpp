@@ -1174,7 +1174,24 @@ class HipEngineImpl : public HipEngine {
         float *resOut;
         const float *w;
     };
-    bool fuseNorm() const { return plan_.nRanks == 1 && fuseNormEnv_; }
+    // At TP > 1 the batched path keeps the fused residual + norm too when the wo / w2 tiles can be
+    // all-reduced inside their GEMM epilogue (GemmArgs::tpx over the fused exchange: narrow
+    // launches of <= 64 rows whose tile + Q80 staging fit the launch's LDS); otherwise a separate
+    // all-reduce kernel and a norm kernel follow each of them. DL_TP_BATCHED=0 disables it.
+    bool tpBatchedOk(int n) const {
+        static const bool on = [] {
+            const char *e = std::getenv("DL_TP_BATCHED");
+            return !(e && *e == '0');
+        }();
+        return on && tpFused_ && q40_ && !hipk::gemmUsesWide(n) &&
+               (size_t)n * h_.dim <= (size_t)tpVec_.stride && hipk::gemmTpxFits(n, plan_.nRanks, tpVec_.q80 != 0);
+    }
+    bool fuseNorm(int n) const { return fuseNormEnv_ && (plan_.nRanks == 1 || tpBatchedOk(n)); }
+
+  public:
+    bool tpBatchedFused(int n) const override { return plan_.nRanks > 1 && batchedPath(n) && fuseNorm(n); }
+
+  private:
 
     void gemmBatched(const DevMat &m, int n, int epi, const float *in, int ldIn, const float *add, float *xNext,
                      const float *normW, const _Float16 *xh, float *out, int ldOut, _Float16 *outH,
@@ -1229,6 +1246,10 @@ class HipEngineImpl : public HipEngine {
                 a.vcache = L->v;
                 a.kvBf16 = kvBf16_ ? 1 : 0;
             }
+            if (rf && plan_.nRanks > 1) {  // the residual update needs the rank-summed tile
+                g.tpx = 1;
+                a.tp = tpVec_;
+            }
             if (rf) {
                 g.resIn = rf->resIn + (size_t)c0 * ldOut;
                 g.resOut = rf->resOut + (size_t)c0 * ldOut;
@@ -1265,7 +1286,7 @@ class HipEngineImpl : public HipEngine {
         const int dim = h_.dim;
         int cur = 0;
         const bool bat = batchedPath(n);  // MFMA GEMMs on f16 activations instead of GEMVs
-        const bool fz = bat && fuseNorm();  // residual + norm carried by the GEMM epilogues
+        const bool fz = bat && fuseNorm(n);  // residual + norm carried by the GEMM epilogues
         const bool blk = blockOn_ && n == 1 && !bat;  // fused attention block per layer
         const bool fb = ffnOn_ && n == 1 && !bat;     // fused FFN block per layer
         {
@@ -1330,7 +1351,7 @@ class HipEngineImpl : public HipEngine {
                          nullptr, dY_, dim, nullptr, dAttQ_, dAttS_, nullptr, nullptr, fusedTp(bat));
             }
             }
-            if (!fusedTp(bat)) allReduce(dY_, (size_t)n * dim);
+            if (!fusedTp(bat) && !fz) allReduce(dY_, (size_t)n * dim);
             // Q80 hand-off of h needs one workgroup per 32 hidden units; for skinny TP shards the
             // w13 epilogue emits f32 and w2 quantizes in its prologue instead.
             const bool hQ80 = q40_ && p.hidden0 / 32 >= 192;
@@ -1372,7 +1393,7 @@ class HipEngineImpl : public HipEngine {
                          dim, nullptr, nullptr, nullptr, nullptr, nullptr, fusedTp(bat));
             }
             }
-            if (!fusedTp(bat)) allReduce(dY_, (size_t)n * dim);
+            if (!fusedTp(bat) && !fz) allReduce(dY_, (size_t)n * dim);
         }
         {
             ProfScope ps(this, "gemv_logits");

@@ -40,6 +40,12 @@ class HipEngine : public Backend {
         return {};
     }
     virtual int fusedGridMax() const { return 0; }
+    // Tensor parallel: a batched forward of n rows all-reduces its wo / w2 tiles inside the GEMM
+    // epilogues (no separate all-reduce / norm kernels).
+    virtual bool tpBatchedFused(int n) const {
+        (void)n;
+        return false;
+    }
 };
 
 // comm may be null (single GPU). The engine does not own comm.

@@ -137,6 +137,9 @@ __device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc
         splitCombine(ga.part + (size_t)tileIdx * MP * kGemmRows, (size_t)tiles * MP * kGemmRows, S,
                      MP * kGemmRows / 4, reinterpret_cast<f32x4 *>(tile));
     }
+    // tensor parallel: the tile's partial sums all-reduced over the ranks in place (staging after
+    // the [MP][64] tile; the host checked that the launch's LDS holds it)
+    if (ga.tpx) tpExchangeTile(ga, tile, R0, smem + (size_t)MP * kGemmRows * 4);
     // consumer of a fused residual + norm: per-token RMS scale from the producer's tile partials
     float *rsL = reinterpret_cast<float *>(flag + 4);  // [128] + [256] scratch
     if (ga.ssIn) gemmRowScales(ga, 0, MP, rsL, rsL + 128);
@@ -281,12 +284,22 @@ static int gemmStages1() {  // stage buffers of the 16-token tile (DL_GEMM_STG1 
     return v;
 }
 
+bool gemmTpxFits(int M, int world, bool q80) {
+    if (M < 1 || M > 64 || world > kTpMaxRanks) return false;
+    const int MT = gemmTokenPad(M) / 16;
+    const int stg = MT == 4 ? gemmStages4() : MT == 2 ? gemmStages2() : gemmStages1();
+    const size_t need = (size_t)MT * 16 * kGemmRows * 4 + (q80 ? tpTileQ80Lds(M, world) : 0);
+    return need <= (size_t)stg * gemmStageBytes(MT);
+}
+
 void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
     if (gemmUsesWide(ga.M)) {
         launchGemmWide(ga, epi, s);
         return;
     }
     if (ga.M > kGemmMaxTokens) throw Error("launchGemmQ40: more than 128 tokens per narrow launch");
+    if (ga.tpx && !gemmTpxFits(ga.M, ga.e.tp.world, ga.e.tp.q80 != 0))
+        throw Error("launchGemmQ40: the tile exchange does not fit this launch's LDS");
     const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
     const int MT = gemmTokenPad(ga.M) / 16;
     const int stg = MT == 8 ? 1 : MT == 4 ? gemmStages4() : MT == 2 ? gemmStages2() : gemmStages1();

@@ -106,6 +106,97 @@ __device__ __forceinline__ void splitCombine(const float *P, size_t stride, int 
     }
 }
 
+// Tensor-parallel all-reduce of a GEMM output tile in LDS (tile[t * 64 + r]: tokens t < M, rows R0 +
+// r of ldOut-wide outputs) through the fused exchange of the decode GEMVs (decode_dev.h
+// tpPushCollect: every rank pushes its partials into each peer's receive region as {value, epoch}
+// words, polls its own, sums in rank order: bitwise identical on every rank). Exchange element =
+// token * ldOut + row, the GEMV's convention, so the per-element epochs stay in step. Q80: every
+// rank's partial is quantized once to 32-row blocks (the reference's ZQ wire format, 9 words per
+// block), dequantized and summed. The sums overwrite the tile. `lds` = free staging (Q80:
+// tpTileQ80Lds bytes). Called by one whole workgroup; ends with a barrier.
+__host__ __device__ inline size_t tpTileQ80Lds(int M, int W) {
+    const int nEl = M * 64, nBlk = nEl / 32;
+    return alignUp((size_t)nEl, 16) + alignUp((size_t)nBlk * 4, 16) + (size_t)W * nBlk * 9 * 4;
+}
+__device__ __forceinline__ void tpExchangeTile(const GemmArgs &ga, float *tile, int R0, char *lds) {
+    const TpXchg &x = ga.e.tp;
+    const int M = ga.M, nEl = M * 64, W = x.world;
+    const bool failed = tpFailed(x);
+    __syncthreads();
+    if (!x.q80) {
+        for (int i = threadIdx.x; i < nEl; i += kThreads) {
+            const int t = i >> 6, row = R0 + (i & 63);
+            if (row >= ga.e.rows) continue;
+            const long long el = (long long)t * ga.e.ldOut + row;
+            const unsigned e = x.epochs[el] + 1;
+            unsigned v[kTpMaxRanks];
+            tpPushCollect(x, el, e, __float_as_uint(tile[i]), v, failed);
+            float s = 0.f;
+#pragma unroll
+            for (int p = 0; p < kTpMaxRanks; p++)
+                if (p < W) s += __uint_as_float(v[p]);
+            tile[i] = s;
+            x.epochs[el] = e;
+        }
+        __syncthreads();
+        return;
+    }
+    const int nBlk = nEl >> 5;
+    int8_t *q8 = reinterpret_cast<int8_t *>(lds);
+    uint32_t *dq = reinterpret_cast<uint32_t *>(lds + alignUp((size_t)nEl, 16));
+    uint32_t *rv = reinterpret_cast<uint32_t *>(lds + alignUp((size_t)nEl, 16) + alignUp((size_t)nBlk * 4, 16));
+    for (int base = 0; base < nEl; base += kThreads) {  // whole 32-lane groups per block: uniform
+        const int i = base + threadIdx.x;
+        const float v = i < nEl ? tile[i] : 0.f;
+        const float amax = groupMax<32>(fabsf(v));
+        const float d = amax / 127.0f;
+        const float id = d != 0.f ? 1.0f / d : 0.f;
+        int q = (int)rintf(v * id);
+        q = q > 127 ? 127 : (q < -127 ? -127 : q);
+        if (i < nEl) {
+            q8[i] = (int8_t)q;
+            if ((i & 31) == 0) dq[i >> 5] = __half_as_ushort(__float2half(d));
+        }
+    }
+    __syncthreads();
+    auto blockId = [&](int blk, bool &live) -> long long {  // 32-row block of (token, rows)
+        const int t = blk >> 1, row = R0 + (blk & 1) * 32;
+        live = row < ga.e.rows;
+        return ((long long)t * ga.e.ldOut + row) >> 5;
+    };
+    for (int j = threadIdx.x; j < nBlk * 9; j += kThreads) {
+        const int blk = j / 9, w = j % 9;
+        bool live;
+        const long long gb = blockId(blk, live);
+        if (!live) continue;
+        const unsigned e = x.epochs[gb] + 1;
+        const unsigned payload = w < 8 ? reinterpret_cast<const uint32_t *>(q8)[blk * 8 + w] : dq[blk];
+        unsigned v[kTpMaxRanks];
+        tpPushCollect(x, gb * 9 + w, e, payload, v, failed);
+#pragma unroll
+        for (int p = 0; p < kTpMaxRanks; p++)
+            if (p < W) rv[(p * nBlk + blk) * 9 + w] = v[p];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < nEl; i += kThreads) {
+        const int blk = i >> 5;
+        float s = 0.f;
+        for (int p = 0; p < W; p++) {
+            const uint32_t *bw = rv + (p * nBlk + blk) * 9;
+            const float d = __half2float(__ushort_as_half((uint16_t)(bw[8] & 0xFFFFu)));
+            const int q = (int)(int8_t)(bw[(i & 31) >> 2] >> (8 * (i & 3)));
+            s += (float)q * d;
+        }
+        tile[i] = s;
+    }
+    for (int blk = threadIdx.x; blk < nBlk; blk += kThreads) {
+        bool live;
+        const long long gb = blockId(blk, live);
+        if (live) x.epochs[gb] += 1;
+    }
+    __syncthreads();
+}
+
 // Consumer of a fused residual + norm (ga.ssIn): per-token RMS scale of tokens [t0, t0 + nt) of the
 // launch (nt <= 128) from the producer's 64-row tile partials, into rsL[0, nt). TPT threads per
 // token each sum a strided slice (independent loads in flight), then one thread per token adds the

@@ -180,6 +180,9 @@ struct GemmArgs {
     // 1 / sqrt(sum_j ssIn[j * ldSS + t] / n + eps) (ssTiles partials, summed in tile order)
     const float *ssIn = nullptr;
     int ssTiles = 0, ldSS = 0;
+    // tensor parallel (narrow kernel, wo / w2): the final tile [M][64 rows] is all-reduced over the
+    // ranks in the epilogue (e.tp: f32 or Q80 blocks, summed in rank order) before EPI_RES / STORE
+    int tpx = 0;
 };
 void launchGemmQ40(const GemmArgs &a, int epi, hipStream_t s);
 // Same contract for F32 weights (`e.wf` [rows][n] row-major; EPI_ACT_Q80 not supported).
@@ -199,6 +202,8 @@ int gemmWideSplits(int rows, int n, int M);
 size_t gemmWidePartFloats(int rows, int n, int maxTokens);
 int gemmWideCounters(int rows, int maxTokens);
 void launchGemmWide(const GemmArgs &a, int epi, hipStream_t s);
+// whether a narrow launch of M tokens can run the tensor-parallel tile exchange (GemmArgs::tpx)
+bool gemmTpxFits(int M, int world, bool q80);
 // split-K counter ints for any launch of up to maxTokens tokens on a matrix of `rows`
 int gemmCounterInts(int rows, int maxTokens);
 constexpr int kGemmF32MaxTokens = 64;  // tokens per F32 GEMM launch (16, 32 or 64 padded)

@@ -58,7 +58,9 @@ constexpr int kMaxRanks = 16;
 constexpr int kThreads = 256;
 constexpr int kLLMax = 16384;       // largest LL all-reduce (floats per rank)
 constexpr int kLLSlots = kLLMax / kChunk;
-constexpr long long kFusedVec = 1 << 16;   // fused residual exchange: words per (parity, sender)
+// fused residual exchange: words per (parity, sender); decode rows use <= 4 x dim, the batched
+// GEMMs' exchange (gemm_dev.h tpExchangeTile) up to 64 tokens x dim of the 8B
+constexpr long long kFusedVec = 1 << 18;
 constexpr long long kFusedArg = 2048;      // fused argmax exchange: 2 words per batch row
 constexpr long long kTimeoutTicks = 200LL * 1000 * 1000;  // 2 s at 100 MHz
 

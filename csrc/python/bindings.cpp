@@ -767,6 +767,7 @@ PYBIND11_MODULE(_C, m) {
              py::arg("token"), py::arg("pos"), py::arg("slot") = 0, py::arg("layer") = 1, py::arg("ffn") = false)
         .def_property_readonly("fused_grid_max", [](const PyHipEngine &e) { return e.engine->fusedGridMax(); })
         .def_property_readonly("kv_pages_free", [](const PyHipEngine &e) { return e.engine->kvPagesFree(); })
+        .def("tp_batched_fused", [](const PyHipEngine &e, int n) { return e.engine->tpBatchedFused(n); }, py::arg("n"))
         .def_property_readonly("load_stats",
                                [](const PyHipEngine &e) {
                                    const Backend::LoadStats l = e.engine->loadStats();

@@ -109,6 +109,8 @@ def _engine_tp_batched(rank, world, port, model, tokens, q, sync_type="f32", env
         if comm.timed_out():
             raise AssertionError("a flag wait timed out")
         fused = bool(eng.tp_fused) and (not env or "DL_EXPECT_BLOCKS" not in env or bool(eng.ffn_block))
+        if env and "DL_TP_BATCHED" in env:  # the batched rows' exchange: in the GEMM epilogues or not
+            assert eng.tp_batched_fused(32) == (env["DL_TP_BATCHED"] != "0")
         dist.barrier()
         q.put((rank, (np.concatenate(lg) if rank == 0 else None, ids, fused, list(dec))))
     except Exception as e:
@@ -189,11 +191,13 @@ def test_xgmi_engine_tp_matches_single(C, tmp_path, world, sync_type):
     assert agree >= steps - 2 and res[0][1][:4] == list(ref_toks[:4]), (res[0][1], ref_toks)
 
 
+@pytest.mark.parametrize("batched", ["1", "0"])
 @pytest.mark.parametrize("world,sync_type", [(2, "f32"), (4, "f32"), (2, "q80"), (4, "q80")])
-def test_xgmi_engine_tp_batched_matches_single(C, tmp_path, world, sync_type):
-    """Prefill-sized forwards (32 and 64 rows: MFMA GEMMs, MFMA prefill attention, partial sums
-    all-reduced by separate kernels over xGMI) at TP=2/4 vs TP=1 on the same model: logits within
-    tolerance, argmax ids bitwise identical on every rank."""
+def test_xgmi_engine_tp_batched_matches_single(C, tmp_path, world, sync_type, batched):
+    """Prefill-sized forwards (32 and 64 rows: MFMA GEMMs, MFMA prefill attention) at TP=2/4 vs TP=1
+    on the same model: logits within tolerance, argmax ids bitwise identical on every rank. The
+    partial sums of wo / w2 are all-reduced inside the GEMM epilogues over the fused exchange
+    (batched=1, with the residual + norm fusion) or by separate xGMI all-reduce kernels (0)."""
     from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
     from distributed_llama_multiusers_amd.utils.mfile import FloatType
     m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=11, dim=512, n_heads=8,
@@ -204,7 +208,7 @@ def test_xgmi_engine_tp_batched_matches_single(C, tmp_path, world, sync_type):
     ref = np.concatenate([single.forward(tokens[:32], list(range(32)), [0] * 32),
                           single.forward(tokens[32:], list(range(32, 96)), [0] * 64)])
     del single
-    res = _run(_engine_tp_batched, world, m, tokens, kwargs=dict(sync_type=sync_type))
+    res = _run(_engine_tp_batched, world, m, tokens, kwargs=dict(sync_type=sync_type, env={"DL_TP_BATCHED": batched}))
     assert all(isinstance(v, tuple) for v in res.values()), res
     got = res[0][0]
     assert got.shape == ref.shape
@@ -274,14 +278,16 @@ def test_xgmi_engine_tp_fused_blocks(C, tmp_path):
 def test_fused_exchange_residency_guard(C, tmp_path):
     """A fused-exchange GEMV whose grid is not fully co-resident could deadlock (its workgroups
     spin on peers): the engine checks occupancy x CUs at construction and otherwise falls back to
-    separate all-reduce kernels - forced here with DL_FUSED_RESIDENT=1 - with the same results."""
+    separate all-reduce kernels - forced here with DL_FUSED_RESIDENT=1 - with the same results (the
+    batched rows' in-epilogue exchange, which also fuses the norm, is off in both runs so their
+    numerics compare bitwise)."""
     from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
     from distributed_llama_multiusers_amd.utils.mfile import FloatType
     m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=11, dim=512, n_heads=8,
                                n_kv_heads=4, hidden_dim=1024, vocab_size=1024)
     tokens = [int(t) for t in np.random.default_rng(4).integers(0, 1024, 96)]
-    a = _run(_engine_tp_batched, 2, m, tokens, kwargs=dict(env={"DL_FUSED_RESIDENT": "1"}))
-    b = _run(_engine_tp_batched, 2, m, tokens)
+    a = _run(_engine_tp_batched, 2, m, tokens, kwargs=dict(env={"DL_FUSED_RESIDENT": "1", "DL_TP_BATCHED": "0"}))
+    b = _run(_engine_tp_batched, 2, m, tokens, kwargs=dict(env={"DL_TP_BATCHED": "0"}))
     assert all(isinstance(v, tuple) for v in list(a.values()) + list(b.values())), (a, b)
     assert a[0][2] is False and b[0][2] is True
     assert np.array_equal(a[0][0], b[0][0]) and a[0][1] == b[0][1]
