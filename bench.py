@@ -152,7 +152,7 @@ def main() -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-f32kv", action="store_true", help="skip the f32 KV-cache decode point")
     ap.add_argument("--no-prefill4k", action="store_true", help="skip the 4096-token prompt-eval point")
-    ap.add_argument("--prefill-chunk", type=int, default=256,
+    ap.add_argument("--prefill-chunk", type=int, default=1024,
                     help="rows per forward of the second 4096-token prompt point (the first uses the reference's 32)")
     args = ap.parse_args()
 
@@ -337,7 +337,7 @@ def main() -> int:
 
         p4k_ms = prefill(eng, 32)
         # the same prompt in chunks of `--prefill-chunk` rows (dllama --max-batch / the API's prefill):
-        # each matrix's 64-row GEMM launches follow each other, the repeats read it from the MALL
+        # one wide-GEMM launch per matrix covers every 128-token tile of the chunk
         if args.prefill_chunk > 32:
             del eng
             eng = C.HipEngine(args.model, "q80", max_seq_len=4096 + 8, max_batch=args.prefill_chunk, n_slots=1,
