@@ -208,12 +208,21 @@ class HipEngineImpl : public HipEngine {
         w += matStageBytes(p.vocab0, h_.dim) + (size_t)h_.vocabSize * h_.dim * 4;
         const size_t act = (size_t)cfg_.maxBatch * h_.vocabSize * 4 * 3 + ((size_t)256 << 20);
         if (kv + w + act > freeB) {
-            char msg[512];
-            std::snprintf(msg, sizeof(msg), "Model does not fit on GPU %d: weights %.2f GB + KV cache %.2f GB (%u slots x %u "
-                                  "positions x %u layers, %s) + buffers %.2f GB > %.2f GB free of %.2f GB. Lower "
-                                  "--max-seq-len or the number of slots, or add tensor-parallel ranks.",
-                                  dev_, w / GB, kv / GB, cfg_.nSlots, h_.seqLen, h_.nLayers, kvBf16_ ? "bf16" : "f32",
-                                  act / GB, freeB / GB, totalB / GB);
+            // the page pool that would fit (positions shared by all slots), as a hint
+            const size_t perPos = (size_t)h_.nLayers * 2 * p.kv0 * (kvBf16_ ? 2 : 4);
+            const long long spare = (long long)freeB - (long long)(w + act);
+            const long long pages = spare > 0 ? spare / (long long)(perPos * cfg_.kvPageSize) : 0;
+            char msg[768];
+            std::snprintf(msg, sizeof(msg), "Model does not fit on GPU %d: weights %.2f GB + KV cache %.2f GB (%s x %u "
+                                  "layers, %s) + buffers %.2f GB > %.2f GB free of %.2f GB. Lower "
+                                  "--max-seq-len or the number of slots, add tensor-parallel ranks, or use a paged "
+                                  "KV cache sized to the tokens in flight (--kv-pages %lld fits %lld positions).",
+                                  dev_, w / GB, kv / GB,
+                                  paged() ? (std::to_string(cfg_.kvPages) + " pages").c_str()
+                                          : (std::to_string(cfg_.nSlots) + " slots x " + std::to_string(h_.seqLen) +
+                                             " positions").c_str(),
+                                  h_.nLayers, kvBf16_ ? "bf16" : "f32", act / GB, freeB / GB, totalB / GB, pages,
+                                  pages * (long long)cfg_.kvPageSize);
             throw Error(msg);
         }
     }

@@ -280,10 +280,16 @@ def test_simulated_tensor_parallel_matches_single(C, kv4_gpu, world):
 def test_kv_cache_larger_than_hbm_is_refused(C):
     """64 slots x 131072 positions of bf16 KV for the 8B is ~1.1 TB: refused before allocating,
     with the numbers and what to lower, instead of an out-of-memory fault mid-load."""
-    with pytest.raises(RuntimeError, match="does not fit on GPU"):
-        h = dict(dim=4096, hidden_dim=14336, n_layers=32, n_heads=32, n_kv_heads=8, vocab_size=128256,
-                 seq_len=131072, rope_theta=500000, weight_type=2)
+    h = dict(dim=4096, hidden_dim=14336, n_layers=32, n_heads=32, n_kv_heads=8, vocab_size=128256,
+             seq_len=131072, rope_theta=500000, weight_type=2)
+    with pytest.raises(RuntimeError, match="does not fit on GPU.*--kv-pages"):
         C.HipEngine("", "q80", synthetic=h, max_seq_len=131072, n_slots=64, max_batch=1)
+    # the same 64 slots of 128K context each over a shared pool of 131072 positions (paged KV)
+    g = C.HipEngine("", "q80", synthetic=h, max_seq_len=131072, n_slots=64, max_batch=1, kv_pages=512,
+                    kv_page_size=256)
+    assert g.kv_pages_free == 512
+    g.forward([1], [0], [63])
+    assert g.kv_pages_free == 511
 
 
 @pytest.mark.parametrize("n", [8, 32, 64, 200])
