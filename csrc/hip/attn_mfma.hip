@@ -35,6 +35,12 @@ static constexpr int kAmWaveBytes = 2 * 2 * kAmTileBytes;    // double-buffered 
 static constexpr size_t kAmLds = (size_t)kAmWaves * kAmWaveBytes + 64;
 
 __device__ __forceinline__ int amSwz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+// Key (LDS row within a 32-key tile) of MFMA row m (0..15) of 16-key subtile u. MFMA row m = 4h + q
+// lands on lane group h of the S^T output / P^T operand, and the V^T transposed read of group h
+// fetches the 4 rows of its keys: with rows 8 apart for the two groups of a 32-lane half (h = 0 / 1
+// -> rows 0..3 / 8..11, h = 2 / 3 -> 4..7 / 12..15) that read is bank-conflict free on the image
+// (cdna_hip_programming.md T10), instead of 2-way for adjacent row blocks.
+__host__ __device__ __forceinline__ int amKey(int u, int m) { return 16 * u + 8 * ((m >> 2) & 1) + 4 * (m >> 3) + (m & 3); }
 
 // TR: V^T fragments by the hardware transpose read (default); false: 8 scalar 16-bit LDS reads per
 // fragment (DL_ATTN_TR=0, a cross-check of the transposed-read addressing).
@@ -114,7 +120,7 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
 #pragma unroll
         for (int u = 0; u < 2; u++) {
             st[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-            const int r = 16 * u + col;
+            const int r = amKey(u, col);
 #pragma unroll
             for (int s = 0; s < DS; s++) {
                 const bf16x8 kf = *reinterpret_cast<const bf16x8 *>(kb + r * 256 + 16 * ((4 * s + h) ^ amSwz(r)));
@@ -124,14 +130,14 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
 #ifdef DL_AM_DEBUG
         if (g == 0 && c == 0 && b == 0 && i == 0)
             for (int u = 0; u < 2; u++)
-                for (int e = 0; e < 4; e++) a.partO[(16 * u + 4 * h + e) * 16 + col] = st[u][e];
+                for (int e = 0; e < 4; e++) a.partO[amKey(u, 4 * h + e) * 16 + col] = st[u][e];
 #endif
         float mx = -INFINITY;
 #pragma unroll
         for (int u = 0; u < 2; u++)
 #pragma unroll
             for (int e = 0; e < 4; e++) {
-                if (tb + 16 * u + 4 * h + e >= t1) st[u][e] = -INFINITY;
+                if (tb + amKey(u, 4 * h + e) >= t1) st[u][e] = -INFINITY;
                 mx = fmaxf(mx, st[u][e]);
             }
         mx = fmaxf(mx, __shfl_xor(mx, 16));
@@ -158,14 +164,14 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
 #pragma unroll
             for (int u = 0; u < 2; u++) {
                 if constexpr (TR) {
-                    const int r = 16 * u + 4 * h + tq;
+                    const int r = amKey(u, 4 * h + tq);
                     const char *ad = vb + r * 256 + 16 * ((2 * n + (tp >> 1)) ^ amSwz(r)) + 8 * (tp & 1);
                     vv[u] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                         reinterpret_cast<__attribute__((address_space(3))) s16x4 *>(reinterpret_cast<uintptr_t>(ad)));
                 } else {
 #pragma unroll
                     for (int e = 0; e < 4; e++) {
-                        const int r = 16 * u + 4 * h + e;
+                        const int r = amKey(u, 4 * h + e);
                         vv[u][e] = *reinterpret_cast<const short *>(vb + r * 256 + 16 * ((2 * n + (col >> 3)) ^ amSwz(r)) +
                                                                     2 * (col & 7));
                     }
@@ -337,7 +343,7 @@ __global__ __launch_bounds__(kAmThreads) void attnPrefillDmaKernel(AttnArgs a, i
 #pragma unroll
             for (int u = 0; u < 2; u++) {
                 st[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-                const int rr = 16 * u + col;
+                const int rr = amKey(u, col);
 #pragma unroll
                 for (int s = 0; s < DS; s++) {
                     const bf16x8 kf = *reinterpret_cast<const bf16x8 *>(kb + rr * 256 + 16 * ((4 * s + h) ^ amSwz(rr)));
@@ -349,7 +355,7 @@ __global__ __launch_bounds__(kAmThreads) void attnPrefillDmaKernel(AttnArgs a, i
             for (int u = 0; u < 2; u++)
 #pragma unroll
                 for (int e = 0; e < 4; e++) {
-                    const int key = tb + 16 * u + 4 * h + e;
+                    const int key = tb + amKey(u, 4 * h + e);
                     if (key >= k1 || key >= myLen) st[u][e] = -INFINITY;
                     mx = fmaxf(mx, st[u][e]);
                 }
@@ -374,7 +380,7 @@ __global__ __launch_bounds__(kAmThreads) void attnPrefillDmaKernel(AttnArgs a, i
                 s16x4 vv[2];
 #pragma unroll
                 for (int u = 0; u < 2; u++) {
-                    const int rr = 16 * u + 4 * h + tq;
+                    const int rr = amKey(u, 4 * h + tq);
                     const char *ad = vb + rr * 256 + 16 * ((2 * n + (tp >> 1)) ^ amSwz(rr)) + 8 * (tp & 1);
                     vv[u] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                         reinterpret_cast<__attribute__((address_space(3))) s16x4 *>(reinterpret_cast<uintptr_t>(ad)));

@@ -147,8 +147,15 @@ __global__ __launch_bounds__(kThreads) void gemmWideKernel(GemmArgs ga, int rowT
 #pragma unroll
             for (int f = 0; f < 4; f++) {
                 const int rl = wr * 64 + f * 16 + col;
-                const u32x2 wv = *reinterpret_cast<const u32x2 *>(st + (rl * 2 + (kb ^ ((rl >> 3) & 1))) * 16 + byteHalf * 8);
-                const uint32_t dw = *reinterpret_cast<const uint32_t *>(st + kWStW + (kb * 64 + (rl >> 1)) * 4);
+                // opaque addresses: hipcc would otherwise pair the fragments (rows 16 apart) into
+                // ds_read2st64_b64 / _b32, whose 32-bank rule makes the 32-B weight rows 2-way
+                // conflicted (SQ_LDS_BANK_CONFLICT 27.6 % of LDS cycles); single ds_read_b64 follow
+                // the 64-bank rule this image is conflict-free for
+                uint32_t aw = (uint32_t)((rl * 2 + (kb ^ ((rl >> 3) & 1))) * 16 + byteHalf * 8);
+                uint32_t ad = (uint32_t)(kWStW + (kb * 64 + (rl >> 1)) * 4);
+                asm volatile("" : "+v"(aw), "+v"(ad));
+                const u32x2 wv = *reinterpret_cast<const u32x2 *>(st + aw);
+                const uint32_t dw = *reinterpret_cast<const uint32_t *>(st + ad);
                 b[f] = dequantQ40x8(wv, nibHi, (rl & 1) ? dw >> 16 : dw & 0xFFFFu);
             }
 #pragma unroll

@@ -55,7 +55,7 @@ int main(int argc, char **argv) {
     int bad = 0;
     for (int l = 0; l < 64; l++)
         for (int j = 0; j < 8; j++) {
-            const int cc = l & 15, hh = l >> 4, key = j < 4 ? 4 * hh + j : 16 + 4 * hh + j - 4;
+            const int cc = l & 15, hh = l >> 4, key = amKey(j < 4 ? 0 : 1, 4 * hh + (j & 3));
             const float want = v[(size_t)key * kv0 + cc], got = dbg[8192 + l * 8 + j];
             if (want != got && bad++ < 6) printf("vf lane %d el %d: want V[%d][%d]=%.4f got %.4f\n", l, j, key, cc, want, got);
         }
