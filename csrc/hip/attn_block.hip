@@ -6,22 +6,22 @@
 namespace dl {
 namespace hipk {
 
-const void *attnBlockFn_16_32_128(int hg, bool bf16, bool tp);
-const void *attnBlockFn_32_32_128(int hg, bool bf16, bool tp);
-const void *attnBlockFn_64_32_128(int hg, bool bf16, bool tp);
-const void *attnBlockFn_64_16_128(int hg, bool bf16, bool tp);
-const void *attnBlockFn_64_64_128(int hg, bool bf16, bool tp);
-const void *attnBlockFn_32_64_128(int hg, bool bf16, bool tp);
-const void *attnBlockFn_64_64_64(int hg, bool bf16, bool tp);
+const void *attnBlockFn_16_32_128(int hg, bool bf16, int md);
+const void *attnBlockFn_32_32_128(int hg, bool bf16, int md);
+const void *attnBlockFn_64_32_128(int hg, bool bf16, int md);
+const void *attnBlockFn_64_16_128(int hg, bool bf16, int md);
+const void *attnBlockFn_64_64_128(int hg, bool bf16, int md);
+const void *attnBlockFn_32_64_128(int hg, bool bf16, int md);
+const void *attnBlockFn_64_64_64(int hg, bool bf16, int md);
 
-static const void *attnBlockFn(int lq, int lw, int hs, int hg, bool bf16, bool tp) {
-    if (lq == 16 && lw == 32 && hs == 128) return attnBlockFn_16_32_128(hg, bf16, tp);
-    if (lq == 32 && lw == 32 && hs == 128) return attnBlockFn_32_32_128(hg, bf16, tp);
-    if (lq == 64 && lw == 32 && hs == 128) return attnBlockFn_64_32_128(hg, bf16, tp);
-    if (lq == 64 && lw == 16 && hs == 128) return attnBlockFn_64_16_128(hg, bf16, tp);
-    if (lq == 64 && lw == 64 && hs == 128) return attnBlockFn_64_64_128(hg, bf16, tp);
-    if (lq == 32 && lw == 64 && hs == 128) return attnBlockFn_32_64_128(hg, bf16, tp);
-    if (lq == 64 && lw == 64 && hs == 64) return attnBlockFn_64_64_64(hg, bf16, tp);
+static const void *attnBlockFn(int lq, int lw, int hs, int hg, bool bf16, int md) {
+    if (lq == 16 && lw == 32 && hs == 128) return attnBlockFn_16_32_128(hg, bf16, md);
+    if (lq == 32 && lw == 32 && hs == 128) return attnBlockFn_32_32_128(hg, bf16, md);
+    if (lq == 64 && lw == 32 && hs == 128) return attnBlockFn_64_32_128(hg, bf16, md);
+    if (lq == 64 && lw == 16 && hs == 128) return attnBlockFn_64_16_128(hg, bf16, md);
+    if (lq == 64 && lw == 64 && hs == 128) return attnBlockFn_64_64_128(hg, bf16, md);
+    if (lq == 32 && lw == 64 && hs == 128) return attnBlockFn_32_64_128(hg, bf16, md);
+    if (lq == 64 && lw == 64 && hs == 64) return attnBlockFn_64_64_64(hg, bf16, md);
     return nullptr;
 }
 
@@ -41,11 +41,16 @@ static int gemvGrid(const GemvArgs &g) {
 
 AttnBlockPlan attnBlockPlan(const AttnBlockArgs &a, bool tp) {
     AttnBlockPlan p;
-    p.fn = attnBlockFn(a.qkv.lanes, a.wo.lanes, a.at.hs, a.hg, a.at.kvBf16 != 0, tp);
+    // md: 0 plain, 1 tensor-parallel wo exchange, 2 residual + norm split (qkv PRO_UNORM, wo EPI_STORE_UN)
+    p.fn = attnBlockFn(a.qkv.lanes, a.wo.lanes, a.at.hs, a.hg, a.at.kvBf16 != 0, tp ? 1 : (a.un ? 2 : 0));
     p.gq = gemvGrid(a.qkv);
     p.ga = a.at.nHeads0 / a.hg * a.at.splitGrid;
     p.gw = gemvGrid(a.wo);
     const int Rq = (kThreads / a.qkv.lanes) * 2 * a.qkv.passes, Rw = (kThreads / a.wo.lanes) * 2 * a.wo.passes;
+    if (a.un && (tp || Rw > kThreads || a.qkv.ssCount > kUnMaxPartials)) {
+        p.fn = nullptr;  // EPI_STORE_UN stages one row per thread; PRO_UNORM reads <= kUnMaxPartials
+        return p;
+    }
     size_t lq = gemvLayout(a.qkv.n, 1, true, Rq, PRO_RESNORM).total;
     size_t lw = gemvLayout(a.wo.n, 1, true, Rw, PRO_RESNORM).total;
     if (tp && a.wo.tp.q80) lw = std::max(lw, gemvLayout(a.wo.n, 1, true, Rw, PRO_RESNORM).act + tpQ80Lds(Rw, a.wo.tp.world));

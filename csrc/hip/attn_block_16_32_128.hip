@@ -3,6 +3,6 @@
 
 namespace dl {
 namespace hipk {
-const void *attnBlockFn_16_32_128(int hg, bool bf16, bool tp) { return attnBlockFnT<16, 32, 128>(hg, bf16, tp); }
+const void *attnBlockFn_16_32_128(int hg, bool bf16, int md) { return attnBlockFnT<16, 32, 128>(hg, bf16, md); }
 }  // namespace hipk
 }  // namespace dl

@@ -3,6 +3,6 @@
 
 namespace dl {
 namespace hipk {
-const void *attnBlockFn_32_64_128(int hg, bool bf16, bool tp) { return attnBlockFnT<32, 64, 128>(hg, bf16, tp); }
+const void *attnBlockFn_32_64_128(int hg, bool bf16, int md) { return attnBlockFnT<32, 64, 128>(hg, bf16, md); }
 }  // namespace hipk
 }  // namespace dl

@@ -102,6 +102,7 @@ class HipEngineImpl : public HipEngine {
         DL_HIP(hipStreamSynchronize(stream_));
         setupAttnBlock();
         setupFfnBlock();
+        setupUn();
         load_.ms = timer.elapsedMs();
         load_.deviceBytes = deviceBytes_;
     }
@@ -282,6 +283,7 @@ class HipEngineImpl : public HipEngine {
   public:
     bool tpFused() const override { return tpFused_; }
     bool attnBlock() const override { return blockOn_; }
+    bool unNorm() const override { return unOn_; }
     bool ffnBlock() const override { return ffnOn_; }
     std::vector<unsigned long long> traceAttnBlock(int token, int pos, int slot, int layer, bool ffn) override {
         if (ffn ? !ffnOn_ : !blockOn_) return {};
@@ -515,6 +517,10 @@ class HipEngineImpl : public HipEngine {
         dX_[0] = dalloc<float>((size_t)MB * h_.dim);
         dX_[1] = dalloc<float>((size_t)MB * h_.dim);
         dY_ = dalloc<float>((size_t)MB * h_.dim);
+        for (int i = 0; i < 2; i++) {
+            dU_[i] = dalloc<float>(h_.dim);
+            dUnSS_[i] = dalloc<float>(hipk::kUnMaxPartials);
+        }
         dQ_ = dalloc<float>((size_t)MB * p.q0);
         dAtt_ = dalloc<float>((size_t)MB * p.q0);
         dH_ = dalloc<float>((size_t)MB * p.hidden0);
@@ -1142,6 +1148,59 @@ class HipEngineImpl : public HipEngine {
         ffnW13PassMul_ = 1;
     }
 
+    // Decide once whether single decode rows split each residual update + RMS norm between the GEMV
+    // that produces the update and the one that consumes the norm (kernels.h EPI_STORE_UN /
+    // PRO_UNORM): the wo / w2 epilogues add their rows into x in place and leave u = normW * x plus
+    // one partial sum of squares per workgroup, so the qkv / w13 / logits prologues read u and the
+    // partials instead of x, delta and normW per workgroup (qkv 6.0 -> 4.8 us, w13 14.3 -> 13.8 us
+    // with fully precomputed activations, scripts/bench_gemv.py). TP1, Q40, Q80 hidden hand-off,
+    // no fused FFN block. Opt-in (DL_UNORM=1): measured a wash on 8B decode (1.3453 -> 1.3496
+    // ms/token: w13 14.64 -> 14.17 us, but the w2 producer 7.94 -> 8.49 us and the attention block
+    // 16.29 -> 16.52 us; profiles/r3_prefill_attention.md).
+    void setupUn() {
+        const char *e = std::getenv("DL_UNORM");
+        if (!(e && *e == '1') || !q40_ || plan_.nRanks != 1 || ffnOn_ || plan_.hidden0 / 32 < 192 || h_.dim > 8192)
+            return;
+        const DevLayer &L = layers_[0];
+        auto rowsPerWg = [&](const DevMat &m) {
+            return (256 / m.lanes) * 2 * passesFor(m, hipk::EPI_STORE_UN, 1);
+        };
+        if (rowsPerWg(L.wo) > 256 || rowsPerWg(L.w2) > 256) return;
+        unWoGrid_ = (L.wo.rows + rowsPerWg(L.wo) - 1) / rowsPerWg(L.wo);
+        unW2Grid_ = (L.w2.rows + rowsPerWg(L.w2) - 1) / rowsPerWg(L.w2);
+        if (unWoGrid_ > hipk::kUnMaxPartials || unW2Grid_ > hipk::kUnMaxPartials) return;
+        if (blockOn_) {
+            hipk::AttnBlockArgs b = attnBlockArgs(L, 0, 0);
+            unBlockArgs(b, L, 0);
+            if (!hipk::attnBlockPlan(b, false).fn) return;
+            const hipk::GemvResidency r = hipk::attnBlockResidency(b, false);
+            if (r.maxResident <= 0 || r.grid > r.maxResident) return;
+        }
+        unOn_ = true;
+    }
+    const float *unNextNorm(u32 l) const { return l + 1 < h_.nLayers ? layers_[l + 1].rmsAtt : rmsFinal_; }
+    // PRO_UNORM consumer of u[i] / ss[i] with `count` partials
+    void unIn(hipk::GemvArgs &a, int i, int count) const {
+        a.in = dU_[i];
+        a.addIn = nullptr;
+        a.xNext = nullptr;
+        a.normW = nullptr;
+        a.ssIn = dUnSS_[i];
+        a.ssCount = count;
+    }
+    // EPI_STORE_UN producer: x updated in place, u[i] = w * x, ss[i][workgroup]
+    void unOut(hipk::GemvArgs &a, int i, const float *w) const {
+        a.out = dX_[0];
+        a.uOut = dU_[i];
+        a.unW = w;
+        a.ssOut = dUnSS_[i];
+    }
+    void unBlockArgs(hipk::AttnBlockArgs &b, const DevLayer &L, u32 l) const {
+        b.un = 1;
+        unIn(b.qkv, 1, l == 0 ? 1 : unW2Grid_);
+        unOut(b.wo, 0, L.rmsFfn);
+    }
+
     // A fused-block wait gave up (a workgroup of the launch never arrived): reset the monotonic
     // counters and the epoch so the engine stays usable, then raise.
     void resetAttnBlockState() {
@@ -1298,10 +1357,15 @@ class HipEngineImpl : public HipEngine {
         const bool fz = bat && fuseNorm(n);  // residual + norm carried by the GEMM epilogues
         const bool blk = blockOn_ && n == 1 && !bat;  // fused attention block per layer
         const bool fb = ffnOn_ && n == 1 && !bat;     // fused FFN block per layer
+        const bool un = unOn_ && n == 1 && !bat;      // residual + norm split (setupUn): x stays in dX_[0]
         {
             ProfScope ps(this, "embedding");
             // the epoch counts the forwards that run a fused block (its counters' targets)
-            hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_, blk || fb ? dEpoch_ : nullptr);
+            if (un)
+                hipk::launchEmbeddingUn(emb_, dTok_, dX_[0], dim, stream_, blk ? dEpoch_ : nullptr, layers_[0].rmsAtt,
+                                        dU_[1], dUnSS_[1]);
+            else
+                hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_, blk || fb ? dEpoch_ : nullptr);
         }
         for (u32 l = 0; l < h_.nLayers; l++) {
             DevLayer &L = layers_[l];
@@ -1309,9 +1373,10 @@ class HipEngineImpl : public HipEngine {
             if (blk) {
                 ProfScope ps(this, "attn_block");
                 hipk::AttnBlockArgs ba = attnBlockArgs(L, l, cur);
+                if (un) unBlockArgs(ba, L, l);
                 if ((int)l == traceLayer_ && !traceFfn_) ba.trace = traceBuf_;
                 hipk::launchAttnBlock(ba, fusedTp(false), stream_);
-                if (hasDelta) cur ^= 1;
+                if (hasDelta && !un) cur ^= 1;
             } else {
             {
                 ProfScope ps(this, "gemv_qkv");
@@ -1321,11 +1386,16 @@ class HipEngineImpl : public HipEngine {
                 else if (bat)
                     gemmBatched(L.qkv, n, hipk::EPI_QKV, dX_[cur], dim, hasDelta ? dY_ : nullptr,
                                 hasDelta ? dX_[cur ^ 1] : nullptr, L.rmsAtt, nullptr, dQ_, p.q0, nullptr, &L);
-                else
+                else if (un) {
+                    hipk::GemvArgs a = gemvArgs(L.qkv, 0, 1, hipk::EPI_QKV, nullptr, dim, nullptr, nullptr, nullptr, dQ_,
+                                                p.q0, &L, nullptr, nullptr, nullptr, nullptr, false);
+                    unIn(a, 1, l == 0 ? 1 : unW2Grid_);
+                    hipk::launchGemv(a, 1, hipk::PRO_UNORM, hipk::EPI_QKV, true, stream_);
+                } else
                     gemv(L.qkv, n, hipk::PRO_RESNORM, hipk::EPI_QKV, dX_[cur], dim, hasDelta ? dY_ : nullptr,
                          hasDelta ? dX_[cur ^ 1] : nullptr, L.rmsAtt, dQ_, p.q0, &L);
             }
-            if (hasDelta) cur ^= 1;
+            if (hasDelta && !un) cur ^= 1;
             const bool pf = mallPrefetch() && q40_ && !profile_;
             {
                 ProfScope ps(this, "attention");
@@ -1355,7 +1425,12 @@ class HipEngineImpl : public HipEngine {
                 } else if (bat)
                     gemmBatched(L.wo, n, hipk::EPI_STORE, nullptr, 0, nullptr, nullptr, nullptr, dAttH_, dY_, dim,
                                 nullptr, nullptr);
-                else
+                else if (un) {
+                    hipk::GemvArgs a = gemvArgs(L.wo, 0, 1, hipk::EPI_STORE_UN, nullptr, p.q0, nullptr, nullptr, nullptr,
+                                                nullptr, dim, nullptr, dAttQ_, dAttS_, nullptr, nullptr, false);
+                    unOut(a, 0, L.rmsFfn);
+                    hipk::launchGemv(a, 1, hipk::PRO_GLOBAL, hipk::EPI_STORE_UN, true, stream_);
+                } else
                     gemv(L.wo, n, hipk::PRO_GLOBAL, hipk::EPI_STORE, q40_ ? nullptr : dAtt_, p.q0, nullptr, nullptr,
                          nullptr, dY_, dim, nullptr, dAttQ_, dAttS_, nullptr, nullptr, fusedTp(bat));
             }
@@ -1379,11 +1454,16 @@ class HipEngineImpl : public HipEngine {
                 else if (bat)
                     gemmBatched(L.w13, n, hipk::EPI_ACT_F16, dX_[cur], dim, dY_, dX_[cur ^ 1], L.rmsFfn, nullptr,
                                 nullptr, p.hidden0, dHh_, nullptr);
-                else
+                else if (un) {
+                    hipk::GemvArgs a = gemvArgs(L.w13, 0, 1, hipk::EPI_ACT_Q80, nullptr, dim, nullptr, nullptr, nullptr,
+                                                dH_, p.hidden0, nullptr, nullptr, nullptr, dHQ_, dHS_, false);
+                    unIn(a, 0, unWoGrid_);
+                    hipk::launchGemv(a, 1, hipk::PRO_UNORM, hipk::EPI_ACT_Q80, true, stream_);
+                } else
                     gemv(L.w13, n, hipk::PRO_RESNORM, hQ80 ? hipk::EPI_ACT_Q80 : hipk::EPI_ACT, dX_[cur], dim, dY_,
                          dX_[cur ^ 1], L.rmsFfn, dH_, p.hidden0, nullptr, nullptr, nullptr, dHQ_, dHS_);
             }
-            cur ^= 1;
+            if (!un) cur ^= 1;
             {
                 ProfScope ps(this, "gemv_w2");
                 if (fz) {
@@ -1394,7 +1474,12 @@ class HipEngineImpl : public HipEngine {
                 } else if (bat)
                     gemmBatched(L.w2, n, hipk::EPI_STORE, nullptr, 0, nullptr, nullptr, nullptr, dHh_, dY_, dim,
                                 nullptr, nullptr);
-                else if (hQ80 || !q40_)
+                else if (un) {
+                    hipk::GemvArgs a = gemvArgs(L.w2, 0, 1, hipk::EPI_STORE_UN, nullptr, p.hidden0, nullptr, nullptr,
+                                                nullptr, nullptr, dim, nullptr, dHQ_, dHS_, nullptr, nullptr, false);
+                    unOut(a, 1, unNextNorm(l));
+                    hipk::launchGemv(a, 1, hipk::PRO_GLOBAL, hipk::EPI_STORE_UN, true, stream_);
+                } else if (hQ80 || !q40_)
                     gemv(L.w2, n, hipk::PRO_GLOBAL, hipk::EPI_STORE, q40_ ? nullptr : dH_, p.hidden0, nullptr,
                          nullptr, nullptr, dY_, dim, nullptr, dHQ_, dHS_, nullptr, nullptr, fusedTp(bat));
                 else
@@ -1412,7 +1497,12 @@ class HipEngineImpl : public HipEngine {
             else if (bat)
                 gemmBatched(wcls_, n, hipk::EPI_STORE, dX_[cur], dim, dY_, nullptr, rmsFinal_, nullptr, dLogits_,
                             p.vocab0, nullptr, nullptr);
-            else
+            else if (un) {
+                hipk::GemvArgs a = gemvArgs(wcls_, 0, 1, hipk::EPI_STORE, nullptr, dim, nullptr, nullptr, nullptr, dLogits_,
+                                            p.vocab0, nullptr, nullptr, nullptr, nullptr, nullptr, false);
+                unIn(a, 1, unW2Grid_);
+                hipk::launchGemv(a, 1, hipk::PRO_UNORM, hipk::EPI_STORE, true, stream_);
+            } else
                 gemv(wcls_, n, hipk::PRO_RESNORM, hipk::EPI_STORE, dX_[cur], dim, dY_, nullptr, rmsFinal_, dLogits_,
                      p.vocab0, nullptr);
         }
@@ -1497,6 +1587,8 @@ class HipEngineImpl : public HipEngine {
     unsigned *dEpoch_ = nullptr, *dBlockCnt_ = nullptr, *dBlockExpect_ = nullptr;
     int *dBlockErr_ = nullptr;
     bool blockOn_ = false;  // decode rows run the fused attention block (setupAttnBlock)
+    bool unOn_ = false;     // decode rows split residual + norm between producer and consumer (setupUn)
+    int unWoGrid_ = 0, unW2Grid_ = 0;  // partial sums the wo / w2 producers leave (one per workgroup)
     bool ffnOn_ = false;
     static constexpr int kAttnMfmaMinPos = 1024;
     bool attnLong_ = false;  // this forward's decode attention runs the MFMA kernel (setInputs)
@@ -1527,6 +1619,8 @@ class HipEngineImpl : public HipEngine {
     int *hIn_ = nullptr, *hIds_ = nullptr, *hErr_ = nullptr;
     float *hLogits_ = nullptr;
     float *dX_[2] = {nullptr, nullptr};
+    float *dU_[2] = {nullptr, nullptr};   // normW * x from EPI_STORE_UN producers ([0] wo, [1] w2 / embedding)
+    float *dUnSS_[2] = {nullptr, nullptr};  // their per-workgroup partial sums of squares
     float *dY_ = nullptr, *dQ_ = nullptr, *dAtt_ = nullptr, *dH_ = nullptr, *dLogits_ = nullptr;
     float *dLogitsAll_ = nullptr, *dLogitsFull_ = nullptr;
     float *dPartO_ = nullptr, *dPartML_ = nullptr;

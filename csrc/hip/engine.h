@@ -30,6 +30,7 @@ class HipEngine : public Backend {
     virtual bool tpFused() const { return false; }
     // Single decode rows run the fused attention block (qkv + attention + wo in one launch).
     virtual bool attnBlock() const { return false; }
+    virtual bool unNorm() const { return false; }  // decode residual + norm split (EPI_STORE_UN / PRO_UNORM)
     // Single decode rows run the fused FFN block (w13 + w2 in one launch).
     virtual bool ffnBlock() const { return false; }
     // Diagnostics: one eager single-row forward with the fused attention block of `layer` traced

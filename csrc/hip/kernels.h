@@ -25,12 +25,19 @@ namespace hipk {
 //             Q40 weights, f32 for F32 weights) - no prologue, no LDS, no barrier.
 // PRO_RESNORM: (x + delta) -> RMS norm -> Q80 (or f32) staged once per workgroup in LDS
 //             (normW == null: no norm, plain quantization of `in`).
-enum Prologue : int { PRO_GLOBAL = 0, PRO_RESNORM = 1 };
+// PRO_UNORM (Q40, batch 1): the producer of x already stored u = normW * x and its partial sums of
+//             squares (EPI_STORE_UN): only 1 / rms is left (u * inv -> Q80 in LDS), so a
+//             workgroup reads n + ssCount floats instead of x, delta and normW (3n floats).
+enum Prologue : int { PRO_GLOBAL = 0, PRO_RESNORM = 1, PRO_UNORM = 2 };
 // EPI_ACT_Q80: act(w1 x) * (w3 x), quantized to Q80 blocks for the next GEMV (32 hidden units/block).
 // EPI_STORE_TP: EPI_STORE whose rows are first all-reduced over the tensor-parallel ranks (GemvArgs::tp).
 // EPI_RES (batched GEMMs): residual update fused with the next RMS norm's elementwise half - see
 // GemmArgs::resIn.
-enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2, EPI_ACT_Q80 = 3, EPI_ACT_F16 = 4, EPI_STORE_TP = 5, EPI_RES = 6 };
+// EPI_STORE_UN (Q40 GEMV, batch 1, the wo / w2 rows of decode at TP1): the residual update
+// x[r] += out[r] in place, u[r] = unW[r] * x[r] for the next norm and one partial sum of squares
+// per workgroup (ssOut[blockIdx]): the consumer's PRO_UNORM finishes the RMS norm.
+enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2, EPI_ACT_Q80 = 3, EPI_ACT_F16 = 4, EPI_STORE_TP = 5, EPI_RES = 6,
+                      EPI_STORE_UN = 7 };
 
 // Q40 weights live on the device TILED in the ring GEMV's consumption order, for a lanes-per-row
 // count L fixed per matrix (NG = 256/L row pairs per workgroup pass, K = ceil(nb/L) steps):
@@ -131,6 +138,13 @@ struct GemvArgs {
     float *xNext = nullptr;       // PRO_RESNORM: receives in+addIn (written by workgroup 0)
     const float *normW = nullptr; // PRO_RESNORM: rms weights (null = no norm)
     float eps = 1e-5f;
+    // PRO_UNORM: `in` = u (normW * x from the producer), ssIn = its ssCount partial sums of squares
+    const float *ssIn = nullptr;
+    int ssCount = 0;
+    // EPI_STORE_UN: `out` = x (updated in place), uOut = unW * x, ssOut[workgroup] = sum of x^2
+    float *uOut = nullptr;
+    const float *unW = nullptr;
+    float *ssOut = nullptr;
     // epilogue
     float *out = nullptr;
     int ldOut = 0;
@@ -267,6 +281,9 @@ struct AttnBlockArgs {
     AttnArgs at;                  // one row; outQ / outS = the wo input
     GemvArgs wo;                  // PRO_GLOBAL + EPI_STORE (or EPI_STORE_TP: wo.tp set)
     int hg = 1;                   // query heads per attention workgroup (attnBlockHG)
+    // 1: residual + norm split (TP1): the qkv role reads PRO_UNORM input (qkv.in = u, qkv.ssIn),
+    // the wo role ends with EPI_STORE_UN (wo.out = x in place, wo.uOut / unW / ssOut)
+    int un = 0;
     int layer = 0, nLayers = 1;
     const unsigned *epoch = nullptr;  // per-forward epoch (1, 2, ...), incremented by launchEmbedding
     unsigned *qkvCnt = nullptr;       // [kv groups * 64] monotonic counters, one per 256-B line (zeroed once)
@@ -335,6 +352,12 @@ int attnChunkMax(int seqLen, int splitGrid);
 // epoch (optional): one thread increments it - the per-forward epoch of the fused attention block.
 void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s,
                      unsigned *epoch = nullptr);
+// Batch-1 embedding that also produces the first norm's PRO_UNORM input: u = normW * x and the
+// sum of squares ss[0] (one partial).
+void launchEmbeddingUn(const float *table, const int *tokens, float *x, int dim, hipStream_t s, unsigned *epoch,
+                       const float *normW, float *u, float *ss);
+// Largest partial count a PRO_UNORM prologue reads (its producer's workgroups).
+constexpr int kUnMaxPartials = 1024;
 // Parallel argmax over [B][vocab]; partials need B*256 floats + ints, counters B ints (zeroed).
 // When `tokens` is non-null the result is also fed back (tokens[b] = id; hist[b][pos] = id; pos += 1).
 struct ArgmaxArgs {

@@ -541,6 +541,28 @@ void launchEmbedding(const float *table, const int *tokens, float *x, int dim, i
     hipLaunchKernelGGL(embeddingKernel, dim3(B), dim3(256), 0, s, table, tokens, x, dim, epoch);
 }
 
+// Batch-1 embedding + the first norm's PRO_UNORM input (u = normW * x, ss[0] = sum of x^2).
+__global__ __launch_bounds__(kThreads) void embeddingUnKernel(const float *table, const int *tokens, float *x, int dim,
+                                                              unsigned *epoch, const float *normW, float *u, float *ss) {
+    __shared__ float scratch[kThreads / kWave];
+    if (epoch && threadIdx.x == 0) *epoch += 1;
+    const float *src = table + (size_t)tokens[0] * dim;
+    float acc = 0.f;
+    for (int i = threadIdx.x * 4; i < dim; i += kThreads * 4) {
+        const float4 v = ld4(src + i), w = ld4(normW + i);
+        st4(x + i, v);
+        st4(u + i, make_float4(w.x * v.x, w.y * v.y, w.z * v.z, w.w * v.w));
+        acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
+    acc = blockSum<kThreads>(acc, scratch);
+    if (threadIdx.x == 0) ss[0] = acc;
+}
+
+void launchEmbeddingUn(const float *table, const int *tokens, float *x, int dim, hipStream_t s, unsigned *epoch,
+                       const float *normW, float *u, float *ss) {
+    hipLaunchKernelGGL(embeddingUnKernel, dim3(1), dim3(kThreads), 0, s, table, tokens, x, dim, epoch, normW, u, ss);
+}
+
 __device__ __forceinline__ void argBetter(float &bv, int &bi, float ov, int oi) {
     if (ov > bv || (ov == bv && oi < bi)) {
         bv = ov;

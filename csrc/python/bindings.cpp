@@ -759,6 +759,7 @@ PYBIND11_MODULE(_C, m) {
         .def_property_readonly("tp_fused", [](const PyHipEngine &e) { return e.engine->tpFused(); })
         .def_property_readonly("attn_block", [](const PyHipEngine &e) { return e.engine->attnBlock(); })
         .def_property_readonly("ffn_block", [](const PyHipEngine &e) { return e.engine->ffnBlock(); })
+        .def_property_readonly("unorm", [](const PyHipEngine &e) { return e.engine->unNorm(); })
         .def("trace_attn_block",
              [](PyHipEngine &e, int token, int pos, int slot, int layer, bool ffn) {
                  py::gil_scoped_release rel;
