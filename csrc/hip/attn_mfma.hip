@@ -533,6 +533,9 @@ static bool attnTrRead() {
     return v;
 }
 
+// preloadModules(): one kernel of this translation unit's code object
+const void *attnMfmaModuleKernel() { return (const void *)attnDecodeMfmaKernel<4, true>; }
+
 void launchAttentionMfma(const AttnArgs &a, int B, hipStream_t s) {
     const dim3 grid(a.nHeads0 / a.kvMul, a.splitGrid, B);
     if (2 * a.kvMul * a.splitGrid * 4 + 4096 > (int)kAmLds) throw Error("attention split grid too large");

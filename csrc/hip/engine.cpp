@@ -103,6 +103,7 @@ class HipEngineImpl : public HipEngine {
         setupAttnBlock();
         setupFfnBlock();
         setupUn();
+        hipk::preloadModules();  // no code-object load inside the first forwards
         load_.ms = timer.elapsedMs();
         load_.deviceBytes = deviceBytes_;
     }

@@ -469,6 +469,9 @@ __global__ __launch_bounds__(kThreads) void normF16Kernel(GemvArgs a, _Float16 *
     }
 }
 
+// preloadModules(): one kernel of this translation unit's code object
+const void *gemmModuleKernel() { return (const void *)normF16Kernel; }
+
 void launchNormF16(const GemvArgs &a, _Float16 *out, int M, hipStream_t s) {
     hipLaunchKernelGGL(normF16Kernel, dim3(M), dim3(kThreads), 0, s, a, out);
 }

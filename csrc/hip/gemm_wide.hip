@@ -202,6 +202,9 @@ __global__ __launch_bounds__(kThreads) void gemmWideKernel(GemmArgs ga, int rowT
                                   ga.ssIn ? rsL : nullptr);
 }
 
+// preloadModules(): one kernel of this translation unit's code object
+const void *gemmWideModuleKernel() { return (const void *)gemmWideKernel<EPI_STORE>; }
+
 void launchGemmWide(const GemmArgs &ga, int epi, hipStream_t s) {
     const int rowTiles = (ga.e.rows + kWRows - 1) / kWRows, tokTiles = (ga.M + kWTok - 1) / kWTok;
     if (ga.e.n % 64 != 0 || (ga.e.n / 32) % (kWKB * ga.splits) != 0) throw Error("launchGemmWide: bad K split");

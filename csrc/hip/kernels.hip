@@ -1213,5 +1213,49 @@ void launchFillF32Const(float *p, size_t n, float v, hipStream_t s) {
     hipLaunchKernelGGL(fillConstKernel, dim3(1024), dim3(256), 0, s, p, n, v);
 }
 
+// one kernel per translation unit (each .hip file is its own code object)
+const void *gemmModuleKernel();
+const void *gemmWideModuleKernel();
+const void *attnMfmaModuleKernel();
+const void *xgmiModuleKernel();
+const void *gemvFnL16(bool q40, int B, int pro, int epi);
+const void *gemvFnL32(bool q40, int B, int pro, int epi);
+const void *gemvFnL64(bool q40, int B, int pro, int epi);
+const void *attnBlockFn_16_32_128(int hg, bool bf16, int md);
+const void *attnBlockFn_32_32_128(int hg, bool bf16, int md);
+const void *attnBlockFn_64_32_128(int hg, bool bf16, int md);
+const void *attnBlockFn_64_16_128(int hg, bool bf16, int md);
+const void *attnBlockFn_64_64_128(int hg, bool bf16, int md);
+const void *attnBlockFn_32_64_128(int hg, bool bf16, int md);
+const void *attnBlockFn_64_64_64(int hg, bool bf16, int md);
+const void *ffnBlockFn_16_16(bool tp);
+const void *ffnBlockFn_16_32(bool tp);
+const void *ffnBlockFn_16_64(bool tp);
+const void *ffnBlockFn_32_32(bool tp);
+const void *ffnBlockFn_64_64(bool tp);
+
+void preloadModules() {
+    typedef const void *(*BlockFn)(int, bool, int);
+    const BlockFn blocks[] = {attnBlockFn_16_32_128, attnBlockFn_32_32_128, attnBlockFn_64_32_128, attnBlockFn_64_16_128,
+                              attnBlockFn_64_64_128, attnBlockFn_32_64_128, attnBlockFn_64_64_64};
+    std::vector<const void *> fns = {(const void *)argmaxKernel, gemmModuleKernel(), gemmWideModuleKernel(),
+                                     attnMfmaModuleKernel(), xgmiModuleKernel(), gemvFnL16(true, 1, 0, 0),
+                                     gemvFnL32(true, 1, 0, 0), gemvFnL64(true, 1, 0, 0), ffnBlockFn_16_16(false),
+                                     ffnBlockFn_16_32(false), ffnBlockFn_16_64(false), ffnBlockFn_32_32(false),
+                                     ffnBlockFn_64_64(false)};
+    for (BlockFn b : blocks) {  // any instance of the unit will do
+        const void *f = nullptr;
+        for (int hg = 1; hg <= 8 && !f; hg *= 2) f = b(hg, true, 0);
+        fns.push_back(f);
+    }
+    // resolving a kernel's attributes builds (loads) its code object for the current device
+    for (const void *f : fns) {
+        if (!f) continue;
+        hipFuncAttributes at;
+        (void)hipFuncGetAttributes(&at, f);
+    }
+    (void)hipGetLastError();  // a unit without a usable instance must not leave a sticky error
+}
+
 }  // namespace hipk
 }  // namespace dl

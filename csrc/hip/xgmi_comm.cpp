@@ -448,5 +448,9 @@ void xgmiSetLowLatency(DeviceComm *c, bool on) { static_cast<XgmiComm *>(c)->set
 void xgmiResetError(DeviceComm *c) { static_cast<XgmiComm *>(c)->resetError(); }
 bool xgmiCrossDevice(DeviceComm *c) { return static_cast<XgmiComm *>(c)->crossDevice(); }
 bool xgmiFenced(DeviceComm *c) { return static_cast<XgmiComm *>(c)->fenced(); }
+namespace hipk {
+// preloadModules(): one kernel of this translation unit's code object
+const void *xgmiModuleKernel() { return (const void *)xgmiKernel; }
+}  // namespace hipk
 
 }  // namespace dl
