@@ -57,20 +57,16 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
     const int t0 = c * ch, t1 = min(t0 + ch, len);
     const int nTiles = (t1 - t0 + kAmTile - 1) / kAmTile;
 
-    // this lane's column: query head g * KM + col (columns >= KM are zero and discarded)
+    // this lane's column: query head g * KM + col (columns >= KM are zero and discarded); the q
+    // loads are issued first, then the K / V DMA of the first two tiles, and only then are the q
+    // values waited for (one memory round trip at entry instead of two)
     const float scale = 1.0f / sqrtf((float)HS);
-    bf16x8 qf[DS];
+    float4 qx[DS][2];
 #pragma unroll
     for (int s = 0; s < DS; s++) {
-        float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (col < KM) {
-            const float *qp = a.q + (size_t)b * a.ldq + (size_t)(g * KM + col) * HS + 32 * s + 8 * h;
-            const float4 x0 = ld4(qp), x1 = ld4(qp + 4);
-            v[0] = x0.x * scale; v[1] = x0.y * scale; v[2] = x0.z * scale; v[3] = x0.w * scale;
-            v[4] = x1.x * scale; v[5] = x1.y * scale; v[6] = x1.z * scale; v[7] = x1.w * scale;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) qf[s][j] = (__bf16)v[j];
+        const float *qp = a.q + (size_t)b * a.ldq + (size_t)(g * KM + min(col, KM - 1)) * HS + 32 * s + 8 * h;
+        qx[s][0] = ld4(qp);
+        qx[s][1] = ld4(qp + 4);
     }
 
     char *wbuf = smem + wave * kAmWaveBytes;  // [2 buffers][K tile | V tile]
@@ -104,8 +100,19 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
     // for a ds_read only by the issuing wave's counted vmcnt FOLLOWED BY a workgroup barrier
     // (cdna_hip_programming.md, "Read a staged buffer one phase after the wait that retires it")
     const int nRounds = (nTiles + kAmWaves - 1) / kAmWaves;
-    if (wave < nTiles) issue(wave, 0);
-    if (wave + kAmWaves < nTiles) issue(wave + kAmWaves, 1);
+    // both prologue tiles are issued unconditionally (a tile past the chunk re-reads its last key:
+    // harmless, never consumed), so the vmcnt the q values wait for is the same on every wave
+    issue(wave, 0);
+    issue(wave + kAmWaves, 1);
+    const float qs = col < KM ? scale : 0.f;
+    bf16x8 qf[DS];
+#pragma unroll
+    for (int s = 0; s < DS; s++) {
+        const float4 x0 = qx[s][0], x1 = qx[s][1];
+        const float v[8] = {x0.x * qs, x0.y * qs, x0.z * qs, x0.w * qs, x1.x * qs, x1.y * qs, x1.z * qs, x1.w * qs};
+#pragma unroll
+        for (int j = 0; j < 8; j++) qf[s][j] = (__bf16)v[j];
+    }
     for (int k = 0; k < nRounds; k++) {
         const int i = k * kAmWaves + wave;
         if (i + kAmWaves < nTiles)
