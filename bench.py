@@ -11,9 +11,12 @@ random-init on device with the real Llama-3.1-8B shapes (no network for checkpoi
   logits -> argmax, the token fed back on device), K steps between barrier + device syncs;
 * value = B * 1000 / ((eval_ms_per_token + pred_ms_per_token) / 2), the named metric; the decode-only
   rate is reported as config.pred_tokens_per_s.
-Extra points in `config`: decode at position >= 4096 (long_ctx_pred_ms_per_token) and, on one GPU,
-the product path through `build/dllama inference --synthetic llama3_1_8b` (cli_*: per-token host
-round trips included).
+The engine is sized to --max-seq-len positions (default 4096, the reference run script's
+`--max-seq-len 4096`); attention launches follow the context actually reached (context buckets),
+not the capacity. Extra points in `config`: decode at position >= 4096 (long_ctx_pred_ms_per_token),
+the same short-context decode on an engine sized to the model's full 131072-position context
+(cap131072_pred_ms_per_token) and, on one GPU, the product path through
+`build/dllama inference --synthetic llama3_1_8b` (cli_*: per-token host round trips included).
 
     python bench.py --gpus 1 --steps 128 --warmup 16
     python bench.py --gpus 8 --steps 128 --warmup 16        # launches its own 8 ranks
@@ -49,7 +52,7 @@ LLAMA31_8B = dict(dim=4096, hidden_dim=14336, n_layers=32, n_heads=32, n_kv_head
                   weight_type=2, hidden_act=1)
 
 
-def _cli_point(local: int, prompt_tokens: int, steps: int) -> dict:
+def _cli_point(local: int, prompt_tokens: int, steps: int, max_seq: int) -> dict:
     """Product path on one GPU: `dllama inference --synthetic llama3_1_8b` with greedy sampling
     (per forward: H2D inputs, graph replay, D2H token, host sync), parsed from the reference's
     Evaluation / Prediction summary lines (src/dllama.cpp:98-113)."""
@@ -67,7 +70,7 @@ def _cli_point(local: int, prompt_tokens: int, steps: int) -> dict:
         prompt = ("The quick brown fox jumps over the lazy dog " * 8)[:prompt_tokens]
         cmd = [exe, "inference", "--synthetic", "llama3_1_8b", "--tokenizer", tok, "--prompt", prompt, "--steps",
                str(prompt_tokens + steps), "--temperature", "0", "--gpu-index", str(local), "--max-seq-len",
-               str(prompt_tokens + steps + 8), "--buffer-float-type", "q80", "--log-level", "0"]
+               str(max_seq), "--buffer-float-type", "q80", "--log-level", "0"]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
         except subprocess.TimeoutExpired:
@@ -147,6 +150,9 @@ def main() -> int:
                     help="synthetic shape (models/synthetic.py LLAMA_SHAPES); the headline metric is llama3_1_8b")
     ap.add_argument("--sync-type", default=os.environ.get("DL_SYNC_TYPE", "q80"), choices=["f32", "q80"],
                     help="TP partial-sum exchange: q80 (the reference's ZQ wire format, default) or f32 (exact)")
+    ap.add_argument("--max-seq-len", type=int, default=4096,
+                    help="engine context capacity (KV cache positions) of the headline engine")
+    ap.add_argument("--no-cap128k", action="store_true", help="skip the 131072-capacity decode point")
     ap.add_argument("--long-ctx", type=int, default=4096, help="position of the long-context decode point (0: off)")
     ap.add_argument("--no-cli", action="store_true", help="skip the dllama CLI product-path point (1 GPU)")
     ap.add_argument("--no-graphs", action="store_true")
@@ -192,14 +198,13 @@ def main() -> int:
                                                 comm_kind)
 
     long_pos = args.long_ctx if args.long_ctx > 0 else 0
-    seq_len = args.prompt + args.warmup + args.steps + 8
+    seq_len = max(args.max_seq_len, args.prompt + args.warmup + args.steps + 8)
     shape = LLAMA31_8B
     if args.shape != "llama3_1_8b":
         from distributed_llama_multiusers_amd.models.synthetic import LLAMA_SHAPES
         shape = dict(LLAMA31_8B, **LLAMA_SHAPES[args.shape])
 
     def make_engine(max_seq=seq_len, kv_bf16=True, sync=None):
-        # the context length is sized to the run (attention split grids follow it)
         synthetic = None if args.model else dict(shape, seq_len=max_seq)
         return C.HipEngine(args.model, "q80", max_seq_len=max_seq, max_batch=max_batch, n_slots=args.batch,
                            kv_bf16=kv_bf16,
@@ -280,7 +285,7 @@ def main() -> int:
     long_ms = None
     if long_pos:  # decode at a long context, own engine sized for it (KV rows it never wrote are
         del eng   # zeros: same work, same time)
-        eng = make_engine(long_pos + 24)
+        eng = make_engine(max(seq_len, long_pos + 24))
         eng.decode_greedy(4, tokens, [long_pos] * B, list(range(B)))
         barrier()
         torch.cuda.synchronize()
@@ -288,6 +293,19 @@ def main() -> int:
         eng.decode_greedy(16, tokens, [long_pos + 4] * B, list(range(B)))
         torch.cuda.synchronize()
         long_ms = (time.perf_counter() - tl) * 1000.0 / 16
+        barrier()
+
+    cap_ms = None
+    if not args.no_cap128k and not args.model:  # same short-context decode, full 131072-position capacity
+        del eng
+        eng = make_engine(131072)
+        eng.decode_greedy(4, tokens, [pos0] * B, list(range(B)))
+        barrier()
+        torch.cuda.synchronize()
+        tc = time.perf_counter()
+        eng.decode_greedy(32, tokens, [pos0 + 4] * B, list(range(B)))
+        torch.cuda.synchronize()
+        cap_ms = (time.perf_counter() - tc) * 1000.0 / 32
         barrier()
 
     f32kv_ms = None
@@ -319,7 +337,7 @@ def main() -> int:
     p4k_ms = p4k_big_ms = None
     if not args.no_prefill4k:  # a 4096-token prompt evaluated in 32-token chunks (attention grows with it)
         del eng
-        eng = make_engine(4096 + 8)
+        eng = make_engine(max(seq_len, 4096 + 8))
         p4k = [(i * 7919 + 13) % 128000 for i in range(4096)]
 
         def prefill(e, chunk):
@@ -340,15 +358,16 @@ def main() -> int:
         # one wide-GEMM launch per matrix covers every 128-token tile of the chunk
         if args.prefill_chunk > 32:
             del eng
-            eng = C.HipEngine(args.model, "q80", max_seq_len=4096 + 8, max_batch=args.prefill_chunk, n_slots=1,
+            sl = max(seq_len, 4096 + 8)
+            eng = C.HipEngine(args.model, "q80", max_seq_len=sl, max_batch=args.prefill_chunk, n_slots=1,
                               kv_bf16=True, gpu_index=local, use_graphs=not args.no_graphs,
-                              synthetic=None if args.model else dict(shape, seq_len=4096 + 8), seed=1234, rank=rank,
+                              synthetic=None if args.model else dict(shape, seq_len=sl), seed=1234, rank=rank,
                               world=world, uid=uid, comm=comm, sync_type=args.sync_type)
             p4k_big_ms = prefill(eng, args.prefill_chunk)
 
     if dist is not None:
         t = torch.tensor([elapsed, eval_s, long_ms or 0.0, f32kv_ms or 0.0, p4k_ms or 0.0, tpf32_ms or 0.0,
-                          p4k_big_ms or 0.0], dtype=torch.float64)
+                          p4k_big_ms or 0.0, cap_ms or 0.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, eval_s = float(t[0]), float(t[1])
         long_ms = float(t[2]) if long_ms is not None else None
@@ -356,6 +375,7 @@ def main() -> int:
         p4k_ms = float(t[4]) if p4k_ms is not None else None
         tpf32_ms = float(t[5]) if tpf32_ms is not None else None
         p4k_big_ms = float(t[6]) if p4k_big_ms is not None else None
+        cap_ms = float(t[7]) if cap_ms is not None else None
 
     ms_per_step = elapsed * 1000.0 / args.steps
     pred_ms_tok = ms_per_step / B
@@ -370,7 +390,7 @@ def main() -> int:
     cli = {}
     if world == 1 and not args.no_cli and args.shape == "llama3_1_8b" and not args.model:
         del eng
-        cli = _cli_point(local, min(args.prompt, 64), min(args.steps, 64))
+        cli = _cli_point(local, min(args.prompt, 64), min(args.steps, 64), seq_len)
     result = {
         "metric": METRIC,
         "value": round(tok_s, 3),
@@ -400,6 +420,7 @@ def main() -> int:
             "device_ms_per_step": round(dev_ms / args.steps, 4),
             "long_ctx_pos": long_pos or None,
             "long_ctx_pred_ms_per_token": round(long_ms / B, 4) if long_ms is not None else None,
+            "cap131072_pred_ms_per_token": round(cap_ms / B, 4) if cap_ms is not None else None,
             "f32_kv_pred_ms_per_token": round(f32kv_ms / B, 4) if f32kv_ms is not None else None,
             "prompt_4k_eval_ms_per_token": round(p4k_ms, 4) if p4k_ms is not None else None,
             "prompt_4k_chunk": args.prefill_chunk if p4k_big_ms is not None else None,

@@ -41,16 +41,12 @@ static int gemvGrid(const GemvArgs &g) {
 
 AttnBlockPlan attnBlockPlan(const AttnBlockArgs &a, bool tp) {
     AttnBlockPlan p;
-    // md: 0 plain, 1 tensor-parallel wo exchange, 2 residual + norm split (qkv PRO_UNORM, wo EPI_STORE_UN)
-    p.fn = attnBlockFn(a.qkv.lanes, a.wo.lanes, a.at.hs, a.hg, a.at.kvBf16 != 0, tp ? 1 : (a.un ? 2 : 0));
+    // md: 0 plain, 1 tensor-parallel wo exchange
+    p.fn = attnBlockFn(a.qkv.lanes, a.wo.lanes, a.at.hs, a.hg, a.at.kvBf16 != 0, tp ? 1 : 0);
     p.gq = gemvGrid(a.qkv);
     p.ga = a.at.nHeads0 / a.hg * a.at.splitGrid;
     p.gw = gemvGrid(a.wo);
     const int Rq = (kThreads / a.qkv.lanes) * 2 * a.qkv.passes, Rw = (kThreads / a.wo.lanes) * 2 * a.wo.passes;
-    if (a.un && (tp || Rw > kThreads || a.qkv.ssCount > kUnMaxPartials)) {
-        p.fn = nullptr;  // EPI_STORE_UN stages one row per thread; PRO_UNORM reads <= kUnMaxPartials
-        return p;
-    }
     size_t lq = gemvLayout(a.qkv.n, 1, true, Rq, PRO_RESNORM).total;
     size_t lw = gemvLayout(a.wo.n, 1, true, Rw, PRO_RESNORM).total;
     if (tp && a.wo.tp.q80) lw = std::max(lw, gemvLayout(a.wo.n, 1, true, Rw, PRO_RESNORM).act + tpQ80Lds(Rw, a.wo.tp.world));

@@ -27,7 +27,7 @@ __global__ __launch_bounds__(kThreads) void attnBlockKernel(AttnBlockArgs ba) {
     bs.timeoutTicks = ba.timeoutTicks;
     int x = blockIdx.x;
     if (x < gq) {  // producers first: dispatched ahead of the roles that wait on them
-        gemvQ40Body<LQ, 1, MD == 2 ? PRO_UNORM : PRO_RESNORM, EPI_QKV, GEMV_PRODUCER>(ba.qkv, x, smem, &bs);
+        gemvQ40Body<LQ, 1, PRO_RESNORM, EPI_QKV, GEMV_PRODUCER>(ba.qkv, x, smem, &bs);
         return;
     }
     x -= gq;
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(kThreads) void attnBlockKernel(AttnBlockArgs ba) {
         return;
     }
     x -= ga;
-    gemvQ40Body<LW, 1, PRO_GLOBAL, MD == 1 ? EPI_STORE_TP : (MD == 2 ? EPI_STORE_UN : EPI_STORE), GEMV_CONSUMER>(ba.wo, x, smem,
+    gemvQ40Body<LW, 1, PRO_GLOBAL, MD == 1 ? EPI_STORE_TP : EPI_STORE, GEMV_CONSUMER>(ba.wo, x, smem,
                                                                                                         &bs);
 }
 
@@ -59,7 +59,7 @@ template <int LQ, int LW, int HS>
 static const void *attnBlockFnT(int hg, bool bf16, int md) {
 #define DL_AB(G, F, M) \
     if (hg == G && bf16 == F && md == M) return (const void *)attnBlockKernel<LQ, LW, G, HS, F, M>;
-#define DL_AB4(G) DL_AB(G, true, 0) DL_AB(G, true, 1) DL_AB(G, true, 2) DL_AB(G, false, 0) DL_AB(G, false, 1) DL_AB(G, false, 2)
+#define DL_AB4(G) DL_AB(G, true, 0) DL_AB(G, true, 1) DL_AB(G, false, 0) DL_AB(G, false, 1)
     DL_AB4(1) DL_AB4(2) DL_AB4(4) DL_AB4(8)
 #undef DL_AB4
 #undef DL_AB

@@ -488,11 +488,7 @@ __global__ __launch_bounds__(kAmThreads) void attnPrefillDmaKernel(AttnArgs a, i
 }
 
 bool attnPrefillDmaSupported(const AttnArgs &a) {
-    static const bool on = [] {
-        const char *e = std::getenv("DL_PF_ATTN_DMA");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return on && a.kvBf16 && a.hs == kAmHS && (a.kvMul == 1 || a.kvMul == 2 || a.kvMul == 4 || a.kvMul == 8 ||
+    return a.kvBf16 && a.hs == kAmHS && (a.kvMul == 1 || a.kvMul == 2 || a.kvMul == 4 || a.kvMul == 8 ||
                                                 a.kvMul == 16);
 }
 
@@ -512,7 +508,7 @@ void launchAttentionPrefillDma(const AttnArgs &a, int nRows, hipStream_t s) {
 
 bool attnMfmaSupported(const AttnArgs &a) {
     return a.kvBf16 && a.hs == kAmHS && (a.kvMul == 1 || a.kvMul == 2 || a.kvMul == 4 || a.kvMul == 8) &&
-           a.nHeads0 % a.kvMul == 0 && a.pfBlocks == 0;
+           a.nHeads0 % a.kvMul == 0;
 }
 
 // DL_ATTN_MFMA: 0 = the VALU kernel everywhere, 1 = this kernel for every supported launch,
@@ -532,13 +528,7 @@ bool attnUsesMfma(const AttnArgs &a) {
     return a.mfma >= 0 ? a.mfma == 1 : a.seqLen >= 1024;
 }
 
-static bool attnTrRead() {
-    static const bool v = [] {
-        const char *e = std::getenv("DL_ATTN_TR");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return v;
-}
+static bool attnTrRead() { return true; }  // the scalar-read variant stays compiled as a cross-check
 
 // preloadModules(): one kernel of this translation unit's code object
 const void *attnMfmaModuleKernel() { return (const void *)attnDecodeMfmaKernel<4, true>; }

@@ -41,7 +41,7 @@ __host__ __device__ static GemvLds gemvLayout(int n, int B, bool q40, int rowsPe
     off += 64 * sizeof(float);
     l.rope = off;  // RoPE rows of the batch's positions (QKV epilogue of the Q40 ring kernel)
     off += (size_t)B * (kMaxHeadSize / 2) * sizeof(float2);
-    l.res = off;  // TP partial rows, or EPI_STORE_UN's x rows then unW rows
+    l.res = off;  // TP partial rows
     off = alignUp(off + (size_t)2 * B * rowsPerWg * sizeof(float), 16);
     l.hbuf = off;
     off = alignUp(off + (size_t)B * (rowsPerWg / 2) * sizeof(float), 16);
@@ -188,22 +188,6 @@ __device__ __forceinline__ void resNormPrologue(const GemvArgs &a, float *scratc
                            w8[4] * (inv * v1.x), w8[5] * (inv * v1.y), w8[6] * (inv * v1.z), w8[7] * (inv * v1.w)};
             stageChunk<Q40>(vv, b, c, n, sq, ssc, sf);
         }
-    }
-    __syncthreads();
-}
-
-// PRO_UNORM, batch 1, any n: 1 / rms from the producer's partial sums of squares, then u * inv ->
-// Q80 blocks in LDS (u = normW * x was stored by the producer's EPI_STORE_UN epilogue).
-__device__ __forceinline__ void unNormPrologue(const GemvArgs &a, float *scratch, int8_t *sq, float2 *ssc) {
-    const int n = a.n, tid = threadIdx.x, nChunks = n >> 3;
-    float ss = 0.f;
-    for (int i = tid; i < a.ssCount; i += kThreads) ss += a.ssIn[i];
-    ss = blockSum<kThreads>(ss, scratch);
-    const float inv = 1.0f / sqrtf(ss / (float)n + a.eps);
-    for (int c = tid; c < nChunks; c += kThreads) {
-        const float4 u0 = ld4(a.in + c * 8), u1 = ld4(a.in + c * 8 + 4);
-        float v[8] = {u0.x * inv, u0.y * inv, u0.z * inv, u0.w * inv, u1.x * inv, u1.y * inv, u1.z * inv, u1.w * inv};
-        stageChunk<true>(v, 0, c, n, sq, ssc, nullptr);
     }
     __syncthreads();
 }
@@ -685,25 +669,12 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
         // waited for on its own inside it (the first slot's dot products start while the rest of
         // the first round is still in flight). Loads are unconditional and clamped.
         auto ld4a = [](f32x4 &r, const float *p) { asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p)); };
-        auto ld1a = [](float &r, const float *p) { asm volatile("global_load_dword %0, %1, off" : "=v"(r) : "v"(p)); };
-        constexpr int NP = kUnMaxPartials / kThreads;  // PRO_UNORM partials per thread
-        float ep[NP];
-        float xr = 0.f, wr = 0.f;  // EPI_STORE_UN: this thread's row of x and of the next norm's weight
         u32x2 ropeV = {0u, 0u};
         if constexpr (EPI == EPI_QKV) {
             const float2 *rp = a.rope + (size_t)posB[0] * (a.hs >> 1) + min(tid, (a.hs >> 1) - 1);
             asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(ropeV) : "v"(rp));
         }
-        if constexpr (PRO == PRO_UNORM) {
-#pragma unroll
-            for (int k = 0; k < PK; k++) {
-                const int c = min(tid + k * kThreads, nChunks - 1);
-                ld4a(ex[k][0], a.in + c * 8);
-                ld4a(ex[k][1], a.in + c * 8 + 4);
-            }
-#pragma unroll
-            for (int k = 0; k < NP; k++) ld1a(ep[k], a.ssIn + min(tid + k * kThreads, a.ssCount - 1));
-        } else if constexpr (PRO == PRO_RESNORM) {
+        if constexpr (PRO == PRO_RESNORM) {
             const float *yp = a.addIn ? a.addIn : a.in;
             const float *wp = a.normW ? a.normW : a.in;
 #pragma unroll
@@ -727,11 +698,6 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
                 const u32x2 *src = reinterpret_cast<const u32x2 *>(a.as) + min(tid + k * kThreads, nb - 1);
                 asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(es[k]) : "v"(src));
             }
-            if constexpr (EPI == EPI_STORE_UN) {
-                const int r = min(rowBase + min(tid, R - 1), a.rows - 1);
-                ld1a(xr, a.out + r);
-                ld1a(wr, a.unW + r);
-            }
         }
         // A CU returns vector loads in issue order across its waves: without this barrier a wave's
         // prologue loads queue behind the other waves' ring rounds (~3 us at the CU's share of
@@ -750,19 +716,13 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
         }
         // the prologue's loads are older than the ring's 3 * KE: wait for them only
         if constexpr (EPI == EPI_QKV) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(ropeV) : "i"(3 * KE));
-        if constexpr (PRO == PRO_UNORM) {
-#pragma unroll
-            for (int k = 0; k < PK; k++) asm volatile("s_waitcnt vmcnt(%2)" : "+v"(ex[k][0]), "+v"(ex[k][1]) : "i"(3 * KE));
-#pragma unroll
-            for (int k = 0; k < NP; k++) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(ep[k]) : "i"(3 * KE));
-        } else if constexpr (PRO == PRO_RESNORM) {
+        if constexpr (PRO == PRO_RESNORM) {
 #pragma unroll
             for (int k = 0; k < PK; k++)
                 asm volatile("s_waitcnt vmcnt(%6)"
                              : "+v"(ex[k][0]), "+v"(ex[k][1]), "+v"(ey[k][0]), "+v"(ey[k][1]), "+v"(ew[k][0]), "+v"(ew[k][1])
                              : "i"(3 * KE));
         } else {
-            if constexpr (EPI == EPI_STORE_UN) asm volatile("s_waitcnt vmcnt(%2)" : "+v"(xr), "+v"(wr) : "i"(3 * KE));
 #pragma unroll
             for (int k = 0; k < PK; k++) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(eq[k]) : "i"(3 * KE));
 #pragma unroll
@@ -771,25 +731,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
         if (a.trace) tLoaded = wall_clock64();
         if constexpr (EPI == EPI_QKV)
             if (tid < (a.hs >> 1)) sRope[tid] = make_float2(__uint_as_float(ropeV.x), __uint_as_float(ropeV.y));
-        if constexpr (PRO == PRO_UNORM) {
-            float ss = 0.f;
-#pragma unroll
-            for (int k = 0; k < NP; k++)
-                if (tid + k * kThreads < a.ssCount) ss += ep[k];
-            ss = blockSum<kThreads>(ss, scratch);
-            const float inv = 1.0f / sqrtf(ss / (float)n + a.eps);
-#pragma unroll
-            for (int k = 0; k < PK; k++) {
-                const int c = tid + k * kThreads;
-                if (c < nChunks) {
-                    float v[8] = {ex[k][0].x, ex[k][0].y, ex[k][0].z, ex[k][0].w,
-                                  ex[k][1].x, ex[k][1].y, ex[k][1].z, ex[k][1].w};
-#pragma unroll
-                    for (int i = 0; i < 8; i++) v[i] *= inv;
-                    stageChunk<true>(v, 0, c, n, sq, ssc, nullptr);
-                }
-            }
-        } else if constexpr (PRO == PRO_RESNORM) {
+        if constexpr (PRO == PRO_RESNORM) {
             float *xo = (blk == 0 && a.xNext) ? a.xNext : nullptr;
             float v[PK][8];
             float ss = 0.f;
@@ -837,11 +779,6 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
 #pragma unroll
             for (int k = 0; k < PS; k++)
                 if (tid + k * kThreads < nb) reinterpret_cast<u32x2 *>(ssc)[tid + k * kThreads] = es[k];
-            if constexpr (EPI == EPI_STORE_UN)
-                if (tid < R) {
-                    res[tid] = xr;
-                    res[R + tid] = wr;
-                }
         }
         __syncthreads();
         if (a.trace) tReady = wall_clock64();
@@ -877,25 +814,11 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
         if constexpr (MODE == GEMV_CONSUMER) {
             // the activations are produced in this launch: wait for every producer (the ring's
             // weight loads are already in flight), then read them write-through
-            if constexpr (EPI == EPI_STORE_UN)  // this workgroup's rows of x and the next norm's weight
-                if (tid < R) {
-                    const int r = min(rowBase + tid, a.rows - 1);
-                    res[tid] = a.out[r];
-                    res[R + tid] = a.unW[r];
-                }
             tWaited = blockWait(bs->attnFlag + xccId() * kCntStride, bs->step, *bs, bs->codeBase + 3);
             stageQ80<B, true>(a, sq, ssc);
         } else if constexpr (PRO == PRO_RESNORM)
             resNormPrologue<B, true>(a, scratch, sq, ssc, nullptr);
-        else if constexpr (PRO == PRO_UNORM)
-            unNormPrologue(a, scratch, sq, ssc);
         else {
-            if constexpr (EPI == EPI_STORE_UN)
-                if (tid < R) {
-                    const int r = min(rowBase + tid, a.rows - 1);
-                    res[tid] = a.out[r];
-                    res[R + tid] = a.unW[r];
-                }
             stageQ80<B>(a, sq, ssc);
         }
         waitAll();
@@ -904,7 +827,6 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
 
     // The ring's consume loop. Each prologue path below inlines its own copy, so no ring register
     // is live across a join of two paths (a join could copy a register whose load is in flight).
-    float ssAcc = 0.f;  // EPI_STORE_UN: this thread's rows' sum of squares
     auto mainLoop = [&]() __attribute__((always_inline)) {
     float acc[RG][B];
 #pragma unroll
@@ -937,17 +859,6 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
                 if constexpr (EPI == EPI_STORE_TP) {
                     res[b * R + (r0 - rowBase)] = v0;
                     res[b * R + (r0 - rowBase) + 1] = v1;
-                } else if constexpr (EPI == EPI_STORE_UN) {  // batch 1: residual update + u + partial
-                    const int i0 = r0 - rowBase;
-                    const float x0 = res[i0] + v0, x1 = res[i0 + 1] + v1;
-                    a.out[r0] = x0;
-                    a.uOut[r0] = res[R + i0] * x0;
-                    ssAcc += x0 * x0;
-                    if (r0 + 1 < a.rows) {
-                        a.out[r0 + 1] = x1;
-                        a.uOut[r0 + 1] = res[R + i0 + 1] * x1;
-                        ssAcc += x1 * x1;
-                    }
                 } else if constexpr (EPI == EPI_STORE) {
                     float *o = a.out + (size_t)b * a.ldOut + r0;
                     o[0] = v0;
@@ -1019,10 +930,6 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
     if constexpr (EPI == EPI_ACT_Q80) {
         __syncthreads();
         storeHiddenQ80<B, MODE == GEMV_PRODUCER>(a, hbuf, R >> 1, rowBase >> 1);
-    }
-    if constexpr (EPI == EPI_STORE_UN) {
-        const float t = blockSum<kThreads>(ssAcc, scratch);
-        if (tid == 0) a.ssOut[blk] = t;
     }
     if constexpr (MODE == GEMV_PRODUCER) {  // rows published write-through: drain, then count in
         blockDrain();

@@ -30,14 +30,10 @@ class HipEngine : public Backend {
     virtual bool tpFused() const { return false; }
     // Single decode rows run the fused attention block (qkv + attention + wo in one launch).
     virtual bool attnBlock() const { return false; }
-    virtual bool unNorm() const { return false; }  // decode residual + norm split (EPI_STORE_UN / PRO_UNORM)
-    // Single decode rows run the fused FFN block (w13 + w2 in one launch).
-    virtual bool ffnBlock() const { return false; }
     // Diagnostics: one eager single-row forward with the fused attention block of `layer` traced
     // (kernels.h AttnBlockArgs::trace, 8 u64 per workgroup); returns {gq, ga, gw, trace...}.
-    // ffn: trace the fused FFN block instead; returns {g13, 0, g2, trace...}.
-    virtual std::vector<unsigned long long> traceAttnBlock(int token, int pos, int slot, int layer, bool ffn) {
-        (void)token, (void)pos, (void)slot, (void)layer, (void)ffn;
+    virtual std::vector<unsigned long long> traceAttnBlock(int token, int pos, int slot, int layer) {
+        (void)token, (void)pos, (void)slot, (void)layer;
         return {};
     }
     virtual int fusedGridMax() const { return 0; }

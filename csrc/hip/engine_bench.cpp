@@ -1,0 +1,275 @@
+// Kernel microbenchmarks (scripts/bench_gemv.py, bench_gemm.py, bench_attn.py): each cycles
+// `copies` operand sets through a graph of `iters` launches so the 256 MB Infinity Cache cannot
+// serve them, and returns microseconds per launch.
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "engine.h"
+#include "kernels.h"
+
+namespace dl {
+
+double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int passes, int copies, int iters,
+                    std::vector<unsigned long long> *trace) {
+    hipStream_t s;
+    DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<void *> mem;
+    auto alloc = [&](size_t bytes) {
+        void *p;
+        DL_HIP(hipMalloc(&p, bytes));
+        mem.push_back(p);
+        return p;
+    };
+    const int L = lanes > 0 ? lanes : hipk::gemvLanesPerRow(n, rows, B, true);
+    const hipk::Q40Tiling t = hipk::q40Tiling(rows, n, L);
+    std::vector<uint8_t *> qs(copies);
+    std::vector<uint16_t *> d(copies);
+    for (int c = 0; c < copies; c++) {
+        qs[c] = (uint8_t *)alloc(t.qsBytes);
+        d[c] = (uint16_t *)alloc(t.dBytes);
+        hipk::launchFillQ40(qs[c], d[c], t.qsBytes / 16, 0.01f, 77 + c, s);
+    }
+    float *x = (float *)alloc((size_t)B * n * 4), *y = (float *)alloc((size_t)B * n * 4);
+    float *xn = (float *)alloc((size_t)B * n * 4), *w = (float *)alloc((size_t)n * 4);
+    hipk::launchFillF32Uniform(x, (size_t)B * n, 1.f, 1, s);
+    hipk::launchFillF32Uniform(y, (size_t)B * n, 1.f, 2, s);
+    hipk::launchFillF32Const(w, n, 1.f, s);
+    int8_t *aq = (int8_t *)alloc((size_t)B * n);
+    float2 *as = (float2 *)alloc((size_t)B * n / 32 * 8);
+    DL_HIP(hipMemsetAsync(aq, 1, (size_t)B * n, s));
+    DL_HIP(hipMemsetAsync(as, 0, (size_t)B * n / 32 * 8, s));
+    const int outRows = epi == hipk::EPI_ACT_Q80 ? rows / 2 : rows;
+    float *out = (float *)alloc((size_t)B * rows * 4);
+    int8_t *oq = (int8_t *)alloc((size_t)B * outRows);
+    float2 *os = (float2 *)alloc((size_t)B * outRows / 32 * 8);
+    hipk::GemvArgs a;
+    a.rows = rows;
+    a.n = n;
+    a.lanes = L;
+    a.passes = passes > 0 ? passes : hipk::gemvDefaultPasses(n, rows, B, true, epi);
+    if (passes <= 0 && lanes > 0) {  // forced lane count: same residency rule with its rows/pass
+        const int rp = 256 / lanes * 2, grid0 = (rows + rp - 1) / rp;
+        a.passes = (grid0 + 511) / 512;
+        if (epi == hipk::EPI_ACT_Q80)
+            while ((rp * a.passes) % 64) a.passes++;
+    }
+    a.in = x;
+    a.ldIn = n;
+    a.addIn = y;
+    a.xNext = xn;
+    a.normW = w;
+    a.aq = aq;
+    a.as = as;
+    a.out = out;
+    a.ldOut = outRows;
+    a.oq = oq;
+    a.os = os;
+    if (epi == hipk::EPI_QKV) {  // Llama-like split: q = 2/3 of the rows, k = v = 1/6, one position
+        a.hs = 128;
+        a.kv0 = rows / 6;
+        a.q0 = rows - 2 * a.kv0;
+        a.seqLen = 1;
+        a.kvBf16 = 1;
+        float2 *rope = (float2 *)alloc(64 * sizeof(float2));
+        int *zeros = (int *)alloc(64 * sizeof(int));
+        DL_HIP(hipMemsetAsync(rope, 0, 64 * sizeof(float2), s));
+        DL_HIP(hipMemsetAsync(zeros, 0, 64 * sizeof(int), s));
+        a.rope = rope;
+        a.pos = zeros;
+        a.slot = zeros;
+        a.kcache = alloc((size_t)a.kv0 * 2);
+        a.vcache = alloc((size_t)a.kv0 * 2);
+    }
+    const int grid = (rows + (256 / L) * 2 * a.passes - 1) / ((256 / L) * 2 * a.passes);
+    unsigned long long *tbuf = trace ? (unsigned long long *)alloc((size_t)iters * grid * 8 * 8) : nullptr;
+    auto launch = [&](int c) {
+        a.qs = qs[c % copies];
+        a.wd = d[c % copies];
+        a.trace = tbuf ? tbuf + (size_t)c * grid * 8 : nullptr;
+        hipk::launchGemv(a, B, pro, epi, true, s);
+    };
+    launch(0);
+    DL_HIP(hipGetLastError());
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    DL_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < iters; i++) launch(i);
+    DL_HIP(hipStreamEndCapture(s, &g));
+    DL_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    DL_HIP(hipGraphLaunch(ge, s));
+    DL_HIP(hipStreamSynchronize(s));
+    hipEvent_t e0, e1;
+    DL_HIP(hipEventCreate(&e0));
+    DL_HIP(hipEventCreate(&e1));
+    DL_HIP(hipEventRecord(e0, s));
+    DL_HIP(hipGraphLaunch(ge, s));
+    DL_HIP(hipEventRecord(e1, s));
+    DL_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    DL_HIP(hipEventElapsedTime(&ms, e0, e1));
+    if (trace) {
+        trace->resize((size_t)iters * grid * 8);
+        DL_HIP(hipMemcpy(trace->data(), tbuf, trace->size() * 8, hipMemcpyDeviceToHost));
+    }
+    (void)hipGraphExecDestroy(ge);
+    (void)hipGraphDestroy(g);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    for (void *p : mem) (void)hipFree(p);
+    (void)hipStreamDestroy(s);
+    return ms * 1000.0 / iters;
+}
+
+double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters) {
+    DL_CHECK(M >= 1 && M <= hipk::kGemmMaxTokens && hipk::gemmSupported(n) && rows % 64 == 0, "bad gemm bench shape");
+    hipStream_t s;
+    DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<void *> mem;
+    auto alloc = [&](size_t bytes) {
+        void *p;
+        DL_HIP(hipMalloc(&p, bytes));
+        DL_HIP(hipMemsetAsync(p, 0, bytes, s));
+        mem.push_back(p);
+        return p;
+    };
+    const int L = hipk::gemvLanesPerRow(n, rows, 1, true);
+    const hipk::Q40Tiling t = hipk::q40Tiling(rows, n, L);
+    std::vector<uint8_t *> qs(copies);
+    std::vector<uint16_t *> d(copies);
+    for (int c = 0; c < copies; c++) {
+        qs[c] = (uint8_t *)alloc(t.qsBytes);
+        d[c] = (uint16_t *)alloc(t.dBytes);
+        hipk::launchFillQ40(qs[c], d[c], t.qsBytes / 16, 0.01f, 77 + c, s);
+    }
+    const int MP = hipk::gemmTokenPad(M);
+    _Float16 *x = (_Float16 *)alloc((size_t)MP * n * 2);
+    hipk::launchFillF32Uniform((float *)x, (size_t)MP * n / 2, 1e-3f, 3, s);  // small finite f16 pairs
+    const size_t part = hipk::gemmPartFloats(rows, n, M);
+    hipk::GemmArgs g;
+    g.e.rows = rows;
+    g.e.n = n;
+    g.e.lanes = L;
+    g.e.out = (float *)alloc((size_t)M * rows * 4);
+    g.e.ldOut = epi == hipk::EPI_STORE ? rows : rows / 2;
+    g.outH = (_Float16 *)alloc((size_t)M * rows * 2);
+    g.x = x;
+    g.M = M;
+    g.splits = hipk::gemmSplits(rows, n, M);
+    g.part = part ? (float *)alloc(part * 4) : nullptr;
+    g.counters = (int *)alloc((size_t)(rows / 64 + 1) * 4);
+    auto launch = [&](int c) {
+        g.e.qs = qs[c % copies];
+        g.e.wd = d[c % copies];
+        hipk::launchGemmQ40(g, epi, s);
+    };
+    launch(0);
+    DL_HIP(hipGetLastError());
+    hipGraph_t gr;
+    hipGraphExec_t ge;
+    DL_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < iters; i++) launch(i);
+    DL_HIP(hipStreamEndCapture(s, &gr));
+    DL_HIP(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+    DL_HIP(hipGraphLaunch(ge, s));
+    DL_HIP(hipStreamSynchronize(s));
+    hipEvent_t e0, e1;
+    DL_HIP(hipEventCreate(&e0));
+    DL_HIP(hipEventCreate(&e1));
+    DL_HIP(hipEventRecord(e0, s));
+    DL_HIP(hipGraphLaunch(ge, s));
+    DL_HIP(hipEventRecord(e1, s));
+    DL_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    DL_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipGraphExecDestroy(ge);
+    (void)hipGraphDestroy(gr);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    for (void *p : mem) (void)hipFree(p);
+    (void)hipStreamDestroy(s);
+    return ms * 1000.0 / iters;
+}
+
+double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B, int copies, int iters) {
+    hipStream_t s;
+    DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<void *> mem;
+    auto alloc = [&](size_t bytes) {
+        void *p;
+        DL_HIP(hipMalloc(&p, bytes));
+        DL_HIP(hipMemsetAsync(p, 0, bytes, s));
+        mem.push_back(p);
+        return p;
+    };
+    DL_CHECK(kvMul >= 1 && nHeads0 % kvMul == 0 && pos >= 0 && pos < seqLen && B >= 1, "bad attention bench shape");
+    const int kv0 = nHeads0 / kvMul * hs, q0 = nHeads0 * hs;
+    const size_t kvElems = (size_t)B * seqLen * kv0;  // one slot per row
+    std::vector<void *> kc(copies), vc(copies);
+    for (int c = 0; c < copies; c++) {
+        kc[c] = alloc(kvElems * 2);
+        vc[c] = alloc(kvElems * 2);
+        hipk::launchFillF32Uniform((float *)kc[c], kvElems / 2, 1.f, 5 + c, s);  // bf16 pairs of small values
+        hipk::launchFillF32Uniform((float *)vc[c], kvElems / 2, 1.f, 9 + c, s);
+    }
+    float *q = (float *)alloc((size_t)B * q0 * 4);
+    hipk::launchFillF32Uniform(q, (size_t)B * q0, 1.f, 3, s);
+    std::vector<int> hp(B), hsl(B);
+    for (int b = 0; b < B; b++) hp[b] = pos, hsl[b] = b;
+    int *dpos = (int *)alloc(B * 4), *dslot = (int *)alloc(B * 4);
+    DL_HIP(hipMemcpyAsync(dpos, hp.data(), B * 4, hipMemcpyHostToDevice, s));
+    DL_HIP(hipMemcpyAsync(dslot, hsl.data(), B * 4, hipMemcpyHostToDevice, s));
+    hipk::AttnArgs a;
+    a.q = q;
+    a.ldq = q0;
+    a.pos = dpos;
+    a.slot = dslot;
+    a.nHeads0 = nHeads0;
+    a.kvMul = kvMul;
+    a.hs = hs;
+    a.kv0 = kv0;
+    a.seqLen = seqLen;
+    a.splitGrid = hipk::attnSplitGrid(seqLen);
+    a.chunkMax = hipk::attnChunkMax(seqLen, a.splitGrid);
+    a.partO = (float *)alloc((size_t)B * nHeads0 * a.splitGrid * hs * 4);
+    a.partML = (float *)alloc((size_t)B * nHeads0 * a.splitGrid * 2 * 4);
+    a.outQ = (int8_t *)alloc((size_t)B * q0);
+    a.outS = (float2 *)alloc((size_t)B * q0 / 32 * 8);
+    a.ldOut = q0;
+    a.kvBf16 = 1;
+    a.counters = (int *)alloc((size_t)B * nHeads0 * 4);
+    DL_HIP(hipStreamSynchronize(s));
+    auto launch = [&](int c) {
+        a.kcache = kc[c % copies];
+        a.vcache = vc[c % copies];
+        hipk::launchAttention(a, B, s);
+    };
+    launch(0);
+    DL_HIP(hipGetLastError());
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    DL_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < iters; i++) launch(i);
+    DL_HIP(hipStreamEndCapture(s, &g));
+    DL_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    DL_HIP(hipGraphLaunch(ge, s));
+    DL_HIP(hipStreamSynchronize(s));
+    hipEvent_t e0, e1;
+    DL_HIP(hipEventCreate(&e0));
+    DL_HIP(hipEventCreate(&e1));
+    DL_HIP(hipEventRecord(e0, s));
+    DL_HIP(hipGraphLaunch(ge, s));
+    DL_HIP(hipEventRecord(e1, s));
+    DL_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    DL_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipGraphExecDestroy(ge);
+    (void)hipGraphDestroy(g);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    for (void *p : mem) (void)hipFree(p);
+    (void)hipStreamDestroy(s);
+    return ms * 1000.0 / iters;
+}
+
+}  // namespace dl

@@ -28,24 +28,13 @@ namespace hipk {
 static constexpr int kGemmRows = 64;
 static constexpr int kGemmCh = 8;  // Q40 blocks per pipeline stage (~25 KB at 32 tokens)
 
-// Split-K degree: grow S until the grid reaches the workgroup target (DL_GEMM_WG, read once) or
-// a split would get fewer than kGemmCh blocks. The target is sized so every CU holds its 3
-// resident workgroups: with one chunk in flight per workgroup, bytes in flight per CU (and so
-// HBM bandwidth) scale with resident workgroups, not with tiles.
-static int gemmWgTarget() {
-    static const int v = [] {
-        const char *e = std::getenv("DL_GEMM_WG");
-        return e ? std::max(1, std::atoi(e)) : 256;
-    }();
-    return v;
-}
-static int gemmMaxSplits() {
-    static const int v = [] {
-        const char *e = std::getenv("DL_GEMM_MAXS");
-        return e ? std::max(1, std::atoi(e)) : 8;
-    }();
-    return v;
-}
+// Split-K degree: grow S until the grid reaches the workgroup target or a split would get fewer
+// than kGemmCh blocks. The target is sized so every CU holds its 3 resident workgroups: with one
+// chunk in flight per workgroup, bytes in flight per CU (and so HBM bandwidth) scale with
+// resident workgroups, not with tiles (targets 128-1024 and 2-16 splits re-swept in round 3:
+// profiles/raw/r3_gemm_knobs.md).
+static int gemmWgTarget() { return 256; }
+static int gemmMaxSplits() { return 8; }
 
 GemmPlan gemmPlan(int rows, int n, int M) {
     GemmPlan p;
@@ -258,31 +247,10 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
 // The 128-token tile (prefill chunks): one stage buffer (73 KB), two workgroups per CU; each
 // weight chunk feeds 8 MFMA token tiles, so a 128-token slice streams the weights once instead of
 // twice.
-static int gemmStages4() {  // stage buffers of the 64-token tile (DL_GEMM_STG4, read once)
-    static const int v = [] {
-        const char *e = std::getenv("DL_GEMM_STG4");
-        return e && std::atoi(e) == 2 ? 2 : 1;
-    }();
-    return v;
-}
-
-static int gemmStages2() {  // stage buffers of the 32-token tile (DL_GEMM_STG2, read once)
-    static const int v = [] {
-        const char *e = std::getenv("DL_GEMM_STG2");
-        const int k = e ? std::atoi(e) : kGemmStages;
-        return k >= 1 && k <= 3 ? k : kGemmStages;
-    }();
-    return v;
-}
-
-static int gemmStages1() {  // stage buffers of the 16-token tile (DL_GEMM_STG1 = 2..4, read once)
-    static const int v = [] {
-        const char *e = std::getenv("DL_GEMM_STG1");
-        const int k = e ? std::atoi(e) : kGemmStages;
-        return k >= 2 && k <= 4 ? k : kGemmStages;
-    }();
-    return v;
-}
+// stage buffers per token-tile width (re-swept in round 3: profiles/raw/r3_gemm_knobs.md)
+static int gemmStages4() { return 1; }
+static int gemmStages2() { return kGemmStages; }
+static int gemmStages1() { return kGemmStages; }
 
 bool gemmTpxFits(int M, int world, bool q80) {
     if (M < 1 || M > 64 || world > kTpMaxRanks) return false;

@@ -46,13 +46,7 @@ bool gemmWideOn() {
     }();
     return v;
 }
-int gemmWideMin() {
-    static const int v = [] {
-        const char *e = std::getenv("DL_GEMM_WIDE_MIN");
-        return e ? std::max(17, std::atoi(e)) : 65;
-    }();
-    return v;
-}
+int gemmWideMin() { return 65; }  // below: narrow kernel (wide at 17-64 rows measured slower, r3)
 bool gemmUsesWide(int M) { return gemmWideOn() && M >= gemmWideMin(); }
 
 // K splits: grow while the grid stays under one workgroup per CU (256) and every split keeps >= 16

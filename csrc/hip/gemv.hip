@@ -33,10 +33,6 @@ static GemvLaunch gemvLaunchOf(const GemvArgs &a, int B, int pro, int epi, bool 
 void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_t s) {
     const GemvLaunch g = gemvLaunchOf(a, B, pro, epi, q40);
     if (!g.fn) throw Error("launchGemv: unsupported prologue / epilogue / batch combination");
-    if (epi == EPI_STORE_UN && (kThreads / (a.lanes > 0 ? a.lanes : gemvLanesPerRow(a.n, a.rows, B, q40))) * 2 * a.passes > kThreads)
-        throw Error("launchGemv: EPI_STORE_UN stages one row per thread (rows per workgroup > 256)");
-    if (pro == PRO_UNORM && (a.ssCount < 1 || a.ssCount > kUnMaxPartials))
-        throw Error("launchGemv: PRO_UNORM partial count out of range");
     if (g.lds > 65536) allowLds(g.fn, g.lds);
     GemvArgs args = a;
     void *kargs[] = {&args};

@@ -123,12 +123,6 @@ static const void *gemvFnPE(int pro, int epi) {
     DL_GEMV_CASE(PRO_RESNORM, EPI_ACT)
     if constexpr (Q40) {
         DL_GEMV_CASE(PRO_RESNORM, EPI_ACT_Q80)
-        if constexpr (B == 1) {  // decode at TP1: residual + norm split between producer and consumer
-            DL_GEMV_CASE(PRO_UNORM, EPI_QKV)
-            DL_GEMV_CASE(PRO_UNORM, EPI_ACT_Q80)
-            DL_GEMV_CASE(PRO_UNORM, EPI_STORE)
-            DL_GEMV_CASE(PRO_GLOBAL, EPI_STORE_UN)
-        }
         DL_GEMV_CASE(PRO_GLOBAL, EPI_STORE_TP)
         DL_GEMV_CASE(PRO_RESNORM, EPI_STORE_TP)
     }

@@ -25,19 +25,12 @@ namespace hipk {
 //             Q40 weights, f32 for F32 weights) - no prologue, no LDS, no barrier.
 // PRO_RESNORM: (x + delta) -> RMS norm -> Q80 (or f32) staged once per workgroup in LDS
 //             (normW == null: no norm, plain quantization of `in`).
-// PRO_UNORM (Q40, batch 1): the producer of x already stored u = normW * x and its partial sums of
-//             squares (EPI_STORE_UN): only 1 / rms is left (u * inv -> Q80 in LDS), so a
-//             workgroup reads n + ssCount floats instead of x, delta and normW (3n floats).
-enum Prologue : int { PRO_GLOBAL = 0, PRO_RESNORM = 1, PRO_UNORM = 2 };
+enum Prologue : int { PRO_GLOBAL = 0, PRO_RESNORM = 1 };
 // EPI_ACT_Q80: act(w1 x) * (w3 x), quantized to Q80 blocks for the next GEMV (32 hidden units/block).
 // EPI_STORE_TP: EPI_STORE whose rows are first all-reduced over the tensor-parallel ranks (GemvArgs::tp).
 // EPI_RES (batched GEMMs): residual update fused with the next RMS norm's elementwise half - see
 // GemmArgs::resIn.
-// EPI_STORE_UN (Q40 GEMV, batch 1, the wo / w2 rows of decode at TP1): the residual update
-// x[r] += out[r] in place, u[r] = unW[r] * x[r] for the next norm and one partial sum of squares
-// per workgroup (ssOut[blockIdx]): the consumer's PRO_UNORM finishes the RMS norm.
-enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2, EPI_ACT_Q80 = 3, EPI_ACT_F16 = 4, EPI_STORE_TP = 5, EPI_RES = 6,
-                      EPI_STORE_UN = 7 };
+enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2, EPI_ACT_Q80 = 3, EPI_ACT_F16 = 4, EPI_STORE_TP = 5, EPI_RES = 6 };
 
 // Q40 weights live on the device TILED in the ring GEMV's consumption order, for a lanes-per-row
 // count L fixed per matrix (NG = 256/L row pairs per workgroup pass, K = ceil(nb/L) steps):
@@ -92,10 +85,6 @@ struct AttnArgs {
     int kvBf16 = 1;
     int mfma = -1;              // decode kernel: 1 MFMA, 0 VALU, -1 by cache length (attnUsesMfma)
     int *counters = nullptr;    // [B][nHeads0/HG] arrival counters (zero-initialised, self-resetting)
-    // optional MALL warm-up run by extra workgroups of the same launch (weights of the next GEMVs)
-    const void *pf0 = nullptr, *pf1 = nullptr;
-    size_t pf0Bytes = 0, pf1Bytes = 0;
-    int pfBlocks = 0;
 };
 
 // Tensor-parallel partial-sum exchange fused into the tail of the kernel that produces the partial
@@ -138,13 +127,6 @@ struct GemvArgs {
     float *xNext = nullptr;       // PRO_RESNORM: receives in+addIn (written by workgroup 0)
     const float *normW = nullptr; // PRO_RESNORM: rms weights (null = no norm)
     float eps = 1e-5f;
-    // PRO_UNORM: `in` = u (normW * x from the producer), ssIn = its ssCount partial sums of squares
-    const float *ssIn = nullptr;
-    int ssCount = 0;
-    // EPI_STORE_UN: `out` = x (updated in place), uOut = unW * x, ssOut[workgroup] = sum of x^2
-    float *uOut = nullptr;
-    const float *unW = nullptr;
-    float *ssOut = nullptr;
     // epilogue
     float *out = nullptr;
     int ldOut = 0;
@@ -263,7 +245,7 @@ bool attnMfmaSupported(const AttnArgs &a);
 bool attnUsesMfma(const AttnArgs &a);
 void launchAttentionMfma(const AttnArgs &a, int B, hipStream_t s);
 void launchAttentionValu(const AttnArgs &a, int B, hipStream_t s);  // the VALU kernel (attnTask)
-// Prefill rows with LDS-DMA staged K / V (attn_mfma.hip; DL_PF_ATTN_DMA=0 keeps the register-staged
+// Prefill rows with LDS-DMA staged K / V (attn_mfma.hip; other shapes take the register-staged
 // kernels.hip kernel): bf16 cache, head size 128, kvMul 1..16.
 bool attnPrefillDmaSupported(const AttnArgs &a);
 void launchAttentionPrefillDma(const AttnArgs &a, int nRows, hipStream_t s);
@@ -281,9 +263,6 @@ struct AttnBlockArgs {
     AttnArgs at;                  // one row; outQ / outS = the wo input
     GemvArgs wo;                  // PRO_GLOBAL + EPI_STORE (or EPI_STORE_TP: wo.tp set)
     int hg = 1;                   // query heads per attention workgroup (attnBlockHG)
-    // 1: residual + norm split (TP1): the qkv role reads PRO_UNORM input (qkv.in = u, qkv.ssIn),
-    // the wo role ends with EPI_STORE_UN (wo.out = x in place, wo.uOut / unW / ssOut)
-    int un = 0;
     int layer = 0, nLayers = 1;
     const unsigned *epoch = nullptr;  // per-forward epoch (1, 2, ...), incremented by launchEmbedding
     unsigned *qkvCnt = nullptr;       // [kv groups * 64] monotonic counters, one per 256-B line (zeroed once)
@@ -309,38 +288,6 @@ void attnBlockExpect(const GemvArgs &qkv, int nKv, unsigned *out);
 GemvResidency attnBlockResidency(const AttnBlockArgs &a, bool tp);
 void launchAttnBlock(const AttnBlockArgs &a, bool tp, hipStream_t s);
 
-// Fused FFN block of one decode row (B = 1, Q40, Q80 hidden hand-off): the w13 GEMV (residual + RMS
-// norm prologue, SwiGLU -> Q80 epilogue stored write-through) and the w2 GEMV in ONE launch, roles
-//   [0, g13) w13 rows | [g13, g13 + g2) w2 rows.
-// The last w13 workgroup of a step raises per-XCD "w13 done" flags (monotonic arrival counter, the
-// step numbering of AttnBlockArgs); w2 workgroups issue their weight ring after that flag (or at
-// entry: ringEarly), then read the hidden vector write-through. Removes one kernel boundary and the
-// w2 start-up latency per layer. Requires the whole grid co-resident (ffnBlockResidency); every
-// wait is bounded and raises `error` (codes 13 data, 14 ring start).
-struct FfnBlockArgs {
-    GemvArgs w13;                     // PRO_RESNORM + EPI_ACT_Q80 (oq / os = the w2 input)
-    GemvArgs w2;                      // PRO_GLOBAL + EPI_STORE (or EPI_STORE_TP: w2.tp set)
-    int layer = 0, nLayers = 1;
-    const unsigned *epoch = nullptr;  // per-forward epoch, as AttnBlockArgs
-    unsigned *cnt = nullptr;          // [1] monotonic arrivals of w13 workgroups (own 256-B line)
-    unsigned *flag = nullptr;         // [8 * 64] per-XCD w13-done flags
-    int *error = nullptr;
-    long long timeoutTicks = 200LL * 1000 * 1000;
-    int ringEarly = 0;
-    // 0: w13 producers and w2 consumers are different workgroups (grid g13 + g2); 1: every
-    // workgroup runs its w13 rows, then issues its w2 weight ring at once and waits for the w13
-    // phase (grid max(g13, g2)): the w2 ramp overlaps the w13 stragglers and the flag latency
-    int sameWg = 0;
-    unsigned long long *trace = nullptr;  // GemvArgs::trace layout, w13 workgroups then w2
-};
-struct FfnBlockPlan {
-    const void *fn = nullptr;
-    int g13 = 0, g2 = 0;
-    size_t lds = 0;
-};
-FfnBlockPlan ffnBlockPlan(const FfnBlockArgs &a, bool tp);
-GemvResidency ffnBlockResidency(const FfnBlockArgs &a, bool tp);
-void launchFfnBlock(const FfnBlockArgs &a, bool tp, hipStream_t s);
 // Prefill rows on MFMA (bf16 caches): blocks of attnPrefillRowsPerBlock(kvMul) consecutive rows
 // must share one slot (positions arbitrary, causal per row); counters >= blocks x KV heads.
 void launchAttentionPrefill(const AttnArgs &a, int nRows, hipStream_t s);
@@ -352,12 +299,6 @@ int attnChunkMax(int seqLen, int splitGrid);
 // epoch (optional): one thread increments it - the per-forward epoch of the fused attention block.
 void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s,
                      unsigned *epoch = nullptr);
-// Batch-1 embedding that also produces the first norm's PRO_UNORM input: u = normW * x and the
-// sum of squares ss[0] (one partial).
-void launchEmbeddingUn(const float *table, const int *tokens, float *x, int dim, hipStream_t s, unsigned *epoch,
-                       const float *normW, float *u, float *ss);
-// Largest partial count a PRO_UNORM prologue reads (its producer's workgroups).
-constexpr int kUnMaxPartials = 1024;
 // Parallel argmax over [B][vocab]; partials need B*256 floats + ints, counters B ints (zeroed).
 // When `tokens` is non-null the result is also fed back (tokens[b] = id; hist[b][pos] = id; pos += 1).
 struct ArgmaxArgs {

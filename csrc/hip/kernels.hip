@@ -29,15 +29,6 @@ namespace dl {
 namespace hipk {
 
 
-// Tuning knob (experiments only): DL_GEMV_MIN_LANES=32 forces at least 32 lanes per row.
-static int minLanesOverride() {
-    static const int v = [] {
-        const char *e = getenv("DL_GEMV_MIN_LANES");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-
 int gemvLanesPerRow(int n, int rows, int B, bool q40) {
     int L;
     if (q40) {
@@ -54,8 +45,6 @@ int gemvLanesPerRow(int n, int rows, int B, bool q40) {
         // skinny shards (tensor parallel): fewer rows per workgroup so the grid still covers the CUs
         while (L < 64 && rows / (kThreads / L * gemvRowGroup(B, q40)) < 256) L *= 2;
     }
-    const int mo = minLanesOverride();
-    if (mo > L) L = mo > 64 ? 64 : mo;
     return L;
 }
 
@@ -185,42 +174,14 @@ int attnChunkMax(int seqLen, int splitGrid) {
 template <int HG, int HS, bool BF16>
 __global__ __launch_bounds__(kAttnThreads) void attnKernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int hgx = a.nHeads0 / HG;  // attention workgroups per (split, row) slice
-    if ((int)blockIdx.x >= hgx) {
-        // MALL warm-up role: every extra workgroup of every slice streams its share of the next
-        // GEMVs' weights with plain loads (allocating in the Infinity Cache) and discards them
-        const int pfx = gridDim.x - hgx;
-        const int id = (blockIdx.z * gridDim.y + blockIdx.y) * pfx + (blockIdx.x - hgx);
-        const int nPf = pfx * gridDim.y * gridDim.z;
-        typedef unsigned int u32x4l __attribute__((ext_vector_type(4)));
-        const size_t n0 = a.pf0Bytes / 16, n1 = a.pf1Bytes / 16, tot = n0 + n1;
-        const size_t per = (tot + nPf - 1) / nPf;
-        const size_t i0 = (size_t)id * per, i1 = min(i0 + per, tot);
-        const u32x4l *p0 = reinterpret_cast<const u32x4l *>(a.pf0), *p1 = reinterpret_cast<const u32x4l *>(a.pf1);
-        u32x4l acc = {0u, 0u, 0u, 0u};
-        for (size_t i = i0 + threadIdx.x; i < i1; i += 4 * kAttnThreads) {
-            u32x4l v[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const size_t j = min(i + (size_t)u * kAttnThreads, i1 - 1);
-                v[u] = j < n0 ? p0[j] : p1[j - n0];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) acc ^= v[u];
-        }
-        asm volatile("" ::"v"(acc.x), "v"(acc.y), "v"(acc.z), "v"(acc.w));
-        return;
-    }
     attnTask<HG, HS, BF16, kAttnThreads>(a, blockIdx.z, blockIdx.x, blockIdx.y, smem);
 }
 
 template <int HS, bool BF16>
 static void attnDispatchHG(const AttnArgs &a, int B, int HG, hipStream_t s) {
     constexpr int NW = kAttnThreads / 64;
-    int pfx = 0;  // extra MALL warm-up workgroups per slice (see attnKernel)
-    if (a.pfBlocks > 0 && (a.pf0Bytes + a.pf1Bytes) >= 16) pfx = (a.pfBlocks + a.splitGrid * B - 1) / (a.splitGrid * B);
     const size_t lds = sizeof(float) * (2 * NW * HG + NW * HG * HS + HG * HS + 2 * HG) + 16;
-    const dim3 grid(a.nHeads0 / HG + pfx, a.splitGrid, B);
+    const dim3 grid(a.nHeads0 / HG, a.splitGrid, B);
     switch (HG) {
         case 1: hipLaunchKernelGGL((attnKernel<1, HS, BF16>), grid, dim3(kAttnThreads), lds, s, a); break;
         case 2: hipLaunchKernelGGL((attnKernel<2, HS, BF16>), grid, dim3(kAttnThreads), lds, s, a); break;
@@ -237,10 +198,6 @@ void launchAttention(const AttnArgs &a, int B, hipStream_t s) {
 }
 
 void launchAttentionValu(const AttnArgs &a, int B, hipStream_t s) {
-    static const int hgOverride = [] {  // experiments: DL_ATTN_HG forces query heads per workgroup
-        const char *e = getenv("DL_ATTN_HG");
-        return e ? atoi(e) : 0;
-    }();
     // Query heads per workgroup: sharing a KV head's loads between HG heads costs HG x the serial
     // work per workgroup, so take the fewest heads per workgroup that keep the grid (at the
     // longest context this launch can see) within one workgroup per CU. Measured on MI355X
@@ -249,7 +206,6 @@ void launchAttentionValu(const AttnArgs &a, int B, hipStream_t s) {
     const int hgMax = (a.kvMul & (a.kvMul - 1)) == 0 ? (a.kvMul < 8 ? a.kvMul : 8) : 1;
     int HG = 1;
     while (HG < hgMax && (long)(a.nHeads0 / HG) * a.splitGrid * B > 256) HG *= 2;
-    if (hgOverride > 0 && hgOverride <= hgMax && hgMax % hgOverride == 0) HG = hgOverride;
     if (a.hs == 128) {
         if (a.kvBf16) attnDispatchHG<128, true>(a, B, HG, s);
         else attnDispatchHG<128, false>(a, B, HG, s);
@@ -539,28 +495,6 @@ __global__ void embeddingKernel(const float *table, const int *tokens, float *x,
 
 void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s, unsigned *epoch) {
     hipLaunchKernelGGL(embeddingKernel, dim3(B), dim3(256), 0, s, table, tokens, x, dim, epoch);
-}
-
-// Batch-1 embedding + the first norm's PRO_UNORM input (u = normW * x, ss[0] = sum of x^2).
-__global__ __launch_bounds__(kThreads) void embeddingUnKernel(const float *table, const int *tokens, float *x, int dim,
-                                                              unsigned *epoch, const float *normW, float *u, float *ss) {
-    __shared__ float scratch[kThreads / kWave];
-    if (epoch && threadIdx.x == 0) *epoch += 1;
-    const float *src = table + (size_t)tokens[0] * dim;
-    float acc = 0.f;
-    for (int i = threadIdx.x * 4; i < dim; i += kThreads * 4) {
-        const float4 v = ld4(src + i), w = ld4(normW + i);
-        st4(x + i, v);
-        st4(u + i, make_float4(w.x * v.x, w.y * v.y, w.z * v.z, w.w * v.w));
-        acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-    }
-    acc = blockSum<kThreads>(acc, scratch);
-    if (threadIdx.x == 0) ss[0] = acc;
-}
-
-void launchEmbeddingUn(const float *table, const int *tokens, float *x, int dim, hipStream_t s, unsigned *epoch,
-                       const float *normW, float *u, float *ss) {
-    hipLaunchKernelGGL(embeddingUnKernel, dim3(1), dim3(kThreads), 0, s, table, tokens, x, dim, epoch, normW, u, ss);
 }
 
 __device__ __forceinline__ void argBetter(float &bv, int &bi, float ov, int oi) {
@@ -1228,11 +1162,6 @@ const void *attnBlockFn_64_16_128(int hg, bool bf16, int md);
 const void *attnBlockFn_64_64_128(int hg, bool bf16, int md);
 const void *attnBlockFn_32_64_128(int hg, bool bf16, int md);
 const void *attnBlockFn_64_64_64(int hg, bool bf16, int md);
-const void *ffnBlockFn_16_16(bool tp);
-const void *ffnBlockFn_16_32(bool tp);
-const void *ffnBlockFn_16_64(bool tp);
-const void *ffnBlockFn_32_32(bool tp);
-const void *ffnBlockFn_64_64(bool tp);
 
 void preloadModules() {
     typedef const void *(*BlockFn)(int, bool, int);
@@ -1240,9 +1169,7 @@ void preloadModules() {
                               attnBlockFn_64_64_128, attnBlockFn_32_64_128, attnBlockFn_64_64_64};
     std::vector<const void *> fns = {(const void *)argmaxKernel, gemmModuleKernel(), gemmWideModuleKernel(),
                                      attnMfmaModuleKernel(), xgmiModuleKernel(), gemvFnL16(true, 1, 0, 0),
-                                     gemvFnL32(true, 1, 0, 0), gemvFnL64(true, 1, 0, 0), ffnBlockFn_16_16(false),
-                                     ffnBlockFn_16_32(false), ffnBlockFn_16_64(false), ffnBlockFn_32_32(false),
-                                     ffnBlockFn_64_64(false)};
+                                     gemvFnL32(true, 1, 0, 0), gemvFnL64(true, 1, 0, 0)};
     for (BlockFn b : blocks) {  // any instance of the unit will do
         const void *f = nullptr;
         for (int hg = 1; hg <= 8 && !f; hg *= 2) f = b(hg, true, 0);

@@ -26,8 +26,7 @@
 // LL word poll and remote read goes to HBM instead of a cache line that a peer's xGMI write does
 // not invalidate (a plain coarse-grained hipMalloc would let a local L2 line go stale while the
 // peer writes the HBM copy). Writers use system-scope atomic stores, readers system-scope atomic
-// loads, so neither side depends on cache maintenance; DL_XGMI_CACHED=1 selects plain hipMalloc
-// for comparison runs only.
+// loads, so neither side depends on cache maintenance.
 // Fused-exchange regions (TpXchg in kernels.h): producer kernels (wo / w2 GEMV tails, argmax)
 // push their partials straight into these, so TP decode needs no separate all-reduce kernel.
 // Elements are owned by fixed slots: chunk c (kChunk floats) belongs to slot c % kSlots, for
@@ -264,11 +263,7 @@ class XgmiComm : public DeviceComm {
         fvOff_ = (llOff_ + llBytes + kLLSlots * sizeof(unsigned) + 255) / 256 * 256;
         faOff_ = fvOff_ + (size_t)2 * world * kFusedVec * sizeof(uint64_t);
         const size_t total = faOff_ + (size_t)2 * world * kFusedArg * sizeof(uint64_t);
-        const char *cached = std::getenv("DL_XGMI_CACHED");
-        if (cached && *cached == '1')
-            DL_HIP(hipMalloc(&base_, total));
-        else
-            DL_HIP(hipExtMallocWithFlags(&base_, total, hipDeviceMallocUncached));
+        DL_HIP(hipExtMallocWithFlags(&base_, total, hipDeviceMallocUncached));
         DL_HIP(hipMemset(base_, 0, total));
         DL_HIP(hipMalloc(&fusedEpochs_, (kFusedVec + kFusedArg) * sizeof(unsigned)));
         DL_HIP(hipMemset(fusedEpochs_, 0, (kFusedVec + kFusedArg) * sizeof(unsigned)));

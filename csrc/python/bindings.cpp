@@ -758,14 +758,12 @@ PYBIND11_MODULE(_C, m) {
         .def_property_readonly("device_bytes", [](const PyHipEngine &e) { return e.engine->deviceBytes(); })
         .def_property_readonly("tp_fused", [](const PyHipEngine &e) { return e.engine->tpFused(); })
         .def_property_readonly("attn_block", [](const PyHipEngine &e) { return e.engine->attnBlock(); })
-        .def_property_readonly("ffn_block", [](const PyHipEngine &e) { return e.engine->ffnBlock(); })
-        .def_property_readonly("unorm", [](const PyHipEngine &e) { return e.engine->unNorm(); })
         .def("trace_attn_block",
-             [](PyHipEngine &e, int token, int pos, int slot, int layer, bool ffn) {
+             [](PyHipEngine &e, int token, int pos, int slot, int layer) {
                  py::gil_scoped_release rel;
-                 return e.engine->traceAttnBlock(token, pos, slot, layer, ffn);
+                 return e.engine->traceAttnBlock(token, pos, slot, layer);
              },
-             py::arg("token"), py::arg("pos"), py::arg("slot") = 0, py::arg("layer") = 1, py::arg("ffn") = false)
+             py::arg("token"), py::arg("pos"), py::arg("slot") = 0, py::arg("layer") = 1)
         .def_property_readonly("fused_grid_max", [](const PyHipEngine &e) { return e.engine->fusedGridMax(); })
         .def_property_readonly("kv_pages_free", [](const PyHipEngine &e) { return e.engine->kvPagesFree(); })
         .def("tp_batched_fused", [](const PyHipEngine &e, int n) { return e.engine->tpBatchedFused(n); }, py::arg("n"))

@@ -109,31 +109,68 @@ void Scheduler::loop() {
     }
 }
 
-// Under mu_. A request's slot becomes free: its KV pages go back to the pool (every rank).
+// Under mu_. A request's slot becomes free. With a paged KV cache its pages go back to the pool
+// on every rank first: the slot waits in releasing_ until flushReleases() has sent the RELEASE
+// (network I/O, never under mu_, so submit() / stats() on the HTTP threads do not stall).
 void Scheduler::returnSlot(int slot) {
-    freeSlots_.push_back(slot);
-    if (pagesTotal_ >= 0 && slotPages_[slot]) {
+    if (pagesTotal_ >= 0 && slotPages_[slot])
+        releasing_.push_back(slot);
+    else
+        freeSlots_.push_back(slot);
+}
+
+// Scheduler thread, without mu_: release the pages of the slots returned since the last call,
+// then make the slots admissible again (before the next admission / launch).
+void Scheduler::flushReleases() {
+    std::vector<int> rel;
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        rel.swap(releasing_);
+    }
+    if (rel.empty()) return;
+    for (int s : rel) {
         try {
-            sess_.releaseSlot(slot);
+            sess_.releaseSlot(s);
         } catch (const std::exception &) {  // a lost worker surfaces on the next forward
         }
-        slotPages_[slot] = 0;
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    for (int s : rel) {
+        slotPages_[s] = 0;
+        freeSlots_.push_back(s);
     }
 }
 
 void Scheduler::failAll(const std::string &what) {
-    std::lock_guard<std::mutex> lk(mu_);
-    inflight_ = false;
-    flight_.picks.clear();
-    for (auto &r : active_) {
-        r->error = what;
-        r->finished = true;
-        r->finish("error");
-        returnSlot(r->slot);
+    // the launched forward (if any) is collected first: it still writes the slots handed back
+    // below, and the backend refuses the next launch until it has been collected
+    bool hadFlight;
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        hadFlight = inflight_;
     }
-    for (auto &r : draining_) returnSlot(r->slot);
-    active_.clear();
-    draining_.clear();
+    if (hadFlight) {
+        try {
+            std::vector<int> ids(flight_.n);
+            sess_.collectIds(flight_.n, ids.data());
+        } catch (const std::exception &) {
+        }
+    }
+    {
+        std::lock_guard<std::mutex> lk(mu_);
+        inflight_ = false;
+        flight_.picks.clear();
+        for (auto &r : active_) {
+            r->error = what;
+            r->finished = true;
+            r->finish("error");
+            returnSlot(r->slot);
+        }
+        for (auto &r : draining_) returnSlot(r->slot);
+        active_.clear();
+        draining_.clear();
+    }
+    flushReleases();
 }
 
 // Under mu_. Finished requests leave active_; their KV slot is reused only once no forward in
@@ -180,6 +217,7 @@ bool Scheduler::step() {
         for (auto &r : draining_) returnSlot(r->slot);  // their last rows have completed
         draining_.clear();
     }
+    flushReleases();  // slots freed by the previous step's text work and by the collection above
 
     // 1) admission: one free KV slot per request (and, with a paged KV cache, the pages its prompt +
     //    max_tokens can reach; FIFO: the head waits until enough pages are free); cancelled requests

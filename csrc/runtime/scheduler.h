@@ -110,11 +110,14 @@ class Scheduler {
     std::vector<std::shared_ptr<GenRequest>> active_;
     std::vector<std::shared_ptr<GenRequest>> draining_;  // finished, rows still in the forward in flight
     std::vector<int> freeSlots_;
-    // paged KV cache: pages the engine may hold for each slot's current / last request (released by
-    // the engine when the slot's next request starts at position 0); admission needs enough pages
+    // paged KV cache: pages reserved for each slot's request at admission (prompt + max_tokens);
+    // returned to the pool through releaseSlot (a RELEASE to every rank) when the slot is freed,
+    // see flushReleases; admission needs enough unreserved pages
     int pagesTotal_ = -1, pageSize_ = 0;
     std::vector<int> slotPages_;
+    std::vector<int> releasing_;  // freed slots whose pages are not released yet (under mu_)
     void returnSlot(int slot);
+    void flushReleases();
     Flight flight_;
     bool inflight_ = false;
     bool stop_ = false;

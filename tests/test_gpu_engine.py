@@ -359,60 +359,6 @@ def test_attn_block_matches_separate_kernels(C, assets, medium, monkeypatch, kv_
         assert list(ca) == list(cb)
 
 
-@pytest.mark.parametrize("attn", ["0", "1"])
-def test_unorm_matches_resnorm(C, assets, medium, monkeypatch, attn):
-    """Single decode rows at TP1 split each residual update + RMS norm between the GEMVs: wo / w2
-    add their rows into x in place and leave u = normW * x plus per-workgroup sums of squares
-    (EPI_STORE_UN), the qkv / w13 / logits prologues only apply 1 / rms (PRO_UNORM). Same logits as
-    the per-workgroup norm prologues within f32 reassociation (the sum of squares is reduced in
-    another order), same greedy chain, with and without the fused attention block; batched forwards
-    in between keep their own path. Opt-in (DL_UNORM=1): measured a wash on 8B decode."""
-    monkeypatch.setenv("DL_ATTN_BLOCK", attn)
-    for model in (assets["q40"], medium):
-        monkeypatch.setenv("DL_UNORM", "0")
-        ref = C.HipEngine(model, "q80", kv_bf16=True, max_batch=8)
-        monkeypatch.setenv("DL_UNORM", "1")
-        got = C.HipEngine(model, "q80", kv_bf16=True, max_batch=8)
-        assert not ref.unorm and got.attn_block == (attn == "1")
-        # the tiny model's hidden dim is too narrow for the Q80 hidden hand-off: no split there
-        assert got.unorm == (model == medium)
-        toks = [3, 17, 101, 7, 250, 9]
-        a, b = _seq(ref, toks), _seq(got, toks)
-        assert _rel(b, a) < 2e-3
-        ref.forward([5, 6, 7], [6, 7, 8], [0, 0, 0])
-        got.forward([5, 6, 7], [6, 7, 8], [0, 0, 0])
-        _, ca = ref.decode_greedy(24, [int(a[-1].argmax())], [9], [0])
-        _, cb = got.decode_greedy(24, [int(b[-1].argmax())], [9], [0])
-        assert list(ca) == list(cb)
-
-
-@pytest.mark.parametrize("mode,ring_early", [("1", "0"), ("1", "1"), ("2", "0")])
-def test_ffn_block_matches_separate_kernels(C, medium, monkeypatch, mode, ring_early):
-    """Single decode rows run the fused FFN block (w13 GEMV with the SwiGLU -> Q80 hidden stored
-    write-through + the w2 GEMV as one launch): bitwise the same logits as the two separate
-    launches (same kernels, same reduction order), over many forwards and graph replays (monotonic
-    counters), with and without the attention block, w2's weight ring issued at entry or after the
-    w13 phase; mode 2: the same workgroups run their w13 rows, then their w2 rows."""
-    monkeypatch.setenv("DL_FFN_RING_EARLY", ring_early)
-    for attn in ("0", "1"):
-        monkeypatch.setenv("DL_ATTN_BLOCK", attn)
-        monkeypatch.setenv("DL_FFN_BLOCK", "0")
-        ref = C.HipEngine(medium, "q80", kv_bf16=True, max_batch=8)
-        monkeypatch.setenv("DL_FFN_BLOCK", mode)
-        got = C.HipEngine(medium, "q80", kv_bf16=True, max_batch=8)
-        assert got.ffn_block and not ref.ffn_block and got.attn_block == (attn == "1")
-        toks = [3, 17, 101, 7, 250, 9]
-        a, b = _seq(ref, toks), _seq(got, toks)
-        assert np.array_equal(a, b)
-        ref.forward([5, 6, 7], [6, 7, 8], [0, 0, 0])  # batched forward between: the epoch must not advance
-        got.forward([5, 6, 7], [6, 7, 8], [0, 0, 0])
-        _, ca = ref.decode_greedy(24, [int(a[-1].argmax())], [9], [0])
-        _, cb = got.decode_greedy(24, [int(b[-1].argmax())], [9], [0])
-        assert list(ca) == list(cb)
-        tr = got.trace_attn_block(7, 40, 0, 1, ffn=True)
-        assert tr[0] > 0 and tr[2] > 0 and len(tr) == 3 + 8 * (tr[0] + tr[2])
-
-
 @pytest.mark.parametrize("kv_bf16,page", [(True, 32), (False, 64)])
 def test_paged_kv_cache_matches_contiguous(C, medium, kv_bf16, page):
     """Paged KV cache (page table per slot over a shared pool): the same forwards as the contiguous

@@ -108,7 +108,7 @@ def _engine_tp_batched(rank, world, port, model, tokens, q, sync_type="f32", env
         _, dec = eng.decode_greedy(6, [ids[1][-1]], [len(tokens)], [0])  # decode rows: fused exchange if on
         if comm.timed_out():
             raise AssertionError("a flag wait timed out")
-        fused = bool(eng.tp_fused) and (not env or "DL_EXPECT_BLOCKS" not in env or bool(eng.ffn_block))
+        fused = bool(eng.tp_fused) and (not env or "DL_EXPECT_BLOCKS" not in env or bool(eng.attn_block))
         if env and "DL_TP_BATCHED" in env:  # the batched rows' exchange: in the GEMM epilogues or not
             assert eng.tp_batched_fused(32) == (env["DL_TP_BATCHED"] != "0")
         dist.barrier()
@@ -248,30 +248,26 @@ def test_xgmi_engine_tp_sampled_rows_on_root(C, tmp_path):
 
 
 def test_xgmi_engine_tp_fused_blocks(C, tmp_path):
-    """TP=2 with the fused attention and FFN blocks on the decode rows (the wo / w2 exchanges run in
-    the consumer roles' tails): rank 0's logits of the batched forwards vs TP=1, decode tokens equal
+    """TP=2 with the fused attention block on the decode rows (the wo exchange runs in the consumer
+    role's tail): rank 0's logits of the batched forwards vs TP=1, decode tokens equal
     on both ranks and to the TP=1 greedy chain (allowing a late near-tie flip)."""
     from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
     from distributed_llama_multiusers_amd.utils.mfile import FloatType
     m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=13, dim=1024, n_heads=8,
                                n_kv_heads=4, hidden_dim=12288, vocab_size=1024, n_layers=2)
     tokens = [int(t) for t in np.random.default_rng(5).integers(0, 1024, 96)]
-    os.environ["DL_FFN_BLOCK"] = "1"
-    try:
-        single = C.HipEngine(m, "q80", kv_bf16=True, max_batch=64, n_slots=1)
-    finally:
-        del os.environ["DL_FFN_BLOCK"]
+    single = C.HipEngine(m, "q80", kv_bf16=True, max_batch=64, n_slots=1)
     ref = np.concatenate([single.forward(tokens[:32], list(range(32)), [0] * 32),
                           single.forward(tokens[32:], list(range(32, 96)), [0] * 64)])
     _, ref_dec = single.decode_greedy(6, [int(ref[-1].argmax())], [96], [0])
-    assert single.ffn_block
+    assert single.attn_block
     del single
-    res = _run(_engine_tp_batched, 2, m, tokens, kwargs=dict(env={"DL_EXPECT_BLOCKS": "1", "DL_FFN_BLOCK": "1"}))
+    res = _run(_engine_tp_batched, 2, m, tokens, kwargs=dict(env={"DL_EXPECT_BLOCKS": "1"}))
     assert all(isinstance(v, tuple) for v in res.values()), res
     got = res[0][0]
     rel = np.abs(got - ref).max() / np.abs(ref).max()
     assert rel < 3e-2, rel
-    assert res[1][3] == res[0][3] and res[0][2], "fused exchange + FFN block expected on for the decode rows"
+    assert res[1][3] == res[0][3] and res[0][2], "fused exchange + attention block expected on for the decode rows"
     assert res[0][3][:4] == list(ref_dec[:4]), (res[0][3], ref_dec)
 
 
