@@ -49,6 +49,7 @@ HipEngineImpl::HipEngineImpl(const EngineConfig &cfg, DeviceComm *comm) : cfg_(c
                    (size_t)2 * cfg.maxBatch <= (size_t)tpArg_.stride;
         tpVec_.q80 = syncQ80_ ? 1 : 0;
     }
+    decidePde();  // before checkFits / the load: it fixes the layer matrices' tiling
     checkFits();
     if (tpFused_) checkFusedResidency();
     {  // path knobs, read once: a captured graph replays the path it was captured with
@@ -66,6 +67,7 @@ HipEngineImpl::HipEngineImpl(const EngineConfig &cfg, DeviceComm *comm) : cfg_(c
     uploadRope();
     DL_HIP(hipStreamSynchronize(stream_));
     setupAttnBlock();
+    setupPde();
     hipk::preloadModules();  // no code-object load inside the first forwards
     load_.ms = timer.elapsedMs();
     load_.deviceBytes = deviceBytes_;
@@ -222,14 +224,17 @@ void HipEngineImpl::profileForward(int n, const int *tokens, const int *position
 void HipEngineImpl::syncAndCheckComm() {
     const int *flag = comm_ ? comm_->deviceErrorFlag() : nullptr;
     if (flag) DL_HIP(hipMemcpyAsync(hErr_, flag, sizeof(int), hipMemcpyDeviceToHost, stream_));
-    if (blockOn_) DL_HIP(hipMemcpyAsync(hErr_ + 1, dBlockErr_, sizeof(int), hipMemcpyDeviceToHost, stream_));
+    const bool inLaunch = blockOn_ || pdeOn_;  // kernels with in-launch hand-offs
+    if (inLaunch) DL_HIP(hipMemcpyAsync(hErr_ + 1, dBlockErr_, sizeof(int), hipMemcpyDeviceToHost, stream_));
     DL_HIP(hipStreamSynchronize(stream_));
-    if (blockOn_ && hErr_[1] != 0) {
+    if (inLaunch && hErr_[1] != 0) {
         const int code = hErr_[1];
         hErr_[1] = 0;
         resetAttnBlockState();
-        throw Error("fused attention block: a hand-off wait timed out (code " + std::to_string(code) +
-                    ": 2 qkv->attention, 3 attention->wo, 4 qkv phase; not all workgroups resident?)");
+        throw Error("in-launch hand-off wait timed out (code " + std::to_string(code) +
+                    ": attention block 2 qkv->attention, 3 attention->wo, 4 qkv phase; decode engine 21 w2->qkv, "
+                    "22 qkv->attention, 23 attention->wo, 24 wo->w13, 25 w13->w2, 26 final; not all workgroups "
+                    "resident?)");
     }
     if (flag && *hErr_ != 0)
         throw Error("tensor-parallel collective timed out: a peer rank did not arrive within 2 s (worker lost?)");

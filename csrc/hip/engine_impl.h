@@ -86,6 +86,7 @@ class HipEngineImpl : public HipEngine {
     void profileForward(int n, const int *tokens, const int *positions, const int *slots) override;
     bool tpFused() const override { return tpFused_; }
     bool attnBlock() const override { return blockOn_; }
+    bool decodeEngine() const override { return pdeOn_; }
     std::vector<unsigned long long> traceAttnBlock(int token, int pos, int slot, int layer) override;
     int fusedGridMax() const override { return fusedGridMax_; }
     bool tpBatchedFused(int n) const override { return plan_.nRanks > 1 && batchedPath(n) && fuseNorm(n); }
@@ -120,7 +121,13 @@ class HipEngineImpl : public HipEngine {
     void checkFusedResidency();
     void allocBuffers();
     void uploadRope();
-    size_t matStageBytes(u32 rows, u32 n) const;
+    size_t matStageBytes(u32 rows, u32 n, bool layerMat = true) const;
+    // lanes per row of a matrix's Q40 tiling: 64 for the layer matrices when the persistent decode
+    // engine streams them, else the GEMV's choice
+    int lanesFor(int rows, int n, bool layerMat) const {
+        return pdeTiling_ && layerMat ? 64 : hipk::gemvLanesPerRow(n, rows, 1, true);
+    }
+    void placeQ40(DevMat &m, const hipk::Q40Tiling &t, int mi, u32 l);
     struct RowSrc {
         const TensorInfo *t;
         u32 r0, nr;
@@ -130,10 +137,11 @@ class HipEngineImpl : public HipEngine {
     void stageCopy(Loader &ld, void *dst, const u8 *src, size_t bytes);
     void stageRelease(Loader &ld);
     void readRows(Loader &ld, const std::vector<RowSrc> &srcs, bool interleave, u32 c0, u32 nc);
-    void buildMat(Loader &ld, DevMat &m, const std::vector<RowSrc> &srcs, bool interleave, u32 c0, u32 nc);
+    void buildMat(Loader &ld, DevMat &m, const std::vector<RowSrc> &srcs, bool interleave, u32 c0, u32 nc, int mi,
+                  u32 l);
     float *uploadF32(Loader &ld, const TensorInfo &t);
     void loadFromFile();
-    void synthMat(DevMat &m, int rows, int n, u64 seed);
+    void synthMat(DevMat &m, int rows, int n, u64 seed, int mi, u32 l);
     void loadSynthetic();
 
     // engine_kv.cpp
@@ -210,7 +218,10 @@ class HipEngineImpl : public HipEngine {
     size_t deviceBytes_ = 0;
     LoadStats load_;
 
-    // weights
+    // weights (layer matrices of one kind in one slab per kind: placeQ40)
+    uint8_t *qsSlab_[4] = {};
+    uint16_t *dSlab_[4] = {};
+    size_t qsStride_[4] = {}, dStride_[4] = {};
     std::vector<DevLayer> layers_;
     DevMat wcls_;
     float *emb_ = nullptr, *rmsFinal_ = nullptr;
@@ -244,6 +255,16 @@ class HipEngineImpl : public HipEngine {
     int bucket_ = 0;          // index into buckets_
     bool attnLong_ = false;   // decode attention runs the MFMA kernel
     bool prefillOk_ = false;  // the rows qualify for the MFMA prefill attention
+
+    // persistent decode engine (decode_engine.hip; engine_forward.cpp setupPde)
+    bool pdeTiling_ = false;  // layer matrices tiled with 64 lanes per row (decided before the load)
+    bool pdeOn_ = false;      // single decode rows of short contexts run the engine
+    int pdeGrid_ = 0;
+    hipk::PdeArgs pde_;
+    std::vector<int> pdePasses_;  // [4][2 * grid + 1] pass ranges (decidePde)
+    float *dXOut_ = nullptr;
+    void decidePde();
+    void setupPde();
 
     // fused attention block
     unsigned *dEpoch_ = nullptr, *dBlockCnt_ = nullptr, *dBlockExpect_ = nullptr;

@@ -21,7 +21,7 @@ void HipEngineImpl::checkFits() {
     const size_t kv = (size_t)h_.nLayers * 2 * kvPoolRows() * p.kv0 * (kvBf16_ ? 2 : 4);
     size_t w = (size_t)h_.nLayers * (matStageBytes(p.q0 + 2 * p.kv0, h_.dim) + matStageBytes(h_.dim, p.q0) +
                                      matStageBytes(2 * p.hidden0, h_.dim) + matStageBytes(h_.dim, p.hidden0));
-    w += matStageBytes(p.vocab0, h_.dim) + (size_t)h_.vocabSize * h_.dim * 4;
+    w += matStageBytes(p.vocab0, h_.dim, false) + (size_t)h_.vocabSize * h_.dim * 4;
     const size_t act = (size_t)cfg_.maxBatch * h_.vocabSize * 4 * 3 + ((size_t)256 << 20);
     if (kv + w + act > freeB) {
         // the page pool that would fit (positions shared by all slots), as a hint
@@ -276,25 +276,45 @@ void HipEngineImpl::readRows(Loader &ld, const std::vector<RowSrc> &srcs, bool i
     }
 }
 
-size_t HipEngineImpl::matStageBytes(u32 rows, u32 n) const {
+size_t HipEngineImpl::matStageBytes(u32 rows, u32 n, bool layerMat) const {
     if (!q40_) return (size_t)rows * n * 4;
-    const hipk::Q40Tiling t = hipk::q40Tiling((int)rows, (int)n, hipk::gemvLanesPerRow((int)n, (int)rows, 1, true));
+    const hipk::Q40Tiling t = hipk::q40Tiling((int)rows, (int)n, lanesFor((int)rows, (int)n, layerMat));
     return t.qsBytes + t.dBytes;
 }
 
-void HipEngineImpl::buildMat(Loader &ld, DevMat &m, const std::vector<RowSrc> &srcs, bool interleave, u32 c0, u32 nc) {
+// Device storage of a Q40 matrix: layer matrix `mi` (0 qkv, 1 wo, 2 w13, 3 w2) of layer l lives in
+// one slab per matrix kind, all layers back to back (the persistent decode engine addresses layer
+// l as slab + l * stride); other matrices get their own allocation.
+void HipEngineImpl::placeQ40(DevMat &m, const hipk::Q40Tiling &t, int mi, u32 l) {
+    if (mi < 0) {
+        m.qs = dalloc<uint8_t>(t.qsBytes);
+        m.d = dalloc<uint16_t>(t.dBytes / 2);
+        return;
+    }
+    if (!qsSlab_[mi]) {
+        qsStride_[mi] = t.qsBytes;
+        dStride_[mi] = t.dBytes;
+        qsSlab_[mi] = dalloc<uint8_t>(t.qsBytes * h_.nLayers);
+        dSlab_[mi] = dalloc<uint16_t>(t.dBytes / 2 * h_.nLayers);
+    }
+    DL_CHECK(qsStride_[mi] == t.qsBytes && dStride_[mi] == t.dBytes, "layer matrices of one kind differ in size");
+    m.qs = qsSlab_[mi] + (size_t)l * qsStride_[mi];
+    m.d = dSlab_[mi] + (size_t)l * (dStride_[mi] / 2);
+}
+
+void HipEngineImpl::buildMat(Loader &ld, DevMat &m, const std::vector<RowSrc> &srcs, bool interleave, u32 c0, u32 nc,
+                             int mi, u32 l) {
     readRows(ld, srcs, interleave, c0, nc);
     const int rows = (int)ld.rowPtr.size();
     m.rows = rows;
     m.n = (int)nc;
     u8 *st = stageAcquire(ld);
     if (q40_) {
-        m.lanes = hipk::gemvLanesPerRow((int)nc, rows, 1, true);
+        m.lanes = lanesFor(rows, (int)nc, mi >= 0);
         const hipk::Q40Tiling t = hipk::q40Tiling(rows, (int)nc, m.lanes);
         DL_CHECK(t.qsBytes + t.dBytes <= ld.stageBytes, "staging buffer too small");
         hipk::tileQ40AoS(ld.rowPtr.data(), rows, (int)nc, m.lanes, st, reinterpret_cast<uint32_t *>(st + t.qsBytes));
-        m.qs = dalloc<uint8_t>(t.qsBytes);
-        m.d = dalloc<uint16_t>(t.dBytes / 2);
+        placeQ40(m, t, mi, l);
         stageCopy(ld, m.qs, st, t.qsBytes);
         stageCopy(ld, m.d, st + t.qsBytes, t.dBytes);
     } else {
@@ -332,7 +352,7 @@ void HipEngineImpl::loadFromFile() {
     sb = std::max(sb, matStageBytes(h_.dim, p.q0));
     sb = std::max(sb, matStageBytes(2 * p.hidden0, h_.dim));
     sb = std::max(sb, matStageBytes(h_.dim, p.hidden0));
-    sb = std::max(sb, matStageBytes(p.vocab0, h_.dim));
+    sb = std::max(sb, matStageBytes(p.vocab0, h_.dim, false));
     ld.stageBytes = sb;
     for (int i = 0; i < 2; i++) {
         DL_HIP(hipHostMalloc(reinterpret_cast<void **>(&ld.stage[i]), sb, hipHostMallocDefault));
@@ -355,17 +375,17 @@ void HipEngineImpl::loadFromFile() {
                              &w1 = f.find(TensorKind::W1, l), &w2 = f.find(TensorKind::W2, l),
                              &w3 = f.find(TensorKind::W3, l);
             buildMat(ld, L.qkv, {{&wq, p.qStart(), p.q0}, {&wk, p.kvStart(), p.kv0}, {&wv, p.kvStart(), p.kv0}},
-                     false, 0, h_.dim);
-            buildMat(ld, L.wo, {{&wo, 0, h_.dim}}, false, p.qStart(), p.q0);
+                     false, 0, h_.dim, 0, l);
+            buildMat(ld, L.wo, {{&wo, 0, h_.dim}}, false, p.qStart(), p.q0, 1, l);
             buildMat(ld, L.w13, {{&w1, p.hiddenStart(), p.hidden0}, {&w3, p.hiddenStart(), p.hidden0}}, true, 0,
-                     h_.dim);
-            buildMat(ld, L.w2, {{&w2, 0, h_.dim}}, false, p.hiddenStart(), p.hidden0);
+                     h_.dim, 2, l);
+            buildMat(ld, L.w2, {{&w2, 0, h_.dim}}, false, p.hiddenStart(), p.hidden0, 3, l);
             L.rmsAtt = uploadF32(ld, f.find(TensorKind::RMS_ATT, l));
             L.rmsFfn = uploadF32(ld, f.find(TensorKind::RMS_FFN, l));
         }
         emb_ = uploadF32(ld, f.find(TensorKind::EMBEDDING, -1));
         rmsFinal_ = uploadF32(ld, f.find(TensorKind::RMS_FINAL, -1));
-        buildMat(ld, wcls_, {{&f.find(TensorKind::WCLS, -1), p.vocabStart(), p.vocab0}}, false, 0, h_.dim);
+        buildMat(ld, wcls_, {{&f.find(TensorKind::WCLS, -1), p.vocabStart(), p.vocab0}}, false, 0, h_.dim, -1, 0);
         DL_HIP(hipStreamSynchronize(ld.copy));
     } catch (...) {
         cleanup();
@@ -375,16 +395,15 @@ void HipEngineImpl::loadFromFile() {
     load_.fileBytes = ld.reader->bytesRead();
 }
 
-void HipEngineImpl::synthMat(DevMat &m, int rows, int n, u64 seed) {
+void HipEngineImpl::synthMat(DevMat &m, int rows, int n, u64 seed, int mi, u32 l) {
     m.rows = rows;
     m.n = n;
     const float scale = 1.0f / std::sqrt(21.5f * (float)n);
     if (q40_) {
-        m.lanes = hipk::gemvLanesPerRow(n, rows, 1, true);
+        m.lanes = lanesFor(rows, n, mi >= 0);
         const hipk::Q40Tiling t = hipk::q40Tiling(rows, n, m.lanes);
         const size_t nBlocks = t.qsBytes / 16;  // == t.dBytes / 2 f16 scales
-        m.qs = dalloc<uint8_t>(t.qsBytes);
-        m.d = dalloc<uint16_t>(nBlocks);
+        placeQ40(m, t, mi, l);
         hipk::launchFillQ40(m.qs, m.d, nBlocks, scale, seed, stream_);
     } else {
         m.f = dalloc<float>((size_t)rows * n);
@@ -398,10 +417,10 @@ void HipEngineImpl::loadSynthetic() {
     u64 seed = cfg_.seed * 1000003ull + (u64)p.rank * 7919ull;
     for (u32 l = 0; l < h_.nLayers; l++) {
         DevLayer &L = layers_[l];
-        synthMat(L.qkv, p.q0 + 2 * p.kv0, h_.dim, seed++);
-        synthMat(L.wo, h_.dim, p.q0, seed++);
-        synthMat(L.w13, 2 * p.hidden0, h_.dim, seed++);
-        synthMat(L.w2, h_.dim, p.hidden0, seed++);
+        synthMat(L.qkv, p.q0 + 2 * p.kv0, h_.dim, seed++, 0, l);
+        synthMat(L.wo, h_.dim, p.q0, seed++, 1, l);
+        synthMat(L.w13, 2 * p.hidden0, h_.dim, seed++, 2, l);
+        synthMat(L.w2, h_.dim, p.hidden0, seed++, 3, l);
         L.rmsAtt = dalloc<float>(h_.dim);
         L.rmsFfn = dalloc<float>(h_.dim);
         hipk::launchFillF32Const(L.rmsAtt, h_.dim, 1.0f, stream_);
@@ -411,7 +430,7 @@ void HipEngineImpl::loadSynthetic() {
     hipk::launchFillF32Uniform(emb_, (size_t)h_.vocabSize * h_.dim, 1.0f, cfg_.seed ^ 0xE3B, stream_);
     rmsFinal_ = dalloc<float>(h_.dim);
     hipk::launchFillF32Const(rmsFinal_, h_.dim, 1.0f, stream_);
-    synthMat(wcls_, p.vocab0, h_.dim, seed++);
+    synthMat(wcls_, p.vocab0, h_.dim, seed++, -1, 0);
     DL_HIP(hipGetLastError());
 }
 
