@@ -176,6 +176,7 @@ double HipEngineImpl::decodeGreedyBatch(int steps, int nSeq, const int *tokens, 
     // the chained graph: forward -> argmax -> (tokens := ids, pos += 1)
     DL_HIP(hipEventRecord(e0, stream_));
     for (int s = 0; s < steps; s++) runGraph(nSeq, GraphKind::CHAIN);
+    accountForward(nSeq, GraphKind::CHAIN, steps);
     DL_HIP(hipEventRecord(e1, stream_));
     DL_HIP(hipEventSynchronize(e1));
     float ms = 0;
@@ -247,7 +248,37 @@ void HipEngineImpl::syncAndCheckComm() {
     }
 }
 
+// Tensor-parallel data-plane bytes of one forward of n rows on this rank, in the reference's
+// accounting (nn-network.cpp:493-508 counts socket payload): every residual update
+// sends this rank's partial [n][dim] to each peer and receives each peer's (Q80 blocks of 34 B per
+// 32 values with --sync-type q80, the reference's ZQ format, else f32), two per layer; greedy rows on
+// the fused exchange then trade one (value, index) winner per row, other rows gather the vocab
+// slices (to the root only for host logits / sampling). The transport's own framing (the 8-byte
+// {value, epoch} words of the fused exchange) is not payload and not counted.
+void HipEngineImpl::accountForward(int n, GraphKind kind, int times) {
+    stats_.sentBytes = stats_.recvBytes = 0;
+    const ShardPlan &p = plan_;
+    if (p.nRanks <= 1) return;
+    const u64 peers = p.nRanks - 1;
+    const u64 row = syncQ80_ ? (u64)h_.dim / 32 * 34 : (u64)h_.dim * 4;
+    u64 sent = 2ull * h_.nLayers * peers * (u64)n * row, recv = sent;
+    const u64 slice = (u64)n * p.vocab0 * 4;
+    if (tpFused_ && (kind == GraphKind::ARGMAX || kind == GraphKind::CHAIN)) {
+        sent += peers * (u64)n * 8;
+        recv += peers * (u64)n * 8;
+    } else if (kind == GraphKind::LOGITS || kind == GraphKind::SAMPLE) {
+        if (rank() == 0) recv += peers * slice;
+        else sent += slice;
+    } else {
+        sent += peers * slice;
+        recv += peers * slice;
+    }
+    stats_.sentBytes = sent * (u64)times;
+    stats_.recvBytes = recv * (u64)times;
+}
+
 void HipEngineImpl::runGraph(int n, GraphKind kind) {
+    accountForward(n, kind, 1);
     if (!cfg_.useGraphs || graphsBroken_) {
         enqueueForward(n, kind);
         return;

@@ -68,5 +68,7 @@ double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B
 namespace dl {
 // Test helper: `world` tensor-parallel ranks simulated on one GPU (host-staged collectives).
 // Returns rank 0's logits for single-token forwards of `tokens` at positions 0.., [n][vocab].
-std::vector<float> simulateTensorParallel(const EngineConfig &cfg, int world, const std::vector<int> &tokens);
+// attnBlocks (optional): per rank, whether its single decode rows run the fused attention block.
+std::vector<float> simulateTensorParallel(const EngineConfig &cfg, int world, const std::vector<int> &tokens,
+                                          std::vector<int> *attnBlocks = nullptr);
 }  // namespace dl

@@ -98,6 +98,7 @@ class HipEngineImpl : public HipEngine {
     void syncAndCheckComm();
     int rank() const { return comm_ ? comm_->rank() : 0; }
     void runGraph(int n, GraphKind kind);
+    void accountForward(int n, GraphKind kind, int times);
     hipGraphExec_t captureForward(int n, GraphKind kind);
     template <typename T>
     T *dalloc(size_t count) {

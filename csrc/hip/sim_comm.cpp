@@ -87,7 +87,8 @@ class SimComm : public DeviceComm {
 
 // Runs `steps` single-token forwards (token i at position i) on `world` simulated ranks and
 // returns rank 0's logits, [steps][vocab].
-std::vector<float> simulateTensorParallel(const EngineConfig &cfg0, int world, const std::vector<int> &tokens) {
+std::vector<float> simulateTensorParallel(const EngineConfig &cfg0, int world, const std::vector<int> &tokens,
+                                          std::vector<int> *attnBlocks) {
     SimShared sh(world);
     std::vector<std::unique_ptr<SimComm>> comms;
     std::vector<std::unique_ptr<HipEngine>> engines;
@@ -97,6 +98,8 @@ std::vector<float> simulateTensorParallel(const EngineConfig &cfg0, int world, c
         comms.emplace_back(new SimComm(&sh, r));
         engines.push_back(makeHipEngine(cfg, comms.back().get()));
     }
+    if (attnBlocks)
+        for (auto &e : engines) attnBlocks->push_back(e->attnBlock() ? 1 : 0);
     const u32 vocab = engines[0]->header().vocabSize;
     std::vector<float> out((size_t)tokens.size() * vocab);
     std::vector<std::thread> th;

@@ -598,20 +598,22 @@ PYBIND11_MODULE(_C, m) {
 
     m.def("simulate_tp",
           [](const std::string &model, const std::string &bufferType, int world, std::vector<int> tokens, bool kvBf16,
-             int gpuIndex) {
+             int gpuIndex, bool withFlags) -> py::object {
               EngineConfig c = makeConfig(model, bufferType, 1, 0, 8, 1, gpuIndex, false, kvBf16, py::none(), 1);
               std::vector<float> out;
+              std::vector<int> blocks;
               {
                   py::gil_scoped_release rel;
-                  out = simulateTensorParallel(c, world, tokens);
+                  out = simulateTensorParallel(c, world, tokens, &blocks);
               }
               const size_t vocab = out.size() / tokens.size();
               py::array_t<float> a({(py::ssize_t)tokens.size(), (py::ssize_t)vocab});
               std::memcpy(a.mutable_data(), out.data(), out.size() * 4);
+              if (withFlags) return py::make_tuple(a, blocks);
               return a;
           },
           py::arg("model"), py::arg("buffer_type"), py::arg("world"), py::arg("tokens"), py::arg("kv_bf16") = false,
-          py::arg("gpu_index") = 0);
+          py::arg("gpu_index") = 0, py::arg("attn_block_flags") = false);
 
     m.def("shard_bytes",
           [](const std::string &model, u32 world, u32 rank) {

@@ -312,6 +312,12 @@ void InferenceSession::recordMetrics(const char *kind, int n, double ms) {
         recv += w.totalRecvBytes();
     }
     const ForwardStats st = backend_->lastStats();
+    if (gpu_) {  // device data plane of this forward (the CPU data plane is the sockets above)
+        sent += st.sentBytes;
+        recv += st.recvBytes;
+        mSent_ += st.sentBytes;
+        mRecv_ += st.recvBytes;
+    }
     char buf[512];
     std::snprintf(buf, sizeof(buf),
                   "{\"ts_ms\":%.3f,\"event\":\"%s\",\"rows\":%d,\"ms\":%.4f,\"compute_ms\":%.4f,\"sync_ms\":%.4f,"
@@ -331,10 +337,12 @@ bool InferenceSession::profileForward(int n, const int *tokens, const int *posit
 }
 
 ForwardStats InferenceSession::lastStats() {
-    // bytes since the previous call (the reference resets its counters on read, nn-network.cpp:493-501);
-    // on GPUs the RCCL traffic is not visible here, only the control plane.
+    // bytes since the previous call (the reference resets its counters on read, nn-network.cpp:493-501):
+    // the backend's device data plane (GPU tensor parallelism over xGMI / RCCL: the engine's own count
+    // of the exchanged partials and logits) plus the control plane's sockets (and, on CPUs, the TCP
+    // data plane, whose sockets are these same ones: the CPU backend's own count is not added).
     ForwardStats s = backend_->lastStats();
-    s.sentBytes = s.recvBytes = 0;
+    if (!gpu_) s.sentBytes = s.recvBytes = 0;
     for (auto &w : workers_) {
         s.sentBytes += w.sentBytes();
         s.recvBytes += w.recvBytes();

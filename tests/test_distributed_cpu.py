@@ -47,6 +47,18 @@ def kv4(tmp_path_factory, assets):
     return {"q40": m, "tok": t}
 
 
+@pytest.fixture(scope="module", params=[2, 4, 8])
+def kv8(request, tmp_path_factory, assets):
+    """8 KV heads (the TP8 shard: one KV head per rank) with 2 / 4 / 8 query heads per KV head."""
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    kv_mul = request.param
+    d = str(tmp_path_factory.mktemp(f"kv8_{kv_mul}"))
+    m, t, _ = make_test_assets(d, "tiny", FloatType.Q40, seq_len=128, seed=7, dim=1024, n_heads=8 * kv_mul,
+                               n_kv_heads=8, hidden_dim=1024, vocab_size=512)
+    return {"q40": m, "tok": t, "kv_mul": kv_mul}
+
+
 def _inference(assets, workers=(), steps=16, extra=()):
     cmd = [DLLAMA, "inference", "--model", assets["q40"], "--tokenizer", assets["tok"], "--buffer-float-type", "q80",
            "--prompt", "hello world the", "--steps", str(steps), "--nthreads", "1", "--temperature", "0", *extra]
@@ -241,6 +253,40 @@ def test_chat_mode_multi_turn(assets):
     assert r.returncode == 0, out
     assert out.count("🤖 Assistant") == 1 and out.count("👱 User") == 1
     assert out.rstrip().endswith("(end of context)")
+
+
+@pytest.mark.parametrize("sync", ["f32", "q80"])
+def test_thread_group_tp8_matches_single(C, kv8, sync):
+    """TP8 (the only tensor-parallel degree of the 70B / 405B configurations: one KV head per rank)
+    with kvMul 2 / 4 / 8 query heads per KV head: f32 partial sums keep TP1's logits and greedy
+    tokens exactly, Q80 partials (the reference's wire format) stay within its rounding."""
+    import numpy as np
+    tokens = [5, 99, 300, 7, 100, 2]
+    ref, ref_g = C.cpu_simulate_tp(kv8["q40"], "q80", 1, tokens, "f32", 16)
+    got, got_g = C.cpu_simulate_tp(kv8["q40"], "q80", 8, tokens, sync, 16)
+    rel = np.abs(got - ref).max() / np.abs(ref).max()
+    assert rel < (1e-6 if sync == "f32" else 3e-2), rel
+    if sync == "f32":
+        assert got_g == ref_g
+
+
+def test_tensor_parallel_8_ranks_over_tcp(kv8):
+    """Root + 7 TCP workers (world 8, one KV head per rank), exact f32 exchange: the same tokens as
+    one rank."""
+    if kv8["kv_mul"] != 4:
+        pytest.skip("one kvMul suffices for the 8-process run")
+    rc, ref = _inference(kv8)
+    assert rc == 0, ref
+    procs, addrs = _workers(7)
+    try:
+        rc, out = _inference(kv8, addrs, extra=("--sync-type", "f32"))
+        assert rc == 0, out
+        assert _preds(out) == _preds(ref)
+    finally:
+        for p in procs:
+            p.kill()
+        for p in procs:
+            p.communicate()
 
 
 @pytest.mark.parametrize("world,sync", [(1, "f32"), (2, "f32"), (4, "f32"), (2, "q80"), (4, "q80")])

@@ -276,6 +276,46 @@ def test_simulated_tensor_parallel_matches_single(C, kv4_gpu, world):
     assert (got.argmax(-1) == ref.argmax(-1)).all()
 
 
+@pytest.fixture(scope="module")
+def kv8_gpu(tmp_path_factory):
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    d = str(tmp_path_factory.mktemp("kv8g"))
+    # 32 query heads of 64 over 8 KV heads (kvMul 4): TP8 leaves one KV head and 4 query heads per rank
+    m, t, _ = make_test_assets(d, "tiny", FloatType.Q40, seq_len=128, seed=9, dim=2048, n_heads=32, n_kv_heads=8,
+                               hidden_dim=2048, vocab_size=1024)
+    return m
+
+
+def test_simulated_tp8_matches_single(C, kv8_gpu):
+    """TP8 (one KV head per rank, q0 = 256, kv0 = 64) simulated on one GPU: same logits as TP1, and
+    every rank's single decode rows run the fused attention block."""
+    tokens = [5, 99, 300, 7, 1000, 2]
+    single = C.HipEngine(kv8_gpu, "q80", kv_bf16=False)
+    ref = np.stack([single.forward([t], [p], [0])[0] for p, t in enumerate(tokens)])
+    got, blocks = C.simulate_tp(kv8_gpu, "q80", 8, tokens, attn_block_flags=True)
+    assert _rel(got, ref) < 3e-2
+    assert (got.argmax(-1) == ref.argmax(-1)).all()
+    assert all(blocks), blocks
+
+
+def test_simulated_tp8_70b_attention_shapes(C, tmp_path):
+    """Llama-3.3-70B attention shapes at TP8 (dim 8192, 64 query / 8 KV heads of 128: per rank
+    q0 = 1024, kv0 = 128, kvMul 8), one layer with a narrow FFN: simulated TP8 vs TP1 logits, the
+    fused attention block on every rank."""
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=64, seed=21, dim=8192, n_heads=64,
+                               n_kv_heads=8, hidden_dim=2048, n_layers=1, vocab_size=1024)
+    tokens = [5, 99, 300, 7]
+    single = C.HipEngine(m, "q80", kv_bf16=False)
+    ref = np.stack([single.forward([t], [p], [0])[0] for p, t in enumerate(tokens)])
+    del single
+    got, blocks = C.simulate_tp(m, "q80", 8, tokens, attn_block_flags=True)
+    assert _rel(got, ref) < 3e-2
+    assert all(blocks), blocks
+
+
 @pytest.mark.gpu
 def test_kv_cache_larger_than_hbm_is_refused(C):
     """64 slots x 131072 positions of bf16 KV for the 8B is ~1.1 TB: refused before allocating,

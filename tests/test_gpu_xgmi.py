@@ -346,6 +346,57 @@ def test_cli_root_workers_over_xgmi(tmp_path, n_workers):
             p.wait()
 
 
+def _data_plane_bytes(dim, n_layers, world, q80, rows=1):
+    """Reference accounting of one forward's tensor-parallel payload per rank: two
+    residual partials per layer to every peer (Q80: 34 B per 32 values), plus the greedy winner
+    (value, index) per row on the fused exchange."""
+    row = dim // 32 * 34 if q80 else dim * 4
+    return 2 * n_layers * (world - 1) * rows * row + (world - 1) * rows * 8
+
+
+def test_data_plane_bytes_reported(tmp_path):
+    """`dllama inference` at TP2 over xGMI (same GPU) with the reference's Q80 sync: the Sent / Recv
+    of every decode forward in --metrics is the device data plane (formula above: 2 x layers x
+    dim/32 x 34 B + the argmax winner) plus a few bytes of TCP control packets; the formula gives
+    SURVEY §2.6's 272 KiB per token for Llama-3.1-8B at TP2."""
+    import json
+    import subprocess
+    import time
+    from conftest import REPO
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    assert _data_plane_bytes(4096, 32, 2, True) - 8 == 272 * 1024
+    dllama = os.path.join(REPO, "build", "dllama")
+    m, t, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=7, dim=512, n_heads=8,
+                               n_kv_heads=4, hidden_dim=1024)
+    metrics = str(tmp_path / "m.jsonl")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", DL_TP_COMM="xgmi", **_same_gpu_env(2))
+    port = _port()
+    w = subprocess.Popen([dllama, "worker", "--port", str(port), "--gpu-index", "0"], stdout=subprocess.PIPE,
+                         stderr=subprocess.STDOUT, env=env)
+    try:
+        time.sleep(0.5)
+        r = subprocess.run([dllama, "inference", "--model", m, "--tokenizer", t, "--buffer-float-type", "q80",
+                            "--prompt", "hello world the", "--steps", "16", "--temperature", "0", "--gpu-index", "0",
+                            "--sync-type", "q80", "--metrics", metrics, "--workers", f"127.0.0.1:{port}"],
+                           capture_output=True, timeout=180, env=env)
+        out = r.stdout.decode(errors="replace")
+        assert r.returncode == 0, out
+    finally:
+        w.kill()
+        w.wait()
+    rows = [json.loads(l) for l in open(metrics) if l.strip()]
+    dec = [x for x in rows if x.get("rows") == 1]
+    assert dec, rows
+    expect = _data_plane_bytes(512, 2, 2, True)
+    for x in dec:
+        assert expect <= x["sent_bytes"] <= expect + 256, (x, expect)
+        assert expect <= x["recv_bytes"] <= expect + 256, (x, expect)
+    # the Pred lines print the same (kB)
+    kb = [int(l.split("Sent")[1].split("kB")[0]) for l in out.splitlines() if l.startswith("🔶 Pred")]
+    assert kb and all(k == expect // 1024 for k in kb), (kb, expect)
+
+
 def test_stalled_worker_gives_clean_root_error(tmp_path):
     """Fault injection: a GPU worker frozen mid-decode (SIGSTOP, sockets stay open)
     must make the root fail cleanly - its xGMI collectives stop waiting after 2 s, raise the error
