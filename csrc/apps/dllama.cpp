@@ -44,7 +44,7 @@ static int sampleOne(InferenceSession &sess, int token, int pos, std::vector<flo
 
 static void evalPrompt(InferenceSession &sess, const std::vector<int> &tokens, int startIndex, int &pos, int endPos,
                        bool print, double *totalMs) {
-    const int nb = sess.maxBatch();
+    const int nb = sess.prefillChunk();
     std::vector<int> positions, slots;
     int i = startIndex;
     while (pos < endPos) {
@@ -107,7 +107,7 @@ static void inference(InferenceSession &sess, const AppArgs &args) {
     const int nPred = pos - nEval;
     std::printf("\n");
     std::printf("Evaluation\n");
-    std::printf("   nBatches: %d\n", sess.maxBatch());
+    std::printf("   nBatches: %d\n", sess.prefillChunk());
     std::printf("    nTokens: %d\n", nEval);
     std::printf("   tokens/s: %3.2f (%3.2f ms/tok)\n", nEval > 0 ? nEval * 1000.0 / evalMs : 0.0,
                 nEval > 0 ? evalMs / nEval : 0.0);
@@ -188,7 +188,7 @@ static void usage() {
                  "  --gpu-index <i>                     (MI355X device ordinal; -1 = CPU backend)\n"
                  "  --temperature <t> --topp <p> --seed <s>\n"
                  "  --chat-template {llama2|llama3|deepSeek3}\n"
-                 "  --max-seq-len <n> --max-batch <n> --slots <n>\n"
+                 "  --max-seq-len <n> --max-batch <n> --prefill-chunk <n> --slots <n>\n"
                  "  --kv-dtype {bf16|f32} --graph {0|1} --log-level {0|1|2}\n"
                  "  --kv-pages <n> --kv-page-size <p>   (GPU paged KV cache: pool of n pages of p positions)\n"
                  "  --metrics <file|->                  (JSON line per forward)  --profile 1  (GPU kernel table)\n"

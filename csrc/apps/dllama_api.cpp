@@ -255,7 +255,7 @@ void usage() {
     std::fprintf(stderr,
                  "Usage: dllama-api {--model <path>} {--tokenizer <path>} [--port <p>]\n"
                  "        [--buffer-float-type {f32|f16|q40|q80}]\n"
-                 "        [--max-seq-len <max>] [--slots <n>] [--max-batch <n>]\n"
+                 "        [--max-seq-len <max>] [--slots <n>] [--max-batch <n>] [--prefill-chunk <n>]\n"
                  "        [--kv-pages <n> --kv-page-size <p>]   (GPU paged KV: slots share a page pool)\n"
                  "        [--nthreads <n>] [--gpu-index <i>]\n"
                  "        [--workers <ip:port> ...]\n"

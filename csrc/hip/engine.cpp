@@ -78,6 +78,7 @@ HipEngineImpl::~HipEngineImpl() {
     for (auto &kv : graphs_) (void)hipGraphExecDestroy(kv.second);
     for (void *p : allocs_) (void)hipFree(p);
     for (void *p : hostAllocs_) (void)hipHostFree(p);
+    if (hLogits_) (void)hipHostFree(hLogits_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -108,6 +109,11 @@ void HipEngineImpl::forward(int n, const int *tokens, const int *positions, cons
     setInputs(n, tokens, positions, slots);
     runGraph(n, GraphKind::LOGITS);
     const bool root = rank() == 0;
+    if (root && logits && (size_t)n * h_.vocabSize > hLogitsCap_) {  // pinned staging, grown on demand
+        if (hLogits_) DL_HIP(hipHostFree(hLogits_));
+        hLogitsCap_ = (size_t)n * h_.vocabSize;
+        DL_HIP(hipHostMalloc(reinterpret_cast<void **>(&hLogits_), hLogitsCap_ * sizeof(float), hipHostMallocDefault));
+    }
     if (root && logits) {
         const float *src = plan_.nRanks > 1 ? dLogitsFull_ : dLogits_;
         DL_HIP(hipMemcpyAsync(hLogits_, src, (size_t)n * h_.vocabSize * sizeof(float), hipMemcpyDeviceToHost, stream_));

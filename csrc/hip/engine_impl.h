@@ -232,7 +232,8 @@ class HipEngineImpl : public HipEngine {
     int *dTok_ = nullptr, *dPos_ = nullptr, *dSlot_ = nullptr, *dIds_ = nullptr, *dHist_ = nullptr;
     float4 *dSpec_ = nullptr;
     int *hIn_ = nullptr, *hIds_ = nullptr, *hErr_ = nullptr;
-    float *hLogits_ = nullptr;
+    float *hLogits_ = nullptr;  // pinned logits staging (forward with host logits), grown on demand
+    size_t hLogitsCap_ = 0;
     bool inputsInFlight_ = false;  // an H2D copy from hIn_ may still be pending
     int pendingN_ = 0;             // rows of a launchIds forward not collected yet
 

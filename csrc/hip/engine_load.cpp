@@ -110,7 +110,6 @@ void HipEngineImpl::allocBuffers() {
     hIds_ = halloc<int>(MB);
     hErr_ = halloc<int>(2);
     hErr_[0] = hErr_[1] = 0;
-    hLogits_ = halloc<float>((size_t)MB * h_.vocabSize);
     dX_[0] = dalloc<float>((size_t)MB * h_.dim);
     dX_[1] = dalloc<float>((size_t)MB * h_.dim);
     dY_ = dalloc<float>((size_t)MB * h_.dim);

@@ -27,7 +27,10 @@ struct AppArgs {
     std::vector<int> workerPorts;
     int port = 9990;
     int nThreads = 1;
-    int nBatches = 32;  // max rows per forward (reference constant, now --max-batch)
+    int nBatches = 32;  // max decode rows per forward (reference constant, now --max-batch)
+    // --prefill-chunk: prompt rows per forward (0 = 1024 on GPUs, where one wide-GEMM launch covers
+    // every 128-token tile of a chunk, and --max-batch on the CPU backend)
+    int prefillChunk = 0;
     int steps = 0;
     float temperature = 0.8f;
     float topp = 0.9f;
@@ -64,7 +67,8 @@ class InferenceSession {
     Tokenizer &tokenizer() { return *tokenizer_; }
     Sampler &sampler() { return *sampler_; }
     int nSlots() const { return nSlots_; }
-    int maxBatch() const { return maxBatch_; }
+    int maxBatch() const { return maxBatch_; }          // decode rows per forward
+    int prefillChunk() const { return prefillChunk_; }  // prompt rows per forward (engine rows >= both)
     // paged KV cache of the (root) backend: free pages and positions per page (-1 / 0: contiguous)
     int kvPagesFree() const { return backend_->kvPagesFree(); }
     // a sequence ended: its KV slot's pages return to the pool on every rank (no-op when contiguous)
@@ -92,7 +96,7 @@ class InferenceSession {
     void recordMetrics(const char *kind, int n, double ms);
 
     AppArgs args_;
-    int nSlots_, maxBatch_;
+    int nSlots_, maxBatch_, prefillChunk_ = 32;
     bool gpu_ = false;
     std::vector<Socket> workers_;
     std::unique_ptr<HostComm> hostComm_;

@@ -286,13 +286,14 @@ bool Scheduler::step() {
     // 2) build the next batch: decode rows first (latency), then prefill chunks with the remaining
     //    budget. A decode row is launched before the host has decoded the previous token: a request
     //    whose last token turns out to end it (EOS / stop string) wastes one row, dropped at collection.
-    const int maxRows = sess_.maxBatch();
+    // decode rows first (<= --max-batch), then prompt rows up to the prefill chunk
+    const int maxRows = std::max(sess_.maxBatch(), sess_.prefillChunk());
     std::vector<int> tokens, positions, slots;
     Flight next;
     for (auto &rp : active_) {
         GenRequest *r = rp.get();
         if (r->prefilled < r->prompt.size()) continue;
-        if ((int)tokens.size() >= maxRows) break;
+        if ((int)tokens.size() >= sess_.maxBatch()) break;
         const int pos = (int)(r->prompt.size() + r->generated.size()) - 1;
         if ((r->params.maxTokens > 0 && (int)r->generated.size() >= r->params.maxTokens) || (u32)(pos + 1) >= seqLen)
             continue;  // ends at this step's text work (length)
