@@ -19,13 +19,17 @@
 #include "decode_dev.h"
 #include "device_comm.h"
 
+#include <cstdlib>
+
 namespace dl {
 namespace hipk {
 
 constexpr int kPdeRingThreads = 512;
 constexpr int kPdeAuxThreads = 256;
 constexpr int kPdeThreads = kPdeRingThreads + kPdeAuxThreads;
-constexpr int kPdeD = 12;  // ring depth (steps) per lane: 3 loads each, 36 in flight per wave
+// Ring depth D (steps per lane, 3 loads each): the kernel is instantiated for several; deeper rings
+// prefetch more of the next phase across a hand-off but queue the aux waves' loads behind more
+// weight traffic on the same CU (pdeRingDepth picks; decode_engine trace in profiles/).
 
 // LDS image of one workgroup.
 struct PdeLds {
@@ -46,8 +50,8 @@ __host__ __device__ static inline PdeLds pdeLayout(int dim, int nMax, int nPhase
     off += (size_t)(kMaxHeadSize / 2) * 8;
     l.attn = off;  // attention: q, per-wave (m, l, o), output
     off += (size_t)(kMaxHeadSize + 4 * (2 + kMaxHeadSize) + kMaxHeadSize) * 4 + 64;
-    l.misc = off;  // reductions + aux barrier counter
-    off += 64;
+    l.misc = off;  // reductions + aux barrier counter + ring-wave trace stamps (PdeArgs::trace)
+    off += 192;
     l.seg = off;  // [2 VWGs][4 * nLayers] stream segments
     off += (size_t)2 * nPhases * 32;
     l.total = alignUp(off, 16);
@@ -138,10 +142,28 @@ __device__ __forceinline__ void auxCopyWT(const AuxCtx &c, const void *src, void
     }
 }
 
+// The RMS norm's weights for auxResNorm, issued early (before the hand-off wait): <= 4 chunks of
+// 8 floats per aux thread, asm loads waited inside auxResNorm.
+struct NormW {
+    f32x4 w[4][2];
+};
+__device__ __forceinline__ NormW auxNormIssue(const AuxCtx &c, const PdeArgs &a, const float *w) {
+    NormW r;
+    const int nChunks = a.dim >> 3;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int ch = min(c.at + k * kPdeAuxThreads, nChunks - 1);
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r.w[k][0]) : "v"(w + ch * 8));
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r.w[k][1]) : "v"(w + ch * 8 + 4));
+    }
+    return r;
+}
+
 // x (LDS) += delta (write-through global, or the embedding output when init), then RMS norm with
-// w -> the Q80 activation image. dim is a multiple of 8 * 4 (whole Q80 blocks per quad), <= 8192.
+// the pre-issued weights -> the Q80 activation image. dim is a multiple of 32 (whole Q80 blocks
+// per quad of 8-float chunks), <= 8192.
 __device__ __forceinline__ void auxResNorm(AuxCtx &c, const PdeArgs &a, float *xs, const float *delta, bool init,
-                                           const float *w, int8_t *sq, float2 *ssc) {
+                                           NormW &nw, int8_t *sq, float2 *ssc) {
     const int nChunks = a.dim >> 3;  // 8 floats per chunk, <= 4 chunks per thread
     f32x4 d[4][2];
 #pragma unroll
@@ -158,6 +180,8 @@ __device__ __forceinline__ void auxResNorm(AuxCtx &c, const PdeArgs &a, float *x
     }
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(d[0][0]), "+v"(d[0][1]), "+v"(d[1][0]), "+v"(d[1][1]), "+v"(d[2][0]),
                  "+v"(d[2][1]), "+v"(d[3][0]), "+v"(d[3][1])::"memory");
+    asm volatile("" : "+v"(nw.w[0][0]), "+v"(nw.w[0][1]), "+v"(nw.w[1][0]), "+v"(nw.w[1][1]), "+v"(nw.w[2][0]),
+                 "+v"(nw.w[2][1]), "+v"(nw.w[3][0]), "+v"(nw.w[3][1]));  // (landed with the wait above)
     float ss = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -170,19 +194,23 @@ __device__ __forceinline__ void auxResNorm(AuxCtx &c, const PdeArgs &a, float *x
             }
             *reinterpret_cast<f32x4 *>(xs + ch * 8) = v0;
             *reinterpret_cast<f32x4 *>(xs + ch * 8 + 4) = v1;
+            d[k][0] = v0;
+            d[k][1] = v1;
             ss += v0.x * v0.x + v0.y * v0.y + v0.z * v0.z + v0.w * v0.w + v1.x * v1.x + v1.y * v1.y + v1.z * v1.z +
                   v1.w * v1.w;
         }
     }
     ss = auxSum(c, ss);
     const float inv = 1.0f / sqrtf(ss / (float)a.dim + a.eps);
-    for (int ch = c.at; ch < nChunks; ch += kPdeAuxThreads) {
-        const float4 w0 = ld4(w + ch * 8), w1 = ld4(w + ch * 8 + 4);
-        const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-        float v[8];
 #pragma unroll
-        for (int i = 0; i < 8; i++) v[i] = wv[i] * (inv * xs[ch * 8 + i]);
-        stageChunk<true>(v, 0, ch, a.dim, sq, ssc, nullptr);
+    for (int k = 0; k < 4; k++) {
+        const int ch = c.at + k * kPdeAuxThreads;
+        if (ch < nChunks) {
+            const f32x4 w0 = nw.w[k][0], w1 = nw.w[k][1], x0 = d[k][0], x1 = d[k][1];
+            float v[8] = {w0.x * (inv * x0.x), w0.y * (inv * x0.y), w0.z * (inv * x0.z), w0.w * (inv * x0.w),
+                          w1.x * (inv * x1.x), w1.y * (inv * x1.y), w1.z * (inv * x1.z), w1.w * (inv * x1.w)};
+            stageChunk<true>(v, 0, ch, a.dim, sq, ssc, nullptr);
+        }
     }
 }
 
@@ -209,16 +237,61 @@ __device__ __forceinline__ void q80StoreWT(float v, int8_t *qDst, float2 *sDst, 
     if ((idx & 31) == 0) stF2<true>(reinterpret_cast<float *>(sDst + (idx >> 5)), roundF16(d), qs);
 }
 
+// RW 32-bit words (RW = 2, 4 or 8) of one cache row per lane, asm load (waited by the caller).
+template <int RW>
+__device__ __forceinline__ void ldRow(const uint32_t *p, uint32_t (&r)[RW]) {
+    if constexpr (RW == 2) {
+        u32x2 v;
+        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(p));
+        r[0] = v.x, r[1] = v.y;
+    } else if constexpr (RW == 4) {
+        u32x4 v;
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p));
+        r[0] = v.x, r[1] = v.y, r[2] = v.z, r[3] = v.w;
+    } else {
+        u32x4 v0, v1;
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v0) : "v"(p));
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v1) : "v"(p + 4));
+        r[0] = v0.x, r[1] = v0.y, r[2] = v0.z, r[3] = v0.w, r[4] = v1.x, r[5] = v1.y, r[6] = v1.z, r[7] = v1.w;
+    }
+}
+
 // One decode attention head over keys [0, pos]: the current key / value rows come from the qkv
 // hand-off (write-through), earlier ones from the cache. 16 groups of 16 lanes, HS/16 dims per
-// lane, TU keys per group in flight; online softmax; output -> Q80 hand-off.
+// lane, TU keys per group per round; the first round of cached keys is loaded BEFORE waiting for
+// this head's qkv producers (those keys do not depend on them), so a context of <= 16 TU keys
+// costs one memory round trip after the hand-off. Online softmax; output -> Q80 hand-off.
 template <int HS, bool BF16>
-__device__ __forceinline__ void auxAttention(AuxCtx &c, const PdeArgs &a, int head, int l, int pos, int sl,
-                                             float *sm) {
+__device__ __forceinline__ void auxAttention(AuxCtx &c, const PdeArgs &a, int head, int l, int pos, int sl, float *sm,
+                                             const unsigned *groupCnt, unsigned target) {
     constexpr int DPL = HS / 16, RW = BF16 ? DPL / 2 : DPL, TU = 4;
     const int g16 = c.at >> 4, l16 = c.at & 15, kvh = head / a.kvMul;
     const void *kc = a.kcache[l], *vc = a.vcache[l];
     const float scale = 1.0f / sqrtf((float)HS);
+    uint32_t kr[TU][RW], vr[TU][RW];
+    auto loadRound = [&](int tb) {
+#pragma unroll
+        for (int u = 0; u < TU; u++) {
+            const int t = max(min(tb + u * 16, pos - 1), 0);
+            const size_t off = kvRow(a.kvMap, a.seqLen, sl, t) * a.kv0 + kvh * HS + l16 * DPL;
+            const uint32_t *kp = reinterpret_cast<const uint32_t *>(
+                BF16 ? (const void *)(reinterpret_cast<const uint16_t *>(kc) + off)
+                     : (const void *)(reinterpret_cast<const float *>(kc) + off));
+            const uint32_t *vp = reinterpret_cast<const uint32_t *>(
+                BF16 ? (const void *)(reinterpret_cast<const uint16_t *>(vc) + off)
+                     : (const void *)(reinterpret_cast<const float *>(vc) + off));
+            ldRow<RW>(kp, kr[u]);
+            ldRow<RW>(vp, vr[u]);
+        }
+    };
+    auto waitRound = [&] {
+#pragma unroll
+        for (int u = 0; u < TU; u++)
+#pragma unroll
+            for (int w = 0; w < RW; w++) asm volatile("s_waitcnt vmcnt(0)" : "+v"(kr[u][w]), "+v"(vr[u][w])::"memory");
+    };
+    loadRound(g16);  // (clamped addresses: always valid, position 0 exists)
+    auxWait(a, groupCnt, 1, target, 22, c.lane);
     float qr[DPL], kcur[DPL], vcur[DPL];
     {
         const float *qp = a.eQkv + head * HS + l16 * DPL;
@@ -259,23 +332,8 @@ __device__ __forceinline__ void auxAttention(AuxCtx &c, const PdeArgs &a, int he
         m = mn;
     };
     for (int tb = g16; tb < pos; tb += TU * 16) {
-        uint32_t kr[TU][RW], vr[TU][RW];
-#pragma unroll
-        for (int u = 0; u < TU; u++) {
-            const int t = min(tb + u * 16, pos - 1);
-            const size_t off = kvRow(a.kvMap, a.seqLen, sl, t) * a.kv0 + kvh * HS + l16 * DPL;
-            const uint32_t *kp = reinterpret_cast<const uint32_t *>(
-                BF16 ? (const void *)(reinterpret_cast<const uint16_t *>(kc) + off)
-                     : (const void *)(reinterpret_cast<const float *>(kc) + off));
-            const uint32_t *vp = reinterpret_cast<const uint32_t *>(
-                BF16 ? (const void *)(reinterpret_cast<const uint16_t *>(vc) + off)
-                     : (const void *)(reinterpret_cast<const float *>(vc) + off));
-#pragma unroll
-            for (int w = 0; w < RW; w++) {
-                kr[u][w] = kp[w];
-                vr[u][w] = vp[w];
-            }
-        }
+        if (tb != g16) loadRound(tb);
+        waitRound();
 #pragma unroll
         for (int u = 0; u < TU; u++) {
             if (tb + u * 16 >= pos) break;
@@ -295,6 +353,7 @@ __device__ __forceinline__ void auxAttention(AuxCtx &c, const PdeArgs &a, int he
             accum(kv, vv);
         }
     }
+    waitRound();  // (a context without cached keys still drains the prefetch)
     if (g16 == (pos & 15)) accum(kcur, vcur);  // key `pos` in the group that owns it
     // merge the 4 groups of each wave, then the 4 waves through LDS
 #pragma unroll
@@ -349,7 +408,7 @@ __device__ __forceinline__ T sel4(int m, T x0, T x1, T x2, T x3) {
     return m == 0 ? x0 : (m == 1 ? x1 : (m == 2 ? x2 : x3));
 }
 
-template <int HS, bool BF16>
+template <int HS, bool BF16, int kPdeD>
 __global__ __launch_bounds__(kPdeThreads) void pdeKernel(PdeArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nMax = max(max(a.dim, a.hidden), a.q0);
@@ -401,6 +460,7 @@ __global__ __launch_bounds__(kPdeThreads) void pdeKernel(PdeArgs a) {
         const int u = tid >> 8;  // VWG within the workgroup
         const int t256 = tid & 255, w = t256 >> 6, lane = t256 & 63;
         const PdeSeg *segs = reinterpret_cast<const PdeSeg *>(smem + lay.seg) + u * nPhases;
+        unsigned long long *rtr = reinterpret_cast<unsigned long long *>(misc + 16);  // [8] LDS stamps
         auto segSteps = [&](int ph) { return __builtin_amdgcn_readfirstlane(segs[ph].steps); };
         auto nextSeg = [&](int ph) {  // first non-empty segment after ph (nPhases: none)
             do {
@@ -469,6 +529,8 @@ __global__ __launch_bounds__(kPdeThreads) void pdeKernel(PdeArgs a) {
                 }
                 barrier();  // activations of `sc` staged
                 entered = sc;
+                if (a.trace && (sc >> 2) == a.traceLayer && t256 == 0 && u == 0)
+                    rtr[2 * (sc & 3)] = wall_clock64();
                 rc = segSteps(sc);
                 cK = __builtin_amdgcn_readfirstlane(segs[sc].K);
                 cN = __builtin_amdgcn_readfirstlane(segs[sc].n);
@@ -491,7 +553,10 @@ __global__ __launch_bounds__(kPdeThreads) void pdeKernel(PdeArgs a) {
                 kc = 0;
                 ++pc;
             }
-            if (--rc == 0) sc = nextSeg(sc);
+            if (--rc == 0) {
+                if (a.trace && (sc >> 2) == a.traceLayer && t256 == 0 && u == 0) rtr[2 * (sc & 3) + 1] = wall_clock64();
+                sc = nextSeg(sc);
+            }
         };
         for (int t0 = 0; t0 < Ttot; t0 += kPdeD) {
 #pragma unroll
@@ -534,14 +599,23 @@ __global__ __launch_bounds__(kPdeThreads) void pdeKernel(PdeArgs a) {
     unsigned *cntAtt = a.cnt + kPdeMaxKv * kCntStride;
     unsigned *cntWo = cntAtt + 8 * kCntStride, *cntH = cntWo + 8 * kCntStride, *cntW2 = cntH + 8 * kCntStride;
     const int h2 = HS / 2;
+    unsigned long long *tr = a.trace ? a.trace + (size_t)blockIdx.x * 32 : nullptr;
     for (int l = 0; l < a.nLayers; l++) {
         const unsigned st = stepOf(l);
+        const bool trL = tr && l == a.traceLayer && c.at == 0;
+#define PDE_TR(k) \
+    if (trL) tr[k] = wall_clock64();
+        PDE_TR(0)
         // ---- qkv: x (+= w2 output of layer l - 1) -> norm -> Q80; RoPE row
+        NormW nw = auxNormIssue(c, a, a.rmsAtt[l]);
         if (l > 0) auxWait(a, cntW2, 8, (st - 1u) * (unsigned)G, 21, c.lane);
-        auxResNorm(c, a, xs, a.eW2, l == 0, a.rmsAtt[l], sq, ssc);
+        PDE_TR(1)
+        auxResNorm(c, a, xs, a.eW2, l == 0, nw, sq, ssc);
         if (c.at < h2) sRope[c.at] = a.rope[(size_t)pos * h2 + c.at];
+        PDE_TR(2)
         barrier();  // activations staged
         barrier();  // qkv rows in LDS
+        PDE_TR(3)
         {
             // RoPE on q / k pairs, publish q | k | v write-through, append k / v to the cache
             unsigned long long gm = 0ull;
@@ -578,27 +652,37 @@ __global__ __launch_bounds__(kPdeThreads) void pdeKernel(PdeArgs a) {
                     __hip_atomic_fetch_add(a.cnt + g * kCntStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
         }
+        PDE_TR(4)
         // ---- attention: workgroup h < nHeads0 owns query head h
         if ((int)blockIdx.x < a.nHeads0) {
             const int head = blockIdx.x, g = head / a.kvMul;
-            auxWait(a, a.cnt + g * kCntStride, 1, st * a.groupExpect[g], 22, c.lane);
-            auxAttention<HS, BF16>(c, a, head, l, pos, sl, sAttn);
+            PDE_TR(5)
+            auxAttention<HS, BF16>(c, a, head, l, pos, sl, sAttn, a.cnt + g * kCntStride, st * a.groupExpect[g]);
             auxSignal(c, cntAtt, true);
+            PDE_TR(6)
         }
         auxWait(a, cntAtt, 8, st * (unsigned)a.nHeads0, 23, c.lane);
+        PDE_TR(7)
         auxStageQ80(c, a.eAttQ, a.eAttS, a.q0, sq, ssc);
+        PDE_TR(8)
         barrier();  // wo activations staged
         barrier();  // wo rows in LDS
+        PDE_TR(9)
 #pragma unroll
         for (int u = 0; u < 2; u++)
             for (int i = c.at; i < re[1][u] - rb[1][u]; i += kPdeAuxThreads)
                 st32<true>(a.eWo + rb[1][u] + i, __float_as_uint(res[u * kPdeMaxRes + i]));
         auxSignal(c, cntWo, true);
+        PDE_TR(10)
         // ---- w13: x += wo output -> norm -> Q80
+        nw = auxNormIssue(c, a, a.rmsFfn[l]);
         auxWait(a, cntWo, 8, st * (unsigned)G, 24, c.lane);
-        auxResNorm(c, a, xs, a.eWo, false, a.rmsFfn[l], sq, ssc);
+        PDE_TR(11)
+        auxResNorm(c, a, xs, a.eWo, false, nw, sq, ssc);
+        PDE_TR(12)
         barrier();  // w13 activations staged
         barrier();  // w13 rows in LDS
+        PDE_TR(13)
         // SwiGLU of the row pairs (w1, w3 interleaved), Q80 blocks of 32 hidden units
 #pragma unroll
         for (int u = 0; u < 2; u++) {
@@ -615,16 +699,24 @@ __global__ __launch_bounds__(kPdeThreads) void pdeKernel(PdeArgs a) {
             }
         }
         auxSignal(c, cntH, true);
+        PDE_TR(14)
         auxWait(a, cntH, 8, st * (unsigned)G, 25, c.lane);
+        PDE_TR(15)
         auxStageQ80(c, a.eHQ, a.eHS, a.hidden, sq, ssc);
+        PDE_TR(16)
         barrier();  // w2 activations staged
         barrier();  // w2 rows in LDS
+        PDE_TR(17)
 #pragma unroll
         for (int u = 0; u < 2; u++)
             for (int i = c.at; i < re[3][u] - rb[3][u]; i += kPdeAuxThreads)
                 st32<true>(a.eW2 + rb[3][u] + i, __float_as_uint(res[u * kPdeMaxRes + i]));
         auxSignal(c, cntW2, true);
+        PDE_TR(18)
+#undef PDE_TR
     }
+    if (tr && c.at < 8) tr[20 + c.at] = reinterpret_cast<const unsigned long long *>(misc + 16)[c.at];  // ring stamps
+    if (tr && c.at == 0) tr[31] = (unsigned long long)xccId();
     // final residual for the logits GEMV (workgroup 0)
     if (blockIdx.x == 0) {
         auxWait(a, cntW2, 8, stepOf(a.nLayers - 1) * (unsigned)G, 26, c.lane);
@@ -638,10 +730,29 @@ __global__ __launch_bounds__(kPdeThreads) void pdeKernel(PdeArgs a) {
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
-static const void *pdeFn(int hs, bool bf16) {
-    if (hs == 128) return bf16 ? (const void *)pdeKernel<128, true> : (const void *)pdeKernel<128, false>;
-    if (hs == 64) return bf16 ? (const void *)pdeKernel<64, true> : (const void *)pdeKernel<64, false>;
+int pdeRingDepth() {
+    static const int v = [] {
+        const char *e = std::getenv("DL_PDE_RING");
+        const int d = e && *e ? std::atoi(e) : 8;
+        return d == 4 || d == 6 || d == 8 || d == 12 ? d : 8;
+    }();
+    return v;
+}
+
+template <int D>
+static const void *pdeFnD(int hs, bool bf16) {
+    if (hs == 128) return bf16 ? (const void *)pdeKernel<128, true, D> : (const void *)pdeKernel<128, false, D>;
+    if (hs == 64) return bf16 ? (const void *)pdeKernel<64, true, D> : (const void *)pdeKernel<64, false, D>;
     return nullptr;
+}
+
+static const void *pdeFn(int hs, bool bf16) {
+    switch (pdeRingDepth()) {
+        case 4: return pdeFnD<4>(hs, bf16);
+        case 6: return pdeFnD<6>(hs, bf16);
+        case 12: return pdeFnD<12>(hs, bf16);
+        default: return pdeFnD<8>(hs, bf16);
+    }
 }
 
 size_t pdeLdsBytes(int dim, int hidden, int q0, int nLayers) {
@@ -728,7 +839,7 @@ std::vector<unsigned> pdeGroupExpect(const std::vector<int> &passStart, int grid
 }
 
 // preloadModules(): one kernel of this translation unit's code object
-const void *pdeModuleKernel() { return (const void *)pdeKernel<128, true>; }
+const void *pdeModuleKernel() { return pdeFn(128, true); }
 
 }  // namespace hipk
 }  // namespace dl

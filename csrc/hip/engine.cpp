@@ -104,6 +104,23 @@ std::vector<unsigned long long> HipEngineImpl::traceAttnBlock(int token, int pos
     return out;
 }
 
+std::vector<unsigned long long> HipEngineImpl::traceDecodeEngine(int token, int pos, int slot, int layer) {
+    if (!pdeOn_) return {};
+    const size_t words = 32 * (size_t)pdeGrid_;
+    unsigned long long *buf = dalloc<unsigned long long>(words);
+    DL_HIP(hipMemsetAsync(buf, 0, words * 8, stream_));
+    pde_.trace = buf;
+    pde_.traceLayer = layer;
+    setInputs(1, &token, &pos, &slot);
+    enqueueForward(1, GraphKind::LOGITS);
+    syncAndCheckComm();
+    inputsInFlight_ = false;
+    pde_.trace = nullptr;
+    std::vector<unsigned long long> out(words);
+    DL_HIP(hipMemcpy(out.data(), buf, words * 8, hipMemcpyDeviceToHost));
+    return out;
+}
+
 void HipEngineImpl::forward(int n, const int *tokens, const int *positions, const int *slots, float *logits) {
     Timer t;
     setInputs(n, tokens, positions, slots);

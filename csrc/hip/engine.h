@@ -38,6 +38,12 @@ class HipEngine : public Backend {
         (void)token, (void)pos, (void)slot, (void)layer;
         return {};
     }
+    // Diagnostics: one eager single-row forward with the decode engine's layer `layer` traced
+    // (kernels.h PdeArgs::trace): returns grid x 32 u64 stamps.
+    virtual std::vector<unsigned long long> traceDecodeEngine(int token, int pos, int slot, int layer) {
+        (void)token, (void)pos, (void)slot, (void)layer;
+        return {};
+    }
     virtual int fusedGridMax() const { return 0; }
     // Tensor parallel: a batched forward of n rows all-reduces its wo / w2 tiles inside the GEMM
     // epilogues (no separate all-reduce / norm kernels).

@@ -80,7 +80,8 @@ int HipEngineImpl::batchChunk(const DevMat &m, int pro, int epi) const {
     // largest batch chunk (1/2/4) whose LDS footprint stays <= 64 KiB for this input width
     int bc = 4;
     while (bc > 1) {
-        const int rpw = hipk::gemvRowsPerPass(m.n, m.rows, bc, q40_) * passesFor(m, epi, bc);
+        const int rp = q40_ ? 256 / m.lanes * hipk::gemvRowGroup(bc, true) : hipk::gemvRowsPerPass(m.n, m.rows, bc, false);
+        const int rpw = rp * passesFor(m, epi, bc);
         if (hipk::gemvLdsBytes(m.n, bc, q40_, rpw, pro) <= 64 * 1024) break;  // B > 1 only; B = 1 may use up to 160 KB
         bc >>= 1;
     }
@@ -191,6 +192,8 @@ hipk::AttnBlockArgs HipEngineImpl::attnBlockArgs(const DevLayer &L, u32 l, int c
     const bool tp = fusedTp(false);
     b.wo = gemvArgs(L.wo, 0, 1, tp ? hipk::EPI_STORE_TP : hipk::EPI_STORE, nullptr, p.q0, nullptr, nullptr, nullptr,
                     dY_, h_.dim, nullptr, dAttQ_, dAttS_, nullptr, nullptr, tp);
+    b.qkv.passes *= blockPassMul_;  // longer workgroups when the default grids would not be co-resident
+    b.wo.passes *= blockPassMul_;
     b.hg = hipk::attnBlockHG(b.at);
     b.layer = (int)l;
     b.nLayers = (int)h_.nLayers;
@@ -212,6 +215,15 @@ void HipEngineImpl::setupAttnBlock() {
     if ((e && *e == '0') || !q40_ || plan_.nKvHeads0 > kMaxKvGroups) return;
     const int share = comm_ ? std::max(1, comm_->ranksOnDevice()) : 1;
     const int keep = bucket_;
+    // qkv / wo passes per workgroup: the fewest that make the shortest-context grid co-resident
+    // (64-lane tilings of the decode engine give 8-row passes and 4x the default grids)
+    bucket_ = 0;
+    for (blockPassMul_ = 1; blockPassMul_ < 8; blockPassMul_ *= 2) {
+        const hipk::AttnBlockArgs b = attnBlockArgs(layers_[0], 0, 0);
+        if (!hipk::attnBlockPlan(b, fusedTp(false)).fn) break;
+        const hipk::GemvResidency r = hipk::attnBlockResidency(b, fusedTp(false));
+        if (r.maxResident > 0 && r.grid <= r.maxResident / share) break;
+    }
     int lastOn = -1;
     hipk::GemvResidency off;
     for (size_t i = 0; i < buckets_.size(); i++) {

@@ -88,6 +88,7 @@ class HipEngineImpl : public HipEngine {
     bool attnBlock() const override { return blockOn_; }
     bool decodeEngine() const override { return pdeOn_; }
     std::vector<unsigned long long> traceAttnBlock(int token, int pos, int slot, int layer) override;
+    std::vector<unsigned long long> traceDecodeEngine(int token, int pos, int slot, int layer) override;
     int fusedGridMax() const override { return fusedGridMax_; }
     bool tpBatchedFused(int n) const override { return plan_.nRanks > 1 && batchedPath(n) && fuseNorm(n); }
 
@@ -162,7 +163,7 @@ class HipEngineImpl : public HipEngine {
     int tpPasses(const DevMat &m, int bc) const;
     int batchChunk(const DevMat &m, int pro, int epi) const;
     int passesFor(const DevMat &m, int epi, int B) const {
-        return hipk::gemvDefaultPasses(m.n, m.rows, B, q40_, epi);
+        return hipk::gemvDefaultPasses(m.n, m.rows, B, q40_, epi, q40_ ? m.lanes : 0);
     }
     hipk::GemvArgs gemvArgs(const DevMat &m, int c0, int bc, int epi, const float *in, int ldIn, const float *add,
                             float *xNext, const float *normW, float *out, int ldOut, const DevLayer *L,
@@ -272,6 +273,7 @@ class HipEngineImpl : public HipEngine {
     unsigned *dEpoch_ = nullptr, *dBlockCnt_ = nullptr, *dBlockExpect_ = nullptr;
     int *dBlockErr_ = nullptr;
     bool blockOn_ = false;   // decode rows may run the fused attention block (per bucket: CtxBucket::block)
+    int blockPassMul_ = 1;   // qkv / wo passes multiplier of the block's roles (setupAttnBlock)
     int traceLayer_ = -1;    // traceAttnBlock: the layer whose block launch is traced
     unsigned long long *traceBuf_ = nullptr;
 

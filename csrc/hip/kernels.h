@@ -238,7 +238,8 @@ inline int gemvRowsPerPass(int n, int rows, int B, bool q40) {
 size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg, int pro);
 // Passes (row groups per lane group) for a launch: Q40 ring kernel -> enough that the whole grid is
 // resident at once (DL_GEMV_RESIDENT workgroups, default 512); ACT_Q80 -> whole Q80 blocks per WG.
-int gemvDefaultPasses(int n, int rows, int B, bool q40, int epi);
+// lanes: the matrix's tiling L when known (0: the GEMV's own choice for this shape).
+int gemvDefaultPasses(int n, int rows, int B, bool q40, int epi, int lanes = 0);
 
 void launchAttention(const AttnArgs &a, int B, hipStream_t s);
 // MFMA decode attention (attn_mfma.hip): bf16 cache, head size 128, kvMul 1/2/4/8; launchAttention
@@ -329,6 +330,10 @@ struct PdeArgs {
     const unsigned *epoch = nullptr;
     int *error = nullptr;
     long long timeoutTicks = 200LL * 1000 * 1000;
+    // diagnostics: 32 u64 per workgroup of s_memrealtime stamps of layer traceLayer (aux events
+    // 0-18 in decode_engine.hip order, ring waves' phase start / end 20-27, XCC id at 31)
+    unsigned long long *trace = nullptr;
+    int traceLayer = 0;
 };
 constexpr int kPdeCntWords = (kPdeMaxKv + 4 * 8) * 64;
 struct PdePlan {

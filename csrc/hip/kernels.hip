@@ -130,12 +130,12 @@ void tileQ40AoS(const uint8_t *const *rowBlocks, int rows, int n, int L, uint8_t
     tileQ40Parallel(src, rows, n, L, qsOut, dOut);
 }
 
-int gemvDefaultPasses(int n, int rows, int B, bool q40, int epi) {
+int gemvDefaultPasses(int n, int rows, int B, bool q40, int epi, int lanes) {
     static const int resident = [] {
         const char *e = getenv("DL_GEMV_RESIDENT");
         return e ? atoi(e) : 512;
     }();
-    const int rp = gemvRowsPerPass(n, rows, B, q40);
+    const int rp = lanes > 0 ? kThreads / lanes * gemvRowGroup(B, q40) : gemvRowsPerPass(n, rows, B, q40);
     const int grid0 = (rows + rp - 1) / rp;
     int passes;
     if (q40) {

@@ -767,6 +767,12 @@ PYBIND11_MODULE(_C, m) {
                  return e.engine->traceAttnBlock(token, pos, slot, layer);
              },
              py::arg("token"), py::arg("pos"), py::arg("slot") = 0, py::arg("layer") = 1)
+        .def("trace_decode_engine",
+             [](PyHipEngine &e, int token, int pos, int slot, int layer) {
+                 py::gil_scoped_release rel;
+                 return e.engine->traceDecodeEngine(token, pos, slot, layer);
+             },
+             py::arg("token"), py::arg("pos"), py::arg("slot") = 0, py::arg("layer") = 1)
         .def_property_readonly("fused_grid_max", [](const PyHipEngine &e) { return e.engine->fusedGridMax(); })
         .def_property_readonly("kv_pages_free", [](const PyHipEngine &e) { return e.engine->kvPagesFree(); })
         .def("tp_batched_fused", [](const PyHipEngine &e, int n) { return e.engine->tpBatchedFused(n); }, py::arg("n"))

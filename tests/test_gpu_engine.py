@@ -434,7 +434,7 @@ def test_decode_engine_matches_layer_launches(C, assets, medium, gqa4, monkeypat
         _, cb = got.decode_greedy(24, [int(b[-1].argmax())], [9], [0])
         assert list(ca)[:12] == list(cb)[:12], (model, list(ca), list(cb))
         # the engine covers contexts up to 256 positions; beyond, the per-layer launches take over
-        for pos in (255, 300):
+        for pos in (p for p in (255, 300) if p < ref.header["seq_len"]):
             x, y = ref.forward([11], [pos], [0])[0], got.forward([11], [pos], [0])[0]
             assert np.isfinite(y).all() and _rel(y, x) < 5e-3, (model, pos)
 
