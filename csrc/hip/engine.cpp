@@ -49,7 +49,6 @@ HipEngineImpl::HipEngineImpl(const EngineConfig &cfg, DeviceComm *comm) : cfg_(c
                    (size_t)2 * cfg.maxBatch <= (size_t)tpArg_.stride;
         tpVec_.q80 = syncQ80_ ? 1 : 0;
     }
-    decidePde();  // before checkFits / the load: it fixes the layer matrices' tiling
     checkFits();
     if (tpFused_) checkFusedResidency();
     {  // path knobs, read once: a captured graph replays the path it was captured with
@@ -67,7 +66,6 @@ HipEngineImpl::HipEngineImpl(const EngineConfig &cfg, DeviceComm *comm) : cfg_(c
     uploadRope();
     DL_HIP(hipStreamSynchronize(stream_));
     setupAttnBlock();
-    setupPde();
     hipk::preloadModules();  // no code-object load inside the first forwards
     load_.ms = timer.elapsedMs();
     load_.deviceBytes = deviceBytes_;
@@ -101,23 +99,6 @@ std::vector<unsigned long long> HipEngineImpl::traceAttnBlock(int token, int pos
     DL_HIP(hipMemcpy(out.data() + 3, traceBuf_, words * 8, hipMemcpyDeviceToHost));
     traceLayer_ = -1;
     traceBuf_ = nullptr;  // (one small buffer per call, released with the engine)
-    return out;
-}
-
-std::vector<unsigned long long> HipEngineImpl::traceDecodeEngine(int token, int pos, int slot, int layer) {
-    if (!pdeOn_) return {};
-    const size_t words = 32 * (size_t)pdeGrid_;
-    unsigned long long *buf = dalloc<unsigned long long>(words);
-    DL_HIP(hipMemsetAsync(buf, 0, words * 8, stream_));
-    pde_.trace = buf;
-    pde_.traceLayer = layer;
-    setInputs(1, &token, &pos, &slot);
-    enqueueForward(1, GraphKind::LOGITS);
-    syncAndCheckComm();
-    inputsInFlight_ = false;
-    pde_.trace = nullptr;
-    std::vector<unsigned long long> out(words);
-    DL_HIP(hipMemcpy(out.data(), buf, words * 8, hipMemcpyDeviceToHost));
     return out;
 }
 
@@ -248,7 +229,7 @@ void HipEngineImpl::profileForward(int n, const int *tokens, const int *position
 void HipEngineImpl::syncAndCheckComm() {
     const int *flag = comm_ ? comm_->deviceErrorFlag() : nullptr;
     if (flag) DL_HIP(hipMemcpyAsync(hErr_, flag, sizeof(int), hipMemcpyDeviceToHost, stream_));
-    const bool inLaunch = blockOn_ || pdeOn_;  // kernels with in-launch hand-offs
+    const bool inLaunch = blockOn_;  // kernels with in-launch hand-offs
     if (inLaunch) DL_HIP(hipMemcpyAsync(hErr_ + 1, dBlockErr_, sizeof(int), hipMemcpyDeviceToHost, stream_));
     DL_HIP(hipStreamSynchronize(stream_));
     if (inLaunch && hErr_[1] != 0) {
@@ -256,8 +237,7 @@ void HipEngineImpl::syncAndCheckComm() {
         hErr_[1] = 0;
         resetAttnBlockState();
         throw Error("in-launch hand-off wait timed out (code " + std::to_string(code) +
-                    ": attention block 2 qkv->attention, 3 attention->wo, 4 qkv phase; decode engine 21 w2->qkv, "
-                    "22 qkv->attention, 23 attention->wo, 24 wo->w13, 25 w13->w2, 26 final; not all workgroups "
+                    ": attention block 2 qkv->attention, 3 attention->wo, 4 qkv phase; not all workgroups "
                     "resident?)");
     }
     if (flag && *hErr_ != 0)

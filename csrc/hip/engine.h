@@ -30,17 +30,9 @@ class HipEngine : public Backend {
     virtual bool tpFused() const { return false; }
     // Single decode rows run the fused attention block (qkv + attention + wo in one launch).
     virtual bool attnBlock() const { return false; }
-    // Single decode rows of short contexts run the persistent decode engine (all layers, one launch).
-    virtual bool decodeEngine() const { return false; }
     // Diagnostics: one eager single-row forward with the fused attention block of `layer` traced
     // (kernels.h AttnBlockArgs::trace, 8 u64 per workgroup); returns {gq, ga, gw, trace...}.
     virtual std::vector<unsigned long long> traceAttnBlock(int token, int pos, int slot, int layer) {
-        (void)token, (void)pos, (void)slot, (void)layer;
-        return {};
-    }
-    // Diagnostics: one eager single-row forward with the decode engine's layer `layer` traced
-    // (kernels.h PdeArgs::trace): returns grid x 32 u64 stamps.
-    virtual std::vector<unsigned long long> traceDecodeEngine(int token, int pos, int slot, int layer) {
         (void)token, (void)pos, (void)slot, (void)layer;
         return {};
     }

@@ -216,7 +216,7 @@ void HipEngineImpl::setupAttnBlock() {
     const int share = comm_ ? std::max(1, comm_->ranksOnDevice()) : 1;
     const int keep = bucket_;
     // qkv / wo passes per workgroup: the fewest that make the shortest-context grid co-resident
-    // (64-lane tilings of the decode engine give 8-row passes and 4x the default grids)
+    // (wide shards, e.g. 70B / 405B at TP1, would otherwise exceed one round of workgroups)
     bucket_ = 0;
     for (blockPassMul_ = 1; blockPassMul_ < 8; blockPassMul_ *= 2) {
         const hipk::AttnBlockArgs b = attnBlockArgs(layers_[0], 0, 0);
@@ -250,106 +250,11 @@ void HipEngineImpl::setupAttnBlock() {
                      off.maxResident / share);
 }
 
-// The persistent decode engine (decode_engine.hip) runs single decode rows of short contexts at
-// TP1: decided before the weights are placed (its matrices are tiled with 64 lanes per row and the
-// layers of one matrix kind share a slab). DL_DECODE_ENGINE=0 keeps the per-layer launches.
-void HipEngineImpl::decidePde() {
-    const char *e = std::getenv("DL_DECODE_ENGINE");
-    if ((e && *e == '0') || !q40_ || plan_.nRanks != 1) return;
-    const ShardPlan &p = plan_;
-    if (h_.dim % 32 || h_.dim > 8192 || p.hidden0 % 32 || p.q0 % 32 || p.nKvHeads0 > hipk::kPdeMaxKv ||
-        (p.headSize != 64 && p.headSize != 128))
-        return;
-    const int grid = hipk::pdeGrid((int)h_.dim, (int)p.hidden0, (int)p.q0, (int)p.headSize, (int)h_.nLayers, kvBf16_);
-    if (grid <= 0 || (int)p.nHeads0 > grid) return;
-    const int rows[4] = {(int)(p.q0 + 2 * p.kv0), (int)h_.dim, (int)(2 * p.hidden0), (int)h_.dim};
-    const int n[4] = {(int)h_.dim, (int)p.q0, (int)h_.dim, (int)p.hidden0};
-    const hipk::PdePlan pl = hipk::pdePlan(rows, n, (int)p.hidden0, grid);
-    const int V = 2 * grid;
-    for (int m = 0; m < 4; m++)
-        for (int v = 0; v < V; v++)
-            if ((pl.passStart[m * (V + 1) + v + 1] - pl.passStart[m * (V + 1) + v]) * 8 > hipk::kPdeMaxRes) return;
-    pdeTiling_ = true;
-    pdeGrid_ = grid;
-    for (int m = 0; m < 4; m++) {
-        pde_.rows[m] = rows[m];
-        pde_.n[m] = n[m];
-        pde_.K[m] = pl.K[m];
-    }
-    pdePasses_ = pl.passStart;
-}
-
-// After the load: hand-off buffers, counters and the launch arguments of the decode engine.
-void HipEngineImpl::setupPde() {
-    if (!pdeTiling_) return;
-    const ShardPlan &p = plan_;
-    const int grid = pdeGrid_;
-    int *ps = dalloc<int>(pdePasses_.size());
-    DL_HIP(hipMemcpy(ps, pdePasses_.data(), pdePasses_.size() * sizeof(int), hipMemcpyHostToDevice));
-    const std::vector<unsigned> expect = hipk::pdeGroupExpect(pdePasses_, grid, pde_.rows[0], (int)p.q0, (int)p.kv0,
-                                                              (int)p.headSize, (int)p.kvMul, (int)p.nKvHeads0);
-    unsigned *ge = dalloc<unsigned>(expect.size());
-    DL_HIP(hipMemcpy(ge, expect.data(), expect.size() * sizeof(unsigned), hipMemcpyHostToDevice));
-    std::vector<void *> ptrs;
-    for (const DevLayer &L : layers_) ptrs.push_back(L.rmsAtt);
-    for (const DevLayer &L : layers_) ptrs.push_back(L.rmsFfn);
-    for (const DevLayer &L : layers_) ptrs.push_back(L.k);
-    for (const DevLayer &L : layers_) ptrs.push_back(L.v);
-    void **dp = dalloc<void *>(ptrs.size());
-    DL_HIP(hipMemcpy(dp, ptrs.data(), ptrs.size() * sizeof(void *), hipMemcpyHostToDevice));
-    const size_t nL = h_.nLayers;
-    hipk::PdeArgs &a = pde_;
-    for (int m = 0; m < 4; m++) {
-        a.qs[m] = qsSlab_[m];
-        a.d[m] = reinterpret_cast<const uint32_t *>(dSlab_[m]);
-        a.qsStride[m] = (long long)qsStride_[m];
-        a.dStride[m] = (long long)(dStride_[m] / 4);
-    }
-    a.passStart = ps;
-    a.groupExpect = ge;
-    a.rmsAtt = reinterpret_cast<const float *const *>(dp);
-    a.rmsFfn = reinterpret_cast<const float *const *>(dp + nL);
-    a.kcache = reinterpret_cast<void *const *>(dp + 2 * nL);
-    a.vcache = reinterpret_cast<void *const *>(dp + 3 * nL);
-    a.nLayers = (int)h_.nLayers;
-    a.dim = (int)h_.dim;
-    a.hidden = (int)p.hidden0;
-    a.q0 = (int)p.q0;
-    a.kv0 = (int)p.kv0;
-    a.hs = (int)p.headSize;
-    a.kvMul = (int)p.kvMul;
-    a.nHeads0 = (int)p.nHeads0;
-    a.seqLen = (int)h_.seqLen;
-    a.kvBf16 = kvBf16_ ? 1 : 0;
-    a.eps = h_.normEpsilon;
-    a.act = h_.hiddenAct == HiddenAct::GELU ? 0 : 1;
-    a.rope = dRope_;
-    a.kvMap = kvMap();
-    a.pos = dPos_;
-    a.slot = dSlot_;
-    a.xIn = dX_[0];
-    dXOut_ = dalloc<float>(h_.dim);
-    a.xOut = dXOut_;
-    a.eQkv = dalloc<float>(p.q0 + 2 * p.kv0);
-    a.eAttQ = dalloc<int8_t>(p.q0);
-    a.eAttS = dalloc<float2>(p.q0 / 32);
-    a.eWo = dalloc<float>(h_.dim);
-    a.eHQ = dalloc<int8_t>(p.hidden0);
-    a.eHS = dalloc<float2>(p.hidden0 / 32);
-    a.eW2 = dalloc<float>(h_.dim);
-    a.cnt = dalloc<unsigned>(hipk::kPdeCntWords);
-    DL_HIP(hipMemset(a.cnt, 0, hipk::kPdeCntWords * sizeof(unsigned)));
-    a.epoch = dEpoch_ + 1;  // its own per-forward epoch (the attention block counts its forwards in [0])
-    a.error = dBlockErr_;
-    pdeOn_ = true;
-}
-
 // A fused-block wait gave up (a workgroup of the launch never arrived): reset the monotonic
 // counters and the epoch so the engine stays usable, then raise.
 void HipEngineImpl::resetAttnBlockState() {
     DL_HIP(hipMemsetAsync(dBlockCnt_, 0, sizeof(unsigned) * kBlockCntWords, stream_));
-    if (pdeOn_) DL_HIP(hipMemsetAsync(pde_.cnt, 0, sizeof(unsigned) * hipk::kPdeCntWords, stream_));
-    DL_HIP(hipMemsetAsync(dEpoch_, 0, 2 * sizeof(unsigned), stream_));
+    DL_HIP(hipMemsetAsync(dEpoch_, 0, sizeof(unsigned), stream_));
     DL_HIP(hipMemsetAsync(dBlockErr_, 0, sizeof(int), stream_));
     DL_HIP(hipStreamSynchronize(stream_));
 }
@@ -469,23 +374,16 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
     int cur = 0;
     const bool bat = batchedPath(n);                                   // MFMA GEMMs on f16 activations
     const bool fz = bat && fuseNorm(n);                                // residual + norm in the GEMM epilogues
-    // one persistent decode-engine launch for all layers (short contexts, TP1)
-    const bool pde = pdeOn_ && n == 1 && !bat && buckets_[bucket_].maxLen <= hipk::kPdeMaxCtx;
-    const bool blk = !pde && blockOn_ && buckets_[bucket_].block && n == 1 && !bat;  // fused attention block
+    const bool blk = blockOn_ && buckets_[bucket_].block && n == 1 && !bat;  // fused attention block
     {
         ProfScope ps(this, "embedding");
-        // the epochs count the forwards that run the fused block / the decode engine (their
-        // counters' targets)
-        hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_, blk ? dEpoch_ : (pde ? dEpoch_ + 1 : nullptr));
-    }
-    if (pde) {
-        ProfScope ps(this, "decode_engine");
-        hipk::launchPde(pde_, pdeGrid_, stream_);
+        // the epoch counts the forwards that run the fused block (its counters' targets)
+        hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_, blk ? dEpoch_ : nullptr);
     }
     // Q80 hand-off of h needs one workgroup per 32 hidden units; for skinny TP shards the w13
     // epilogue emits f32 and w2 quantizes in its prologue instead.
     const bool hQ80 = q40_ && p.hidden0 / 32 >= 192;
-    for (u32 l = 0; l < (pde ? 0u : h_.nLayers); l++) {
+    for (u32 l = 0; l < h_.nLayers; l++) {
         DevLayer &L = layers_[l];
         const bool hasDelta = l > 0;
         if (blk) {
@@ -571,9 +469,6 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
         else if (bat)
             gemmBatched(wcls_, n, hipk::EPI_STORE, dX_[cur], dim, dY_, nullptr, rmsFinal_, nullptr, dLogits_, p.vocab0,
                         nullptr, nullptr);
-        else if (pde)
-            gemv(wcls_, n, hipk::PRO_RESNORM, hipk::EPI_STORE, dXOut_, dim, nullptr, nullptr, rmsFinal_, dLogits_,
-                 p.vocab0, nullptr);
         else
             gemv(wcls_, n, hipk::PRO_RESNORM, hipk::EPI_STORE, dX_[cur], dim, dY_, nullptr, rmsFinal_, dLogits_,
                  p.vocab0, nullptr);

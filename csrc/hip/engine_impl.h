@@ -86,9 +86,7 @@ class HipEngineImpl : public HipEngine {
     void profileForward(int n, const int *tokens, const int *positions, const int *slots) override;
     bool tpFused() const override { return tpFused_; }
     bool attnBlock() const override { return blockOn_; }
-    bool decodeEngine() const override { return pdeOn_; }
     std::vector<unsigned long long> traceAttnBlock(int token, int pos, int slot, int layer) override;
-    std::vector<unsigned long long> traceDecodeEngine(int token, int pos, int slot, int layer) override;
     int fusedGridMax() const override { return fusedGridMax_; }
     bool tpBatchedFused(int n) const override { return plan_.nRanks > 1 && batchedPath(n) && fuseNorm(n); }
 
@@ -123,12 +121,9 @@ class HipEngineImpl : public HipEngine {
     void checkFusedResidency();
     void allocBuffers();
     void uploadRope();
-    size_t matStageBytes(u32 rows, u32 n, bool layerMat = true) const;
-    // lanes per row of a matrix's Q40 tiling: 64 for the layer matrices when the persistent decode
-    // engine streams them, else the GEMV's choice
-    int lanesFor(int rows, int n, bool layerMat) const {
-        return pdeTiling_ && layerMat ? 64 : hipk::gemvLanesPerRow(n, rows, 1, true);
-    }
+    size_t matStageBytes(u32 rows, u32 n) const;
+    // lanes per row of a matrix's Q40 tiling (the GEMV's choice)
+    static int lanesFor(int rows, int n) { return hipk::gemvLanesPerRow(n, rows, 1, true); }
     void placeQ40(DevMat &m, const hipk::Q40Tiling &t, int mi, u32 l);
     struct RowSrc {
         const TensorInfo *t;
@@ -258,16 +253,6 @@ class HipEngineImpl : public HipEngine {
     int bucket_ = 0;          // index into buckets_
     bool attnLong_ = false;   // decode attention runs the MFMA kernel
     bool prefillOk_ = false;  // the rows qualify for the MFMA prefill attention
-
-    // persistent decode engine (decode_engine.hip; engine_forward.cpp setupPde)
-    bool pdeTiling_ = false;  // layer matrices tiled with 64 lanes per row (decided before the load)
-    bool pdeOn_ = false;      // single decode rows of short contexts run the engine
-    int pdeGrid_ = 0;
-    hipk::PdeArgs pde_;
-    std::vector<int> pdePasses_;  // [4][2 * grid + 1] pass ranges (decidePde)
-    float *dXOut_ = nullptr;
-    void decidePde();
-    void setupPde();
 
     // fused attention block
     unsigned *dEpoch_ = nullptr, *dBlockCnt_ = nullptr, *dBlockExpect_ = nullptr;

@@ -21,7 +21,7 @@ void HipEngineImpl::checkFits() {
     const size_t kv = (size_t)h_.nLayers * 2 * kvPoolRows() * p.kv0 * (kvBf16_ ? 2 : 4);
     size_t w = (size_t)h_.nLayers * (matStageBytes(p.q0 + 2 * p.kv0, h_.dim) + matStageBytes(h_.dim, p.q0) +
                                      matStageBytes(2 * p.hidden0, h_.dim) + matStageBytes(h_.dim, p.hidden0));
-    w += matStageBytes(p.vocab0, h_.dim, false) + (size_t)h_.vocabSize * h_.dim * 4;
+    w += matStageBytes(p.vocab0, h_.dim) + (size_t)h_.vocabSize * h_.dim * 4;
     const size_t act = (size_t)cfg_.maxBatch * h_.vocabSize * 4 * 3 + ((size_t)256 << 20);
     if (kv + w + act > freeB) {
         // the page pool that would fit (positions shared by all slots), as a hint
@@ -275,15 +275,15 @@ void HipEngineImpl::readRows(Loader &ld, const std::vector<RowSrc> &srcs, bool i
     }
 }
 
-size_t HipEngineImpl::matStageBytes(u32 rows, u32 n, bool layerMat) const {
+size_t HipEngineImpl::matStageBytes(u32 rows, u32 n) const {
     if (!q40_) return (size_t)rows * n * 4;
-    const hipk::Q40Tiling t = hipk::q40Tiling((int)rows, (int)n, lanesFor((int)rows, (int)n, layerMat));
+    const hipk::Q40Tiling t = hipk::q40Tiling((int)rows, (int)n, lanesFor((int)rows, (int)n));
     return t.qsBytes + t.dBytes;
 }
 
 // Device storage of a Q40 matrix: layer matrix `mi` (0 qkv, 1 wo, 2 w13, 3 w2) of layer l lives in
-// one slab per matrix kind, all layers back to back (the persistent decode engine addresses layer
-// l as slab + l * stride); other matrices get their own allocation.
+// one slab per matrix kind, all layers back to back (4 allocations instead of 4 x nLayers);
+// other matrices get their own allocation.
 void HipEngineImpl::placeQ40(DevMat &m, const hipk::Q40Tiling &t, int mi, u32 l) {
     if (mi < 0) {
         m.qs = dalloc<uint8_t>(t.qsBytes);
@@ -309,7 +309,7 @@ void HipEngineImpl::buildMat(Loader &ld, DevMat &m, const std::vector<RowSrc> &s
     m.n = (int)nc;
     u8 *st = stageAcquire(ld);
     if (q40_) {
-        m.lanes = lanesFor(rows, (int)nc, mi >= 0);
+        m.lanes = lanesFor(rows, (int)nc);
         const hipk::Q40Tiling t = hipk::q40Tiling(rows, (int)nc, m.lanes);
         DL_CHECK(t.qsBytes + t.dBytes <= ld.stageBytes, "staging buffer too small");
         hipk::tileQ40AoS(ld.rowPtr.data(), rows, (int)nc, m.lanes, st, reinterpret_cast<uint32_t *>(st + t.qsBytes));
@@ -351,7 +351,7 @@ void HipEngineImpl::loadFromFile() {
     sb = std::max(sb, matStageBytes(h_.dim, p.q0));
     sb = std::max(sb, matStageBytes(2 * p.hidden0, h_.dim));
     sb = std::max(sb, matStageBytes(h_.dim, p.hidden0));
-    sb = std::max(sb, matStageBytes(p.vocab0, h_.dim, false));
+    sb = std::max(sb, matStageBytes(p.vocab0, h_.dim));
     ld.stageBytes = sb;
     for (int i = 0; i < 2; i++) {
         DL_HIP(hipHostMalloc(reinterpret_cast<void **>(&ld.stage[i]), sb, hipHostMallocDefault));
@@ -399,7 +399,7 @@ void HipEngineImpl::synthMat(DevMat &m, int rows, int n, u64 seed, int mi, u32 l
     m.n = n;
     const float scale = 1.0f / std::sqrt(21.5f * (float)n);
     if (q40_) {
-        m.lanes = lanesFor(rows, n, mi >= 0);
+        m.lanes = lanesFor(rows, n);
         const hipk::Q40Tiling t = hipk::q40Tiling(rows, n, m.lanes);
         const size_t nBlocks = t.qsBytes / 16;  // == t.dBytes / 2 f16 scales
         placeQ40(m, t, mi, l);

@@ -291,66 +291,6 @@ void attnBlockExpect(const GemvArgs &qkv, int nKv, unsigned *out);
 GemvResidency attnBlockResidency(const AttnBlockArgs &a, bool tp);
 void launchAttnBlock(const AttnBlockArgs &a, bool tp, hipStream_t s);
 
-// Persistent decode engine (decode_engine.hip): every layer of a single-row decode forward in ONE
-// launch of one 768-thread workgroup per CU (8 weight-ring waves = 2 virtual workgroups of 256
-// lanes + 4 aux waves). Matrix m (0 qkv, 1 wo, 2 w13, 3 w2) is Q40 tiled with 64 lanes per row
-// (Q40Tiling L = 64: 8 rows per pass, K = ceil(nb / 64) steps per pass); layer l's copy lives at
-// qs[m] + l * qsStride[m] bytes / d[m] + l * dStride[m] words. Virtual workgroup v streams passes
-// [passStart[m][v], passStart[m][v + 1]) of every layer in (layer, matrix) order; w13 ranges are
-// whole 32-hidden Q80 blocks (8 passes). Hand-offs between workgroups go through the e* buffers
-// (write-through) and monotonic counters `cnt` (zeroed once): [kPdeMaxKv] qkv arrivals per KV
-// group, then 8 per-XCD shards each for attention, wo, w13 and w2, every word on its own 256-B
-// line; the targets follow the per-forward epoch (incremented by launchEmbedding). Every wait is
-// bounded and sets `error` (codes 21-26). The attention of this engine covers one sequence chunk
-// per head (short contexts: the engine takes forwards whose context bucket is <= kPdeMaxCtx).
-constexpr int kPdeMaxRes = 256;  // rows of one matrix per virtual workgroup (LDS result slots)
-constexpr int kPdeMaxKv = 64;
-constexpr int kPdeMaxCtx = 256;
-struct PdeArgs {
-    const uint8_t *qs[4] = {};
-    const uint32_t *d[4] = {};
-    long long qsStride[4] = {}, dStride[4] = {};
-    int rows[4] = {}, n[4] = {}, K[4] = {};
-    const int *passStart = nullptr;      // [4][V + 1], V = 2 * grid
-    const unsigned *groupExpect = nullptr;  // [KV groups] workgroups publishing rows of each group
-    const float *const *rmsAtt = nullptr, *const *rmsFfn = nullptr;  // [nLayers] norm weights
-    void *const *kcache = nullptr, *const *vcache = nullptr;       // [nLayers] cache bases
-    int nLayers = 0, dim = 0, hidden = 0, q0 = 0, kv0 = 0, hs = 0, kvMul = 1, nHeads0 = 0, seqLen = 0, kvBf16 = 1;
-    float eps = 1e-5f;
-    int act = 1;  // 0 GELU, 1 SiLU
-    const float2 *rope = nullptr;
-    KvMap kvMap;
-    const int *pos = nullptr, *slot = nullptr;
-    const float *xIn = nullptr;  // embedding output
-    float *xOut = nullptr;       // final residual (for the logits GEMV)
-    float *eQkv = nullptr, *eWo = nullptr, *eW2 = nullptr;
-    int8_t *eAttQ = nullptr, *eHQ = nullptr;
-    float2 *eAttS = nullptr, *eHS = nullptr;
-    unsigned *cnt = nullptr;
-    const unsigned *epoch = nullptr;
-    int *error = nullptr;
-    long long timeoutTicks = 200LL * 1000 * 1000;
-    // diagnostics: 32 u64 per workgroup of s_memrealtime stamps of layer traceLayer (aux events
-    // 0-18 in decode_engine.hip order, ring waves' phase start / end 20-27, XCC id at 31)
-    unsigned long long *trace = nullptr;
-    int traceLayer = 0;
-};
-constexpr int kPdeCntWords = (kPdeMaxKv + 4 * 8) * 64;
-struct PdePlan {
-    int K[4] = {};
-    std::vector<int> passStart;  // [4][V + 1]
-};
-// Pass ranges of the 2 * grid virtual workgroups (equal weight-stream length per virtual
-// workgroup; w13 in whole Q80 blocks).
-PdePlan pdePlan(const int rows[4], const int n[4], int hidden, int grid);
-size_t pdeLdsBytes(int dim, int hidden, int q0, int nLayers);
-// Workgroups of a launch (one per CU) when the engine's kernel fits one per CU on this device, else 0.
-int pdeGrid(int dim, int hidden, int q0, int hs, int nLayers, bool bf16);
-void launchPde(const PdeArgs &a, int grid, hipStream_t s);
-// Workgroups whose qkv rows touch each KV group (the attention heads' arrival targets).
-std::vector<unsigned> pdeGroupExpect(const std::vector<int> &passStart, int grid, int rowsQkv, int q0, int kv0, int hs,
-                                     int kvMul, int nKv);
-
 // Prefill rows on MFMA (bf16 caches): blocks of attnPrefillRowsPerBlock(kvMul) consecutive rows
 // must share one slot (positions arbitrary, causal per row); counters >= blocks x KV heads.
 void launchAttentionPrefill(const AttnArgs &a, int nRows, hipStream_t s);

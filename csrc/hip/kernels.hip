@@ -1152,7 +1152,6 @@ const void *gemmModuleKernel();
 const void *gemmWideModuleKernel();
 const void *attnMfmaModuleKernel();
 const void *xgmiModuleKernel();
-const void *pdeModuleKernel();
 const void *gemvFnL16(bool q40, int B, int pro, int epi);
 const void *gemvFnL32(bool q40, int B, int pro, int epi);
 const void *gemvFnL64(bool q40, int B, int pro, int epi);
@@ -1169,7 +1168,7 @@ void preloadModules() {
     const BlockFn blocks[] = {attnBlockFn_16_32_128, attnBlockFn_32_32_128, attnBlockFn_64_32_128, attnBlockFn_64_16_128,
                               attnBlockFn_64_64_128, attnBlockFn_32_64_128, attnBlockFn_64_64_64};
     std::vector<const void *> fns = {(const void *)argmaxKernel, gemmModuleKernel(), gemmWideModuleKernel(),
-                                     attnMfmaModuleKernel(), xgmiModuleKernel(), pdeModuleKernel(), gemvFnL16(true, 1, 0, 0),
+                                     attnMfmaModuleKernel(), xgmiModuleKernel(), gemvFnL16(true, 1, 0, 0),
                                      gemvFnL32(true, 1, 0, 0), gemvFnL64(true, 1, 0, 0)};
     for (BlockFn b : blocks) {  // any instance of the unit will do
         const void *f = nullptr;

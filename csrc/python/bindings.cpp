@@ -760,17 +760,10 @@ PYBIND11_MODULE(_C, m) {
         .def_property_readonly("device_bytes", [](const PyHipEngine &e) { return e.engine->deviceBytes(); })
         .def_property_readonly("tp_fused", [](const PyHipEngine &e) { return e.engine->tpFused(); })
         .def_property_readonly("attn_block", [](const PyHipEngine &e) { return e.engine->attnBlock(); })
-        .def_property_readonly("decode_engine", [](const PyHipEngine &e) { return e.engine->decodeEngine(); })
         .def("trace_attn_block",
              [](PyHipEngine &e, int token, int pos, int slot, int layer) {
                  py::gil_scoped_release rel;
                  return e.engine->traceAttnBlock(token, pos, slot, layer);
-             },
-             py::arg("token"), py::arg("pos"), py::arg("slot") = 0, py::arg("layer") = 1)
-        .def("trace_decode_engine",
-             [](PyHipEngine &e, int token, int pos, int slot, int layer) {
-                 py::gil_scoped_release rel;
-                 return e.engine->traceDecodeEngine(token, pos, slot, layer);
              },
              py::arg("token"), py::arg("pos"), py::arg("slot") = 0, py::arg("layer") = 1)
         .def_property_readonly("fused_grid_max", [](const PyHipEngine &e) { return e.engine->fusedGridMax(); })

@@ -382,7 +382,6 @@ def test_attn_block_matches_separate_kernels(C, assets, medium, monkeypatch, kv_
     launch with in-launch write-through hand-offs): same logits as the three separate launches
     (attention reduces in another order: tolerance), same greedy chain, over many forwards (the
     block's monotonic counters across layers, forwards and graph replays)."""
-    monkeypatch.setenv("DL_DECODE_ENGINE", "0")  # the block serves the rows the engine does not take
     for model in (assets["q40"], medium):
         monkeypatch.setenv("DL_ATTN_BLOCK", "0")
         ref = C.HipEngine(model, "q80", kv_bf16=kv_bf16, max_batch=8)
@@ -400,54 +399,15 @@ def test_attn_block_matches_separate_kernels(C, assets, medium, monkeypatch, kv_
         assert list(ca) == list(cb)
 
 
-@pytest.fixture(scope="module")
-def gqa4(tmp_path_factory):
-    # 16 query heads over 4 KV heads (kvMul 4, as Llama-3.1-8B), head size 128, 3 layers
-    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
-    from distributed_llama_multiusers_amd.utils.mfile import FloatType
-    d = str(tmp_path_factory.mktemp("gqa4"))
-    m, _, _ = make_test_assets(d, "tiny", FloatType.Q40, seq_len=512, seed=11, dim=2048, hidden_dim=5632,
-                               n_heads=16, n_kv_heads=4, n_layers=3, vocab_size=2048)
-    return m
-
-
-@pytest.mark.parametrize("kv_bf16", [True, False])
-def test_decode_engine_matches_layer_launches(C, assets, medium, gqa4, monkeypatch, kv_bf16):
-    """Single decode rows of short contexts run the persistent decode engine (every layer in one
-    launch: per-lane weight rings streaming across matrices and layers, in-launch write-through
-    hand-offs through per-XCD counters): the same logits as the per-layer launches within f32
-    reassociation (rows reduce over 64 lanes instead of 16 / 32), the same greedy chain, over many
-    forwards and graph replays (monotonic counters across layers and forwards), with batched
-    forwards in between (which must not advance the engine's epoch)."""
-    for model in (assets["q40"], medium, gqa4):
-        monkeypatch.setenv("DL_DECODE_ENGINE", "0")
-        ref = C.HipEngine(model, "q80", kv_bf16=kv_bf16, max_batch=8)
-        monkeypatch.delenv("DL_DECODE_ENGINE")
-        got = C.HipEngine(model, "q80", kv_bf16=kv_bf16, max_batch=8)
-        assert got.decode_engine and not ref.decode_engine
-        toks = [3, 17, 101, 7, 250, 9]
-        a, b = _seq(ref, toks), _seq(got, toks)
-        assert _rel(b, a) < 2e-3, model
-        ref.forward([5, 6, 7], [6, 7, 8], [0, 0, 0])
-        got.forward([5, 6, 7], [6, 7, 8], [0, 0, 0])
-        _, ca = ref.decode_greedy(24, [int(a[-1].argmax())], [9], [0])
-        _, cb = got.decode_greedy(24, [int(b[-1].argmax())], [9], [0])
-        assert list(ca)[:12] == list(cb)[:12], (model, list(ca), list(cb))
-        # the engine covers contexts up to 256 positions; beyond, the per-layer launches take over
-        for pos in (p for p in (255, 300) if p < ref.header["seq_len"]):
-            x, y = ref.forward([11], [pos], [0])[0], got.forward([11], [pos], [0])[0]
-            assert np.isfinite(y).all() and _rel(y, x) < 5e-3, (model, pos)
-
-
-def test_decode_engine_8b_shape_matches_cpu(C, tmp_path):
-    """Llama-3.1-8B layer shapes (2 layers, 2048-token vocabulary): the decode engine's logits
-    against the CPU reference backend, prompt then single-row decode."""
+def test_engine_8b_shape_matches_cpu(C, tmp_path):
+    """Llama-3.1-8B layer shapes (2 layers, 2048-token vocabulary, kvMul 4, head size 128): the
+    fused attention block's decode logits against the CPU reference backend, token by token."""
     from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
     from distributed_llama_multiusers_amd.utils.mfile import FloatType
     m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=5, dim=4096,
                                hidden_dim=14336, n_heads=32, n_kv_heads=8, n_layers=2, vocab_size=2048)
     gpu = C.HipEngine(m, "q80", kv_bf16=False, max_batch=8)
-    assert gpu.decode_engine
+    assert gpu.attn_block
     cpu = C.cpu_backend(m, "q80", 8)
     toks = [1, 2, 3, 500, 1000, 7]
     assert _rel(_seq(gpu, toks), _seq(cpu, toks)) < 3e-2
