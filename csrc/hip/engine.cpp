@@ -120,7 +120,6 @@ void HipEngineImpl::forward(int n, const int *tokens, const int *positions, cons
     inputsInFlight_ = false;
     if (root && logits) std::memcpy(logits, hLogits_, (size_t)n * h_.vocabSize * sizeof(float));
     stats_.computeMs = t.elapsedMs();
-    stats_.syncMs = 0;
 }
 
 void HipEngineImpl::forwardArgmax(int n, const int *tokens, const int *positions, const int *slots, int *out) {
@@ -172,6 +171,7 @@ double HipEngineImpl::decodeGreedyBatch(int steps, int nSeq, const int *tokens, 
                                         int *outTokens) {
     DL_CHECK(nSeq >= 1 && (u32)nSeq <= cfg_.maxBatch, "nSeq");
     for (int b = 0; b < nSeq; b++) DL_CHECK((u32)(pos[b] + steps) <= h_.seqLen, "decode exceeds seqLen");
+    exchangeMs(nSeq);  // calibrated outside the timed chain
     setInputs(nSeq, tokens, pos, slots, nullptr, steps - 1);
     DL_HIP(hipMemsetAsync(dHist_, 0xff, sizeof(int) * (size_t)cfg_.maxBatch * h_.seqLen, stream_));
     hipEvent_t e0, e1;
@@ -278,6 +278,32 @@ void HipEngineImpl::accountForward(int n, GraphKind kind, int times) {
     }
     stats_.sentBytes = sent * (u64)times;
     stats_.recvBytes = recv * (u64)times;
+    // sync time estimate: the exchanges run inside the forward's graph (no host-visible boundary),
+    // so each is priced at the calibrated cost of one all-reduce of the same rows
+    stats_.syncMs = exchangeMs(n) * (2.0 * h_.nLayers + 1.0) * times;
+}
+
+// Device time of one all-reduce of n rows on this engine's transport, measured once per row count
+// (8 back-to-back calls on the idle stream). Every rank runs the same forwards in the same order,
+// so every rank calibrates at the same point; dY_ is free before a forward (layer 0 reads no delta).
+double HipEngineImpl::exchangeMs(int n) {
+    if (plan_.nRanks <= 1) return 0;
+    auto it = exchangeMs_.find(n);
+    if (it != exchangeMs_.end()) return it->second;
+    const size_t count = (size_t)n * h_.dim;
+    allReduce(dY_, count);  // warm
+    hipEvent_t e0, e1;
+    DL_HIP(hipEventCreate(&e0));
+    DL_HIP(hipEventCreate(&e1));
+    DL_HIP(hipEventRecord(e0, stream_));
+    for (int i = 0; i < 8; i++) allReduce(dY_, count);
+    DL_HIP(hipEventRecord(e1, stream_));
+    DL_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    DL_HIP(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return exchangeMs_[n] = ms / 8.0;
 }
 
 void HipEngineImpl::runGraph(int n, GraphKind kind) {

@@ -98,6 +98,7 @@ class HipEngineImpl : public HipEngine {
     int rank() const { return comm_ ? comm_->rank() : 0; }
     void runGraph(int n, GraphKind kind);
     void accountForward(int n, GraphKind kind, int times);
+    double exchangeMs(int n);
     hipGraphExec_t captureForward(int n, GraphKind kind);
     template <typename T>
     T *dalloc(size_t count) {
@@ -247,6 +248,7 @@ class HipEngineImpl : public HipEngine {
     int *dAttCnt_ = nullptr, *dArgCnt_ = nullptr, *dArgI_ = nullptr;
     float *dArgV_ = nullptr;
     hipk::SampleScratch sampleScratch_;
+    std::map<int, double> exchangeMs_;  // calibrated all-reduce ms per row count (exchangeMs)
 
     // attention: context buckets (setupBuckets) and this forward's choices (setInputs, graph key)
     std::vector<CtxBucket> buckets_;

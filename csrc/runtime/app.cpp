@@ -316,26 +316,23 @@ void InferenceSession::collectIds(int n, int *out) {
 void InferenceSession::recordMetrics(const char *kind, int n, double ms) {
     MetricsSink &m = MetricsSink::global();
     if (!m.enabled()) return;
-    unsigned long long sent = 0, recv = 0;
+    unsigned long long sent = 0, recv = 0;  // cumulative socket bytes (control plane; CPU data plane)
     for (auto &w : workers_) {
         sent += w.totalSentBytes();
         recv += w.totalRecvBytes();
     }
     const ForwardStats st = backend_->lastStats();
-    if (gpu_) {  // device data plane of this forward (the CPU data plane is the sockets above)
-        sent += st.sentBytes;
-        recv += st.recvBytes;
-        mSent_ += st.sentBytes;
-        mRecv_ += st.recvBytes;
-    }
+    // this forward: the sockets' bytes since the previous record, plus (GPUs) the device data plane
+    // the engine counted for this forward alone (the CPU data plane is the sockets above)
+    const unsigned long long fs = sent - mSent_ + (gpu_ ? st.sentBytes : 0);
+    const unsigned long long fr = recv - mRecv_ + (gpu_ ? st.recvBytes : 0);
+    mSent_ = sent;
+    mRecv_ = recv;
     char buf[512];
     std::snprintf(buf, sizeof(buf),
                   "{\"ts_ms\":%.3f,\"event\":\"%s\",\"rows\":%d,\"ms\":%.4f,\"compute_ms\":%.4f,\"sync_ms\":%.4f,"
                   "\"sent_bytes\":%llu,\"recv_bytes\":%llu,\"nodes\":%d,\"backend\":\"%s\"}",
-                  epochMs(), kind, n, ms, st.computeMs, st.syncMs, sent - mSent_, recv - mRecv_, nNodes(),
-                  gpu_ ? "hip" : "cpu");
-    mSent_ = sent;
-    mRecv_ = recv;
+                  epochMs(), kind, n, ms, st.computeMs, st.syncMs, fs, fr, nNodes(), gpu_ ? "hip" : "cpu");
     m.write(buf);
 }
 

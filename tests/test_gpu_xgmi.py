@@ -358,7 +358,8 @@ def test_data_plane_bytes_reported(tmp_path):
     """`dllama inference` at TP2 over xGMI (same GPU) with the reference's Q80 sync: the Sent / Recv
     of every decode forward in --metrics is the device data plane (formula above: 2 x layers x
     dim/32 x 34 B + the argmax winner) plus a few bytes of TCP control packets; the formula gives
-    SURVEY §2.6's 272 KiB per token for Llama-3.1-8B at TP2."""
+    SURVEY §2.6's 272 KiB per token for Llama-3.1-8B at TP2. Sync ms is the engine's estimate
+    (calibrated all-reduce cost x the forward's exchanges)."""
     import json
     import subprocess
     import time
@@ -392,6 +393,7 @@ def test_data_plane_bytes_reported(tmp_path):
     for x in dec:
         assert expect <= x["sent_bytes"] <= expect + 256, (x, expect)
         assert expect <= x["recv_bytes"] <= expect + 256, (x, expect)
+        assert 0 < x["sync_ms"] < x["ms"], x  # calibrated exchange cost x exchanges per forward
     # the Pred lines print the same (kB)
     kb = [int(l.split("Sent")[1].split("kB")[0]) for l in out.splitlines() if l.startswith("🔶 Pred")]
     assert kb and all(k == expect // 1024 for k in kb), (kb, expect)
