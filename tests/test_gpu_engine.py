@@ -107,15 +107,16 @@ def test_engine_medium_matches_cpu(C, medium):
     assert _rel(_seq(gpu, tokens), _seq(cpu, tokens)) < 3e-2
 
 
-@pytest.mark.parametrize("graphs", [True, False])
-def test_engine_batched_prefill_gemv_chunks(C, assets, graphs, monkeypatch):
-    """GEMV batch path (chunks 4+2+1 of the same int8 kernels) == 7 sequential decodes."""
+@pytest.mark.parametrize("graphs,n", [(True, 7), (False, 7), (True, 8), (False, 13)])
+def test_engine_batched_prefill_gemv_chunks(C, assets, graphs, n, monkeypatch):
+    """GEMV batch path (chunks of 4 / 2 / 1 rows of the same int8 ring kernel: 7 = 4+2+1, 8 = 4+4,
+    13 = 4+4+4+1) == n sequential decodes."""
     monkeypatch.setenv("DL_GEMM_MIN", "1000")
-    a = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=8, use_graphs=graphs)
-    b = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=8, use_graphs=graphs)
-    tokens = [9, 8, 7, 6, 5, 4, 3]
+    a = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=16, use_graphs=graphs)
+    b = C.HipEngine(assets["q40"], "q80", kv_bf16=False, max_batch=16, use_graphs=graphs)
+    tokens = [9, 8, 7, 6, 5, 4, 3, 11, 12, 13, 14, 15, 16][:n]
     seq = _seq(a, tokens)
-    bat = b.forward(tokens, list(range(7)), [0] * 7)
+    bat = b.forward(tokens, list(range(n)), [0] * n)
     assert _rel(bat, seq) < 1e-4
     _assert_replays_equal(b, tokens, bat)
 
