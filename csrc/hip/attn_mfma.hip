@@ -56,6 +56,8 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
     if (c >= nSplit) return;
     const int t0 = c * ch, t1 = min(t0 + ch, len);
     const int nTiles = (t1 - t0 + kAmTile - 1) / kAmTile;
+    // stamps stay in SGPRs until the end (a store would join the vmcnt accounting of the DMA)
+    unsigned long long tr[6] = {a.trace ? wall_clock64() : 0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
 
     // this lane's column: query head g * KM + col (columns >= KM are zero and discarded); the q
     // loads are issued first, then the K / V DMA of the first two tiles, and only then are the q
@@ -113,6 +115,7 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
 #pragma unroll
         for (int j = 0; j < 8; j++) qf[s][j] = (__bf16)v[j];
     }
+    if (a.trace) tr[1] = wall_clock64();
     for (int k = 0; k < nRounds; k++) {
         const int i = k * kAmWaves + wave;
         if (i + kAmWaves < nTiles)
@@ -120,6 +123,7 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
+        if (a.trace && k == 0) tr[2] = wall_clock64();
         if (i >= nTiles) continue;  // wave-uniform; the barrier above is reached by every wave
         const char *kb = wbuf + (k & 1) * 2 * kAmTileBytes, *vb = kb + kAmTileBytes;
         const int tb = t0 + kAmTile * i;
@@ -207,6 +211,7 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
     }
     lsum += __shfl_xor(lsum, 16);
     lsum += __shfl_xor(lsum, 32);
+    if (a.trace) tr[3] = wall_clock64();
 #ifdef DL_AM_DEBUG
     if (g == 0 && c == 0 && b == 0 && wave == 0) {
         for (int n = 0; n < NT; n++)
@@ -255,7 +260,14 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
         }
     }
     __syncthreads();
-    attnFinish<KM, HS, kAmThreads>(a, b, g, c, nSplit, redL, mlL, flagL, scratch);
+    if (a.trace) tr[4] = wall_clock64();
+    const bool fin = attnFinish<KM, HS, kAmThreads>(a, b, g, c, nSplit, redL, mlL, flagL, scratch);
+    if (a.trace && tid == 0) {
+        tr[5] = wall_clock64();
+        unsigned long long *t = a.trace + 8 * (((size_t)b * gridDim.y + c) * gridDim.x + g);
+        for (int i = 0; i < 6; i++) t[i] = tr[i];
+        t[6] = fin ? 1ull : 0ull;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------

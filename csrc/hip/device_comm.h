@@ -39,6 +39,8 @@ class DeviceComm {
     virtual std::string asyncError() { return ""; }
     // Release the communicator without waiting for peers (used after an error).
     virtual void shutdownNow() {}
+    // Clear the device error flag (after a self-test whose failure was handled).
+    virtual void resetError() {}
     // Ranks of this communicator that run on this rank's GPU (1 on a real multi-GPU node; all of
     // them in a same-GPU rehearsal): they share the device's resident workgroup slots.
     virtual int ranksOnDevice() const { return 1; }

@@ -171,6 +171,7 @@ double HipEngineImpl::decodeGreedyBatch(int steps, int nSeq, const int *tokens, 
                                         int *outTokens) {
     DL_CHECK(nSeq >= 1 && (u32)nSeq <= cfg_.maxBatch, "nSeq");
     for (int b = 0; b < nSeq; b++) DL_CHECK((u32)(pos[b] + steps) <= h_.seqLen, "decode exceeds seqLen");
+    if (!tpTested_) tpFusedSelfTest();
     exchangeMs(nSeq);  // calibrated outside the timed chain
     setInputs(nSeq, tokens, pos, slots, nullptr, steps - 1);
     DL_HIP(hipMemsetAsync(dHist_, 0xff, sizeof(int) * (size_t)cfg_.maxBatch * h_.seqLen, stream_));
@@ -306,7 +307,55 @@ double HipEngineImpl::exchangeMs(int n) {
     return exchangeMs_[n] = ms / 8.0;
 }
 
+// The first forward of a tensor-parallel engine with the fused exchange runs its self-test on the
+// real devices (every rank reaches this point in the same forward: the ranks run forwards in
+// lockstep). Pass: rank-order sums of known element-dependent values through both exchange
+// regions, no peer timed out, and every rank's verdict exchanged over region 0 sums to the world
+// size. Anything else switches the fused exchange off on every rank (the verdict sum is the same
+// everywhere), which then runs the separate collectives of the same comm (xGMI all-reduce, itself
+// self-tested at start-up, or RCCL). DL_TP_FUSED=fail makes rank 1 report a failure (tests).
+void HipEngineImpl::tpFusedSelfTest() {
+    tpTested_ = true;
+    if (!tpFused_) return;
+    const int W = plan_.nRanks, me = rank();
+    const char *e = std::getenv("DL_TP_FUSED");
+    bool ok = !(e && std::strcmp(e, "fail") == 0 && me == 1);
+    const int *errFlag = comm_->deviceErrorFlag();
+    auto timedOut = [&]() {
+        if (!errFlag) return false;
+        int v = 0;
+        DL_HIP(hipMemcpy(&v, errFlag, sizeof(int), hipMemcpyDeviceToHost));
+        return v != 0;
+    };
+    std::vector<float> got;
+    for (const hipk::TpXchg *x : {&tpVec_, &tpArg_}) {
+        const int n = (int)std::min<long long>(4096, x->stride);
+        hipk::launchTpSelfTest(*x, dY_, n, (float)(me + 1), stream_);
+        DL_HIP(hipStreamSynchronize(stream_));
+        got.resize(n);
+        DL_HIP(hipMemcpy(got.data(), dY_, n * sizeof(float), hipMemcpyDeviceToHost));
+        for (int el = 0; el < n && ok; el++)
+            ok = got[el] == (float)(W * (W + 1) / 2) + (float)(W * (el & 1023));
+    }
+    if (timedOut()) ok = false;
+    comm_->resetError();
+    hipk::launchTpSelfTest(tpVec_, dY_, 1, ok ? 1.f : 0.f, stream_);  // the verdicts (+ element 0's 0)
+    DL_HIP(hipStreamSynchronize(stream_));
+    float all = 0.f;
+    DL_HIP(hipMemcpy(&all, dY_, sizeof(float), hipMemcpyDeviceToHost));
+    const bool allOk = !timedOut() && all == (float)W;
+    comm_->resetError();
+    if (allOk) return;
+    std::fprintf(stderr, "⚠️  rank %d: fused tensor-parallel exchange self-test failed (%s); using the separate "
+                 "%s collectives\n", me, ok ? "on a peer" : "here", comm_->name().c_str());
+    tpFused_ = false;
+    blockOn_ = false;  // the attention block's wo role was chosen for the fused exchange: decide again
+    for (CtxBucket &b : buckets_) b.block = false;
+    setupAttnBlock();
+}
+
 void HipEngineImpl::runGraph(int n, GraphKind kind) {
+    if (!tpTested_) tpFusedSelfTest();
     accountForward(n, kind, 1);
     if (!cfg_.useGraphs || graphsBroken_) {
         enqueueForward(n, kind);

@@ -59,7 +59,8 @@ double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int pas
 double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters);
 // Micro-benchmark of the decode attention kernel (bf16 KV, Q80 output): `copies` KV caches cycled
 // through a graph of `iters` launches, every row at position `pos`. Returns microseconds per launch.
-double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B, int copies, int iters);
+double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B, int copies, int iters,
+                      std::vector<unsigned long long> *trace = nullptr);
 
 }  // namespace dl
 

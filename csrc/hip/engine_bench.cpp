@@ -191,7 +191,8 @@ double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters) {
     return ms * 1000.0 / iters;
 }
 
-double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B, int copies, int iters) {
+double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B, int copies, int iters,
+                      std::vector<unsigned long long> *trace) {
     hipStream_t s;
     DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     std::vector<void *> mem;
@@ -263,6 +264,14 @@ double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B
     DL_HIP(hipEventSynchronize(e1));
     float ms = 0;
     DL_HIP(hipEventElapsedTime(&ms, e0, e1));
+    if (trace) {  // one more (eager) launch with per-workgroup stamps (MFMA decode kernel)
+        const size_t words = 8 * (size_t)(nHeads0 / kvMul) * a.splitGrid * B;
+        a.trace = (unsigned long long *)alloc(words * 8);
+        launch(iters);
+        DL_HIP(hipStreamSynchronize(s));
+        trace->resize(words);
+        DL_HIP(hipMemcpy(trace->data(), a.trace, words * 8, hipMemcpyDeviceToHost));
+    }
     (void)hipGraphExecDestroy(ge);
     (void)hipGraphDestroy(g);
     (void)hipEventDestroy(e0);

@@ -99,6 +99,7 @@ class HipEngineImpl : public HipEngine {
     void runGraph(int n, GraphKind kind);
     void accountForward(int n, GraphKind kind, int times);
     double exchangeMs(int n);
+    void tpFusedSelfTest();
     hipGraphExec_t captureForward(int n, GraphKind kind);
     template <typename T>
     T *dalloc(size_t count) {
@@ -208,6 +209,7 @@ class HipEngineImpl : public HipEngine {
     ModelHeader h_;
     ShardPlan plan_;
     bool q40_ = true, kvBf16_ = true, syncQ80_ = false, tpFused_ = false;
+    bool tpTested_ = false;  // tpFusedSelfTest ran (first forward)
     int fusedGridMax_ = 0;  // largest grid of a fused-exchange GEMV launch (checked co-resident)
     hipk::TpXchg tpVec_, tpArg_;
     int gemmMin_ = 3;          // DL_GEMM_MIN: rows per forward from which the batched MFMA path runs

@@ -87,6 +87,11 @@ struct AttnArgs {
     int kvBf16 = 1;
     int mfma = -1;              // decode kernel: 1 MFMA, 0 VALU, -1 by cache length (attnUsesMfma)
     int *counters = nullptr;    // [B][nHeads0/HG] arrival counters (zero-initialised, self-resetting)
+    // diagnostics (MFMA decode kernel): 8 u64 s_memrealtime stamps per workgroup, index
+    // (b * splitGrid + chunk) * headGroups + group: [0] entry, [1] DMA issued, [2] first tile
+    // landed, [3] key loop done, [4] waves merged, [5] split hand-off / combine done, [6] 1 if
+    // this workgroup combined the chunks (wave 0's view)
+    unsigned long long *trace = nullptr;
 };
 
 // Tensor-parallel partial-sum exchange fused into the tail of the kernel that produces the partial
@@ -290,6 +295,10 @@ AttnBlockPlan attnBlockPlan(const AttnBlockArgs &a, bool tp);
 void attnBlockExpect(const GemvArgs &qkv, int nKv, unsigned *out);
 GemvResidency attnBlockResidency(const AttnBlockArgs &a, bool tp);
 void launchAttnBlock(const AttnBlockArgs &a, bool tp, hipStream_t s);
+
+// Fused-exchange self-test (tp_check.hip): out[el] = sum over ranks of (val_rank + el % 1024) for
+// el < n (n <= x.stride), through the transport of the fused exchange; every rank must call it.
+void launchTpSelfTest(const TpXchg &x, float *out, int n, float val, hipStream_t s);
 
 // Prefill rows on MFMA (bf16 caches): blocks of attnPrefillRowsPerBlock(kvMul) consecutive rows
 // must share one slot (positions arbitrary, causal per row); counters >= blocks x KV heads.

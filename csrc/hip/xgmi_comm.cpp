@@ -350,7 +350,7 @@ class XgmiComm : public DeviceComm {
     // The LL protocol can be switched off (e.g. when its pre-flight test fails on a platform);
     // resetError clears a timed-out flag so the other protocol can be tested.
     void setLowLatency(bool on) { ll_ = on; }
-    void resetError() {
+    void resetError() override {
         DL_HIP(hipMemset(error_, 0, sizeof(int)));
         DL_HIP(hipDeviceSynchronize());
     }

@@ -592,9 +592,25 @@ PYBIND11_MODULE(_C, m) {
           "bench_gemv_q40 with per-workgroup s_memrealtime stamps: (us, u64[iters*grid*4])");
     m.def("bench_gemm_q40", &benchGemmQ40, py::arg("rows"), py::arg("n"), py::arg("tokens"), py::arg("epi") = 0,
           py::arg("copies") = 8, py::arg("iters") = 100, py::call_guard<py::gil_scoped_release>());
-    m.def("bench_attention", &benchAttention, py::arg("n_heads0"), py::arg("kv_mul"), py::arg("head_size"),
-          py::arg("seq_len"), py::arg("pos"), py::arg("batch") = 1, py::arg("copies") = 32, py::arg("iters") = 200,
-          py::call_guard<py::gil_scoped_release>());
+    m.def("bench_attention",
+          [](int nh, int kvm, int hs, int seq, int pos, int B, int copies, int iters) {
+              return benchAttention(nh, kvm, hs, seq, pos, B, copies, iters);
+          },
+          py::arg("n_heads0"), py::arg("kv_mul"), py::arg("head_size"), py::arg("seq_len"), py::arg("pos"),
+          py::arg("batch") = 1, py::arg("copies") = 32, py::arg("iters") = 200, py::call_guard<py::gil_scoped_release>());
+    m.def("trace_attention",
+          [](int nh, int kvm, int hs, int seq, int pos, int B, int copies, int iters) {
+              std::vector<unsigned long long> t;
+              double us;
+              {
+                  py::gil_scoped_release rel;
+                  us = benchAttention(nh, kvm, hs, seq, pos, B, copies, iters, &t);
+              }
+              return py::make_tuple(us, t);
+          },
+          py::arg("n_heads0"), py::arg("kv_mul"), py::arg("head_size"), py::arg("seq_len"), py::arg("pos"),
+          py::arg("batch") = 1, py::arg("copies") = 32, py::arg("iters") = 50,
+          "bench_attention, then one launch with per-workgroup stamps (kernels.h AttnArgs::trace): (us, u64[])");
 
     m.def("simulate_tp",
           [](const std::string &model, const std::string &bufferType, int world, std::vector<int> tokens, bool kvBf16,

@@ -4,7 +4,7 @@ Q80 output) inside a hipGraph of back-to-back launches, for the Llama-3.1-8B hea
 tensor-parallel degree (heads and KV heads per rank shrink with TP).
 
     python scripts/bench_attn.py                # default sweep
-    DL_ATTN_HG=1 python scripts/bench_attn.py   # force query heads per workgroup
+    DL_ATTN_MFMA=0 python scripts/bench_attn.py # the VALU kernel at every length
 """
 import os
 import sys
@@ -17,7 +17,7 @@ def main():
     C = dl.native()
     copies = 32  # one KV cache per layer: a decode step revisits a layer's KV only every token
     iters = 200
-    print(f"attention µs/launch (graph of {iters}, {copies} KV copies), env DL_ATTN_HG={os.environ.get('DL_ATTN_HG', '')}")
+    print(f"attention µs/launch (graph of {iters}, {copies} KV copies), env DL_ATTN_MFMA={os.environ.get('DL_ATTN_MFMA', '')}")
     for tp in (1, 2, 4, 8):
         nh, kvm = 32 // tp, 4
         for seq, pos in ((256, 150), (2048, 1500), (8192, 8000)):

@@ -497,3 +497,23 @@ def test_api_on_gpu_concurrent_equals_solo(tmp_path, pages):
     finally:
         api.kill()
         api.wait()
+
+
+def test_fused_exchange_self_test_fallback(C, tmp_path):
+    """The fused exchange is trusted only after its first-forward self-test on the real devices
+    (known values through both exchange regions, verdicts exchanged so every rank agrees). A failed
+    self-test - forced on rank 1 with DL_TP_FUSED=fail - switches it off on EVERY rank, which then
+    run the separate all-reduces with the same results as a normal run whose fused path is also off
+    for the batched rows (DL_TP_BATCHED=0): bitwise equal logits and ids, same greedy decode."""
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=12, dim=512, n_heads=8,
+                               n_kv_heads=4, hidden_dim=1024, vocab_size=1024)
+    tokens = [int(t) for t in np.random.default_rng(6).integers(0, 1024, 96)]
+    a = _run(_engine_tp_batched, 2, m, tokens, kwargs=dict(env={"DL_TP_FUSED": "fail", "DL_TP_BATCHED": "0"}))
+    b = _run(_engine_tp_batched, 2, m, tokens, kwargs=dict(env={"DL_TP_FUSED": "0", "DL_TP_BATCHED": "0"}))
+    c = _run(_engine_tp_batched, 2, m, tokens, kwargs=dict(env={"DL_TP_BATCHED": "0"}))
+    assert all(isinstance(v, tuple) for v in list(a.values()) + list(b.values()) + list(c.values())), (a, b, c)
+    assert a[0][2] is False and a[1][2] is False and c[0][2] is True and c[1][2] is True
+    assert np.array_equal(a[0][0], b[0][0]) and a[0][1] == b[0][1] and a[0][3] == b[0][3]
+    assert a[0][1] == c[0][1] and a[0][3][:4] == c[0][3][:4]
