@@ -32,5 +32,7 @@ void launchTpSelfTest(const TpXchg &x, float *out, int n, float val, hipStream_t
     DL_HIP(hipGetLastError());
 }
 
+const void *tpCheckModuleKernel() { return (const void *)tpSelfTestKernel; }
+
 }  // namespace hipk
 }  // namespace dl
