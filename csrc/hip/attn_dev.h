@@ -92,14 +92,14 @@ static constexpr int kAttnThreads = 512;  // 8 waves = 32 groups of 16 lanes, on
 
 // Split epilogue of the attention kernel: redL [HG][HS] holds the unnormalised output of this
 // workgroup's chunk, mlL [HG][2] its (max, sum). One chunk: normalise and write. Several: publish
-// the partial and count arrivals; the last workgroup combines all chunks. The combine stages every
-// chunk's (max, sum) in LDS (`scratch`, >= 2 * HG * splitGrid floats) with one load per thread and
-// keeps 8 partial-output loads in flight per thread: a serial loop over the chunks costs one
-// cross-XCD round trip per chunk (~30 us at 32 chunks).
+// the partial and count arrivals; the last workgroup combines all chunks, with 8 chunks' partial
+// outputs and (max, sum) pairs in flight per thread (a serial loop over the chunks costs one
+// cross-XCD round trip per chunk: ~30 us at 32 chunks). `scratch` is not used (kept for callers).
 template <int HG, int HS, int AT, bool WT = false>
 __device__ __forceinline__ bool attnFinish(const AttnArgs &a, int b, int hgIdx, int c, int nSplit, float *redL,
                                            float *mlL, int *flagL, float *scratch) {
     const int tid = threadIdx.x, head0 = hgIdx * HG;
+    (void)scratch;
     if (nSplit == 1) {
         for (int i = tid; i < HG * HS; i += AT) redL[i] = redL[i] / mlL[(i / HS) * 2 + 1];
         __syncthreads();
@@ -112,7 +112,6 @@ __device__ __forceinline__ bool attnFinish(const AttnArgs &a, int b, int hgIdx, 
     // accesses (sc1, performed at the coherence point), vmcnt(0) before the arrival count; an
     // agent-scope fence would write back / invalidate this XCD's whole L2
     auto st = [](float *q, float v) { __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    auto ld = [](const float *q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     for (int i = tid; i < HG * HS; i += AT) {
         const int h = i / HS, d = i % HS;
         st(a.partO + ((pbase + (size_t)h * G) + c) * HS + d, redL[i]);
@@ -131,58 +130,58 @@ __device__ __forceinline__ bool attnFinish(const AttnArgs &a, int b, int hgIdx, 
     __syncthreads();
     if (!flagL[0]) return false;
     if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // every chunk's (max, sum) -> LDS, then per head: global max and chunk weights w = exp(m - M)
-    for (int i = tid; i < HG * nSplit; i += AT) {
-        const int h = i / nSplit, cc = i % nSplit;
-        const float *ml = a.partML + ((pbase + (size_t)h * G) + cc) * 2;
-        scratch[2 * (h * G + cc)] = ld(ml);
-        scratch[2 * (h * G + cc) + 1] = ld(ml + 1);
-    }
-    __syncthreads();
-    if (tid < HG) {
-        float M = -INFINITY;
-        for (int cc = 0; cc < nSplit; cc++) M = fmaxf(M, scratch[2 * (tid * G + cc)]);
-        float Ls = 0.f;
-        for (int cc = 0; cc < nSplit; cc++) {
-            float *ml = scratch + 2 * (tid * G + cc);
-            const float w = M == -INFINITY ? 0.f : __expf(ml[0] - M);
-            ml[0] = w;
-            Ls += w * ml[1];
-        }
-        mlL[tid * 2 + 1] = Ls;
-    }
-    __syncthreads();
-    // Weighted sum of the chunks' partial outputs: (item = 4 dims of one head) x (part = a strided
-    // subset of the chunks) per thread, the `parts` threads of an item adjacent lanes, every load
-    // of a thread (16-B coherence-point loads, sc1 like the atomic loads above) in flight at once,
-    // then a fixed butterfly over the parts (deterministic). One memory round trip for <= 8 chunks
-    // per thread instead of one per 8 chunks of a head dimension (long contexts: 32 chunks).
+    // Weighted sum of the chunks' partial outputs in ONE memory round trip: (item = 4 dims of one
+    // head) x (part = a strided subset of the chunks) per thread, the `parts` threads of an item
+    // adjacent lanes. Every thread loads its chunks' partial outputs AND their (max, sum) pairs at
+    // once (16-B / 8-B coherence-point loads, sc1 like the atomic accesses above), folds them with an
+    // online softmax rescale in chunk order, then a fixed butterfly merges the parts: deterministic,
+    // and every item of a head derives the same denominator from the same chunks in the same order.
+    // (A separate (max, sum) pass with a serial per-head weight loop cost an extra round trip and
+    // ~7 us per long-context combine: trace_attention.py.)
     constexpr int U = 8, ITEMS = HG * (HS / 4), PARTS = ITEMS >= AT ? 1 : AT / ITEMS;
     for (int base = 0; base < ITEMS * PARTS; base += AT) {
         const int t = base + tid, item = t / PARTS, part = t % PARTS;
         const int h = min(item, ITEMS - 1) / (HS / 4), d = (min(item, ITEMS - 1) % (HS / 4)) * 4;
         const float *po = a.partO + (pbase + (size_t)h * G) * HS + d;
-        const float *wv = scratch + 2 * h * G;
+        const float *pml = a.partML + (pbase + (size_t)h * G) * 2;
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        float M = -INFINITY, Ls = 0.f;
         for (int c0 = part; c0 < nSplit; c0 += U * PARTS) {
             f32x4 v[U];
+            u32x2 ml[U];
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 const int cc = min(c0 + u * PARTS, nSplit - 1);
                 asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v[u]) : "v"(po + (size_t)cc * HS));
+                asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(ml[u]) : "v"(pml + (size_t)cc * 2));
             }
 #pragma unroll
-            for (int u = 0; u < U; u++) {  // each wait pins its own load's registers (no early use)
-                asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v[u]) : "i"(U - 1 - u) : "memory");
-                if (c0 + u * PARTS < nSplit) acc += wv[2 * (c0 + u * PARTS)] * v[u];
+            for (int u = 0; u < U; u++) {  // each wait pins its own loads' registers (no early use)
+                asm volatile("s_waitcnt vmcnt(%2)" : "+v"(v[u]), "+v"(ml[u]) : "i"(2 * (U - 1 - u)) : "memory");
+                if (c0 + u * PARTS < nSplit) {
+                    const float mc = __uint_as_float(ml[u].x), lc = __uint_as_float(ml[u].y);
+                    const float Mn = fmaxf(M, mc);
+                    const float so = M == -INFINITY ? 0.f : __expf(M - Mn), w = mc == -INFINITY ? 0.f : __expf(mc - Mn);
+                    acc = acc * so + w * v[u];
+                    Ls = Ls * so + w * lc;
+                    M = Mn;
+                }
             }
         }
 #pragma unroll
-        for (int off = 1; off < PARTS; off <<= 1)
+        for (int off = 1; off < PARTS; off <<= 1) {
+            const float M2 = __shfl_xor(M, off), L2 = __shfl_xor(Ls, off);
+            f32x4 a2;
 #pragma unroll
-            for (int j = 0; j < 4; j++) acc[j] += __shfl_xor(acc[j], off);
+            for (int j = 0; j < 4; j++) a2[j] = __shfl_xor(acc[j], off);
+            const float Mn = fmaxf(M, M2);
+            const float s1 = M == -INFINITY ? 0.f : __expf(M - Mn), s2 = M2 == -INFINITY ? 0.f : __expf(M2 - Mn);
+            acc = acc * s1 + a2 * s2;
+            Ls = Ls * s1 + L2 * s2;
+            M = Mn;
+        }
         if (part == 0 && item < ITEMS) {
-            const float il = 1.0f / mlL[h * 2 + 1];
+            const float il = 1.0f / Ls;
 #pragma unroll
             for (int j = 0; j < 4; j++) redL[h * HS + d + j] = acc[j] * il;
         }

@@ -414,6 +414,25 @@ def test_engine_8b_shape_matches_cpu(C, tmp_path):
     assert _rel(_seq(gpu, toks), _seq(cpu, toks)) < 3e-2
 
 
+@pytest.mark.parametrize("shape", ["70b", "405b"])
+def test_engine_big_model_shapes_match_cpu(C, tmp_path, shape):
+    """BASELINE configs #4 / #5 layer shapes, one layer, 1024-token vocabulary, decode rows against
+    the CPU reference backend: Llama-3.3-70B (dim 8192, 64 heads over 8 KV heads: kvMul 8, hidden
+    28672) and Llama-3.1-405B attention (dim 16384, 128 heads over 8 KV heads: kvMul 16; hidden cut
+    to 16384 to keep the synthetic file small). Checks the tilings, the attention block's
+    workgroup plan at these widths and the kvMul 8 / 16 attention."""
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    dims = {"70b": dict(dim=8192, hidden_dim=28672, n_heads=64, n_kv_heads=8),
+            "405b": dict(dim=16384, hidden_dim=16384, n_heads=128, n_kv_heads=8)}[shape]
+    m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=64, seed=21, n_layers=1,
+                               vocab_size=1024, **dims)
+    gpu = C.HipEngine(m, "q80", kv_bf16=False, max_batch=8)
+    cpu = C.cpu_backend(m, "q80", 16)
+    toks = [1, 2, 3, 500]
+    assert _rel(_seq(gpu, toks), _seq(cpu, toks)) < 3e-2
+
+
 @pytest.mark.parametrize("kv_bf16,page", [(True, 32), (False, 64)])
 def test_paged_kv_cache_matches_contiguous(C, medium, kv_bf16, page):
     """Paged KV cache (page table per slot over a shared pool): the same forwards as the contiguous
