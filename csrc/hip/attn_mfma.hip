@@ -75,6 +75,26 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
     const uint16_t *kc = reinterpret_cast<const uint16_t *>(a.kcache);
     const uint16_t *vc = reinterpret_cast<const uint16_t *>(a.vcache);
     const size_t kvBase = (size_t)g * HS;
+    // Paged cache: the chunk's page ids are loaded once, one per lane, before any DMA, and each
+    // key's row comes from a lane shuffle. (A table load per key row made the compiler wait for
+    // vmcnt(0) - every DMA already in flight - before each of the 16 wave-instructions of a tile.)
+    const KvMap &km = a.kvMap;
+    const int pg0 = km.table ? t0 >> km.pageShift : 0;
+    const bool pgLanes = km.table && ((t1 - 1) >> km.pageShift) - pg0 < 64;
+    int pgReg = 0;
+    if (pgLanes) {
+        // retired here, before any DMA: the waitcnt pass cannot track this load into the issue
+        // loop's branches and would otherwise wait for vmcnt(0) at every shuffle
+        int v = km.table[sl * km.pagesPerSlot + pg0 + min(lane, ((t1 - 1) >> km.pageShift) - pg0)];
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(v));
+        pgReg = v;
+    }
+    auto rowOf = [&](int key) -> size_t {
+        if (!km.table) return (size_t)sl * a.seqLen + key;
+        if (!pgLanes) return kvRow(km, a.seqLen, sl, key);
+        const int pg = __shfl(pgReg, (key >> km.pageShift) - pg0);
+        return ((size_t)pg << km.pageShift) + (size_t)(key & ((1 << km.pageShift) - 1));
+    };
     // DMA of tile i (keys t0 + 32 i ...) into buffer bf: 8 + 8 wave-instructions of 4 rows x 256 B
     auto issue = [&](int i, int bf) {
         char *kb = wbuf + bf * 2 * kAmTileBytes, *vb = kb + kAmTileBytes;
@@ -82,7 +102,7 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
         for (int j = 0; j < kAmTile / 4; j++) {
             const int r = 4 * j + (lane >> 4), p = lane & 15;
             const int key = min(t0 + kAmTile * i + r, t1 - 1);  // past the chunk: masked below
-            const size_t off = kvBase + kvRow(a.kvMap, a.seqLen, sl, key) * a.kv0 + (size_t)(p ^ amSwz(r)) * 8;
+            const size_t off = kvBase + rowOf(key) * a.kv0 + (size_t)(p ^ amSwz(r)) * 8;
             __builtin_amdgcn_global_load_lds(const_cast<uint16_t *>(kc + off),
                                              reinterpret_cast<__attribute__((address_space(3))) void *>(
                                                  reinterpret_cast<uintptr_t>(kb + j * 1024)), 16, 0, 0);

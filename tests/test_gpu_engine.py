@@ -465,6 +465,28 @@ def test_paged_kv_cache_matches_contiguous(C, medium, kv_bf16, page):
     both([seq[64]], [64], [0])
 
 
+def test_paged_kv_long_context_mfma_attention(C, tmp_path):
+    """Paged KV at long context: decode rows at positions ~1500 of a 2048-position cache run the
+    MFMA decode attention (bf16 cache >= 1024 positions), whose chunk page ids are looked up once
+    per workgroup and shuffled to the key rows: bitwise the contiguous cache's logits, pages of 64
+    and 128 positions."""
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=2048, seed=17, dim=1024,
+                               hidden_dim=2816, n_heads=8, n_kv_heads=2, n_layers=2, vocab_size=1024)
+    seq = [int(t) for t in np.random.default_rng(8).integers(0, 1024, 1504)]
+    ref = C.HipEngine(m, "q80", kv_bf16=True, max_batch=256, n_slots=1)
+    for page in (64, 128):
+        pg = C.HipEngine(m, "q80", kv_bf16=True, max_batch=256, n_slots=1, kv_pages=2048 // page,
+                         kv_page_size=page)
+        for e in (ref, pg):
+            for s0 in range(0, 1500, 250):
+                e.forward_argmax(seq[s0:s0 + 250], list(range(s0, s0 + 250)), [0] * 250)
+        for p in range(1500, 1504):
+            a, b = ref.forward([seq[p]], [p], [0]), pg.forward([seq[p]], [p], [0])
+            assert np.array_equal(a, b), (page, p)
+
+
 def test_paged_kv_pool_exhaustion_raises(C, medium):
     """A forward that needs more pages than the pool has left fails with a clear error instead of
     writing through an unmapped page."""
