@@ -6,6 +6,7 @@
 namespace dl {
 namespace hipk {
 
+const void *attnBlockFn_16_16_128(int hg, bool bf16, int md);
 const void *attnBlockFn_16_32_128(int hg, bool bf16, int md);
 const void *attnBlockFn_32_32_128(int hg, bool bf16, int md);
 const void *attnBlockFn_64_32_128(int hg, bool bf16, int md);
@@ -15,6 +16,7 @@ const void *attnBlockFn_32_64_128(int hg, bool bf16, int md);
 const void *attnBlockFn_64_64_64(int hg, bool bf16, int md);
 
 static const void *attnBlockFn(int lq, int lw, int hs, int hg, bool bf16, int md) {
+    if (lq == 16 && lw == 16 && hs == 128) return attnBlockFn_16_16_128(hg, bf16, md);
     if (lq == 16 && lw == 32 && hs == 128) return attnBlockFn_16_32_128(hg, bf16, md);
     if (lq == 32 && lw == 32 && hs == 128) return attnBlockFn_32_32_128(hg, bf16, md);
     if (lq == 64 && lw == 32 && hs == 128) return attnBlockFn_64_32_128(hg, bf16, md);

@@ -331,6 +331,7 @@ const void *tpCheckModuleKernel();
 const void *gemvFnL16(bool q40, int B, int pro, int epi);
 const void *gemvFnL32(bool q40, int B, int pro, int epi);
 const void *gemvFnL64(bool q40, int B, int pro, int epi);
+const void *attnBlockFn_16_16_128(int hg, bool bf16, int md);
 const void *attnBlockFn_16_32_128(int hg, bool bf16, int md);
 const void *attnBlockFn_32_32_128(int hg, bool bf16, int md);
 const void *attnBlockFn_64_32_128(int hg, bool bf16, int md);
@@ -341,7 +342,7 @@ const void *attnBlockFn_64_64_64(int hg, bool bf16, int md);
 
 void preloadModules() {
     typedef const void *(*BlockFn)(int, bool, int);
-    const BlockFn blocks[] = {attnBlockFn_16_32_128, attnBlockFn_32_32_128, attnBlockFn_64_32_128, attnBlockFn_64_16_128,
+    const BlockFn blocks[] = {attnBlockFn_16_16_128, attnBlockFn_16_32_128, attnBlockFn_32_32_128, attnBlockFn_64_32_128, attnBlockFn_64_16_128,
                               attnBlockFn_64_64_128, attnBlockFn_32_64_128, attnBlockFn_64_64_64};
     std::vector<const void *> fns = {sampleModuleKernel(), attnPrefillModuleKernel(), tpCheckModuleKernel(),
                                      gemmModuleKernel(),   gemmWideModuleKernel(),    attnMfmaModuleKernel(),
