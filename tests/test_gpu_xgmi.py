@@ -156,21 +156,27 @@ def _run(target, world, *args, timeout=240, kwargs=None):
     return res
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_xgmi_collectives_exact(world):
     res = _run(_collectives, world)
     assert all(v == "ok" for v in res.values()), res
 
 
-@pytest.mark.parametrize("world,sync_type", [(2, "f32"), (4, "f32"), (2, "q80"), (4, "q80")])
+@pytest.mark.parametrize("world,sync_type", [(2, "f32"), (4, "f32"), (2, "q80"), (4, "q80"), (8, "f32"), (8, "q80")])
 def test_xgmi_engine_tp_matches_single(C, tmp_path, world, sync_type):
     """TP engine on the fused data plane (wo / w2 partials exchanged in the GEMV tails, distributed
     argmax) vs TP=1: logits within tolerance (Q80 sync rounds every rank's partial to Q80 blocks),
-    every rank decodes bitwise the same tokens, equal to the single-GPU greedy tokens."""
+    every rank decodes bitwise the same tokens, equal to the single-GPU greedy tokens. World 8 (8
+    processes on this one GPU, grids capped to their share): one KV head per rank, as every Llama-3
+    shape at TP8."""
     from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
     from distributed_llama_multiusers_amd.utils.mfile import FloatType
-    m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=9, dim=512, n_heads=8,
-                               n_kv_heads=4, hidden_dim=1024, vocab_size=1024)
+    if world == 8:
+        m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=9, dim=1024, n_heads=16,
+                                   n_kv_heads=8, hidden_dim=2048, vocab_size=1024)
+    else:
+        m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=9, dim=512, n_heads=8,
+                                   n_kv_heads=4, hidden_dim=1024, vocab_size=1024)
     tokens = [5, 99, 300, 7, 1000, 2]
     steps = 12
     single = C.HipEngine(m, "q80", kv_bf16=False, max_batch=8, n_slots=2)
