@@ -155,7 +155,7 @@ double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters) {
     g.outH = (_Float16 *)alloc((size_t)M * rows * 2);
     g.x = x;
     g.M = M;
-    g.splits = hipk::gemmSplits(rows, n, M);
+    g.splits = hipk::gemmSplits(rows, n, M, L);
     g.part = part ? (float *)alloc(part * 4) : nullptr;
     g.counters = (int *)alloc((size_t)(rows / 64 + 1) * 4);
     auto launch = [&](int c) {

@@ -343,7 +343,7 @@ void HipEngineImpl::gemmBatched(const DevMat &m, int n, int epi, const float *in
             g.ldSS = (int)cfg_.maxBatch;
         }
         g.M = bc;
-        g.splits = hipk::gemmSplits(m.rows, m.n, bc);
+        g.splits = hipk::gemmSplits(m.rows, m.n, bc, q40_ ? m.lanes : 0);
         g.part = dPart_;
         g.counters = dGemmCnt_;
         if (q40_)

@@ -46,9 +46,23 @@ GemmPlan gemmPlan(int rows, int n, int M) {
 
 bool gemmSupported(int n) { return n % 32 == 0; }
 
-int gemmSplits(int rows, int n, int M) {
+// 16-lane tilings at <= 32 tokens run the 16-block-chunk kernel (gemmQ40L16Kernel): its splits
+// keep every split a whole number of 16-block tiling steps.
+static constexpr int kG16Ch = 16;
+static bool gemmL16Eligible(int n, int M, int lanes) {
+    return lanes == 16 && M <= 32 && (n / 32) % kG16Ch == 0 && !gemmUsesWide(M);
+}
+
+int gemmSplits(int rows, int n, int M, int lanes) {
     if (gemmUsesWide(M)) return gemmWideSplits(rows, n, M);
     const int tiles = (rows + kGemmRows - 1) / kGemmRows, nb = n / 32;
+    if (gemmL16Eligible(n, M, lanes)) {
+        const int ks = nb / kG16Ch;  // tiling steps
+        int S = 1;
+        while (2 * S <= 8 && tiles * S < 256 && ks % (2 * S) == 0) S *= 2;
+        while (2 * S <= 8 && tiles * 2 * S <= 512 && ks % (2 * S) == 0 && ks / (2 * S) >= 4) S *= 2;
+        return S;
+    }
     const int target = gemmWgTarget(), maxS = gemmMaxSplits();
     int S = 1;
     while (2 * S <= maxS && tiles * S < target && nb % (2 * S) == 0 && nb / (2 * S) >= kGemmCh) S *= 2;
@@ -67,7 +81,7 @@ size_t gemmPartFloats(int rows, int n, int maxTokens) {
     size_t best = 0;
     for (int m = 16; m <= gemmTokenPad(mt); m *= 2) {
         if (gemmUsesWide(m)) break;
-        const int S = gemmSplits(rows, n, m);
+        const int S = std::max(gemmSplits(rows, n, m), gemmSplits(rows, n, m, 16));  // either kernel
         if (S > 1) best = std::max(best, (size_t)S * tiles * m * kGemmRows);
     }
     if (gemmUsesWide(maxTokens)) best = std::max(best, gemmWidePartFloats(rows, n, maxTokens));
@@ -244,6 +258,112 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     gemmFinish<MT, EPI>(ga, acc, smem, flag, blockIdx.x, gridDim.x);
 }
 
+// 16-lane tilings (Q40Tiling L = 16: qkv / w13 / logits of 8B, every layer matrix of 70B and
+// 405B) at <= 32 tokens. A chunk is 16 blocks = one step k of the tiling, so each wave instruction
+// of the weight DMA reads one contiguous 1 KB of the tiled matrix (4 row pairs x 16 blocks of one
+// (group, step, row parity)); the 8-block chunks of gemmQ40Kernel read 128-B runs 256 B apart, and
+// HBM served those at ~2.4 TB/s (w13 at 8 tokens, bench_gemm.py). The LDS weight image keeps the
+// global order of each 1-KB piece with the block slot XOR-swizzled by ((pair & 7) * 2 + parity):
+// a wave's 16 rows read one block at 16 distinct 16-B columns (conflict-free ds_read_b64). Scales
+// are staged in global order ([group][pair][block] u32 pairs), activations as in gemmQ40Kernel
+// (64 units of 8 f16 per token row, unit u of token t at u ^ (t & 15)).
+static constexpr int kG16W = kGemmRows * kG16Ch * 16, kG16D = (kGemmRows / 2) * kG16Ch * 4;
+__host__ __device__ static constexpr int gemm16StageBytes(int MT) { return kG16W + kG16D + MT * 16 * kG16Ch * 64; }
+__device__ __forceinline__ int g16Swz(int pair, int rpar) { return ((pair & 7) * 2 + rpar) & 15; }
+
+template <int MT, int EPI, int STG>
+__global__ __launch_bounds__(kThreads) void gemmQ40L16Kernel(GemmArgs ga) {
+    const GemvArgs &a = ga.e;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int SB = gemm16StageBytes(MT);
+    constexpr int NW = kG16W / 16 / kThreads, ND = kG16D / 4 / kThreads, NX = MT * 16 * kG16Ch * 4 / kThreads;
+    constexpr int NLD = NW + ND + NX;  // DMA instructions per thread per stage
+    int *flag = reinterpret_cast<int *>(smem + STG * SB);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int col = lane & 15, h = lane >> 4;
+    const int n = a.n, nb = n >> 5, KS = nb / kG16Ch;
+    const int tileIdx = blockIdx.x, sp = blockIdx.y, S = ga.splits;
+    const int R0 = tileIdx * kGemmRows, g0 = R0 / 32;  // first 32-row group of the tile
+    const int bps = nb / S, j0 = sp * bps;
+    const int nch = bps / kG16Ch;
+    const uint8_t *qs = a.qs;
+    const uint32_t *wd2 = reinterpret_cast<const uint32_t *>(a.wd);
+    const int lastRow = a.rows - 1;
+    // issue the copies of chunk c (tiling step k0 + c) into stage buffer b
+    auto issue = [&](int c, int b) {
+        char *st = smem + b * SB;
+        const int k = j0 / kG16Ch + c;
+#pragma unroll
+        for (int s = 0; s < NW; s++) {  // piece = (group, parity, 4-pair block), lane = (pair, slot)
+            const int piece = s * 4 + wave, gl = piece >> 3, rpar = (piece >> 2) & 1, gi = (piece & 3) * 4 + (lane >> 4);
+            const int li = (lane & 15) ^ g16Swz(gi, rpar);
+            int row = R0 + gl * 32 + gi * 2 + rpar;
+            size_t unit;
+            if (row <= lastRow) {
+                unit = (((size_t)(g0 + gl) * KS + k) * 2 + rpar) * kThreads + gi * 16 + li;
+            } else {  // past the matrix: the last row's unit (outputs dropped)
+                row = lastRow;
+                unit = (((size_t)(row / 32) * KS + k) * 2 + (row & 1)) * kThreads + ((row % 32) >> 1) * 16 + li;
+            }
+            glds16(qs + unit * 16, st + (size_t)piece * 1024);
+        }
+#pragma unroll
+        for (int s = 0; s < ND; s++) {  // pair scales in global order: [group][pair][block]
+            const int u = s * kThreads + tid, gl = u >> 8;
+            const int gg = min(g0 + gl, lastRow / 32);
+            glds4(wd2 + ((size_t)gg * KS + k) * kThreads + (u & 255), st + kG16W + (size_t)(s * kThreads + wave * 64) * 4);
+        }
+#pragma unroll
+        for (int s = 0; s < NX; s++) {  // activations: one token row (64 units) per wave instruction
+            const int u = s * kThreads + tid, t = u >> 6, pp = u & 63, uu = pp ^ (t & 15);
+            const _Float16 *src = ga.x + (size_t)t * n + (size_t)(k * kG16Ch + (uu >> 2)) * 32 + (uu & 3) * 8;
+            glds16(src, st + kG16W + kG16D + (size_t)(s * kThreads + wave * 64) * 16);
+        }
+    };
+
+    f32x4 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int rl = wave * 16 + col;  // this lane's weight row (local)
+    const int byteHalf = h & 1, nibHi = h >> 1;
+    const int gl = rl >> 5, rpar = rl & 1, gi = (rl >> 1) & 15;
+    const int wBase = (((gl * 2 + rpar) * 4 + (gi >> 2)) * 64 + (gi & 3) * 16) * 16 + byteHalf * 8;
+    const int swz = g16Swz(gi, rpar);
+    const int dBase = (gl * 256 + gi * 16) * 4;
+
+    constexpr int PF = STG - 1;  // chunks in flight ahead of the one consumed
+    for (int c = 0; c < PF && c < nch; c++) issue(c, c);
+    for (int c = 0; c < nch; c++) {
+        if (c + PF < nch) issue(c + PF, (c + PF) % STG);
+        const int after = min(nch - 1, c + PF) - c;  // chunks issued after c, still in flight
+        if (after >= 2)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * NLD) : "memory");
+        else if (after == 1)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NLD) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // ... and for every thread
+        const char *st = smem + (c % STG) * SB;
+#pragma unroll
+        for (int jj = 0; jj < kG16Ch; jj++) {
+            const u32x2 wv = *reinterpret_cast<const u32x2 *>(st + wBase + (jj ^ swz) * 16);
+            const uint32_t dw = *reinterpret_cast<const uint32_t *>(st + kG16W + dBase + jj * 4);
+            const uint32_t d16 = (rl & 1) ? dw >> 16 : dw & 0xFFFFu;
+            const half8 b = dequantQ40x8(wv, nibHi, d16);
+#pragma unroll
+            for (int t = 0; t < MT; t++) {
+                const int tok = t * 16 + col, up = (jj * 4 + h) ^ (tok & 15);
+                const half8 av = *reinterpret_cast<const half8 *>(st + kG16W + kG16D + (size_t)(tok * 64 + up) * 16);
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b, acc[t], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // stage c % STG is refilled at iteration c + 1
+    }
+
+    gemmFinish<MT, EPI>(ga, acc, smem, flag, blockIdx.x, gridDim.x);
+}
+
 // The 128-token tile (prefill chunks): one stage buffer (73 KB), two workgroups per CU; each
 // weight chunk feeds 8 MFMA token tiles, so a 128-token slice streams the weights once instead of
 // twice.
@@ -270,8 +390,23 @@ void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
         throw Error("launchGemmQ40: the tile exchange does not fit this launch's LDS");
     const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
     const int MT = gemmTokenPad(ga.M) / 16;
-    const int stg = MT == 8 ? 1 : MT == 4 ? gemmStages4() : MT == 2 ? gemmStages2() : gemmStages1();
     const dim3 grid(tiles, ga.splits);
+    if (gemmL16Eligible(ga.e.n, ga.M, ga.e.lanes) && (ga.e.n / 32 / kG16Ch) % ga.splits == 0) {
+        const size_t lds = 2 * (size_t)gemm16StageBytes(MT) + 16 + kGemmScaleFloats * 4;
+#define DL_G16_CASE(M_, E)                                                                         \
+    if (MT == M_ && epi == E) {                                                                    \
+        if (lds > 65536) allowLds((const void *)gemmQ40L16Kernel<M_, E, 2>, lds);                  \
+        hipLaunchKernelGGL((gemmQ40L16Kernel<M_, E, 2>), grid, dim3(kThreads), lds, s, ga);        \
+        return;                                                                                    \
+    }
+#define DL_G16_CASES(M_)                                                                           \
+    DL_G16_CASE(M_, EPI_STORE) DL_G16_CASE(M_, EPI_ACT) DL_G16_CASE(M_, EPI_ACT_Q80)               \
+    DL_G16_CASE(M_, EPI_QKV) DL_G16_CASE(M_, EPI_ACT_F16) DL_G16_CASE(M_, EPI_RES)
+        DL_G16_CASES(1) DL_G16_CASES(2)
+#undef DL_G16_CASES
+#undef DL_G16_CASE
+    }
+    const int stg = MT == 8 ? 1 : MT == 4 ? gemmStages4() : MT == 2 ? gemmStages2() : gemmStages1();
     const size_t lds = gemmLds(MT, stg);
 #define DL_GEMM_CASE(M_, E, G)                                                                    \
     if (MT == M_ && epi == E && stg == G) {                                                       \

@@ -212,7 +212,8 @@ int gemmCounterInts(int rows, int maxTokens);
 constexpr int kGemmF32MaxTokens = 64;  // tokens per F32 GEMM launch (16, 32 or 64 padded)
 GemmPlan gemmPlan(int rows, int n, int M);
 bool gemmSupported(int n);  // input width a multiple of 32 (whole Q40 blocks)
-int gemmSplits(int rows, int n, int M);
+// K splits of a launch; lanes = the matrix's tiling L (16: the 16-block-chunk kernel's rule)
+int gemmSplits(int rows, int n, int M, int lanes = 0);
 // split-K partial floats for any launch of up to maxTokens tokens on this matrix
 size_t gemmPartFloats(int rows, int n, int maxTokens);
 // token rows one GEMM launch of M (1..128) tokens reads from its f16 activation operand (16/32/64/128)

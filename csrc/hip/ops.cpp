@@ -207,7 +207,7 @@ std::vector<float> gemmQ40(const std::vector<uint8_t> &blocks, int rows, int n, 
         g.e.ldOut = rows;
         g.x = xh + (size_t)c0 * n;
         g.M = bc;
-        g.splits = splits > 0 ? splits : hipk::gemmSplits(rows, n, bc);
+        g.splits = splits > 0 ? splits : hipk::gemmSplits(rows, n, bc, w.lanes);
         g.part = partBuf;
         g.counters = counters;
         hipk::launchGemmQ40(g, hipk::EPI_STORE, sc.s);

@@ -407,11 +407,19 @@ def test_engine_8b_shape_matches_cpu(C, tmp_path):
     from distributed_llama_multiusers_amd.utils.mfile import FloatType
     m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=5, dim=4096,
                                hidden_dim=14336, n_heads=32, n_kv_heads=8, n_layers=2, vocab_size=2048)
-    gpu = C.HipEngine(m, "q80", kv_bf16=False, max_batch=8)
+    gpu = C.HipEngine(m, "q80", kv_bf16=False, max_batch=32)
     assert gpu.attn_block
-    cpu = C.cpu_backend(m, "q80", 8)
+    cpu = C.cpu_backend(m, "q80", 8, max_batch=32)
     toks = [1, 2, 3, 500, 1000, 7]
     assert _rel(_seq(gpu, toks), _seq(cpu, toks)) < 3e-2
+    # batched rows on the MFMA GEMMs: 16-lane tilings (qkv, w13, logits) run the 16-block-chunk
+    # kernel, wo / w2 the 8-block one; 8 and 24 rows (16- and 32-token tiles, split-K)
+    rng = np.random.default_rng(3)
+    for n in (8, 24):
+        t = [int(x) for x in rng.integers(0, 2048, n)]
+        got = gpu.forward(t, list(range(n)), [0] * n)
+        ref = cpu.forward(t, list(range(n)), [0] * n)
+        assert _rel(got, ref) < 3e-2, n
 
 
 @pytest.mark.parametrize("shape", ["70b", "405b"])
