@@ -46,11 +46,12 @@ GemmPlan gemmPlan(int rows, int n, int M) {
 
 bool gemmSupported(int n) { return n % 32 == 0; }
 
-// 16-lane tilings at <= 32 tokens run the 16-block-chunk kernel (gemmQ40L16Kernel): its splits
-// keep every split a whole number of 16-block tiling steps.
+// 16-lane tilings at <= 16 tokens run the 16-block-chunk kernel (gemmQ40L16Kernel): its splits
+// keep every split a whole number of 16-block tiling steps. (At 32 tokens its 50 KB stages leave
+// one workgroup per CU: w13 42.8 vs 32.5 us, so those stay on gemmQ40Kernel.)
 static constexpr int kG16Ch = 16;
 static bool gemmL16Eligible(int n, int M, int lanes) {
-    return lanes == 16 && M <= 32 && (n / 32) % kG16Ch == 0 && !gemmUsesWide(M);
+    return lanes == 16 && M <= 16 && (n / 32) % kG16Ch == 0 && !gemmUsesWide(M);
 }
 
 int gemmSplits(int rows, int n, int M, int lanes) {
@@ -259,7 +260,7 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
 }
 
 // 16-lane tilings (Q40Tiling L = 16: qkv / w13 / logits of 8B, every layer matrix of 70B and
-// 405B) at <= 32 tokens. A chunk is 16 blocks = one step k of the tiling, so each wave instruction
+// 405B) at <= 16 tokens. A chunk is 16 blocks = one step k of the tiling, so each wave instruction
 // of the weight DMA reads one contiguous 1 KB of the tiled matrix (4 row pairs x 16 blocks of one
 // (group, step, row parity)); the 8-block chunks of gemmQ40Kernel read 128-B runs 256 B apart, and
 // HBM served those at ~2.4 TB/s (w13 at 8 tokens, bench_gemm.py). The LDS weight image keeps the
@@ -402,7 +403,7 @@ void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
 #define DL_G16_CASES(M_)                                                                           \
     DL_G16_CASE(M_, EPI_STORE) DL_G16_CASE(M_, EPI_ACT) DL_G16_CASE(M_, EPI_ACT_Q80)               \
     DL_G16_CASE(M_, EPI_QKV) DL_G16_CASE(M_, EPI_ACT_F16) DL_G16_CASE(M_, EPI_RES)
-        DL_G16_CASES(1) DL_G16_CASES(2)
+        DL_G16_CASES(1)
 #undef DL_G16_CASES
 #undef DL_G16_CASE
     }
