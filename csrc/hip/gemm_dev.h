@@ -12,8 +12,10 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
 // 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d via the 0x6400 | q magic (1024 + q)
 __device__ __forceinline__ half8 dequantQ40x8(u32x2 wv, int nibHi, uint32_t d16) {
-    const uint32_t lo = nibHi ? (wv.x >> 4) & 0x0F0F0F0Fu : wv.x & 0x0F0F0F0Fu;
-    const uint32_t hi = nibHi ? (wv.y >> 4) & 0x0F0F0F0Fu : wv.y & 0x0F0F0F0Fu;
+    // one variable shift per word instead of a shift + select (nibHi is per lane, not uniform)
+    const uint32_t sh = (uint32_t)nibHi << 2;
+    const uint32_t lo = (wv.x >> sh) & 0x0F0F0F0Fu;
+    const uint32_t hi = (wv.y >> sh) & 0x0F0F0F0Fu;
     const uint32_t p0 = __builtin_amdgcn_perm(0x64646464u, lo, 0x07010700u);
     const uint32_t p1 = __builtin_amdgcn_perm(0x64646464u, lo, 0x07030702u);
     const uint32_t p2 = __builtin_amdgcn_perm(0x64646464u, hi, 0x07010700u);
