@@ -192,8 +192,6 @@ hipk::AttnBlockArgs HipEngineImpl::attnBlockArgs(const DevLayer &L, u32 l, int c
     const bool tp = fusedTp(false);
     b.wo = gemvArgs(L.wo, 0, 1, tp ? hipk::EPI_STORE_TP : hipk::EPI_STORE, nullptr, p.q0, nullptr, nullptr, nullptr,
                     dY_, h_.dim, nullptr, dAttQ_, dAttS_, nullptr, nullptr, tp);
-    b.qkv.passes *= blockPassMul_;  // longer workgroups when the default grids would not be co-resident
-    b.wo.passes *= blockPassMul_;
     b.hg = hipk::attnBlockHG(b.at);
     b.layer = (int)l;
     b.nLayers = (int)h_.nLayers;
@@ -215,15 +213,10 @@ void HipEngineImpl::setupAttnBlock() {
     if ((e && *e == '0') || !q40_ || plan_.nKvHeads0 > kMaxKvGroups) return;
     const int share = comm_ ? std::max(1, comm_->ranksOnDevice()) : 1;
     const int keep = bucket_;
-    // qkv / wo passes per workgroup: the fewest that make the shortest-context grid co-resident
-    // (wide shards, e.g. 70B / 405B at TP1, would otherwise exceed one round of workgroups)
+    // The block only runs with the GEMVs' own grids: 70B / 405B at TP1 (grids beyond one round of
+    // co-resident workgroups) measured slower with longer qkv / wo workgroups (70B 8.10 -> 8.26,
+    // 405B 40.4 -> 43.3 ms/token), so they keep the three launches.
     bucket_ = 0;
-    for (blockPassMul_ = 1; blockPassMul_ < 8; blockPassMul_ *= 2) {
-        const hipk::AttnBlockArgs b = attnBlockArgs(layers_[0], 0, 0);
-        if (!hipk::attnBlockPlan(b, fusedTp(false)).fn) break;
-        const hipk::GemvResidency r = hipk::attnBlockResidency(b, fusedTp(false));
-        if (r.maxResident > 0 && r.grid <= r.maxResident / share) break;
-    }
     int lastOn = -1;
     hipk::GemvResidency off;
     for (size_t i = 0; i < buckets_.size(); i++) {
