@@ -242,8 +242,10 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
             // the old key rl & 7 left 2-way conflicts: SQ_LDS_BANK_CONFLICT 25 % of LDS cycles)
             const int pp = jj ^ ((rl >> 1) & (kGemmCh - 1));
             const u32x2 wv = *reinterpret_cast<const u32x2 *>(st + (size_t)(rl * kGemmCh + pp) * 16 + byteHalf * 8);
-            const uint32_t dw = *reinterpret_cast<const uint32_t *>(st + kStW + (size_t)((rl >> 1) * kGemmCh + jj) * 4);
-            const uint32_t d16 = jj < cn ? ((rl & 1) ? dw >> 16 : dw & 0xFFFFu) : 0u;
+            // this row's f16 half of the pair scale, read directly (no per-lane shift)
+            const uint32_t dh = *reinterpret_cast<const uint16_t *>(st + kStW + (size_t)((rl >> 1) * kGemmCh + jj) * 4 +
+                                                                    (rl & 1) * 2);
+            const uint32_t d16 = jj < cn ? dh : 0u;
             const half8 b = dequantQ40x8(wv, nibHi, d16);
 #pragma unroll
             for (int t = 0; t < MT; t++) {
@@ -330,7 +332,7 @@ __global__ __launch_bounds__(kThreads) void gemmQ40L16Kernel(GemmArgs ga) {
     const int gl = rl >> 5, rpar = rl & 1, gi = (rl >> 1) & 15;
     const int wBase = (((gl * 2 + rpar) * 4 + (gi >> 2)) * 64 + (gi & 3) * 16) * 16 + byteHalf * 8;
     const int swz = g16Swz(gi, rpar);
-    const int dBase = (gl * 256 + gi * 16) * 4;
+    const int dBase = (gl * 256 + gi * 16) * 4 + rpar * 2;  // this row's f16 half of the pair scale
 
     constexpr int PF = STG - 1;  // chunks in flight ahead of the one consumed
     for (int c = 0; c < PF && c < nch; c++) issue(c, c);
@@ -348,8 +350,7 @@ __global__ __launch_bounds__(kThreads) void gemmQ40L16Kernel(GemmArgs ga) {
 #pragma unroll
         for (int jj = 0; jj < kG16Ch; jj++) {
             const u32x2 wv = *reinterpret_cast<const u32x2 *>(st + wBase + (jj ^ swz) * 16);
-            const uint32_t dw = *reinterpret_cast<const uint32_t *>(st + kG16W + dBase + jj * 4);
-            const uint32_t d16 = (rl & 1) ? dw >> 16 : dw & 0xFFFFu;
+            const uint32_t d16 = *reinterpret_cast<const uint16_t *>(st + kG16W + dBase + jj * 4);
             const half8 b = dequantQ40x8(wv, nibHi, d16);
 #pragma unroll
             for (int t = 0; t < MT; t++) {

@@ -9,7 +9,7 @@ timeout -k 10 400 python -u -m pytest $R/tests/test_gpu_engine.py $R/tests/test_
 rc=$?; tail -3 $O/tests.log
 case $rc in 0|1|5) ;; *) echo "tests rc=$rc: stopping"; exit $rc ;; esac
 timeout -k 10 300 python -u $R/scripts/bench_gemm.py 8 16 32 > $O/gemm.log 2>&1 || exit $?
-for b in 8 16 32; do
+for b in 8 16 32 64; do
   timeout -k 10 240 python3 $R/bench.py --batch $b --steps 16 --warmup 4 --no-cli --long-ctx 0 --no-f32kv --no-prefill4k --no-cap128k > $O/b$b.log 2>&1 || exit $?
 done
 exit 0
