@@ -234,7 +234,7 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
             const int t = min(tb + u * NG, t1 - 1);  // clamped: no divergent loads
             const bool cur = SYNC && t == pos;
             if ((phase == 1 && cur) || (phase == 2 && !cur)) continue;
-            const size_t off = kvRow(a.kvMap, a.seqLen, sl, t) * a.kv0 + kvh * HS + l16 * DPL;
+            const size_t off = kvOff(a.kvMap, a.seqLen, a.kv0 / HS, HS, sl, t, kvh) + l16 * DPL;
             const uint32_t *kp = reinterpret_cast<const uint32_t *>(
                 BF16 ? (const void *)(reinterpret_cast<const uint16_t *>(a.kcache) + off)
                      : (const void *)(reinterpret_cast<const float *>(a.kcache) + off));

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
     char *wbuf = smem + wave * kAmWaveBytes;  // [2 buffers][K tile | V tile]
     const uint16_t *kc = reinterpret_cast<const uint16_t *>(a.kcache);
     const uint16_t *vc = reinterpret_cast<const uint16_t *>(a.vcache);
-    const size_t kvBase = (size_t)g * HS;
+    const int nKv = a.kv0 / HS;
     // Paged cache: the chunk's page ids are loaded once, one per lane, before any DMA, and each
     // key's row comes from a lane shuffle. (A table load per key row made the compiler wait for
     // vmcnt(0) - every DMA already in flight - before each of the 16 wave-instructions of a tile.)
@@ -89,11 +89,11 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
         asm volatile("s_waitcnt vmcnt(0)" : "+v"(v));
         pgReg = v;
     }
-    auto rowOf = [&](int key) -> size_t {
-        if (!km.table) return (size_t)sl * a.seqLen + key;
-        if (!pgLanes) return kvRow(km, a.seqLen, sl, key);
+    auto offOf = [&](int key) -> size_t {  // element offset of head g's vector at this key
+        if (!km.table) return kvOffAt(km, a.seqLen, nKv, HS, (size_t)sl, key, g);
+        if (!pgLanes) return kvOff(km, a.seqLen, nKv, HS, sl, key, g);
         const int pg = __shfl(pgReg, (key >> km.pageShift) - pg0);
-        return ((size_t)pg << km.pageShift) + (size_t)(key & ((1 << km.pageShift) - 1));
+        return kvOffAt(km, a.seqLen, nKv, HS, (size_t)pg, key, g);
     };
     // DMA of tile i (keys t0 + 32 i ...) into buffer bf: 8 + 8 wave-instructions of 4 rows x 256 B
     auto issue = [&](int i, int bf) {
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
         for (int j = 0; j < kAmTile / 4; j++) {
             const int r = 4 * j + (lane >> 4), p = lane & 15;
             const int key = min(t0 + kAmTile * i + r, t1 - 1);  // past the chunk: masked below
-            const size_t off = kvBase + rowOf(key) * a.kv0 + (size_t)(p ^ amSwz(r)) * 8;
+            const size_t off = offOf(key) + (size_t)(p ^ amSwz(r)) * 8;
             __builtin_amdgcn_global_load_lds(const_cast<uint16_t *>(kc + off),
                                              reinterpret_cast<__attribute__((address_space(3))) void *>(
                                                  reinterpret_cast<uintptr_t>(kb + j * 1024)), 16, 0, 0);
@@ -338,7 +338,6 @@ __global__ __launch_bounds__(kAmThreads) void attnPrefillDmaKernel(AttnArgs a, i
     }
     const uint16_t *kc = reinterpret_cast<const uint16_t *>(a.kcache);
     const uint16_t *vc = reinterpret_cast<const uint16_t *>(a.vcache);
-    const size_t kvBase = (size_t)g * HS;
     const int nTiles = (k1 - k0 + kAmTile - 1) / kAmTile, nRounds = (nTiles + kApRound - 1) / kApRound;
     auto tileBuf = [&](int bf, int tt) { return smem + (size_t)(bf * kApRound + tt) * 2 * kAmTileBytes; };
     // wave w copies tile kApRound * r + w of round r into buffer bf (16 wave-instructions, or none)
@@ -350,7 +349,7 @@ __global__ __launch_bounds__(kAmThreads) void attnPrefillDmaKernel(AttnArgs a, i
         for (int j = 0; j < kAmTile / 4; j++) {
             const int rr = 4 * j + (lane >> 4), p = lane & 15;
             const int key = min(k0 + kAmTile * t + rr, k1 - 1);  // past the chunk: masked below
-            const size_t off = kvBase + kvRow(a.kvMap, a.seqLen, sl, key) * a.kv0 + (size_t)(p ^ amSwz(rr)) * 8;
+            const size_t off = kvOff(a.kvMap, a.seqLen, nKv, HS, sl, key, g) + (size_t)(p ^ amSwz(rr)) * 8;
             __builtin_amdgcn_global_load_lds(const_cast<uint16_t *>(kc + off),
                                              reinterpret_cast<__attribute__((address_space(3))) void *>(
                                                  reinterpret_cast<uintptr_t>(kb + j * 1024)), 16, 0, 0);

@@ -78,14 +78,13 @@ __global__ __launch_bounds__(kPfThreads) void attnPrefillKernel(AttnArgs a, int 
     }
     const uint16_t *kc = reinterpret_cast<const uint16_t *>(a.kcache);
     const uint16_t *vc = reinterpret_cast<const uint16_t *>(a.vcache);
-    const size_t kvBase = (size_t)g * HS;
     u32x4 kr[PER], vr[PER];
     auto gload = [&](int t0) {
 #pragma unroll
         for (int u = 0; u < PER; u++) {
             const int e = tid + u * kPfThreads;
             const int key = min(t0 + e / U8, k1 - 1);  // past the range: masked in compute (and mapped)
-            const size_t off = kvBase + kvRow(a.kvMap, a.seqLen, sl, key) * a.kv0 + (e % U8) * 8;
+            const size_t off = kvOff(a.kvMap, a.seqLen, nKv, HS, sl, key, g) + (e % U8) * 8;
             kr[u] = *reinterpret_cast<const u32x4 *>(kc + off);
             vr[u] = *reinterpret_cast<const u32x4 *>(vc + off);
         }

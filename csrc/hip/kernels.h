@@ -62,16 +62,26 @@ struct KvMap {
     int pageShift = 0;
     int pagesPerSlot = 0;
 };
-__host__ __device__ inline size_t kvRow(const KvMap &m, int seqLen, int slot, int pos) {
-    if (!m.table) return (size_t)slot * seqLen + pos;
-    const int pg = m.table[slot * m.pagesPerSlot + (pos >> m.pageShift)];
-    return ((size_t)pg << m.pageShift) + (size_t)(pos & ((1 << m.pageShift) - 1));
+// KV caches are head-major, so one KV head's keys are contiguous (a decode-attention workgroup
+// streams one range instead of 2 * hs-byte slices kv0 apart): element offset of the head vector
+// of (slot, pos, KV head kvh) in a layer's cache, contiguous [slot][nKv][seqLen][hs] or paged
+// [page][nKv][pageSize][hs] (the page table maps a slot's position blocks to pool pages).
+__host__ __device__ inline size_t kvPageOf(const KvMap &m, int slot, int pos) {
+    return (size_t)m.table[slot * m.pagesPerSlot + (pos >> m.pageShift)];
+}
+__host__ __device__ inline size_t kvOffAt(const KvMap &m, int seqLen, int nKv, int hs, size_t block, int pos, int kvh) {
+    // block = slot (contiguous) or pool page (paged)
+    if (!m.table) return ((block * nKv + kvh) * seqLen + pos) * hs;
+    return (((block * nKv + kvh) << m.pageShift) + (size_t)(pos & ((1 << m.pageShift) - 1))) * hs;
+}
+__host__ __device__ inline size_t kvOff(const KvMap &m, int seqLen, int nKv, int hs, int slot, int pos, int kvh) {
+    return kvOffAt(m, seqLen, nKv, hs, m.table ? kvPageOf(m, slot, pos) : (size_t)slot, pos, kvh);
 }
 
 struct AttnArgs {
     const float *q = nullptr;   // [B][ldq], rotated queries
     int ldq = 0;
-    const void *kcache = nullptr, *vcache = nullptr;  // layer base [slot][seqLen][kv0] (or a page pool)
+    const void *kcache = nullptr, *vcache = nullptr;  // layer base [slot][nKv][seqLen][hs] (or a page pool: kvOff)
     KvMap kvMap;
     const int *pos = nullptr, *slot = nullptr;
     int nHeads0 = 0, kvMul = 1, hs = 0, kv0 = 0, seqLen = 0;
@@ -146,7 +156,7 @@ struct GemvArgs {
     const float2 *rope = nullptr; // [seqLen][hs/2] (cos, sin)
     const int *pos = nullptr;     // per batch row
     const int *slot = nullptr;
-    void *kcache = nullptr;       // layer base: [slot][seqLen][kv0] (or a page pool: kvMap)
+    void *kcache = nullptr;       // layer base: [slot][nKv][seqLen][hs] (or a page pool: kvOff)
     void *vcache = nullptr;
     KvMap kvMap;
     int kvBf16 = 1;

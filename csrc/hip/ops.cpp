@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 
 #include "../core/quant.h"
@@ -299,17 +300,20 @@ std::vector<float> qkvRope(const std::vector<uint8_t> &blocks, int q0, int kv0, 
     a.kvBf16 = kvBf16 ? 1 : 0;
     hipk::launchGemv(a, B, hipk::PRO_RESNORM, hipk::EPI_QKV, true, sc.s);
     sc.sync();
-    auto row = [&](void *cache, int b) {
+    auto row = [&](void *cache, int b) {  // the [kv0] row of (slot b, pos[b]) from the head-major cache
         std::vector<float> r(kv0);
-        const size_t off = ((size_t)b * seqLen + pos[b]) * kv0;
-        if (kvBf16) {
-            const std::vector<uint16_t> h = sc.download(static_cast<uint16_t *>(cache) + off, kv0);
-            for (int i = 0; i < kv0; i++) {
-                const uint32_t u = (uint32_t)h[i] << 16;
-                std::memcpy(&r[i], &u, 4);
+        for (int kh = 0; kh < kv0 / hs; kh++) {
+            const size_t off = hipk::kvOff(hipk::KvMap{}, seqLen, kv0 / hs, hs, b, pos[b], kh);
+            if (kvBf16) {
+                const std::vector<uint16_t> h = sc.download(static_cast<uint16_t *>(cache) + off, hs);
+                for (int i = 0; i < hs; i++) {
+                    const uint32_t u = (uint32_t)h[i] << 16;
+                    std::memcpy(&r[kh * hs + i], &u, 4);
+                }
+            } else {
+                const std::vector<float> f = sc.download(static_cast<float *>(cache) + off, hs);
+                std::copy(f.begin(), f.end(), r.begin() + (size_t)kh * hs);
             }
-        } else {
-            r = sc.download(static_cast<float *>(cache) + off, kv0);
         }
         return r;
     };
@@ -345,7 +349,15 @@ std::vector<float> attention(const std::vector<float> &q, const std::vector<floa
     for (int b = 0; b < B; b++)
         DL_CHECK(pos[b] >= 0 && pos[b] < seqLen && slot[b] >= 0 && slot[b] < nSlots, "attention row out of range");
     Scratch sc;
-    auto cache = [&](const std::vector<float> &x) -> void * {
+    auto cache = [&](const std::vector<float> &xs) -> void * {
+        // the caller's [slot][seqLen][kv0] rows -> the engine's head-major [slot][nKv][seqLen][hs]
+        const int nKv = kv0 / hs;
+        std::vector<float> x(xs.size());
+        for (int sl = 0; sl < nSlots; sl++)
+            for (int p = 0; p < seqLen; p++)
+                for (int kh = 0; kh < nKv; kh++)
+                    std::memcpy(&x[hipk::kvOff(hipk::KvMap{}, seqLen, nKv, hs, sl, p, kh)],
+                                &xs[((size_t)sl * seqLen + p) * kv0 + (size_t)kh * hs], hs * sizeof(float));
         if (!kvBf16) return sc.upload(x);
         std::vector<uint16_t> h(x.size());
         for (size_t i = 0; i < x.size(); i++) {  // round to nearest even, as the QKV epilogue stores
