@@ -192,6 +192,8 @@ hipk::AttnBlockArgs HipEngineImpl::attnBlockArgs(const DevLayer &L, u32 l, int c
     const bool tp = fusedTp(false);
     b.wo = gemvArgs(L.wo, 0, 1, tp ? hipk::EPI_STORE_TP : hipk::EPI_STORE, nullptr, p.q0, nullptr, nullptr, nullptr,
                     dY_, h_.dim, nullptr, dAttQ_, dAttS_, nullptr, nullptr, tp);
+    b.qkv.passes *= blockPassMul_;  // same-GPU rehearsals: longer workgroups (setupAttnBlock)
+    b.wo.passes *= blockPassMul_;
     b.hg = hipk::attnBlockHG(b.at);
     b.layer = (int)l;
     b.nLayers = (int)h_.nLayers;
@@ -213,10 +215,20 @@ void HipEngineImpl::setupAttnBlock() {
     if ((e && *e == '0') || !q40_ || plan_.nKvHeads0 > kMaxKvGroups) return;
     const int share = comm_ ? std::max(1, comm_->ranksOnDevice()) : 1;
     const int keep = bucket_;
-    // The block only runs with the GEMVs' own grids: 70B / 405B at TP1 (grids beyond one round of
-    // co-resident workgroups) measured slower with longer qkv / wo workgroups (70B 8.10 -> 8.26,
-    // 405B 40.4 -> 43.3 ms/token), so they keep the three launches.
+    // qkv / wo passes per workgroup: the GEMVs' own grids, except in same-GPU rehearsals (ranks
+    // sharing one GPU's resident slots), which may double them so the block stays co-resident.
+    // On a GPU of its own a grid beyond one round of co-resident workgroups (70B / 405B at TP1)
+    // keeps the three launches: longer qkv / wo workgroups measured slower there (70B 8.10 ->
+    // 8.26, 405B 40.4 -> 43.3 ms/token).
     bucket_ = 0;
+    blockPassMul_ = 1;
+    if (share > 1) {
+        const hipk::AttnBlockArgs b = attnBlockArgs(layers_[0], 0, 0);
+        if (hipk::attnBlockPlan(b, fusedTp(false)).fn) {
+            const hipk::GemvResidency r = hipk::attnBlockResidency(b, fusedTp(false));
+            if (r.maxResident > 0 && r.grid > r.maxResident / share) blockPassMul_ = 2;
+        }
+    }
     int lastOn = -1;
     hipk::GemvResidency off;
     for (size_t i = 0; i < buckets_.size(); i++) {

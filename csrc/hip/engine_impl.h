@@ -262,6 +262,7 @@ class HipEngineImpl : public HipEngine {
     unsigned *dEpoch_ = nullptr, *dBlockCnt_ = nullptr, *dBlockExpect_ = nullptr;
     int *dBlockErr_ = nullptr;
     bool blockOn_ = false;   // decode rows may run the fused attention block (per bucket: CtxBucket::block)
+    int blockPassMul_ = 1;   // qkv / wo passes multiplier of the block's roles (same-GPU rehearsals)
     int traceLayer_ = -1;    // traceAttnBlock: the layer whose block launch is traced
     unsigned long long *traceBuf_ = nullptr;
 
