@@ -96,6 +96,7 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
         return kvOffAt(km, a.seqLen, nKv, HS, (size_t)pg, key, g);
     };
     // DMA of tile i (keys t0 + 32 i ...) into buffer bf: 8 + 8 wave-instructions of 4 rows x 256 B
+    // (non-temporal: a decode row reads each layer's K / V once)
     auto issue = [&](int i, int bf) {
         char *kb = wbuf + bf * 2 * kAmTileBytes, *vb = kb + kAmTileBytes;
 #pragma unroll
@@ -105,10 +106,10 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
             const size_t off = offOf(key) + (size_t)(p ^ amSwz(r)) * 8;
             __builtin_amdgcn_global_load_lds(const_cast<uint16_t *>(kc + off),
                                              reinterpret_cast<__attribute__((address_space(3))) void *>(
-                                                 reinterpret_cast<uintptr_t>(kb + j * 1024)), 16, 0, 0);
+                                                 reinterpret_cast<uintptr_t>(kb + j * 1024)), 16, 0, 2);
             __builtin_amdgcn_global_load_lds(const_cast<uint16_t *>(vc + off),
                                              reinterpret_cast<__attribute__((address_space(3))) void *>(
-                                                 reinterpret_cast<uintptr_t>(vb + j * 1024)), 16, 0, 0);
+                                                 reinterpret_cast<uintptr_t>(vb + j * 1024)), 16, 0, 2);
         }
     };
 

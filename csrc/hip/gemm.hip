@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
         for (int s = 0; s < NW; s++) {
             const int u = s * kThreads + tid, rl = u / kGemmCh, pp = u % kGemmCh;
             const size_t unit = unitOf(R0 + rl, c0 + (pp ^ ((rl >> 1) & (kGemmCh - 1))));
-            glds16(qs + unit * 16, st + (size_t)(s * kThreads + wave * 64) * 16);
+            glds16<true>(qs + unit * 16, st + (size_t)(s * kThreads + wave * 64) * 16);
         }
         // pair scales: u = tid -> (pair_l = u/8, block u%8), 4 B each
         {
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(kThreads) void gemmQ40L16Kernel(GemmArgs ga) {
                 row = lastRow;
                 unit = (((size_t)(row / 32) * KS + k) * 2 + (row & 1)) * kThreads + ((row % 32) >> 1) * 16 + li;
             }
-            glds16(qs + unit * 16, st + (size_t)piece * 1024);
+            glds16<true>(qs + unit * 16, st + (size_t)piece * 1024);
         }
 #pragma unroll
         for (int s = 0; s < ND; s++) {  // pair scales in global order: [group][pair][block]

@@ -35,10 +35,12 @@ __device__ __forceinline__ half8 dequantQ40x8(u32x2 wv, int nibHi, uint32_t d16)
     return out;
 }
 
-// one 16-B global -> LDS copy per lane; `lds` = this wave's base (lane l lands at lds + 16 l)
+// one 16-B global -> LDS copy per lane; `lds` = this wave's base (lane l lands at lds + 16 l).
+// NT: non-temporal (streamed once: weights, KV), as the GEMV ring's loads (cache policy nt = 2)
+template <bool NT = false>
 __device__ __forceinline__ void glds16(const void *g, void *lds) {
     __builtin_amdgcn_global_load_lds(const_cast<void *>(g), reinterpret_cast<__attribute__((address_space(3))) void *>(
-                                         reinterpret_cast<uintptr_t>(lds)), 16, 0, 0);
+                                         reinterpret_cast<uintptr_t>(lds)), 16, 0, NT ? 2 : 0);
 }
 __device__ __forceinline__ void glds4(const void *g, void *lds) {
     __builtin_amdgcn_global_load_lds(const_cast<void *>(g), reinterpret_cast<__attribute__((address_space(3))) void *>(
