@@ -273,7 +273,8 @@ __device__ __forceinline__ void qkvPairStore(const GemvArgs &a, int r0, float v0
             stF2<WT>(qRow + r0, o0, o1);
         } else {
             const int x = r0 - a.q0;  // K row: head x / hs, dim x % hs (a row pair stays in one head)
-            const size_t off = kvOff(a.kvMap, a.seqLen, a.kv0 / a.hs, a.hs, sl, p, x / a.hs) + x % a.hs;
+            const int lg = __builtin_ctz(a.hs);  // hs is a power of two (64 / 128)
+            const size_t off = kvOff(a.kvMap, a.seqLen, a.kv0 >> lg, a.hs, sl, p, x >> lg) + (x & (a.hs - 1));
             if (a.kvBf16) {
                 const uint32_t pk = (uint32_t)f32ToBf16(o0) | ((uint32_t)f32ToBf16(o1) << 16);
                 st32<WT>(reinterpret_cast<uint16_t *>(a.kcache) + off, pk);
@@ -282,8 +283,8 @@ __device__ __forceinline__ void qkvPairStore(const GemvArgs &a, int r0, float v0
             }
         }
     } else {
-        const int x = r0 - a.q0 - a.kv0;
-        const size_t off = kvOff(a.kvMap, a.seqLen, a.kv0 / a.hs, a.hs, sl, p, x / a.hs) + x % a.hs;
+        const int x = r0 - a.q0 - a.kv0, lg = __builtin_ctz(a.hs);
+        const size_t off = kvOff(a.kvMap, a.seqLen, a.kv0 >> lg, a.hs, sl, p, x >> lg) + (x & (a.hs - 1));
         if (a.kvBf16) {
             const uint32_t pk = (uint32_t)f32ToBf16(v0) | ((uint32_t)f32ToBf16(v1) << 16);
             st32<WT>(reinterpret_cast<uint16_t *>(a.vcache) + off, pk);

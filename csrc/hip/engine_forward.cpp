@@ -221,13 +221,11 @@ void HipEngineImpl::setupAttnBlock() {
     // keeps the three launches: longer qkv / wo workgroups measured slower there (70B 8.10 ->
     // 8.26, 405B 40.4 -> 43.3 ms/token).
     bucket_ = 0;
-    blockPassMul_ = 1;
-    if (share > 1) {
+    for (blockPassMul_ = 1; share > 1 && blockPassMul_ < 8; blockPassMul_ *= 2) {
         const hipk::AttnBlockArgs b = attnBlockArgs(layers_[0], 0, 0);
-        if (hipk::attnBlockPlan(b, fusedTp(false)).fn) {
-            const hipk::GemvResidency r = hipk::attnBlockResidency(b, fusedTp(false));
-            if (r.maxResident > 0 && r.grid > r.maxResident / share) blockPassMul_ = 2;
-        }
+        if (!hipk::attnBlockPlan(b, fusedTp(false)).fn) break;
+        const hipk::GemvResidency r = hipk::attnBlockResidency(b, fusedTp(false));
+        if (r.maxResident > 0 && r.grid <= r.maxResident / share) break;
     }
     int lastOn = -1;
     hipk::GemvResidency off;
