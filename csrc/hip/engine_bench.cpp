@@ -205,7 +205,7 @@ double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B
     };
     DL_CHECK(kvMul >= 1 && nHeads0 % kvMul == 0 && pos >= 0 && pos < seqLen && B >= 1, "bad attention bench shape");
     const int kv0 = nHeads0 / kvMul * hs, q0 = nHeads0 * hs;
-    const size_t kvElems = (size_t)B * hipk::kvSlotRows(seqLen) * kv0;  // one slot per row
+    const size_t kvElems = (size_t)B * seqLen * kv0;  // one slot per row
     std::vector<void *> kc(copies), vc(copies);
     for (int c = 0; c < copies; c++) {
         kc[c] = alloc(kvElems * 2);

@@ -145,7 +145,7 @@ class HipEngineImpl : public HipEngine {
 
     // engine_kv.cpp
     size_t kvPoolRows() const {
-        return cfg_.kvPages ? (size_t)cfg_.kvPages * cfg_.kvPageSize : (size_t)cfg_.nSlots * hipk::kvSlotRows(h_.seqLen);
+        return cfg_.kvPages ? (size_t)cfg_.kvPages * cfg_.kvPageSize : (size_t)cfg_.nSlots * h_.seqLen;
     }
     bool paged() const { return cfg_.kvPages > 0; }
     void setupPages();

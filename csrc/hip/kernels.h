@@ -62,25 +62,16 @@ struct KvMap {
     int pageShift = 0;
     int pagesPerSlot = 0;
 };
-// KV caches are blocked head-major: positions in blocks of kKvBlock, and inside a block one KV
-// head's vectors are contiguous, so an attention chunk of a head streams one 64 KB range instead
-// of 2 * hs-byte slices kv0 apart, while short contexts still touch only the first blocks of each
-// slot (a plain [slot][kv head][pos] layout spread them over 2 x kv heads regions per layer at
-// large capacities: +4 % decode at 131072 positions). Element offset of the head vector of (slot,
-// pos, kv head): contiguous [slot][pos / kKvBlock][nKv][kKvBlock][hs] (slot capacity rounded up
-// to whole blocks: kvSlotRows), paged [page][nKv][pageSize][hs] (the page table maps a slot's
-// position blocks to pool pages).
-constexpr int kKvBlockShift = 8, kKvBlock = 1 << kKvBlockShift;
-__host__ __device__ inline size_t kvSlotRows(int seqLen) { return (size_t)(seqLen + kKvBlock - 1) >> kKvBlockShift << kKvBlockShift; }
+// KV caches are head-major, so one KV head's keys are contiguous (a decode-attention workgroup
+// streams one range instead of 2 * hs-byte slices kv0 apart): element offset of the head vector
+// of (slot, pos, KV head kvh) in a layer's cache, contiguous [slot][nKv][seqLen][hs] or paged
+// [page][nKv][pageSize][hs] (the page table maps a slot's position blocks to pool pages).
 __host__ __device__ inline size_t kvPageOf(const KvMap &m, int slot, int pos) {
     return (size_t)m.table[slot * m.pagesPerSlot + (pos >> m.pageShift)];
 }
-// block = the pool page holding pos (paged) or the slot (contiguous)
 __host__ __device__ inline size_t kvOffAt(const KvMap &m, int seqLen, int nKv, int hs, size_t block, int pos, int kvh) {
-    if (!m.table) {
-        const size_t b = block * (kvSlotRows(seqLen) >> kKvBlockShift) + (size_t)(pos >> kKvBlockShift);
-        return (((b * nKv + kvh) << kKvBlockShift) + (size_t)(pos & (kKvBlock - 1))) * hs;
-    }
+    // block = slot (contiguous) or pool page (paged)
+    if (!m.table) return ((block * nKv + kvh) * seqLen + pos) * hs;
     return (((block * nKv + kvh) << m.pageShift) + (size_t)(pos & ((1 << m.pageShift) - 1))) * hs;
 }
 __host__ __device__ inline size_t kvOff(const KvMap &m, int seqLen, int nKv, int hs, int slot, int pos, int kvh) {
@@ -90,7 +81,7 @@ __host__ __device__ inline size_t kvOff(const KvMap &m, int seqLen, int nKv, int
 struct AttnArgs {
     const float *q = nullptr;   // [B][ldq], rotated queries
     int ldq = 0;
-    const void *kcache = nullptr, *vcache = nullptr;  // layer base, blocked head-major (kvOff)
+    const void *kcache = nullptr, *vcache = nullptr;  // layer base [slot][nKv][seqLen][hs] (or a page pool: kvOff)
     KvMap kvMap;
     const int *pos = nullptr, *slot = nullptr;
     int nHeads0 = 0, kvMul = 1, hs = 0, kv0 = 0, seqLen = 0;
@@ -165,7 +156,7 @@ struct GemvArgs {
     const float2 *rope = nullptr; // [seqLen][hs/2] (cos, sin)
     const int *pos = nullptr;     // per batch row
     const int *slot = nullptr;
-    void *kcache = nullptr;       // layer base, blocked head-major (kvOff)
+    void *kcache = nullptr;       // layer base: [slot][nKv][seqLen][hs] (or a page pool: kvOff)
     void *vcache = nullptr;
     KvMap kvMap;
     int kvBf16 = 1;

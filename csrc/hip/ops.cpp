@@ -272,7 +272,7 @@ std::vector<float> qkvRope(const std::vector<uint8_t> &blocks, int q0, int kv0, 
     const DevQ40 w = uploadQ40(sc, blocks, rows, n);
     std::vector<int> slots(B);
     for (int b = 0; b < B; b++) slots[b] = b;
-    const size_t cacheElems = (size_t)B * hipk::kvSlotRows(seqLen) * kv0;
+    const size_t cacheElems = (size_t)B * seqLen * kv0;
     void *kc = kvBf16 ? (void *)sc.alloc<uint16_t>(cacheElems) : (void *)sc.alloc<float>(cacheElems);
     void *vc = kvBf16 ? (void *)sc.alloc<uint16_t>(cacheElems) : (void *)sc.alloc<float>(cacheElems);
     hipk::GemvArgs a;
@@ -350,9 +350,9 @@ std::vector<float> attention(const std::vector<float> &q, const std::vector<floa
         DL_CHECK(pos[b] >= 0 && pos[b] < seqLen && slot[b] >= 0 && slot[b] < nSlots, "attention row out of range");
     Scratch sc;
     auto cache = [&](const std::vector<float> &xs) -> void * {
-        // the caller's [slot][seqLen][kv0] rows -> the engine's blocked head-major layout (kvOff)
+        // the caller's [slot][seqLen][kv0] rows -> the engine's head-major [slot][nKv][seqLen][hs]
         const int nKv = kv0 / hs;
-        std::vector<float> x((size_t)nSlots * hipk::kvSlotRows(seqLen) * kv0);
+        std::vector<float> x(xs.size());
         for (int sl = 0; sl < nSlots; sl++)
             for (int p = 0; p < seqLen; p++)
                 for (int kh = 0; kh < nKv; kh++)
