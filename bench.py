@@ -194,8 +194,9 @@ def main() -> int:
         dist.init_process_group("gloo")
         from distributed_llama_multiusers_amd.parallel import init_device_comm
         vocab0 = -(-hdr["vocab_size"] // world)
-        comm, uid, comm_kind = init_device_comm(C, dist, rank, world, max_batch * max(hdr["dim"], vocab0), local,
-                                                comm_kind)
+        # largest single message: a batch's logits slices, or a --prefill-chunk forward's [chunk][dim]
+        max_floats = max(max_batch * max(hdr["dim"], vocab0), args.prefill_chunk * hdr["dim"])
+        comm, uid, comm_kind = init_device_comm(C, dist, rank, world, max_floats, local, comm_kind)
 
     long_pos = args.long_ctx if args.long_ctx > 0 else 0
     seq_len = max(args.max_seq_len, args.prompt + args.warmup + args.steps + 8)
@@ -206,15 +207,17 @@ def main() -> int:
 
     def make_engine(max_seq=seq_len, kv_bf16=True, sync=None):
         synthetic = None if args.model else dict(shape, seq_len=max_seq)
-        return C.HipEngine(args.model, "q80", max_seq_len=max_seq, max_batch=max_batch, n_slots=args.batch,
-                           kv_bf16=kv_bf16,
-                           gpu_index=local, use_graphs=not args.no_graphs, synthetic=synthetic, seed=1234, rank=rank,
-                           world=world, uid=uid, comm=comm, sync_type=sync or args.sync_type)
+        e = C.HipEngine(args.model, "q80", max_seq_len=max_seq, max_batch=max_batch, n_slots=args.batch,
+                        kv_bf16=kv_bf16,
+                        gpu_index=local, use_graphs=not args.no_graphs, synthetic=synthetic, seed=1234, rank=rank,
+                        world=world, uid=uid, comm=comm, sync_type=sync or args.sync_type)
+        if dist is not None:  # ranks build their engines seconds apart; start the next phase together
+            dist.barrier()
+        return e
 
     t0 = time.time()
     eng = make_engine()
     load_s = time.time() - t0
-    tp_fused = bool(eng.tp_fused) if world > 1 else None
     B = args.batch
 
     def barrier():
@@ -281,6 +284,7 @@ def main() -> int:
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
     barrier()
+    tp_fused = bool(eng.tp_fused) if world > 1 else None  # after the first forward's self-test
 
     long_ms = None
     if long_pos:  # decode at a long context, own engine sized for it (KV rows it never wrote are
@@ -363,6 +367,7 @@ def main() -> int:
                               kv_bf16=True, gpu_index=local, use_graphs=not args.no_graphs,
                               synthetic=None if args.model else dict(shape, seq_len=sl), seed=1234, rank=rank,
                               world=world, uid=uid, comm=comm, sync_type=args.sync_type)
+            barrier()
             p4k_big_ms = prefill(eng, args.prefill_chunk)
 
     if dist is not None:

@@ -327,10 +327,17 @@ void HipEngineImpl::tpFusedSelfTest() {
         DL_HIP(hipMemcpy(&v, errFlag, sizeof(int), hipMemcpyDeviceToHost));
         return v != 0;
     };
+    // the first pass is also the rendezvous: ranks reach their first forward seconds apart (model
+    // load / synthetic init time differs per rank), so the self-test waits up to 60 s for a peer
+    // instead of the data plane's 2 s
+    auto patient = [](hipk::TpXchg x) {
+        x.timeoutTicks = 6000LL * 1000 * 1000;
+        return x;
+    };
     std::vector<float> got;
     for (const hipk::TpXchg *x : {&tpVec_, &tpArg_}) {
         const int n = (int)std::min<long long>(4096, x->stride);
-        hipk::launchTpSelfTest(*x, dY_, n, (float)(me + 1), stream_);
+        hipk::launchTpSelfTest(patient(*x), dY_, n, (float)(me + 1), stream_);
         DL_HIP(hipStreamSynchronize(stream_));
         got.resize(n);
         DL_HIP(hipMemcpy(got.data(), dY_, n * sizeof(float), hipMemcpyDeviceToHost));
@@ -339,7 +346,7 @@ void HipEngineImpl::tpFusedSelfTest() {
     }
     if (timedOut()) ok = false;
     comm_->resetError();
-    hipk::launchTpSelfTest(tpVec_, dY_, 1, ok ? 1.f : 0.f, stream_);  // the verdicts (+ element 0's 0)
+    hipk::launchTpSelfTest(patient(tpVec_), dY_, 1, ok ? 1.f : 0.f, stream_);  // the verdicts (+ element 0's 0)
     DL_HIP(hipStreamSynchronize(stream_));
     float all = 0.f;
     DL_HIP(hipMemcpy(&all, dY_, sizeof(float), hipMemcpyDeviceToHost));

@@ -30,7 +30,7 @@ def test_same_gpu_rehearsal_self_launch_is_labelled():
     env = dict(os.environ, DL_BENCH_SAME_GPU="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--shape", "llama3_2_1b", "--steps", "8", "--warmup", "2",
-                        "--prompt", "32", "--long-ctx", "0", "--no-f32kv", "--no-prefill4k", "--no-cli"],
+                        "--prompt", "32", "--long-ctx", "0", "--no-f32kv", "--no-cli"],
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -40,3 +40,6 @@ def test_same_gpu_rehearsal_self_launch_is_labelled():
     cfg = res["config"]
     assert cfg["tp_ranks"] == 2 and cfg["tp_sync"] == "q80" and cfg["parallelism"] == "tp2"
     assert cfg["tp_f32_pred_ms_per_token"] > 0 and res["value"] > 0
+    # ranks reach their first forward seconds apart: the fused exchange's self-test must wait for them
+    assert cfg["tp_fused_exchange"] is True and "self-test failed" not in r.stderr, r.stderr[-3000:]
+    assert cfg["prompt_4k_eval_big_chunk_ms_per_token"] > 0  # --prefill-chunk rows fit the comm buffer
