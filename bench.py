@@ -175,6 +175,10 @@ def main() -> int:
     same_gpu = world > 1 and os.environ.get("DL_BENCH_SAME_GPU") == "1"
     if same_gpu:  # rehearsal of the multi-rank path on one GPU (not a scaling point)
         local = 0
+        # ranks sharing one GPU: a rank spinning in a collective can hold off its peer's wide
+        # prefill kernels past the 2 s peer timeout (seen from ~320 rows up), so the rehearsal
+        # prefills in chunks of <= 256 rows
+        args.prefill_chunk = min(args.prefill_chunk, 256)
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     dist = None
@@ -194,7 +198,8 @@ def main() -> int:
         dist.init_process_group("gloo")
         from distributed_llama_multiusers_amd.parallel import init_device_comm
         vocab0 = -(-hdr["vocab_size"] // world)
-        # largest single message: a batch's logits slices, or a --prefill-chunk forward's [chunk][dim]
+        # largest single message: a batch's logits slices (host logits) or a --prefill-chunk forward's
+        # [chunk][dim] partial sums (greedy rows exchange 2 floats per row)
         max_floats = max(max_batch * max(hdr["dim"], vocab0), args.prefill_chunk * hdr["dim"])
         comm, uid, comm_kind = init_device_comm(C, dist, rank, world, max_floats, local, comm_kind)
 

@@ -351,6 +351,10 @@ __device__ __forceinline__ void stageQ80(const GemvArgs &a, int8_t *sq, float2 *
 // granules in uncached memory: one relaxed system-scope store publishes data and flag together,
 // a relaxed system-scope load polls them (cdna_hip_programming.md Guideline 16 "R2": the data is
 // the flag, no fence needed); a wait gives up after tp.timeoutTicks and raises tp.error.
+// Every user keeps ONE epoch per exchange word (epochs[w] = the last epoch word w carried): every
+// write of a word then carries a larger epoch than any earlier write of it, whichever user (f32 or
+// Q80 rows, argmax winners, the self-test) or engine on the same comm wrote it, so a stale word
+// can never pass for a fresh one.
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t tpLoad(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -385,7 +389,7 @@ __device__ __forceinline__ void tpPushCollect(const TpXchg &x, long long w, unsi
                     __builtin_amdgcn_s_sleep(1);
                     v = tpLoad(mine + p * x.stride);
                     if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > x.timeoutTicks) {
-                        __hip_atomic_store(x.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __hip_atomic_store(x.error, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // 3: fused exchange
                         break;
                     }
                 }
@@ -458,13 +462,15 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
         bool live;
         const long long gb = blockId(blk, live);
         if (!live) continue;
-        const unsigned e = x.epochs[gb] + 1;
+        const long long wd = gb * 9 + w;
+        const unsigned e = x.epochs[wd] + 1;
         const unsigned payload = w < 8 ? reinterpret_cast<const uint32_t *>(q8)[blk * 8 + w] : dq[blk];
         unsigned v[kTpMaxRanks];
-        tpPushCollect(x, gb * 9 + w, e, payload, v, failed);
+        tpPushCollect(x, wd, e, payload, v, failed);
 #pragma unroll
         for (int p = 0; p < kTpMaxRanks; p++)
             if (p < W) rv[(p * nBlk + blk) * 9 + w] = v[p];
+        x.epochs[wd] = e;
     }
     __syncthreads();
     // 3. dequantize and sum in rank order
@@ -479,12 +485,6 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
             s += (float)q * d;
         }
         a.out[(size_t)b * a.ldOut + row] = s;
-    }
-    // 4. advance the block epochs (every word of step 2 has read them)
-    for (int blk = threadIdx.x; blk < nBlk; blk += kThreads) {
-        bool live;
-        const long long gb = blockId(blk, live);
-        if (live) x.epochs[gb] += 1;
     }
 }
 

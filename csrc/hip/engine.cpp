@@ -120,6 +120,7 @@ void HipEngineImpl::forward(int n, const int *tokens, const int *positions, cons
     inputsInFlight_ = false;
     if (root && logits) std::memcpy(logits, hLogits_, (size_t)n * h_.vocabSize * sizeof(float));
     stats_.computeMs = t.elapsedMs();
+    stats_.syncMs = std::min(stats_.syncMs, stats_.computeMs);  // the estimate never exceeds the forward
 }
 
 void HipEngineImpl::forwardArgmax(int n, const int *tokens, const int *positions, const int *slots, int *out) {
@@ -131,6 +132,7 @@ void HipEngineImpl::forwardArgmax(int n, const int *tokens, const int *positions
     inputsInFlight_ = false;
     std::memcpy(out, hIds_, n * sizeof(int));
     stats_.computeMs = t.elapsedMs();
+    stats_.syncMs = std::min(stats_.syncMs, stats_.computeMs);  // the estimate never exceeds the forward
 }
 
 void HipEngineImpl::forwardSample(int n, const int *tokens, const int *positions, const int *slots,
@@ -143,6 +145,7 @@ void HipEngineImpl::forwardSample(int n, const int *tokens, const int *positions
     inputsInFlight_ = false;
     std::memcpy(out, hIds_, n * sizeof(int));
     stats_.computeMs = t.elapsedMs();
+    stats_.syncMs = std::min(stats_.syncMs, stats_.computeMs);  // the estimate never exceeds the forward
 }
 
 // Pipelined serving: the forward and the D2H copy of its ids are enqueued; the host returns at
@@ -156,6 +159,7 @@ void HipEngineImpl::launchIds(int n, const int *tokens, const int *positions, co
     DL_HIP(hipMemcpyAsync(hIds_, dIds_, n * sizeof(int), hipMemcpyDeviceToHost, stream_));
     pendingN_ = n;
     stats_.computeMs = t.elapsedMs();
+    stats_.syncMs = std::min(stats_.syncMs, stats_.computeMs);  // the estimate never exceeds the forward
 }
 
 void HipEngineImpl::collectIds(int *out) {
@@ -242,7 +246,9 @@ void HipEngineImpl::syncAndCheckComm() {
                     "resident?)");
     }
     if (flag && *hErr_ != 0)
-        throw Error("tensor-parallel collective timed out: a peer rank did not arrive within 2 s (worker lost?)");
+        throw Error(std::string("tensor-parallel collective timed out: a peer rank did not arrive within 2 s (") +
+                    (*hErr_ == 1 ? "all-reduce / all-gather" : *hErr_ == 2 ? "low-latency all-reduce" : "fused exchange") +
+                    "; worker lost?)");
     if (comm_) {
         const std::string e = comm_->asyncError();
         if (!e.empty()) {
@@ -255,9 +261,9 @@ void HipEngineImpl::syncAndCheckComm() {
 // Tensor-parallel data-plane bytes of one forward of n rows on this rank, in the reference's
 // accounting (nn-network.cpp:493-508 counts socket payload): every residual update
 // sends this rank's partial [n][dim] to each peer and receives each peer's (Q80 blocks of 34 B per
-// 32 values with --sync-type q80, the reference's ZQ format, else f32), two per layer; greedy rows on
-// the fused exchange then trade one (value, index) winner per row, other rows gather the vocab
-// slices (to the root only for host logits / sampling). The transport's own framing (the 8-byte
+// 32 values with --sync-type q80, the reference's ZQ format, else f32), two per layer; greedy rows
+// then trade one (value, index) winner per row (in the fused exchange or one all-gather), host
+// logits and sampled rows gather the vocab slices to the root. The transport's own framing (the 8-byte
 // {value, epoch} words of the fused exchange) is not payload and not counted.
 void HipEngineImpl::accountForward(int n, GraphKind kind, int times) {
     stats_.sentBytes = stats_.recvBytes = 0;
@@ -267,15 +273,13 @@ void HipEngineImpl::accountForward(int n, GraphKind kind, int times) {
     const u64 row = syncQ80_ ? (u64)h_.dim / 32 * 34 : (u64)h_.dim * 4;
     u64 sent = 2ull * h_.nLayers * peers * (u64)n * row, recv = sent;
     const u64 slice = (u64)n * p.vocab0 * 4;
-    if (tpFused_ && (kind == GraphKind::ARGMAX || kind == GraphKind::CHAIN)) {
+    if (kind == GraphKind::ARGMAX || kind == GraphKind::CHAIN) {  // (value, index) winners only
         sent += peers * (u64)n * 8;
         recv += peers * (u64)n * 8;
-    } else if (kind == GraphKind::LOGITS || kind == GraphKind::SAMPLE) {
-        if (rank() == 0) recv += peers * slice;
-        else sent += slice;
-    } else {
-        sent += peers * slice;
+    } else if (rank() == 0) {  // LOGITS / SAMPLE: the vocab slices go to the root
         recv += peers * slice;
+    } else {
+        sent += slice;
     }
     stats_.sentBytes = sent * (u64)times;
     stats_.recvBytes = recv * (u64)times;
@@ -335,16 +339,27 @@ void HipEngineImpl::tpFusedSelfTest() {
         return x;
     };
     std::vector<float> got;
-    for (const hipk::TpXchg *x : {&tpVec_, &tpArg_}) {
-        const int n = (int)std::min<long long>(4096, x->stride);
-        hipk::launchTpSelfTest(patient(*x), dY_, n, (float)(me + 1), stream_);
+    std::string why = ok ? "" : "DL_TP_FUSED=fail";
+    for (int r = 0; r < 2; r++) {
+        const hipk::TpXchg &x = r == 0 ? tpVec_ : tpArg_;
+        const int n = (int)std::min<long long>(4096, x.stride);
+        hipk::launchTpSelfTest(patient(x), dY_, n, (float)(me + 1), stream_);
         DL_HIP(hipStreamSynchronize(stream_));
         got.resize(n);
         DL_HIP(hipMemcpy(got.data(), dY_, n * sizeof(float), hipMemcpyDeviceToHost));
-        for (int el = 0; el < n && ok; el++)
-            ok = got[el] == (float)(W * (W + 1) / 2) + (float)(W * (el & 1023));
+        for (int el = 0; el < n && ok; el++) {
+            const float want = (float)(W * (W + 1) / 2) + (float)(W * (el & 1023));
+            if (got[el] != want) {
+                ok = false;
+                why = "region " + std::to_string(r) + " element " + std::to_string(el) + ": got " +
+                      std::to_string(got[el]) + ", want " + std::to_string(want);
+            }
+        }
     }
-    if (timedOut()) ok = false;
+    if (timedOut()) {
+        ok = false;
+        why += " (a peer wait timed out)";
+    }
     comm_->resetError();
     hipk::launchTpSelfTest(patient(tpVec_), dY_, 1, ok ? 1.f : 0.f, stream_);  // the verdicts (+ element 0's 0)
     DL_HIP(hipStreamSynchronize(stream_));
@@ -354,7 +369,7 @@ void HipEngineImpl::tpFusedSelfTest() {
     comm_->resetError();
     if (allOk) return;
     std::fprintf(stderr, "⚠️  rank %d: fused tensor-parallel exchange self-test failed (%s); using the separate "
-                 "%s collectives\n", me, ok ? "on a peer" : "here", comm_->name().c_str());
+                 "%s collectives\n", me, ok ? "on a peer" : ("here: " + why).c_str(), comm_->name().c_str());
     tpFused_ = false;
     blockOn_ = false;  // the attention block's wo role was chosen for the fused exchange: decide again
     for (CtxBucket &b : buckets_) b.block = false;

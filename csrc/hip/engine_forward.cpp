@@ -477,10 +477,12 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
                  p.vocab0, nullptr);
     }
     const float *full = dLogits_;
-    // greedy rows on a fused TP data plane: each rank reduces its own vocab slice and only the
+    // greedy rows under tensor parallelism: each rank reduces its own vocab slice and only the
     // (value, index) winners cross the links (reference: logits gathered to the root,
-    // llm.cpp:432); the full logits are gathered only when the host samples them
-    const bool distArgmax = tpFused_ && (kind == GraphKind::ARGMAX || kind == GraphKind::CHAIN);
+    // llm.cpp:432) - inside the argmax kernel on the fused data plane, else as one all-gather of
+    // 2 floats per row; the full logits are gathered only when the host samples them
+    const bool greedy = kind == GraphKind::ARGMAX || kind == GraphKind::CHAIN;
+    const bool distArgmax = p.nRanks > 1 && greedy;
     // logits for the host (LOGITS) and sampled rows (SAMPLE) are needed on the root only: the
     // vocab slices are gathered to rank 0 (the reference's SYNC_NODE_SLICES_EXCEPT_ROOT), the
     // other ranks publish theirs and skip the unshard and the draw (the root's ids are used)
@@ -513,7 +515,8 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
         if (distArgmax) {
             g.vocab = p.vocab0;
             g.vocabStart = p.vocabStart();
-            g.tp = tpArg_;
+            if (tpFused_) g.tp = tpArg_;
+            else g.pairs = dArgPairs_;
         }
         g.ids = dIds_;
         g.partV = dArgV_;
@@ -527,6 +530,10 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
             g.seqLen = h_.seqLen;
         }
         hipk::launchArgmax(g, n, stream_);
+        if (g.pairs) {
+            comm_->allGather(dArgPairs_, dArgPairsAll_, 2 * (size_t)n, stream_);
+            hipk::launchArgmaxPick(g, dArgPairsAll_, n, p.nRanks, stream_);
+        }
     }
     DL_HIP(hipGetLastError());
 }

@@ -249,6 +249,7 @@ class HipEngineImpl : public HipEngine {
     float *dPartO_ = nullptr, *dPartML_ = nullptr;
     int *dAttCnt_ = nullptr, *dArgCnt_ = nullptr, *dArgI_ = nullptr;
     float *dArgV_ = nullptr;
+    float *dArgPairs_ = nullptr, *dArgPairsAll_ = nullptr;  // separate-collective TP argmax
     hipk::SampleScratch sampleScratch_;
     std::map<int, double> exchangeMs_;  // calibrated all-reduce ms per row count (exchangeMs)
 

@@ -173,6 +173,8 @@ void HipEngineImpl::allocBuffers() {
     if (p.nRanks > 1) {
         dLogitsAll_ = dalloc<float>((size_t)MB * h_.vocabSize);
         dLogitsFull_ = dalloc<float>((size_t)MB * h_.vocabSize);
+        dArgPairs_ = dalloc<float>((size_t)MB * 2);
+        dArgPairsAll_ = dalloc<float>((size_t)MB * 2 * p.nRanks);
     }
     setupBuckets();  // the largest bucket sizes the split-attention partials
     const int splitMax = buckets_.back().splitGrid;

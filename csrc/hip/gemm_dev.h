@@ -173,13 +173,15 @@ __device__ __forceinline__ void tpExchangeTile(const GemmArgs &ga, float *tile, 
         bool live;
         const long long gb = blockId(blk, live);
         if (!live) continue;
-        const unsigned e = x.epochs[gb] + 1;
+        const long long wd = gb * 9 + w;
+        const unsigned e = x.epochs[wd] + 1;
         const unsigned payload = w < 8 ? reinterpret_cast<const uint32_t *>(q8)[blk * 8 + w] : dq[blk];
         unsigned v[kTpMaxRanks];
-        tpPushCollect(x, gb * 9 + w, e, payload, v, failed);
+        tpPushCollect(x, wd, e, payload, v, failed);
 #pragma unroll
         for (int p = 0; p < kTpMaxRanks; p++)
             if (p < W) rv[(p * nBlk + blk) * 9 + w] = v[p];
+        x.epochs[wd] = e;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < nEl; i += kThreads) {
@@ -192,11 +194,6 @@ __device__ __forceinline__ void tpExchangeTile(const GemmArgs &ga, float *tile, 
             s += (float)q * d;
         }
         tile[i] = s;
-    }
-    for (int blk = threadIdx.x; blk < nBlk; blk += kThreads) {
-        bool live;
-        const long long gb = blockId(blk, live);
-        if (live) x.epochs[gb] += 1;
     }
     __syncthreads();
 }

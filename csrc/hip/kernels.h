@@ -337,6 +337,10 @@ struct ArgmaxArgs {
     // (value, index) winners are exchanged (tp.world > 1) and every rank picks the same global one
     TpXchg tp;
     int vocabStart = 0;
+    // tensor parallel over separate collectives: the row's slice winner {value, global index bits}
+    // goes to pairs[2b .. 2b+1] and nothing else; after an all-gather of the pairs,
+    // launchArgmaxPick picks the same global winner on every rank
+    float *pairs = nullptr;
 };
 // Device sampling of B rows of full-vocabulary logits (the reference's Sampler::sample:
 // logits / temperature -> softmax -> coin -> multinomial in index order, or top-p: candidates
@@ -381,6 +385,8 @@ void launchSample(const SampleArgs &a, int B, hipStream_t s);
 // exchange) - used ahead of a plain all-reduce when the fused exchange is not available.
 void launchQ80Roundtrip(float *x, size_t n, hipStream_t s);
 void launchArgmax(const ArgmaxArgs &a, int B, hipStream_t s);
+// all[p * 2B + 2b ..]: rank p's pairs of row b (ArgmaxArgs::pairs, all-gathered over W ranks)
+void launchArgmaxPick(const ArgmaxArgs &a, const float *all, int B, int W, hipStream_t s);
 // logits gathered rank-major [nRanks][B][vocab0] -> row-major [B][vocab]
 void launchUnshardLogits(const float *in, float *out, int nRanks, int B, int vocab0, hipStream_t s);
 

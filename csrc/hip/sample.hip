@@ -29,6 +29,17 @@ __device__ __forceinline__ void blockArgmax(float &bv, int &bi, float *sv, int *
 
 constexpr int kArgmaxBlocks = 64;
 
+// The row's winner: ids, and for a chained decode the next step's token / position / history.
+__device__ __forceinline__ void argmaxStore(const ArgmaxArgs &a, int b, int bi) {
+    a.ids[b] = bi;
+    if (a.tokens) {
+        const int p = a.pos[b];
+        a.hist[(size_t)b * a.seqLen + p] = bi;
+        a.tokens[b] = bi;
+        a.pos[b] = p + 1;
+    }
+}
+
 // grid (kArgmaxBlocks, B): each workgroup reduces a slice; the last arriver reduces the partials.
 __global__ __launch_bounds__(256) void argmaxKernel(ArgmaxArgs a) {
     __shared__ float sv[4];
@@ -72,33 +83,48 @@ __global__ __launch_bounds__(256) void argmaxKernel(ArgmaxArgs a) {
         argBetter(bv, bi, __hip_atomic_load(a.partV + b * kArgmaxBlocks + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                   __hip_atomic_load(a.partI + b * kArgmaxBlocks + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     blockArgmax(bv, bi, sv, si);
+    if (a.pairs) {
+        if (threadIdx.x == 0) {
+            a.pairs[2 * b] = bv;
+            a.pairs[2 * b + 1] = __int_as_float(bi + a.vocabStart);
+        }
+        return;
+    }
     if (threadIdx.x == 0 && a.tp.world > 1) {
         // tensor parallel: every rank offers its slice's winner (value, global index); all ranks
         // pick the same one in rank order (ties -> lowest index, like a full-vocabulary argmax)
         const TpXchg &x = a.tp;
         const bool failed = tpFailed(x);
-        const unsigned e = x.epochs[b] + 1;
+        const unsigned ev = x.epochs[2 * b] + 1, ei = x.epochs[2 * b + 1] + 1;  // one epoch per word
         unsigned vv[kTpMaxRanks], vi[kTpMaxRanks];
-        tpPushCollect(x, 2LL * b, e, __float_as_uint(bv), vv, failed);
-        tpPushCollect(x, 2LL * b + 1, e, (unsigned)(bi + a.vocabStart), vi, failed);
+        tpPushCollect(x, 2LL * b, ev, __float_as_uint(bv), vv, failed);
+        tpPushCollect(x, 2LL * b + 1, ei, (unsigned)(bi + a.vocabStart), vi, failed);
         bv = -INFINITY;
         bi = 0x7fffffff;
         for (int p = 0; p < x.world; p++) argBetter(bv, bi, __uint_as_float(vv[p]), (int)vi[p]);
-        x.epochs[b] = e;
+        x.epochs[2 * b] = ev;
+        x.epochs[2 * b + 1] = ei;
     }
-    if (threadIdx.x == 0) {
-        a.ids[b] = bi;
-        if (a.tokens) {
-            const int p = a.pos[b];
-            a.hist[(size_t)b * a.seqLen + p] = bi;
-            a.tokens[b] = bi;
-            a.pos[b] = p + 1;
-        }
-    }
+    if (threadIdx.x == 0) argmaxStore(a, b, bi);
+}
+
+// One thread per row: the global winner of the all-gathered per-rank pairs, in rank order.
+__global__ __launch_bounds__(64) void argmaxPickKernel(ArgmaxArgs a, const float *all, int B, int W) {
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= B) return;
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int p = 0; p < W; p++)
+        argBetter(bv, bi, all[(size_t)p * 2 * B + 2 * b], __float_as_int(all[(size_t)p * 2 * B + 2 * b + 1]));
+    argmaxStore(a, b, bi);
 }
 
 void launchArgmax(const ArgmaxArgs &a, int B, hipStream_t s) {
     hipLaunchKernelGGL(argmaxKernel, dim3(kArgmaxBlocks, B), dim3(256), 0, s, a);
+}
+
+void launchArgmaxPick(const ArgmaxArgs &a, const float *all, int B, int W, hipStream_t s) {
+    hipLaunchKernelGGL(argmaxPickKernel, dim3((B + 63) / 64), dim3(64), 0, s, a, all, B, W);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -235,7 +235,7 @@ __global__ __launch_bounds__(kThreads) void xgmiLLKernel(XgmiCall a, unsigned *l
                     __builtin_amdgcn_s_sleep(1);
                     x = __hip_atomic_load(mine + (size_t)p * kLLMax + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     if (rtClock() - t0 > a.timeoutTicks) {  // a peer never arrived: flag it, stop waiting
-                        __hip_atomic_store(a.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __hip_atomic_store(a.error, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                         break;
                     }
                 }

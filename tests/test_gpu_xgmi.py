@@ -50,9 +50,10 @@ def _setup(rank, world, port, max_floats):
 
 def _collectives(rank, world, port, q):
     try:
-        C, comm, dist = _setup(rank, world, port, 1 << 17)
+        big = [(1 << 20) + 7] if world == 2 else []  # a 1024-row prefill's [rows][dim] partials
+        C, comm, dist = _setup(rank, world, port, (1 << 21) if big else (1 << 17))
         for it in range(3):
-            for n in SIZES:
+            for n in SIZES + big:
                 xs = [np.random.default_rng(1000 * it + 10 * p + n).standard_normal(n).astype(np.float32)
                       for p in range(world)]
                 ref = np.zeros(n, np.float32)
@@ -131,6 +132,28 @@ def _engine_tp_sample(rank, world, port, model, tokens, temps, topps, coins, q):
             raise AssertionError("a flag wait timed out")
         dist.barrier()
         q.put((rank, (got, lg if rank == 0 else None)))
+    except Exception as e:
+        q.put((rank, repr(e)))
+
+
+def _engines_one_comm(rank, world, port, model, tokens, q):
+    """Engines built one after another on ONE comm (as bench.py does), alternating the exchange's
+    wire format: every engine's fused-exchange self-test must pass and the q80 engines must decode
+    the same tokens (the comm's exchange words carry epochs from every earlier engine)."""
+    try:
+        C, comm, dist = _setup(rank, world, port, 1 << 16)
+        out = []
+        for sync in ("q80", "f32", "q80"):
+            eng = C.HipEngine(model, "q80", kv_bf16=True, rank=rank, world=world, comm=comm, sync_type=sync,
+                              max_batch=8, n_slots=1)
+            eng.forward_argmax(tokens, list(range(len(tokens))), [0] * len(tokens))
+            _, toks = eng.decode_greedy(6, [tokens[-1]], [len(tokens)], [0])
+            out.append((bool(eng.tp_fused), list(toks)))
+            del eng
+            dist.barrier()
+        if comm.timed_out():
+            raise AssertionError("a flag wait timed out")
+        q.put((rank, out))
     except Exception as e:
         q.put((rank, repr(e)))
 
@@ -523,3 +546,19 @@ def test_fused_exchange_self_test_fallback(C, tmp_path):
     assert a[0][2] is False and a[1][2] is False and c[0][2] is True and c[1][2] is True
     assert np.array_equal(a[0][0], b[0][0]) and a[0][1] == b[0][1] and a[0][3] == b[0][3]
     assert a[0][1] == c[0][1] and a[0][3][:4] == c[0][3][:4]
+
+
+def test_fused_exchange_engines_share_a_comm(C, tmp_path):
+    """Exchange words keep one epoch each, whichever user wrote them last (f32 rows, Q80 blocks,
+    argmax winners, the self-test): engines of either wire format built in turn on the same comm
+    keep the fused exchange (their self-tests pass) and decode the same tokens."""
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=12, dim=512, n_heads=8,
+                               n_kv_heads=4, hidden_dim=1024, vocab_size=1024)
+    tokens = [int(t) for t in np.random.default_rng(7).integers(0, 1024, 8)]
+    res = _run(_engines_one_comm, 2, m, tokens)
+    assert all(isinstance(v, list) for v in res.values()), res
+    for r in (0, 1):
+        assert [f for f, _ in res[r]] == [True, True, True], res
+        assert res[r][0][1] == res[r][2][1] == res[0][0][1], res
