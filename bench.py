@@ -175,10 +175,10 @@ def main() -> int:
     same_gpu = world > 1 and os.environ.get("DL_BENCH_SAME_GPU") == "1"
     if same_gpu:  # rehearsal of the multi-rank path on one GPU (not a scaling point)
         local = 0
-        # ranks sharing one GPU: a rank spinning in a collective can hold off its peer's wide
-        # prefill kernels past the 2 s peer timeout (seen from ~320 rows up), so the rehearsal
-        # prefills in chunks of <= 256 rows
-        args.prefill_chunk = min(args.prefill_chunk, 256)
+        # ranks sharing one GPU: with 256+ prompt rows per forward a rank's kernels spinning on a
+        # peer (argmax winners, all-reduce flags) can keep that peer's kernels from being
+        # dispatched until the wait gives up, so the rehearsal keeps to the 32-row prompt chunks
+        args.prefill_chunk = 32
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     dist = None

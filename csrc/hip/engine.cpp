@@ -246,7 +246,7 @@ void HipEngineImpl::syncAndCheckComm() {
                     "resident?)");
     }
     if (flag && *hErr_ != 0)
-        throw Error(std::string("tensor-parallel collective timed out: a peer rank did not arrive within 2 s (") +
+        throw Error(std::string("tensor-parallel collective timed out: a peer rank did not arrive in time (2 s; 20 s for ranks sharing a GPU; ") +
                     (*hErr_ == 1 ? "all-reduce / all-gather" : *hErr_ == 2 ? "low-latency all-reduce" : "fused exchange") +
                     "; worker lost?)");
     if (comm_) {

@@ -62,6 +62,10 @@ constexpr int kLLSlots = kLLMax / kChunk;
 constexpr long long kFusedVec = 1 << 18;
 constexpr long long kFusedArg = 2048;      // fused argmax exchange: 2 words per batch row
 constexpr long long kTimeoutTicks = 200LL * 1000 * 1000;  // 2 s at 100 MHz
+// ranks sharing one GPU (rehearsals, tests) time-share its CUs: a rank spinning in a collective
+// can hold off its peer's kernels for seconds (seen: 2-4 s around wide prefill launches), so
+// their waits give up after 20 s instead
+constexpr long long kSharedTimeoutTicks = 2000LL * 1000 * 1000;
 
 struct XgmiPeers {
     float *pub[kMaxRanks];          // each rank's pub base (pub[p] + parity * maxFloats)
@@ -342,7 +346,7 @@ class XgmiComm : public DeviceComm {
         x->epochs = region == 0 ? fusedEpochs_ : fusedEpochs_ + kFusedVec;
         x->error = error_;
         x->stride = region == 0 ? kFusedVec : kFusedArg;
-        x->timeoutTicks = kTimeoutTicks;
+        x->timeoutTicks = timeoutTicks();
         x->rank = rank_;
         x->world = world_;
         return true;
@@ -367,6 +371,7 @@ class XgmiComm : public DeviceComm {
         const char *e = std::getenv("DL_XGMI_FENCE");
         return !(e && *e == '0');
     }
+    long long timeoutTicks() const { return sameDevice_ > 1 ? kSharedTimeoutTicks : kTimeoutTicks; }
     static bool pullOnly() {  // DL_XGMI_LL=0: always the pull protocol (comparison runs)
         static const bool v = [] {
             const char *e = std::getenv("DL_XGMI_LL");
@@ -388,7 +393,7 @@ class XgmiComm : public DeviceComm {
         c.gather = gather;
         const char *fe = std::getenv("DL_XGMI_FENCE");
         c.fenced = fenced_ || (fe && *fe == '1') ? 1 : 0;
-        c.timeoutTicks = kTimeoutTicks;
+        c.timeoutTicks = timeoutTicks();
         return c;
     }
     void launchLL(float *buf, size_t n, hipStream_t s) {

@@ -42,4 +42,4 @@ def test_same_gpu_rehearsal_self_launch_is_labelled():
     assert cfg["tp_f32_pred_ms_per_token"] > 0 and res["value"] > 0
     # ranks reach their first forward seconds apart: the fused exchange's self-test must wait for them
     assert cfg["tp_fused_exchange"] is True and "self-test failed" not in r.stderr, r.stderr[-3000:]
-    assert cfg["prompt_4k_eval_big_chunk_ms_per_token"] > 0  # --prefill-chunk rows fit the comm buffer
+    assert cfg["prompt_4k_eval_ms_per_token"] > 0

@@ -430,7 +430,7 @@ def test_data_plane_bytes_reported(tmp_path):
 
 def test_stalled_worker_gives_clean_root_error(tmp_path):
     """Fault injection: a GPU worker frozen mid-decode (SIGSTOP, sockets stay open)
-    must make the root fail cleanly - its xGMI collectives stop waiting after 2 s, raise the error
+    must make the root fail cleanly - its xGMI collectives stop waiting (2 s across GPUs, 20 s on one), raise the error
     flag, and the engine turns it into an exception - instead of hanging or printing tokens computed
     without the peer's partial sums."""
     import signal
