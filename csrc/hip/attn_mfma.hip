@@ -42,9 +42,7 @@ __device__ __forceinline__ int amSwz(int r) { return ((r & 3) << 2) | ((r >> 2) 
 // (cdna_hip_programming.md T10), instead of 2-way for adjacent row blocks.
 __host__ __device__ __forceinline__ int amKey(int u, int m) { return 16 * u + 8 * ((m >> 2) & 1) + 4 * (m >> 3) + (m & 3); }
 
-// TR: V^T fragments by the hardware transpose read (default); false: 8 scalar 16-bit LDS reads per
-// fragment (DL_ATTN_TR=0, a cross-check of the transposed-read addressing).
-template <int KM, bool TR>
+template <int KM>
 __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
     constexpr int HS = kAmHS, DS = HS / 32, NT = HS / 16;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -195,19 +193,10 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
             s16x4 vv[2];
 #pragma unroll
             for (int u = 0; u < 2; u++) {
-                if constexpr (TR) {
-                    const int r = amKey(u, 4 * h + tq);
-                    const char *ad = vb + r * 256 + 16 * ((2 * n + (tp >> 1)) ^ amSwz(r)) + 8 * (tp & 1);
-                    vv[u] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        reinterpret_cast<__attribute__((address_space(3))) s16x4 *>(reinterpret_cast<uintptr_t>(ad)));
-                } else {
-#pragma unroll
-                    for (int e = 0; e < 4; e++) {
-                        const int r = amKey(u, 4 * h + e);
-                        vv[u][e] = *reinterpret_cast<const short *>(vb + r * 256 + 16 * ((2 * n + (col >> 3)) ^ amSwz(r)) +
-                                                                    2 * (col & 7));
-                    }
-                }
+                const int r = amKey(u, 4 * h + tq);
+                const char *ad = vb + r * 256 + 16 * ((2 * n + (tp >> 1)) ^ amSwz(r)) + 8 * (tp & 1);
+                vv[u] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    reinterpret_cast<__attribute__((address_space(3))) s16x4 *>(reinterpret_cast<uintptr_t>(ad)));
             }
             // whole-register bit casts (per-element short -> __bf16 inserts were miscompiled by
             // ROCm 7.2's hipcc into a broadcast of element 0: scripts/probe_attn.hip)
@@ -560,22 +549,20 @@ bool attnUsesMfma(const AttnArgs &a) {
     return a.mfma >= 0 ? a.mfma == 1 : a.seqLen >= 1024;
 }
 
-static bool attnTrRead() { return true; }  // the scalar-read variant stays compiled as a cross-check
 
 // preloadModules(): one kernel of this translation unit's code object
-const void *attnMfmaModuleKernel() { return (const void *)attnDecodeMfmaKernel<4, true>; }
+const void *attnMfmaModuleKernel() { return (const void *)attnDecodeMfmaKernel<4>; }
 
 void launchAttentionMfma(const AttnArgs &a, int B, hipStream_t s) {
     const dim3 grid(a.nHeads0 / a.kvMul, a.splitGrid, B);
     if (2 * a.kvMul * a.splitGrid * 4 + 4096 > (int)kAmLds) throw Error("attention split grid too large");
-#define DL_AM_CASE(K, T)                                                                          \
-    if (a.kvMul == K && attnTrRead() == T) {                                                      \
-        allowLds((const void *)attnDecodeMfmaKernel<K, T>, kAmLds);                               \
-        hipLaunchKernelGGL((attnDecodeMfmaKernel<K, T>), grid, dim3(kAmThreads), kAmLds, s, a);   \
+#define DL_AM_CASE(K)                                                                             \
+    if (a.kvMul == K) {                                                                           \
+        allowLds((const void *)attnDecodeMfmaKernel<K>, kAmLds);                                  \
+        hipLaunchKernelGGL((attnDecodeMfmaKernel<K>), grid, dim3(kAmThreads), kAmLds, s, a);      \
         return;                                                                                   \
     }
-    DL_AM_CASE(1, true) DL_AM_CASE(2, true) DL_AM_CASE(4, true) DL_AM_CASE(8, true)
-    DL_AM_CASE(1, false) DL_AM_CASE(2, false) DL_AM_CASE(4, false) DL_AM_CASE(8, false)
+    DL_AM_CASE(1) DL_AM_CASE(2) DL_AM_CASE(4) DL_AM_CASE(8)
 #undef DL_AM_CASE
     throw Error("launchAttentionMfma: unsupported kvMul");
 }
