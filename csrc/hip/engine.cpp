@@ -178,7 +178,15 @@ double HipEngineImpl::decodeGreedyBatch(int steps, int nSeq, const int *tokens, 
     if (!tpTested_) tpFusedSelfTest();
     exchangeMs(nSeq);  // calibrated outside the timed chain
     setInputs(nSeq, tokens, pos, slots, nullptr, steps - 1);
-    DL_HIP(hipMemsetAsync(dHist_, 0xff, sizeof(int) * (size_t)cfg_.maxBatch * h_.seqLen, stream_));
+    // the history window the chain writes: rows 0..nSeq, positions [p0, p1) (not the whole
+    // maxBatch x seqLen buffer: 16 MB at a 131072-position capacity, set and copied every call)
+    int p0 = pos[0], p1 = pos[0] + steps;
+    for (int b = 1; b < nSeq; b++) {
+        p0 = std::min(p0, pos[b]);
+        p1 = std::max(p1, pos[b] + steps);
+    }
+    const size_t pitch = sizeof(int) * (size_t)h_.seqLen, width = sizeof(int) * (size_t)(p1 - p0);
+    DL_HIP(hipMemset2DAsync(dHist_ + p0, pitch, 0xff, width, nSeq, stream_));
     hipEvent_t e0, e1;
     DL_HIP(hipEventCreate(&e0));
     DL_HIP(hipEventCreate(&e1));
@@ -195,10 +203,11 @@ double HipEngineImpl::decodeGreedyBatch(int steps, int nSeq, const int *tokens, 
     syncAndCheckComm();
     inputsInFlight_ = false;
     if (outTokens) {
-        std::vector<int> hist((size_t)cfg_.maxBatch * h_.seqLen);
-        DL_HIP(hipMemcpy(hist.data(), dHist_, hist.size() * sizeof(int), hipMemcpyDeviceToHost));
+        const int w = p1 - p0;
+        std::vector<int> hist((size_t)nSeq * w);
+        DL_HIP(hipMemcpy2D(hist.data(), width, dHist_ + p0, pitch, width, nSeq, hipMemcpyDeviceToHost));
         for (int b = 0; b < nSeq; b++)
-            for (int s = 0; s < steps; s++) outTokens[b * steps + s] = hist[(size_t)b * h_.seqLen + pos[b] + s];
+            for (int s = 0; s < steps; s++) outTokens[b * steps + s] = hist[(size_t)b * w + pos[b] - p0 + s];
     }
     return ms;
 }
