@@ -17,10 +17,11 @@
 
 using namespace dl;
 
+// The reference's per-token line (dllama.cpp:57-64, 86-93) with its integer milliseconds widened to
+// two decimals: a GPU token takes ~1 ms. Sync is measured on the device (the exchanges' spans).
 static void printStatsLine(const char *kind, double ms, const ForwardStats &s, const std::string &tail) {
-    std::printf("%s%5u ms Sync%5u ms | Sent%6llu kB Recv%6llu kB | %s\n", kind, (unsigned)(ms - s.syncMs),
-                (unsigned)s.syncMs, (unsigned long long)(s.sentBytes / 1024), (unsigned long long)(s.recvBytes / 1024),
-                tail.c_str());
+    std::printf("%s%8.2f ms Sync%7.2f ms | Sent%6llu kB Recv%6llu kB | %s\n", kind, ms - s.syncMs, s.syncMs,
+                (unsigned long long)(s.sentBytes / 1024), (unsigned long long)(s.recvBytes / 1024), tail.c_str());
 }
 
 static int sampleOne(InferenceSession &sess, int token, int pos, std::vector<float> &logits, double &ms) {

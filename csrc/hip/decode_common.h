@@ -399,6 +399,19 @@ __device__ __forceinline__ void tpPushCollect(const TpXchg &x, long long w, unsi
     }
 }
 
+// Measured sync: a workgroup's exchange span (ticks of s_memrealtime, 10 ns) raised into x.ticks
+// by thread 0 once every thread of the workgroup is past its collect (the caller's barrier).
+__device__ __forceinline__ long long tpSpanBegin(const TpXchg &x) {
+    return x.ticks ? (long long)__builtin_amdgcn_s_memrealtime() : 0ll;
+}
+__device__ __forceinline__ void tpSpanEnd(const TpXchg &x, long long t0) {
+    if (x.ticks && threadIdx.x == 0) {
+        const long long dt = (long long)__builtin_amdgcn_s_memrealtime() - t0;
+        __hip_atomic_fetch_max(x.ticks, (unsigned)(dt > 0xFFFFFFFFll ? 0xFFFFFFFFll : dt), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // LDS bytes of the Q80 exchange staging for nEl elements over W ranks.
 __host__ __device__ static inline size_t tpQ80Lds(int nEl, int W) {
     return alignUp((size_t)nEl, 16) + alignUp((size_t)nEl / 32 * 4, 16) + (size_t)W * (nEl / 32) * 9 * 4;
@@ -409,6 +422,7 @@ template <int B>
 __device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *res, int R, int rowBase) {
     const TpXchg &x = a.tp;
     const bool failed = tpFailed(x);
+    const long long t0 = tpSpanBegin(x);
     for (int i = threadIdx.x; i < B * R; i += kThreads) {
         const int b = i / R, row = rowBase + i % R;
         if (row >= a.rows) continue;
@@ -423,6 +437,10 @@ __device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *re
         a.out[el] = s;
         x.epochs[el] = e;
     }
+    if (x.ticks) {
+        __syncthreads();
+        tpSpanEnd(x, t0);
+    }
 }
 
 // Q80 exchange (the reference's ZQ pipe: every rank's partial quantized once to Q80 blocks of 32
@@ -436,6 +454,7 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
     uint32_t *dq = reinterpret_cast<uint32_t *>(lds + alignUp((size_t)nEl, 16));
     uint32_t *rv = reinterpret_cast<uint32_t *>(lds + alignUp((size_t)nEl, 16) + alignUp((size_t)nBlk * 4, 16));
     const bool failed = tpFailed(x);
+    const long long t0 = tpSpanBegin(x);
     // 1. quantize this rank's partial (whole 32-lane groups per block: the loop is uniform)
     for (int base = 0; base < nEl; base += kThreads) {
         const int i = base + threadIdx.x;
@@ -473,6 +492,7 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
         x.epochs[wd] = e;
     }
     __syncthreads();
+    tpSpanEnd(x, t0);
     // 3. dequantize and sum in rank order
     for (int i = threadIdx.x; i < nEl; i += kThreads) {
         const int b = i / R, row = rowBase + i % R, blk = i >> 5;

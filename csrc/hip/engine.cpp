@@ -42,11 +42,12 @@ HipEngineImpl::HipEngineImpl(const EngineConfig &cfg, DeviceComm *comm) : cfg_(c
     DL_CHECK(cfg.maxBatch >= 1 && cfg.nSlots >= 1, "maxBatch/nSlots");
     kvBf16_ = cfg.kvBf16;
     syncQ80_ = cfg.syncType == FloatType::Q80;
+    decodeRows_ = (int)(cfg.maxDecode ? std::min(cfg.maxDecode, cfg.maxBatch) : cfg.maxBatch);
     if (comm_ && plan_.nRanks > 1) {
         const char *e = std::getenv("DL_TP_FUSED");  // 0: separate all-reduce kernels (comparison)
         tpFused_ = !(e && *e == '0') && comm_->fusedXchg(0, &tpVec_) && comm_->fusedXchg(1, &tpArg_) &&
                    (size_t)std::min<u32>(cfg.maxBatch, 4) * h_.dim <= (size_t)tpVec_.stride &&
-                   (size_t)2 * cfg.maxBatch <= (size_t)tpArg_.stride;
+                   (size_t)2 * decodeRows_ <= (size_t)tpArg_.stride;  // larger argmax forwards: all-gather
         tpVec_.q80 = syncQ80_ ? 1 : 0;
     }
     checkFits();
@@ -120,7 +121,7 @@ void HipEngineImpl::forward(int n, const int *tokens, const int *positions, cons
     inputsInFlight_ = false;
     if (root && logits) std::memcpy(logits, hLogits_, (size_t)n * h_.vocabSize * sizeof(float));
     stats_.computeMs = t.elapsedMs();
-    stats_.syncMs = std::min(stats_.syncMs, stats_.computeMs);  // the estimate never exceeds the forward
+    stats_.syncMs = std::min(readSyncMs(), stats_.computeMs);
 }
 
 void HipEngineImpl::forwardArgmax(int n, const int *tokens, const int *positions, const int *slots, int *out) {
@@ -132,7 +133,7 @@ void HipEngineImpl::forwardArgmax(int n, const int *tokens, const int *positions
     inputsInFlight_ = false;
     std::memcpy(out, hIds_, n * sizeof(int));
     stats_.computeMs = t.elapsedMs();
-    stats_.syncMs = std::min(stats_.syncMs, stats_.computeMs);  // the estimate never exceeds the forward
+    stats_.syncMs = std::min(readSyncMs(), stats_.computeMs);
 }
 
 void HipEngineImpl::forwardSample(int n, const int *tokens, const int *positions, const int *slots,
@@ -145,7 +146,7 @@ void HipEngineImpl::forwardSample(int n, const int *tokens, const int *positions
     inputsInFlight_ = false;
     std::memcpy(out, hIds_, n * sizeof(int));
     stats_.computeMs = t.elapsedMs();
-    stats_.syncMs = std::min(stats_.syncMs, stats_.computeMs);  // the estimate never exceeds the forward
+    stats_.syncMs = std::min(readSyncMs(), stats_.computeMs);
 }
 
 // Pipelined serving: the forward and the D2H copy of its ids are enqueued; the host returns at
@@ -158,8 +159,7 @@ void HipEngineImpl::launchIds(int n, const int *tokens, const int *positions, co
     runGraph(n, specs ? GraphKind::SAMPLE : GraphKind::ARGMAX);
     DL_HIP(hipMemcpyAsync(hIds_, dIds_, n * sizeof(int), hipMemcpyDeviceToHost, stream_));
     pendingN_ = n;
-    stats_.computeMs = t.elapsedMs();
-    stats_.syncMs = std::min(stats_.syncMs, stats_.computeMs);  // the estimate never exceeds the forward
+    stats_.computeMs = t.elapsedMs();  // host enqueue time; the sync is read when collected
 }
 
 void HipEngineImpl::collectIds(int *out) {
@@ -169,14 +169,14 @@ void HipEngineImpl::collectIds(int *out) {
     syncAndCheckComm();
     inputsInFlight_ = false;
     std::memcpy(out, hIds_, n * sizeof(int));
+    stats_.syncMs = readSyncMs();
 }
 
 double HipEngineImpl::decodeGreedyBatch(int steps, int nSeq, const int *tokens, const int *pos, const int *slots,
                                         int *outTokens) {
-    DL_CHECK(nSeq >= 1 && (u32)nSeq <= cfg_.maxBatch, "nSeq");
+    DL_CHECK(nSeq >= 1 && nSeq <= decodeRows_, "nSeq exceeds the engine's decode rows (max_decode)");
     for (int b = 0; b < nSeq; b++) DL_CHECK((u32)(pos[b] + steps) <= h_.seqLen, "decode exceeds seqLen");
     if (!tpTested_) tpFusedSelfTest();
-    exchangeMs(nSeq);  // calibrated outside the timed chain
     setInputs(nSeq, tokens, pos, slots, nullptr, steps - 1);
     // the history window the chain writes: rows 0..nSeq, positions [p0, p1) (not the whole
     // maxBatch x seqLen buffer: 16 MB at a 131072-position capacity, set and copied every call)
@@ -202,6 +202,7 @@ double HipEngineImpl::decodeGreedyBatch(int steps, int nSeq, const int *tokens, 
     (void)hipEventDestroy(e1);
     syncAndCheckComm();
     inputsInFlight_ = false;
+    stats_.syncMs = std::min(readSyncMs() * steps, (double)ms);  // the last step's exchanges x steps
     if (outTokens) {
         const int w = p1 - p0;
         std::vector<int> hist((size_t)nSeq * w);
@@ -292,33 +293,25 @@ void HipEngineImpl::accountForward(int n, GraphKind kind, int times) {
     }
     stats_.sentBytes = sent * (u64)times;
     stats_.recvBytes = recv * (u64)times;
-    // sync time estimate: the exchanges run inside the forward's graph (no host-visible boundary),
-    // so each is priced at the calibrated cost of one all-reduce of the same rows
-    stats_.syncMs = exchangeMs(n) * (2.0 * h_.nLayers + 1.0) * times;
 }
 
-// Device time of one all-reduce of n rows on this engine's transport, measured once per row count
-// (8 back-to-back calls on the idle stream). Every rank runs the same forwards in the same order,
-// so every rank calibrates at the same point; dY_ is free before a forward (layer 0 reads no delta).
-double HipEngineImpl::exchangeMs(int n) {
-    if (plan_.nRanks <= 1) return 0;
-    auto it = exchangeMs_.find(n);
-    if (it != exchangeMs_.end()) return it->second;
-    const size_t count = (size_t)n * h_.dim;
-    allReduce(dY_, count);  // warm
-    hipEvent_t e0, e1;
-    DL_HIP(hipEventCreate(&e0));
-    DL_HIP(hipEventCreate(&e1));
-    DL_HIP(hipEventRecord(e0, stream_));
-    for (int i = 0; i < 8; i++) allReduce(dY_, count);
-    DL_HIP(hipEventRecord(e1, stream_));
-    DL_HIP(hipEventSynchronize(e1));
-    float ms = 0;
-    DL_HIP(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    return exchangeMs_[n] = ms / 8.0;
+// Measured sync of the last forward (the host copy of its slots, enqueued by runGraph): per
+// exchange the slowest workgroup's fused-exchange span, or the stamped span of a separate
+// collective (launch gaps included), summed over the forward's exchanges. The reference times its
+// sync steps the same way, per forward (nn-executor.cpp:150-155, printed per token dllama.cpp:57-64).
+double HipEngineImpl::readSyncMs() const {
+    if (plan_.nRanks <= 1 || !hSync_) return 0;
+    const int S = syncSlots();
+    const unsigned long long *st = reinterpret_cast<const unsigned long long *>(hSync_ + S);
+    double ticks = 0;
+    for (int i = 0; i < S; i++) {
+        ticks += hSync_[i];
+        if (st[2 * i] && st[2 * i + 1] > st[2 * i]) ticks += (double)(st[2 * i + 1] - st[2 * i]);
+    }
+    return ticks * 1e-5;  // s_memrealtime: 100 MHz
 }
+
+void HipEngineImpl::launchStampAt(unsigned long long *p) { hipk::launchStamp(p, stream_); }
 
 // The first forward of a tensor-parallel engine with the fused exchange runs its self-test on the
 // real devices (every rank reaches this point in the same forward: the ranks run forwards in
@@ -351,7 +344,8 @@ void HipEngineImpl::tpFusedSelfTest() {
     std::string why = ok ? "" : "DL_TP_FUSED=fail";
     for (int r = 0; r < 2; r++) {
         const hipk::TpXchg &x = r == 0 ? tpVec_ : tpArg_;
-        const int n = (int)std::min<long long>(4096, x.stride);
+        // dY_ holds maxBatch x dim floats: a small engine tests fewer elements
+        const int n = (int)std::min<long long>(std::min<long long>(4096, x.stride), (long long)cfg_.maxBatch * h_.dim);
         hipk::launchTpSelfTest(patient(x), dY_, n, (float)(me + 1), stream_);
         DL_HIP(hipStreamSynchronize(stream_));
         got.resize(n);
@@ -374,8 +368,20 @@ void HipEngineImpl::tpFusedSelfTest() {
     DL_HIP(hipStreamSynchronize(stream_));
     float all = 0.f;
     DL_HIP(hipMemcpy(&all, dY_, sizeof(float), hipMemcpyDeviceToHost));
-    const bool allOk = !timedOut() && all == (float)W;
+    bool allOk = !timedOut() && all == (float)W;
     comm_->resetError();
+    // The decision must be the same on every rank: a rank whose verdict wait timed out (a peer
+    // more than 60 s late) would switch the fused exchange off while the late peer, seeing every
+    // verdict, keeps it, and their next forward would wait on different data planes. So the ranks
+    // agree through the separate collectives (self-tested at start-up) on the sum of verdicts.
+    float agree = allOk ? 1.f : 0.f;
+    DL_HIP(hipMemcpy(dY_, &agree, sizeof(float), hipMemcpyHostToDevice));
+    comm_->allReduceSum(dY_, 1, stream_);
+    DL_HIP(hipStreamSynchronize(stream_));
+    DL_HIP(hipMemcpy(&agree, dY_, sizeof(float), hipMemcpyDeviceToHost));
+    if (timedOut()) throw Error("tensor-parallel self-test: a peer never reached the verdict agreement");
+    if (agree != (float)W && allOk) why = "a peer's verdict";
+    allOk = agree == (float)W;
     if (allOk) return;
     std::fprintf(stderr, "⚠️  rank %d: fused tensor-parallel exchange self-test failed (%s); using the separate "
                  "%s collectives\n", me, ok ? "on a peer" : ("here: " + why).c_str(), comm_->name().c_str());
@@ -388,8 +394,13 @@ void HipEngineImpl::tpFusedSelfTest() {
 void HipEngineImpl::runGraph(int n, GraphKind kind) {
     if (!tpTested_) tpFusedSelfTest();
     accountForward(n, kind, 1);
+    auto copySync = [&]() {  // the forward's measured-sync slots to the host (read after the sync)
+        if (plan_.nRanks > 1)
+            DL_HIP(hipMemcpyAsync(hSync_, dSync_, (size_t)syncSlots() * 5 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
+    };
     if (!cfg_.useGraphs || graphsBroken_) {
         enqueueForward(n, kind);
+        copySync();
         return;
     }
     const int key = ((((n * 4 + (int)kind) * 2 + (prefillOk_ ? 1 : 0)) * 2 + (attnLong_ ? 1 : 0)) << 4) + bucket_;
@@ -400,6 +411,7 @@ void HipEngineImpl::runGraph(int n, GraphKind kind) {
         // (several ms for ~170 kernel nodes) for a graph that would never be replayed
         if (graphSeen_.insert(key).second) {
             enqueueForward(n, kind);
+            copySync();
             return;
         }
         hipGraphExec_t ge = captureForward(n, kind);
@@ -408,11 +420,13 @@ void HipEngineImpl::runGraph(int n, GraphKind kind) {
             graphsBroken_ = true;
             std::fprintf(stderr, "⚠️  hipGraph capture failed; falling back to eager launches\n");
             enqueueForward(n, kind);
+            copySync();
             return;
         }
         it = graphs_.emplace(key, ge).first;
     }
     DL_HIP(hipGraphLaunch(it->second, stream_));
+    copySync();
 }
 
 hipGraphExec_t HipEngineImpl::captureForward(int n, GraphKind kind) {

@@ -3,6 +3,7 @@
 // serve them, and returns microseconds per launch.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <vector>
 
 #include "engine.h"
@@ -121,7 +122,7 @@ double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int pas
     return ms * 1000.0 / iters;
 }
 
-double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters) {
+double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters, std::vector<unsigned long long> *trace) {
     DL_CHECK(M >= 1 && M <= hipk::kGemmMaxTokens && hipk::gemmSupported(n) && rows % 64 == 0, "bad gemm bench shape");
     hipStream_t s;
     DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -142,7 +143,9 @@ double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters) {
         d[c] = (uint16_t *)alloc(t.dBytes);
         hipk::launchFillQ40(qs[c], d[c], t.qsBytes / 16, 0.01f, 77 + c, s);
     }
-    const int MP = hipk::gemmTokenPad(M);
+    // the operand rows a launch reads: the narrow kernel's 16/32/64/128-row pad, the wide kernel's
+    // whole 128-token tiles
+    const int MP = hipk::gemmUsesWide(M) ? (M + 127) / 128 * 128 : hipk::gemmTokenPad(M);
     _Float16 *x = (_Float16 *)alloc((size_t)MP * n * 2);
     hipk::launchFillF32Uniform((float *)x, (size_t)MP * n / 2, 1e-3f, 3, s);  // small finite f16 pairs
     const size_t part = hipk::gemmPartFloats(rows, n, M);
@@ -157,7 +160,7 @@ double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters) {
     g.M = M;
     g.splits = hipk::gemmSplits(rows, n, M, L);
     g.part = part ? (float *)alloc(part * 4) : nullptr;
-    g.counters = (int *)alloc((size_t)(rows / 64 + 1) * 4);
+    g.counters = (int *)alloc((size_t)std::max(rows / 64 + 1, hipk::gemmCounterInts(rows, M)) * 4);
     auto launch = [&](int c) {
         g.e.qs = qs[c % copies];
         g.e.wd = d[c % copies];
@@ -182,6 +185,16 @@ double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters) {
     DL_HIP(hipEventSynchronize(e1));
     float ms = 0;
     DL_HIP(hipEventElapsedTime(&ms, e0, e1));
+    if (trace) {
+        const size_t words = 8 * (size_t)((rows + 63) / 64) * g.splits;
+        unsigned long long *tb = (unsigned long long *)alloc(words * 8);
+        g.e.trace = tb;
+        launch(1);
+        DL_HIP(hipStreamSynchronize(s));
+        trace->resize(words);
+        DL_HIP(hipMemcpy(trace->data(), tb, words * 8, hipMemcpyDeviceToHost));
+        g.e.trace = nullptr;
+    }
     (void)hipGraphExecDestroy(ge);
     (void)hipGraphDestroy(gr);
     (void)hipEventDestroy(e0);
@@ -279,6 +292,97 @@ double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B
     for (void *p : mem) (void)hipFree(p);
     (void)hipStreamDestroy(s);
     return ms * 1000.0 / iters;
+}
+
+}  // namespace dl
+
+namespace dl {
+
+// The separate-collective schedule of a tensor-parallel forward (engine_forward.cpp: per layer two
+// Q80-rounded all-reduces of [rows][dim] partial sums, then the logits slices gathered to the root
+// and the argmax winner pairs all-gathered), on `comm`, run eagerly or captured once into a hipGraph
+// and replayed. Rank r contributes c * k(r, i) with integer k and c = 2^-4 (every Q80 block holds a
+// 127 * c element, so the Q80 round trip and the sums are exact); returns the largest |got - want|
+// over every output of every run (0 when the transport is right), checked on the host.
+double commScheduleCheck(DeviceComm &comm, int layers, int rows, int dim, int vocab0, int runs, bool graph) {
+    DL_CHECK(layers >= 1 && rows >= 1 && dim % 32 == 0 && vocab0 >= 1 && runs >= 1, "bad schedule shape");
+    const int W = comm.size(), me = comm.rank();
+    const float c = 1.0f / 16.0f;
+    auto k = [](int r, size_t i) { return (i % 32) == 0 ? 127.f : (float)((int)((i * 37 + (size_t)r * 11) % 255) - 127); };
+    const size_t ny = (size_t)rows * dim, nl = (size_t)rows * vocab0, np = 2 * (size_t)rows;
+    std::vector<float> hy(ny), hl(nl), hp(np);
+    for (size_t i = 0; i < ny; i++) hy[i] = c * k(me, i);
+    for (size_t i = 0; i < nl; i++) hl[i] = (float)(me * 1000 + (int)(i % 997));
+    for (size_t i = 0; i < np; i++) hp[i] = (float)(me * 7 + (int)i);
+    hipStream_t s;
+    DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<void *> mem;
+    auto alloc = [&](size_t floats) {
+        void *p;
+        DL_HIP(hipMalloc(&p, floats * sizeof(float)));
+        DL_HIP(hipMemset(p, 0, floats * sizeof(float)));
+        mem.push_back(p);
+        return (float *)p;
+    };
+    float *ySrc = alloc(ny), *y = alloc(ny), *outs = alloc(ny * layers), *lg = alloc(nl), *lgAll = alloc(nl * W);
+    float *pr = alloc(np), *prAll = alloc(np * W);
+    DL_HIP(hipMemcpy(ySrc, hy.data(), ny * 4, hipMemcpyHostToDevice));
+    DL_HIP(hipMemcpy(lg, hl.data(), nl * 4, hipMemcpyHostToDevice));
+    DL_HIP(hipMemcpy(pr, hp.data(), np * 4, hipMemcpyHostToDevice));
+    auto schedule = [&]() {
+        for (int l = 0; l < layers; l++) {
+            DL_HIP(hipMemcpyAsync(y, ySrc, ny * 4, hipMemcpyDeviceToDevice, s));
+            hipk::launchQ80Roundtrip(y, ny, s);
+            comm.allReduceSum(y, ny, s);
+            DL_HIP(hipMemcpyAsync(outs + (size_t)l * ny, y, ny * 4, hipMemcpyDeviceToDevice, s));
+        }
+        comm.gatherToRoot(lg, lgAll, nl, s);
+        comm.allGather(pr, prAll, np, s);
+    };
+    hipGraphExec_t ge = nullptr;
+    if (graph) {
+        hipGraph_t g;
+        DL_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        schedule();
+        DL_HIP(hipStreamEndCapture(s, &g));
+        DL_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        (void)hipGraphDestroy(g);
+    }
+    double err = 0;
+    std::vector<float> got;
+    for (int run = 0; run < runs; run++) {
+        DL_HIP(hipMemsetAsync(outs, 0, ny * layers * 4, s));
+        DL_HIP(hipMemsetAsync(lgAll, 0, nl * W * 4, s));
+        DL_HIP(hipMemsetAsync(prAll, 0, np * W * 4, s));
+        if (graph)
+            DL_HIP(hipGraphLaunch(ge, s));
+        else
+            schedule();
+        DL_HIP(hipStreamSynchronize(s));
+        got.resize(ny * layers);
+        DL_HIP(hipMemcpy(got.data(), outs, ny * layers * 4, hipMemcpyDeviceToHost));
+        for (int l = 0; l < layers; l++)
+            for (size_t i = 0; i < ny; i++) {
+                float want = 0;
+                for (int r = 0; r < W; r++) want += c * k(r, i);
+                err = std::max(err, (double)std::fabs(got[(size_t)l * ny + i] - want));
+            }
+        if (me == 0) {
+            got.resize(nl * W);
+            DL_HIP(hipMemcpy(got.data(), lgAll, nl * W * 4, hipMemcpyDeviceToHost));
+            for (int r = 0; r < W; r++)
+                for (size_t i = 0; i < nl; i++)
+                    err = std::max(err, (double)std::fabs(got[r * nl + i] - (float)(r * 1000 + (int)(i % 997))));
+        }
+        got.resize(np * W);
+        DL_HIP(hipMemcpy(got.data(), prAll, np * W * 4, hipMemcpyDeviceToHost));
+        for (int r = 0; r < W; r++)
+            for (size_t i = 0; i < np; i++) err = std::max(err, (double)std::fabs(got[r * np + i] - (float)(r * 7 + (int)i)));
+    }
+    if (ge) (void)hipGraphExecDestroy(ge);
+    for (void *p : mem) (void)hipFree(p);
+    (void)hipStreamDestroy(s);
+    return err;
 }
 
 }  // namespace dl

@@ -77,7 +77,8 @@ void HipEngineImpl::setInputs(int n, const int *tokens, const int *positions, co
 }
 
 int HipEngineImpl::batchChunk(const DevMat &m, int pro, int epi) const {
-    // largest batch chunk (1/2/4) whose LDS footprint stays <= 64 KiB for this input width
+    // largest batch chunk (1/2/4) whose LDS footprint stays <= 64 KiB for this input width (8 rows
+    // measured 2x slower than the MFMA GEMM: the GEMV's per-row int8 dots are VALU-bound there)
     int bc = 4;
     while (bc > 1) {
         const int rp = q40_ ? 256 / m.lanes * hipk::gemvRowGroup(bc, true) : hipk::gemvRowsPerPass(m.n, m.rows, bc, false);
@@ -100,7 +101,10 @@ hipk::GemvArgs HipEngineImpl::gemvArgs(const DevMat &m, int c0, int bc, int epi,
     a.n = m.n;
     a.passes = tp ? tpPasses(m, bc) : passesFor(m, epi, bc);
     a.lanes = m.lanes;
-    if (tp) a.tp = tpVec_;
+    if (tp) {
+        a.tp = tpVec_;
+        a.tp.ticks = syncTicks(xSlot_);
+    }
     a.in = in ? in + (size_t)c0 * ldIn : nullptr;
     a.aq = aq ? aq + (size_t)c0 * m.n : nullptr;
     a.as = as ? as + (size_t)c0 * (m.n / 32) : nullptr;
@@ -141,7 +145,7 @@ void HipEngineImpl::gemv(const DevMat &m, int n, int pro, int epi, const float *
     for (int c0 = 0; c0 < n;) {
         int bc = n - c0;
         if (bc > bcMax) bc = bcMax;
-        if (bc == 3) bc = 2;
+        while (bc & (bc - 1)) bc &= bc - 1;  // 1, 2 or 4 rows per launch
         const hipk::GemvArgs a = gemvArgs(m, c0, bc, epi, in, ldIn, add, xNext, normW, out, ldOut, L, aq, as, oq, os, tp);
         hipk::launchGemv(a, bc, pro, epi, q40_, stream_);
         c0 += bc;
@@ -336,6 +340,7 @@ void HipEngineImpl::gemmBatched(const DevMat &m, int n, int epi, const float *in
         if (rf && plan_.nRanks > 1) {  // the residual update needs the rank-summed tile
             g.tpx = 1;
             a.tp = tpVec_;
+            a.tp.ticks = syncTicks(xSlot_);
         }
         if (rf) {
             g.resIn = rf->resIn + (size_t)c0 * ldOut;
@@ -361,8 +366,10 @@ void HipEngineImpl::gemmBatched(const DevMat &m, int n, int epi, const float *in
 void HipEngineImpl::allReduce(float *buf, size_t count) {
     if (plan_.nRanks > 1) {
         ProfScope ps(this, "allreduce");
-        if (syncQ80_) hipk::launchQ80Roundtrip(buf, count, stream_);
-        comm_->allReduceSum(buf, count, stream_);
+        stamped([&] {
+            if (syncQ80_) hipk::launchQ80Roundtrip(buf, count, stream_);
+            comm_->allReduceSum(buf, count, stream_);
+        });
     }
 }
 
@@ -381,7 +388,8 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
     {
         ProfScope ps(this, "embedding");
         // the epoch counts the forwards that run the fused block (its counters' targets)
-        hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_, blk ? dEpoch_ : nullptr);
+        hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_, blk ? dEpoch_ : nullptr,
+                              p.nRanks > 1 ? dSync_ : nullptr, p.nRanks > 1 ? syncSlots() * 5 : 0);
     }
     // Q80 hand-off of h needs one workgroup per 32 hidden units; for skinny TP shards the w13
     // epilogue emits f32 and w2 quantizes in its prologue instead.
@@ -389,6 +397,7 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
     for (u32 l = 0; l < h_.nLayers; l++) {
         DevLayer &L = layers_[l];
         const bool hasDelta = l > 0;
+        xSlot_ = 2 * (int)l;  // the wo exchange (fused in the wo kernel, or the all-reduce after it)
         if (blk) {
             ProfScope ps(this, "attn_block");
             hipk::AttnBlockArgs ba = attnBlockArgs(L, l, cur);
@@ -412,10 +421,21 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
             {
                 ProfScope ps(this, "attention");
                 const hipk::AttnArgs a = attnArgs(L, bat);
-                if (bat && prefillOk_)
-                    hipk::launchAttentionPrefill(a, n, stream_);
-                else
-                    hipk::launchAttention(a, n, stream_);
+                for (int r0 = 0; r0 < n; r0 += attRows_) {  // one launch unless the partials cap the rows
+                    const int nr = std::min(attRows_, n - r0);
+                    hipk::AttnArgs ar = a;
+                    ar.q += (size_t)r0 * a.ldq;
+                    ar.pos += r0;
+                    ar.slot += r0;
+                    ar.out += (size_t)r0 * a.ldOut;
+                    if (ar.outH) ar.outH += (size_t)r0 * a.ldOut;
+                    if (ar.outQ) ar.outQ += (size_t)r0 * a.ldOut;
+                    if (ar.outS) ar.outS += (size_t)r0 * (a.ldOut / 32);
+                    if (bat && prefillOk_)
+                        hipk::launchAttentionPrefill(ar, nr, stream_);
+                    else
+                        hipk::launchAttention(ar, nr, stream_);
+                }
             }
             {
                 ProfScope ps(this, "gemv_wo");
@@ -432,6 +452,7 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
             }
         }
         if (!fusedTp(bat) && !fz) allReduce(dY_, (size_t)n * dim);
+        xSlot_ = 2 * (int)l + 1;  // the w2 exchange
         {
             ProfScope ps(this, "gemv_w13");
             if (fz)
@@ -464,6 +485,7 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
         }
         if (!fusedTp(bat) && !fz) allReduce(dY_, (size_t)n * dim);
     }
+    xSlot_ = 2 * (int)h_.nLayers;  // logits gather / argmax winners
     {
         ProfScope ps(this, "gemv_logits");
         if (fz)
@@ -489,10 +511,12 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
     const bool rootOnly = kind == GraphKind::LOGITS || kind == GraphKind::SAMPLE;
     if (p.nRanks > 1 && !distArgmax) {
         ProfScope ps(this, "allgather");
-        if (rootOnly)
-            comm_->gatherToRoot(dLogits_, dLogitsAll_, (size_t)n * p.vocab0, stream_);
-        else
-            comm_->allGather(dLogits_, dLogitsAll_, (size_t)n * p.vocab0, stream_);
+        stamped([&] {
+            if (rootOnly)
+                comm_->gatherToRoot(dLogits_, dLogitsAll_, (size_t)n * p.vocab0, stream_);
+            else
+                comm_->allGather(dLogits_, dLogitsAll_, (size_t)n * p.vocab0, stream_);
+        });
         if (!rootOnly || rank() == 0) hipk::launchUnshardLogits(dLogitsAll_, dLogitsFull_, p.nRanks, n, p.vocab0, stream_);
         full = dLogitsFull_;
     }
@@ -515,8 +539,13 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
         if (distArgmax) {
             g.vocab = p.vocab0;
             g.vocabStart = p.vocabStart();
-            if (tpFused_) g.tp = tpArg_;
-            else g.pairs = dArgPairs_;
+            // fused winners exchange up to its region's rows (2 words per row), else one all-gather
+            if (tpFused_ && (size_t)2 * n <= (size_t)tpArg_.stride) {
+                g.tp = tpArg_;
+                g.tp.ticks = syncTicks(xSlot_);
+            } else {
+                g.pairs = dArgPairs_;
+            }
         }
         g.ids = dIds_;
         g.partV = dArgV_;
@@ -531,7 +560,7 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
         }
         hipk::launchArgmax(g, n, stream_);
         if (g.pairs) {
-            comm_->allGather(dArgPairs_, dArgPairsAll_, 2 * (size_t)n, stream_);
+            stamped([&] { comm_->allGather(dArgPairs_, dArgPairsAll_, 2 * (size_t)n, stream_); });
             hipk::launchArgmaxPick(g, dArgPairsAll_, n, p.nRanks, stream_);
         }
     }

@@ -98,7 +98,23 @@ class HipEngineImpl : public HipEngine {
     int rank() const { return comm_ ? comm_->rank() : 0; }
     void runGraph(int n, GraphKind kind);
     void accountForward(int n, GraphKind kind, int times);
-    double exchangeMs(int n);
+    // measured sync (ForwardStats::syncMs): one slot per exchange of a forward (layer l: wo 2l,
+    // w2 2l + 1; the logits / argmax exchange 2L): a u32 of fused-exchange ticks (max over the
+    // workgroups) and a pair of u64 stamps around a separate collective; cleared by the forward's
+    // embedding kernel, copied to the host after each forward
+    int syncSlots() const { return 2 * (int)h_.nLayers + 2; }
+    unsigned *syncTicks(int slot) const { return dSync_ + slot; }
+    unsigned long long *syncStamps(int slot) const {
+        return reinterpret_cast<unsigned long long *>(dSync_ + syncSlots()) + 2 * slot;
+    }
+    double readSyncMs() const;
+    template <typename F>
+    void stamped(F &&collective) {  // a separate collective of slot xSlot_, bracketed by stamps
+        launchStampAt(syncStamps(xSlot_));
+        collective();
+        launchStampAt(syncStamps(xSlot_) + 1);
+    }
+    void launchStampAt(unsigned long long *p);
     void tpFusedSelfTest();
     hipGraphExec_t captureForward(int n, GraphKind kind);
     template <typename T>
@@ -213,6 +229,8 @@ class HipEngineImpl : public HipEngine {
     int fusedGridMax_ = 0;  // largest grid of a fused-exchange GEMV launch (checked co-resident)
     hipk::TpXchg tpVec_, tpArg_;
     int gemmMin_ = 3;          // DL_GEMM_MIN: rows per forward from which the batched MFMA path runs
+    int decodeRows_ = 1;       // EngineConfig::maxDecode (<= maxBatch): greedy-chain rows, fused argmax rows
+    int attRows_ = 1;          // rows per attention launch (the split partials hold this many rows)
     bool fuseNormEnv_ = true;  // DL_GEMM_FUSE_NORM
     std::vector<void *> allocs_, hostAllocs_;
     size_t deviceBytes_ = 0;
@@ -251,7 +269,8 @@ class HipEngineImpl : public HipEngine {
     float *dArgV_ = nullptr;
     float *dArgPairs_ = nullptr, *dArgPairsAll_ = nullptr;  // separate-collective TP argmax
     hipk::SampleScratch sampleScratch_;
-    std::map<int, double> exchangeMs_;  // calibrated all-reduce ms per row count (exchangeMs)
+    unsigned *dSync_ = nullptr, *hSync_ = nullptr;  // measured-sync slots (syncSlots) and their host copy
+    int xSlot_ = 0;                                  // slot of the exchange being enqueued
 
     // attention: context buckets (setupBuckets) and this forward's choices (setInputs, graph key)
     std::vector<CtxBucket> buckets_;

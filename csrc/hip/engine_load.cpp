@@ -105,7 +105,7 @@ void HipEngineImpl::allocBuffers() {
     dSlot_ = dTok_ + 2 * MB;
     dSpec_ = reinterpret_cast<float4 *>(dTok_ + 3 * MB);
     dIds_ = dalloc<int>(MB);
-    dHist_ = dalloc<int>((size_t)MB * h_.seqLen);
+    dHist_ = dalloc<int>((size_t)decodeRows_ * h_.seqLen);  // greedy chains only (decode rows)
     hIn_ = halloc<int>(7 * MB);
     hIds_ = halloc<int>(MB);
     hErr_ = halloc<int>(2);
@@ -150,6 +150,12 @@ void HipEngineImpl::allocBuffers() {
     }
     {  // fused attention block: epoch, monotonic counters, expected counts, timeout flag
         dEpoch_ = dalloc<unsigned>(4);
+        // measured-sync slots: syncSlots() u32 tick words + 2 u64 stamps per slot (cleared by the
+        // embedding kernel of every forward)
+        dSync_ = dalloc<unsigned>((size_t)syncSlots() * 5);
+        hSync_ = halloc<unsigned>((size_t)syncSlots() * 5);
+        DL_HIP(hipMemsetAsync(dSync_, 0, (size_t)syncSlots() * 5 * sizeof(unsigned), stream_));
+        std::memset(hSync_, 0, (size_t)syncSlots() * 5 * sizeof(unsigned));
         dBlockCnt_ = dalloc<unsigned>(kBlockCntWords);
         dBlockExpect_ = dalloc<unsigned>(kMaxKvGroups);
         dBlockErr_ = dalloc<int>(4);
@@ -178,8 +184,14 @@ void HipEngineImpl::allocBuffers() {
     }
     setupBuckets();  // the largest bucket sizes the split-attention partials
     const int splitMax = buckets_.back().splitGrid;
-    dPartO_ = dalloc<float>((size_t)MB * p.nHeads0 * splitMax * p.headSize);
-    dPartML_ = dalloc<float>((size_t)MB * p.nHeads0 * splitMax * 2);
+    {  // attention split partials: every row of a forward while they stay <= 256 MB, else the
+       // launches take row chunks (multiples of 64 rows: whole prefill row blocks of one slot)
+        const size_t perRow = (size_t)p.nHeads0 * splitMax * (p.headSize + 2) * sizeof(float);
+        const size_t fit = ((size_t)256 << 20) / perRow / 64 * 64;
+        attRows_ = (int)std::min<size_t>(MB, std::max<size_t>({fit, (size_t)decodeRows_, 64}));
+    }
+    dPartO_ = dalloc<float>((size_t)attRows_ * p.nHeads0 * splitMax * p.headSize);
+    dPartML_ = dalloc<float>((size_t)attRows_ * p.nHeads0 * splitMax * 2);
     dRope_ = dalloc<float2>((size_t)h_.seqLen * (p.headSize / 2));
     layers_.resize(h_.nLayers);
     const size_t kvElems = kvPoolRows() * p.kv0;

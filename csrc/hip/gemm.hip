@@ -25,7 +25,6 @@ namespace hipk {
 // release/acquire counter: deterministic), which runs the fused epilogues (store / SwiGLU /
 // SwiGLU -> f16 / SwiGLU -> Q80 / RoPE + KV append).
 // ------------------------------------------------------------------------------------------------
-static constexpr int kGemmRows = 64;
 static constexpr int kGemmCh = 8;  // Q40 blocks per pipeline stage (~25 KB at 32 tokens)
 
 // Split-K degree: grow S until the grid reaches the workgroup target or a split would get fewer
@@ -33,8 +32,12 @@ static constexpr int kGemmCh = 8;  // Q40 blocks per pipeline stage (~25 KB at 3
 // chunk in flight per workgroup, bytes in flight per CU (and so HBM bandwidth) scale with
 // resident workgroups, not with tiles (targets 128-1024 and 2-16 splits re-swept in round 3:
 // profiles/raw/r3_gemm_knobs.md).
-static int gemmWgTarget() { return 256; }
-static int gemmMaxSplits() { return 8; }
+static int gemmEnvInt(const char *name, int dflt) {
+    const char *e = std::getenv(name);
+    return e && std::atoi(e) > 0 ? std::atoi(e) : dflt;
+}
+static int gemmWgTarget() { static const int v = gemmEnvInt("DL_GEMM_WG_TARGET", 256); return v; }
+static int gemmMaxSplits() { static const int v = gemmEnvInt("DL_GEMM_MAX_SPLITS", 8); return v; }
 
 GemmPlan gemmPlan(int rows, int n, int M) {
     GemmPlan p;
@@ -50,8 +53,26 @@ bool gemmSupported(int n) { return n % 32 == 0; }
 // keep every split a whole number of 16-block tiling steps. (At 32 tokens its 50 KB stages leave
 // one workgroup per CU: w13 42.8 vs 32.5 us, so those stay on gemmQ40Kernel.)
 static constexpr int kG16Ch = 16;
+static bool gemmL16On() {
+    static const bool v = [] {
+        const char *e = std::getenv("DL_GEMM_L16");
+        return !(e && *e == '0');
+    }();
+    return v;
+}
+// 64-row tiles per narrow workgroup by token tile width (gemmQ40Kernel RT; DL_GEMM_RT1/2/4)
+static int gemmRowTiles(int M) {
+    auto env = [](const char *name, int dflt) {
+        const char *e = std::getenv(name);
+        const int v = e ? std::atoi(e) : dflt;
+        return v == 1 || v == 2 ? v : dflt;
+    };
+    static const int r1 = env("DL_GEMM_RT1", 1), r2 = env("DL_GEMM_RT2", 1), r4 = env("DL_GEMM_RT4", 1);
+    const int MT = gemmTokenPad(M) / 16;
+    return MT == 1 ? r1 : MT == 2 ? r2 : MT == 4 ? r4 : 1;
+}
 static bool gemmL16Eligible(int n, int M, int lanes) {
-    return lanes == 16 && M <= 16 && (n / 32) % kG16Ch == 0 && !gemmUsesWide(M);
+    return gemmL16On() && lanes == 16 && M <= 16 && (n / 32) % kG16Ch == 0 && !gemmUsesWide(M) && gemmRowTiles(M) == 1;
 }
 
 int gemmSplits(int rows, int n, int M, int lanes) {
@@ -60,16 +81,18 @@ int gemmSplits(int rows, int n, int M, int lanes) {
     if (gemmL16Eligible(n, M, lanes)) {
         const int ks = nb / kG16Ch;  // tiling steps
         int S = 1;
-        while (2 * S <= 8 && tiles * S < 256 && ks % (2 * S) == 0) S *= 2;
-        while (2 * S <= 8 && tiles * 2 * S <= 512 && ks % (2 * S) == 0 && ks / (2 * S) >= 4) S *= 2;
+        const int target = gemmWgTarget(), maxS = gemmMaxSplits();
+        while (2 * S <= maxS && tiles * S < target && ks % (2 * S) == 0) S *= 2;
+        while (2 * S <= maxS && tiles * 2 * S <= 2 * target && ks % (2 * S) == 0 && ks / (2 * S) >= 4) S *= 2;
         return S;
     }
     const int target = gemmWgTarget(), maxS = gemmMaxSplits();
+    const int wgs = (rows + kGemmRows * gemmRowTiles(M) - 1) / (kGemmRows * gemmRowTiles(M));
     int S = 1;
-    while (2 * S <= maxS && tiles * S < target && nb % (2 * S) == 0 && nb / (2 * S) >= kGemmCh) S *= 2;
+    while (2 * S <= maxS && wgs * S < target && nb % (2 * S) == 0 && nb / (2 * S) >= kGemmCh) S *= 2;
     // deep K (w2: 4096 x 14336): keep splitting up to two workgroups per CU while every split
     // still streams >= 4 chunks (measured w2 M=8 23.9 -> 19.6 us; shallower matrices lose)
-    while (2 * S <= maxS && tiles * 2 * S <= 2 * target && nb % (2 * S) == 0 && nb / (2 * S) >= 4 * kGemmCh) S *= 2;
+    while (2 * S <= maxS && wgs * 2 * S <= 2 * target && nb % (2 * S) == 0 && nb / (2 * S) >= 4 * kGemmCh) S *= 2;
     return S;
 }
 
@@ -94,79 +117,41 @@ int gemmCounterInts(int rows, int maxTokens) {
     return std::max(narrow, gemmUsesWide(maxTokens) ? gemmWideCounters(rows, maxTokens) : 0);
 }
 
-// stage layout (bytes): weights [64 rows][8 units] x 16 B | scales [32 pairs][8] u32 | x [MP][32 units] x 16 B
+// stage layout (bytes): weights [64 RT rows][8 units] x 16 B | scales [32 RT pairs][8] u32 | x [MP][32 units] x 16 B
 static constexpr int kStW = kGemmRows * kGemmCh * 16, kStD = (kGemmRows / 2) * kGemmCh * 4;
-__host__ __device__ static constexpr int gemmStageBytes(int MT) { return kStW + kStD + MT * 16 * kGemmCh * 64; }
+__host__ __device__ static constexpr int gemmStageBytes(int MT, int RT = 1) {
+    return RT * (kStW + kStD) + MT * 16 * kGemmCh * 64;
+}
 #ifndef DL_GEMM_STAGES
 #define DL_GEMM_STAGES 2  // 3 stages (2 WGs/CU) measured slower: batch-32 8.1k vs 8.8k tok/s
 #endif
 static constexpr int kGemmStages = DL_GEMM_STAGES;  // stage buffers (kGemmStages-1 chunks in flight)
 static constexpr int kGemmScaleFloats = 128 + 256;  // gemmFinish: per-token RMS scales + per-thread slices
-static size_t gemmLds(int MT, int stages) { return stages * (size_t)gemmStageBytes(MT) + 16 + kGemmScaleFloats * 4; }  // + flag
-
-// Split-K combine and fused epilogues shared by the batched GEMMs (Q40 and f32): `acc` holds this
-// lane's C fragments (weight row (local) wave*16 + col, token t*16 + h*4 + i); `smem` must hold
-// MP x 64 floats and is free (all K-loop LDS reads retired behind a barrier); `flag` one int.
-// tileIdx / tiles: this 64-row tile and the launch's tile count (split-K partial slots, counters).
-template <int MT, int EPI>
-__device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc)[MT], char *smem, int *flag,
-                                           int tileIdx, int tiles) {
-    constexpr int MP = MT * 16;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int col = lane & 15, h = lane >> 4, rl = wave * 16 + col;
-    const int sp = blockIdx.y, S = ga.splits;
-    const int R0 = tileIdx * kGemmRows;
-    float *tile = reinterpret_cast<float *>(smem);  // [MP][64], stages are free now
-    // C layout: weight row (local) wave*16 + col, token t*16 + h*4 + i
-    if (S == 1) {
-#pragma unroll
-        for (int t = 0; t < MT; t++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) tile[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
-    } else {
-        // Partials are written and read with agent-scope atomic accesses (global_store / load sc1:
-        // performed at the coherence point, never held in or served from one XCD's L2), so the
-        // hand-off needs no fence: an agent-scope release / acquire fence is a whole-L2 writeback
-        // (buffer_wbl2) / invalidate (buffer_inv) on gfx950, which measured ~28 us per split level
-        // on w13 (448 -> 896 workgroups) and evicted the other workgroups' cached activations.
-        // vmcnt(0) before the arrival count: every partial store has been performed.
-        float *part = ga.part + ((size_t)sp * tiles + tileIdx) * MP * kGemmRows;
-#pragma unroll
-        for (int t = 0; t < MT; t++)
-#pragma unroll
-            for (int i = 0; i < 4; i++) wtStore(part + (t * 16 + h * 4 + i) * kGemmRows + rl, acc[t][i]);
-        if (!splitArrive(ga.counters + tileIdx, S, flag)) return;
-        // combine in split order (deterministic): this tail runs on one workgroup per tile after
-        // the others finished
-        splitCombine(ga.part + (size_t)tileIdx * MP * kGemmRows, (size_t)tiles * MP * kGemmRows, S,
-                     MP * kGemmRows / 4, reinterpret_cast<f32x4 *>(tile));
-    }
-    // tensor parallel: the tile's partial sums all-reduced over the ranks in place (staging after
-    // the [MP][64] tile; the host checked that the launch's LDS holds it)
-    if (ga.tpx) tpExchangeTile(ga, tile, R0, smem + (size_t)MP * kGemmRows * 4);
-    // consumer of a fused residual + norm: per-token RMS scale from the producer's tile partials
-    float *rsL = reinterpret_cast<float *>(flag + 4);  // [128] + [256] scratch
-    if (ga.ssIn) gemmRowScales(ga, 0, MP, rsL, rsL + 128);
-    __syncthreads();
-    gemmEpilogue<EPI, 32>(ga, tile, kGemmRows, 0, ga.M, 0, R0, tileIdx, ga.ssIn ? rsL : nullptr);
+static size_t gemmLds(int MT, int stages, int RT = 1) {
+    return stages * (size_t)gemmStageBytes(MT, RT) + 16 + kGemmScaleFloats * 4;  // + flag
 }
 
 // STG = stage buffers: 2 double-buffers the chunk stream inside a workgroup; 1 (the 64-token
 // tile) drops that to fit 3 workgroups per CU, which then overlap each other's loads.
-template <int MT, int EPI, int STG>
+// RT = 64-row tiles per workgroup (each wave owns 16 rows of every tile): one activation stage
+// then feeds RT x 64 rows. At 64 tokens a 64-row tile stages 32 KB of activations per 9 KB of
+// weights (PMC: waves wait 47 % of their cycles on those stages), so RT = 2 halves the bytes a
+// workgroup moves per weight byte; the A fragments read from LDS are shared by the RT tiles too.
+template <int MT, int EPI, int STG, int RT = 1>
 __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
     const GemvArgs &a = ga.e;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int SB = gemmStageBytes(MT);
-    constexpr int NW = kGemmRows * kGemmCh / kThreads, NX = MT * 16 * kGemmCh * 4 / kThreads;
-    constexpr int NLD = NW + 1 + NX;  // glds instructions per thread per stage
+    constexpr int SB = gemmStageBytes(MT, RT);
+    constexpr int SW = RT * kStW, SD = RT * kStD;  // weight / scale bytes of a stage
+    constexpr int NW = RT * kGemmRows * kGemmCh / kThreads, NX = MT * 16 * kGemmCh * 4 / kThreads;
+    constexpr int NLD = NW + RT + NX;  // glds instructions per thread per stage
     int *flag = reinterpret_cast<int *>(smem + STG * SB);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int col = lane & 15, h = lane >> 4;
     const int n = a.n, nb = n >> 5, L = a.lanes, NG = kThreads / L, KS = (nb + L - 1) / L;
     const int lgL = 31 - __builtin_clz(L);
-    const int tileIdx = blockIdx.x, sp = blockIdx.y, S = ga.splits;
-    const int R0 = tileIdx * kGemmRows;
+    const int sp = blockIdx.y, S = ga.splits;
+    const int R0 = blockIdx.x * kGemmRows * RT;
     const int bps = nb / S, j0 = sp * bps, j1 = j0 + bps;
     const int nch = (bps + kGemmCh - 1) / kGemmCh;
     const uint8_t *qs = a.qs;
@@ -196,10 +181,11 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
             const size_t unit = unitOf(R0 + rl, c0 + (pp ^ ((rl >> 1) & (kGemmCh - 1))));
             glds16<true>(qs + unit * 16, st + (size_t)(s * kThreads + wave * 64) * 16);
         }
-        // pair scales: u = tid -> (pair_l = u/8, block u%8), 4 B each
-        {
-            const int pl = tid / kGemmCh, jj = tid % kGemmCh;
-            glds4(wd2 + scaleIdx(R0 + 2 * pl, c0 + jj), st + kStW + (size_t)(wave * 64) * 4);
+        // pair scales: u = d*256 + tid -> (pair_l = u/8, block u%8), 4 B each
+#pragma unroll
+        for (int d = 0; d < RT; d++) {
+            const int u = d * kThreads + tid, pl = u / kGemmCh, jj = u % kGemmCh;
+            glds4(wd2 + scaleIdx(R0 + 2 * pl, c0 + jj), st + SW + (size_t)(d * kThreads + wave * 64) * 4);
         }
         // activations: token row t = 4*kGemmCh units of 8 f16; position p holds unit p ^ (t&15)
 #pragma unroll
@@ -208,14 +194,17 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
             const int uu = pp ^ (t & 15);
             const int cb = min(c0 + (uu >> 2), j1 - 1);  // block of this unit (clamped)
             const _Float16 *src = ga.x + (size_t)t * n + (size_t)cb * 32 + (uu & 3) * 8;
-            glds16(src, st + kStW + kStD + (size_t)(s * kThreads + wave * 64) * 16);
+            glds16(src, st + SW + SD + (size_t)(s * kThreads + wave * 64) * 16);
         }
     };
 
-    f32x4 acc[MT];
+    const unsigned long long tEntry = a.trace ? wall_clock64() : 0ull;
+    unsigned long long tFirst = 0ull;
+    f32x4 acc[RT][MT];
 #pragma unroll
-    for (int t = 0; t < MT; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int rl = wave * 16 + col;  // this lane's weight row (local)
+    for (int r = 0; r < RT; r++)
+#pragma unroll
+        for (int t = 0; t < MT; t++) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int byteHalf = h & 1, nibHi = h >> 1;
 
     constexpr int PF = STG - 1;  // chunks in flight ahead of the one consumed
@@ -233,32 +222,64 @@ __global__ __launch_bounds__(kThreads) void gemmQ40Kernel(GemmArgs ga) {
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // ... and for every thread
+        if (a.trace && c == 0) tFirst = wall_clock64();
         const char *st = smem + (c % STG) * SB;
         const int cn = min(kGemmCh, bps - c * kGemmCh);
+        // Software-pipelined over the chunk's blocks: block jj + 1's LDS operands (weights, scale,
+        // activation fragments) are read before block jj is dequantized and fed to the MFMAs, so
+        // each block waits on a counted lgkmcnt instead of a full LDS round trip + the dequant
+        // chain (the serial form spent 38 % of its wave cycles waiting, PMC r5).
+        struct Ops {
+            u32x2 wv[RT];
+            uint32_t dh[RT];
+            half8 av[MT];
+        };
+        auto ldOps = [&](int jj, Ops &o) {
 #pragma unroll
-        for (int jj = 0; jj < kGemmCh; jj++) {
-            // swizzle key (rl >> 1) & 7: the 16 rows of a wave's ds_read_b64 (two 8-B halves per
-            // 16-B unit) land on 32 distinct bank pairs (rows 128 B apart alias every other row;
-            // the old key rl & 7 left 2-way conflicts: SQ_LDS_BANK_CONFLICT 25 % of LDS cycles)
-            const int pp = jj ^ ((rl >> 1) & (kGemmCh - 1));
-            const u32x2 wv = *reinterpret_cast<const u32x2 *>(st + (size_t)(rl * kGemmCh + pp) * 16 + byteHalf * 8);
-            // this row's f16 half of the pair scale, read directly (no per-lane shift)
-            const uint32_t dh = *reinterpret_cast<const uint16_t *>(st + kStW + (size_t)((rl >> 1) * kGemmCh + jj) * 4 +
-                                                                    (rl & 1) * 2);
-            const uint32_t d16 = jj < cn ? dh : 0u;
-            const half8 b = dequantQ40x8(wv, nibHi, d16);
+            for (int r = 0; r < RT; r++) {
+                const int rl = r * kGemmRows + wave * 16 + col;  // this lane's weight row in tile r (local)
+                // swizzle key (rl >> 1) & 7: the 16 rows of a wave's ds_read_b64 (two 8-B halves per
+                // 16-B unit) land on 32 distinct bank pairs (rows 128 B apart alias every other row;
+                // the old key rl & 7 left 2-way conflicts: SQ_LDS_BANK_CONFLICT 25 % of LDS cycles)
+                const int pp = jj ^ ((rl >> 1) & (kGemmCh - 1));
+                o.wv[r] = *reinterpret_cast<const u32x2 *>(st + (size_t)(rl * kGemmCh + pp) * 16 + byteHalf * 8);
+                // this row's f16 half of the pair scale, read directly (no per-lane shift)
+                o.dh[r] = *reinterpret_cast<const uint16_t *>(st + SW + (size_t)((rl >> 1) * kGemmCh + jj) * 4 + (rl & 1) * 2);
+            }
 #pragma unroll
             for (int t = 0; t < MT; t++) {
                 const int tok = t * 16 + col, up = (jj * 4 + h) ^ (tok & 15);
-                const half8 av = *reinterpret_cast<const half8 *>(st + kStW + kStD + (size_t)(tok * 4 * kGemmCh + up) * 16);
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b, acc[t], 0, 0, 0);
+                o.av[t] = *reinterpret_cast<const half8 *>(st + SW + SD + (size_t)(tok * 4 * kGemmCh + up) * 16);
             }
+        };
+        Ops ops[2];
+        ldOps(0, ops[0]);
+#pragma unroll
+        for (int jj = 0; jj < kGemmCh; jj++) {
+            Ops &cur = ops[jj & 1];
+            if (jj + 1 < kGemmCh) ldOps(jj + 1, ops[(jj + 1) & 1]);
+            half8 b[RT];
+#pragma unroll
+            for (int r = 0; r < RT; r++) b[r] = dequantQ40x8(cur.wv[r], nibHi, jj < cn ? cur.dh[r] : 0u);
+#pragma unroll
+            for (int t = 0; t < MT; t++)
+#pragma unroll
+                for (int r = 0; r < RT; r++)
+                    acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cur.av[t], b[r], acc[r][t], 0, 0, 0);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // stage c % STG is refilled at iteration c + 1
     }
 
-    gemmFinish<MT, EPI>(ga, acc, smem, flag, blockIdx.x, gridDim.x);
+    const unsigned long long tLoop = a.trace ? wall_clock64() : 0ull;
+    const int tiles = (a.rows + kGemmRows - 1) / kGemmRows;
+#pragma unroll
+    for (int r = 0; r < RT; r++) {  // one 64-row tile at a time through the split-K combine + epilogue
+        const int tileIdx = blockIdx.x * RT + r;
+        if (tileIdx >= tiles) break;
+        if (r) __syncthreads();  // the previous tile's epilogue read the LDS tile
+        gemmFinish<MT, EPI>(ga, acc[r], smem, flag, tileIdx, tiles, tEntry, tFirst, tLoop);
+    }
 }
 
 // 16-lane tilings (Q40Tiling L = 16: qkv / w13 / logits of 8B, every layer matrix of 70B and
@@ -324,6 +345,8 @@ __global__ __launch_bounds__(kThreads) void gemmQ40L16Kernel(GemmArgs ga) {
         }
     };
 
+    const unsigned long long tEntry = a.trace ? wall_clock64() : 0ull;
+    unsigned long long tFirst = 0ull;
     f32x4 acc[MT];
 #pragma unroll
     for (int t = 0; t < MT; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -346,40 +369,60 @@ __global__ __launch_bounds__(kThreads) void gemmQ40L16Kernel(GemmArgs ga) {
         else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // ... and for every thread
+        if (a.trace && c == 0) tFirst = wall_clock64();
         const char *st = smem + (c % STG) * SB;
-#pragma unroll
-        for (int jj = 0; jj < kG16Ch; jj++) {
-            const u32x2 wv = *reinterpret_cast<const u32x2 *>(st + wBase + (jj ^ swz) * 16);
-            const uint32_t d16 = *reinterpret_cast<const uint16_t *>(st + kG16W + dBase + jj * 4);
-            const half8 b = dequantQ40x8(wv, nibHi, d16);
+        // software-pipelined as gemmQ40Kernel: block jj + 1's LDS operands are read before block jj
+        // is dequantized
+        struct Ops {
+            u32x2 wv;
+            uint32_t d16;
+            half8 av[MT];
+        };
+        auto ldOps = [&](int jj, Ops &o) {
+            o.wv = *reinterpret_cast<const u32x2 *>(st + wBase + (jj ^ swz) * 16);
+            o.d16 = *reinterpret_cast<const uint16_t *>(st + kG16W + dBase + jj * 4);
 #pragma unroll
             for (int t = 0; t < MT; t++) {
                 const int tok = t * 16 + col, up = (jj * 4 + h) ^ (tok & 15);
-                const half8 av = *reinterpret_cast<const half8 *>(st + kG16W + kG16D + (size_t)(tok * 64 + up) * 16);
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, b, acc[t], 0, 0, 0);
+                o.av[t] = *reinterpret_cast<const half8 *>(st + kG16W + kG16D + (size_t)(tok * 64 + up) * 16);
             }
+        };
+        Ops ops[2];
+        ldOps(0, ops[0]);
+#pragma unroll
+        for (int jj = 0; jj < kG16Ch; jj++) {
+            Ops &cur = ops[jj & 1];
+            if (jj + 1 < kG16Ch) ldOps(jj + 1, ops[(jj + 1) & 1]);
+            const half8 b = dequantQ40x8(cur.wv, nibHi, cur.d16);
+#pragma unroll
+            for (int t = 0; t < MT; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(cur.av[t], b, acc[t], 0, 0, 0);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // stage c % STG is refilled at iteration c + 1
     }
 
-    gemmFinish<MT, EPI>(ga, acc, smem, flag, blockIdx.x, gridDim.x);
+    gemmFinish<MT, EPI>(ga, acc, smem, flag, blockIdx.x, gridDim.x, tEntry, tFirst, a.trace ? wall_clock64() : 0ull);
 }
 
 // The 128-token tile (prefill chunks): one stage buffer (73 KB), two workgroups per CU; each
 // weight chunk feeds 8 MFMA token tiles, so a 128-token slice streams the weights once instead of
 // twice.
 // stage buffers per token-tile width (re-swept in round 3: profiles/raw/r3_gemm_knobs.md)
-static int gemmStages4() { return 1; }
-static int gemmStages2() { return kGemmStages; }
-static int gemmStages1() { return kGemmStages; }
+static int envStages(const char *name, int dflt) {
+    const char *e = std::getenv(name);
+    const int v = e ? std::atoi(e) : dflt;
+    return v >= 1 && v <= 4 ? v : dflt;
+}
+static int gemmStages4() { static const int v = envStages("DL_GEMM_STG4", 1); return v; }
+static int gemmStages2() { static const int v = envStages("DL_GEMM_STG2", kGemmStages); return v; }
+static int gemmStages1() { static const int v = envStages("DL_GEMM_STG1", kGemmStages); return v; }
 
 bool gemmTpxFits(int M, int world, bool q80) {
     if (M < 1 || M > 64 || world > kTpMaxRanks) return false;
     const int MT = gemmTokenPad(M) / 16;
     const int stg = MT == 4 ? gemmStages4() : MT == 2 ? gemmStages2() : gemmStages1();
     const size_t need = (size_t)MT * 16 * kGemmRows * 4 + (q80 ? tpTileQ80Lds(M, world) : 0);
-    return need <= (size_t)stg * gemmStageBytes(MT);
+    return need <= (size_t)stg * gemmStageBytes(MT, gemmRowTiles(M));
 }
 
 void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
@@ -409,19 +452,25 @@ void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
 #undef DL_G16_CASE
     }
     const int stg = MT == 8 ? 1 : MT == 4 ? gemmStages4() : MT == 2 ? gemmStages2() : gemmStages1();
-    const size_t lds = gemmLds(MT, stg);
-#define DL_GEMM_CASE(M_, E, G)                                                                    \
-    if (MT == M_ && epi == E && stg == G) {                                                       \
-        if (lds > 65536) allowLds((const void *)gemmQ40Kernel<M_, E, G>, lds); /* per device */  \
-        hipLaunchKernelGGL((gemmQ40Kernel<M_, E, G>), grid, dim3(kThreads), lds, s, ga);         \
-        return;                                                                                   \
+    const int RT = MT == 8 ? 1 : gemmRowTiles(ga.M);
+    const size_t lds = gemmLds(MT, stg, RT);
+    const dim3 gridRt((ga.e.rows + kGemmRows * RT - 1) / (kGemmRows * RT), ga.splits);
+#define DL_GEMM_CASE(M_, E, G, R)                                                                     \
+    if (MT == M_ && epi == E && stg == G && RT == R) {                                                \
+        if (lds > 65536) allowLds((const void *)gemmQ40Kernel<M_, E, G, R>, lds); /* per device */   \
+        hipLaunchKernelGGL((gemmQ40Kernel<M_, E, G, R>), gridRt, dim3(kThreads), lds, s, ga);        \
+        return;                                                                                       \
     }
-#define DL_GEMM_CASES(M_, G)                                                                      \
-    DL_GEMM_CASE(M_, EPI_STORE, G) DL_GEMM_CASE(M_, EPI_ACT, G) DL_GEMM_CASE(M_, EPI_ACT_Q80, G)  \
-    DL_GEMM_CASE(M_, EPI_QKV, G) DL_GEMM_CASE(M_, EPI_ACT_F16, G) DL_GEMM_CASE(M_, EPI_RES, G)
-    DL_GEMM_CASES(1, kGemmStages) DL_GEMM_CASES(1, 3) DL_GEMM_CASES(1, 4) DL_GEMM_CASES(2, kGemmStages) DL_GEMM_CASES(2, 1) DL_GEMM_CASES(2, 3) DL_GEMM_CASES(4, 1) DL_GEMM_CASES(4, 2) DL_GEMM_CASES(8, 1)
+#define DL_GEMM_CASES(M_, G, R)                                                                         \
+    DL_GEMM_CASE(M_, EPI_STORE, G, R) DL_GEMM_CASE(M_, EPI_ACT, G, R) DL_GEMM_CASE(M_, EPI_ACT_Q80, G, R) \
+    DL_GEMM_CASE(M_, EPI_QKV, G, R) DL_GEMM_CASE(M_, EPI_ACT_F16, G, R) DL_GEMM_CASE(M_, EPI_RES, G, R)
+    DL_GEMM_CASES(1, kGemmStages, 1) DL_GEMM_CASES(1, 3, 1) DL_GEMM_CASES(1, 4, 1) DL_GEMM_CASES(2, kGemmStages, 1)
+    DL_GEMM_CASES(2, 1, 1) DL_GEMM_CASES(2, 3, 1) DL_GEMM_CASES(2, 4, 1) DL_GEMM_CASES(4, 1, 1) DL_GEMM_CASES(4, 2, 1)
+    DL_GEMM_CASES(4, 3, 1) DL_GEMM_CASES(8, 1, 1)
+    DL_GEMM_CASES(1, kGemmStages, 2) DL_GEMM_CASES(2, kGemmStages, 2) DL_GEMM_CASES(4, 1, 2)
 #undef DL_GEMM_CASES
 #undef DL_GEMM_CASE
+    throw Error("launchGemmQ40: no narrow kernel instance for this stage / row-tile choice");
 }
 
 // Batched matmul for F32 weights on MFMA (the reference runs F32 batches through

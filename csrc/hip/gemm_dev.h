@@ -9,6 +9,7 @@ namespace dl {
 namespace hipk {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+static constexpr int kGemmRows = 64;  // weight rows per narrow-GEMM workgroup (4 waves x 16)
 
 // 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d via the 0x6400 | q magic (1024 + q)
 __device__ __forceinline__ half8 dequantQ40x8(u32x2 wv, int nibHi, uint32_t d16) {
@@ -86,25 +87,24 @@ __device__ __forceinline__ bool splitArrive(int *counter, int S, int *flag) {
     return last;
 }
 // Sum S partials (P + s * stride, f32x4 units [0, n4)) in split order into dst (LDS; unit i lands
-// at dst[(i / rowU) * ldU + i % rowU], a padded row stride): every split's load of a unit is in
-// flight before the adds.
+// at dst[(i / rowU) * ldU + i % rowU], a padded row stride): the loads of 4 splits are in flight
+// before their adds. Register-lean on purpose: an 8-deep fully unrolled form set the whole
+// narrow kernel's VGPR allocation (224-231 at <= 16 tokens: 2 waves per SIMD for the main loop).
 __device__ __forceinline__ void splitCombine(const float *P, size_t stride, int S, int n4, f32x4 *dst, int rowU = 1,
                                              int ldU = 1) {
+    auto ld = [](const float *q) { return f32x4{wtLoad(q), wtLoad(q + 1), wtLoad(q + 2), wtLoad(q + 3)}; };
+#pragma clang loop unroll(disable)
     for (int i = threadIdx.x; i < n4; i += kThreads) {
-        f32x4 v[8];
+        f32x4 r = ld(P + 4 * i);
+#pragma clang loop unroll(disable)
+        for (int s0 = 1; s0 < S; s0 += 4) {
+            f32x4 v[4];
 #pragma unroll
-        for (int s2 = 0; s2 < 8; s2++)
-            if (s2 < S) {
-                const float *q = P + s2 * stride + 4 * i;
-                v[s2] = f32x4{wtLoad(q), wtLoad(q + 1), wtLoad(q + 2), wtLoad(q + 3)};
-            }
-        f32x4 r = v[0];
+            for (int j = 0; j < 4; j++)
+                if (s0 + j < S) v[j] = ld(P + (size_t)(s0 + j) * stride + 4 * i);
 #pragma unroll
-        for (int s2 = 1; s2 < 8; s2++)
-            if (s2 < S) r += v[s2];
-        for (int s2 = 8; s2 < S; s2++) {
-            const float *q = P + s2 * stride + 4 * i;
-            r += f32x4{wtLoad(q), wtLoad(q + 1), wtLoad(q + 2), wtLoad(q + 3)};
+            for (int j = 0; j < 4; j++)
+                if (s0 + j < S) r += v[j];
         }
         dst[(i / rowU) * ldU + i % rowU] = r;
     }
@@ -127,6 +127,7 @@ __device__ __forceinline__ void tpExchangeTile(const GemmArgs &ga, float *tile, 
     const int M = ga.M, nEl = M * 64, W = x.world;
     const bool failed = tpFailed(x);
     __syncthreads();
+    const long long t0 = tpSpanBegin(x);
     if (!x.q80) {
         for (int i = threadIdx.x; i < nEl; i += kThreads) {
             const int t = i >> 6, row = R0 + (i & 63);
@@ -143,6 +144,7 @@ __device__ __forceinline__ void tpExchangeTile(const GemmArgs &ga, float *tile, 
             x.epochs[el] = e;
         }
         __syncthreads();
+        tpSpanEnd(x, t0);
         return;
     }
     const int nBlk = nEl >> 5;
@@ -184,6 +186,7 @@ __device__ __forceinline__ void tpExchangeTile(const GemmArgs &ga, float *tile, 
         x.epochs[wd] = e;
     }
     __syncthreads();
+    tpSpanEnd(x, t0);
     for (int i = threadIdx.x; i < nEl; i += kThreads) {
         const int blk = i >> 5;
         float s = 0.f;
@@ -230,6 +233,9 @@ template <int EPI, int PAIRS>
 __device__ __forceinline__ void gemmEpilogue(const GemmArgs &ga, const float *tile, int ldT, int tl0, int tl1,
                                              int tokBase, int R0, int ssSlot0, const float *rsL) {
     const GemvArgs &a = ga.e;
+    // not unrolled: a fully unrolled short trip (<= 16 tokens) hoisted every iteration's loads and
+    // set the whole kernel's VGPR allocation (224+ -> 2 waves per SIMD for the main loop too)
+#pragma clang loop unroll(disable)
     for (int i = threadIdx.x; i < (tl1 - tl0) * PAIRS; i += kThreads) {
         const int tl = tl0 + i / PAIRS, k = i % PAIRS, r0 = R0 + 2 * k, t = tokBase + tl;
         float v0 = tile[tl * ldT + 2 * k], v1 = tile[tl * ldT + 2 * k + 1];
@@ -278,6 +284,79 @@ __device__ __forceinline__ void gemmEpilogue(const GemmArgs &ga, const float *ti
                              a.out + (size_t)t * a.ldOut);
         }
     }
+}
+
+// Split-K combine and fused epilogues shared by the batched GEMMs (Q40 and f32): `acc` holds this
+// lane's C fragments (weight row (local) wave*16 + col, token t*16 + h*4 + i); `smem` must hold
+// MP x 64 floats and is free (all K-loop LDS reads retired behind a barrier); `flag` one int.
+// tileIdx / tiles: this 64-row tile and the launch's tile count (split-K partial slots, counters).
+// Diagnostics (ga.e.trace): 8 u64 per workgroup (blockIdx.y * gridDim.x + blockIdx.x):
+// [0] entry, [1] first stage / ring slot landed, [2] K loop done, [3] split hand-off done (the
+// combining workgroup: partials summed; the others: arrival counted), [4] exit, [5] XCC id,
+// [6] 1 if this workgroup combined the tile (thread 0's view; s_memrealtime, 100 MHz).
+__device__ __forceinline__ void gemmTrace(const GemmArgs &ga, const unsigned long long (&t)[4], bool combined) {
+    if (!ga.e.trace || threadIdx.x != 0) return;
+    unsigned long long *o = ga.e.trace + 8 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x);
+    o[0] = t[0];
+    o[1] = t[1];
+    o[2] = t[2];
+    o[3] = t[3];
+    o[4] = wall_clock64();
+    o[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;
+    o[6] = combined ? 1ull : 0ull;
+}
+
+template <int MT, int EPI>
+__device__ __forceinline__ void gemmFinish(const GemmArgs &ga, const f32x4 (&acc)[MT], char *smem, int *flag,
+                                           int tileIdx, int tiles, unsigned long long t0 = 0,
+                                           unsigned long long t1 = 0, unsigned long long t2 = 0) {
+    unsigned long long tr[4] = {t0, t1, t2, 0ull};
+    constexpr int MP = MT * 16;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int col = lane & 15, h = lane >> 4, rl = wave * 16 + col;
+    const int sp = blockIdx.y, S = ga.splits;
+    const int R0 = tileIdx * kGemmRows;
+    float *tile = reinterpret_cast<float *>(smem);  // [MP][64], stages are free now
+    // C layout: weight row (local) wave*16 + col, token t*16 + h*4 + i
+    if (S == 1) {
+#pragma unroll
+        for (int t = 0; t < MT; t++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) tile[(t * 16 + h * 4 + i) * kGemmRows + rl] = acc[t][i];
+    } else {
+        // Partials are written and read with agent-scope atomic accesses (global_store / load sc1:
+        // performed at the coherence point, never held in or served from one XCD's L2), so the
+        // hand-off needs no fence: an agent-scope release / acquire fence is a whole-L2 writeback
+        // (buffer_wbl2) / invalidate (buffer_inv) on gfx950, which measured ~28 us per split level
+        // on w13 (448 -> 896 workgroups) and evicted the other workgroups' cached activations.
+        // vmcnt(0) before the arrival count: every partial store has been performed.
+        float *part = ga.part + ((size_t)sp * tiles + tileIdx) * MP * kGemmRows;
+#pragma unroll
+        for (int t = 0; t < MT; t++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) wtStore(part + (t * 16 + h * 4 + i) * kGemmRows + rl, acc[t][i]);
+        if (!splitArrive(ga.counters + tileIdx, S, flag)) {
+            if (ga.e.trace) {
+                tr[3] = wall_clock64();
+                gemmTrace(ga, tr, false);
+            }
+            return;
+        }
+        // combine in split order (deterministic): this tail runs on one workgroup per tile after
+        // the others finished
+        splitCombine(ga.part + (size_t)tileIdx * MP * kGemmRows, (size_t)tiles * MP * kGemmRows, S,
+                     MP * kGemmRows / 4, reinterpret_cast<f32x4 *>(tile));
+    }
+    if (ga.e.trace) tr[3] = wall_clock64();
+    // tensor parallel: the tile's partial sums all-reduced over the ranks in place (staging after
+    // the [MP][64] tile; the host checked that the launch's LDS holds it)
+    if (ga.tpx) tpExchangeTile(ga, tile, R0, smem + (size_t)MP * kGemmRows * 4);
+    // consumer of a fused residual + norm: per-token RMS scale from the producer's tile partials
+    float *rsL = reinterpret_cast<float *>(flag + 4);  // [128] + [256] scratch
+    if (ga.ssIn) gemmRowScales(ga, 0, MP, rsL, rsL + 128);
+    __syncthreads();
+    gemmEpilogue<EPI, 32>(ga, tile, kGemmRows, 0, ga.M, 0, R0, tileIdx, ga.ssIn ? rsL : nullptr);
+    if (ga.e.trace) gemmTrace(ga, tr, true);
 }
 
 }  // namespace hipk

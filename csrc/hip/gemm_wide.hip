@@ -46,7 +46,13 @@ bool gemmWideOn() {
     }();
     return v;
 }
-int gemmWideMin() { return 65; }  // below: narrow kernel (wide at 17-64 rows measured slower, r3)
+int gemmWideMin() {  // below: narrow kernel (wide at 17-64 rows measured slower, r3); DL_GEMM_WIDE_MIN
+    static const int v = [] {
+        const char *e = std::getenv("DL_GEMM_WIDE_MIN");
+        return e && std::atoi(e) > 0 ? std::atoi(e) : 65;
+    }();
+    return v;
+}
 bool gemmUsesWide(int M) { return gemmWideOn() && M >= gemmWideMin(); }
 
 // K splits: grow while the grid stays under one workgroup per CU (256) and every split keeps >= 16

@@ -20,6 +20,21 @@ namespace hipk {
 //   of upstream Q80), row-pair epilogues (SwiGLU, RoPE + KV append) run in registers.
 // ------------------------------------------------------------------------------------------------
 static constexpr int kRing = 8;
+
+// f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>): ring slots addressed by
+// compile-time indices (fixed registers) however large the body (the compiler may decline to
+// unroll a loop, which would index the ring dynamically and spill it).
+template <int I, int N, typename F>
+__device__ __forceinline__ void staticForImpl(F &f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        staticForImpl<I + 1, N>(f);
+    }
+}
+template <int N, typename F>
+__device__ __forceinline__ void staticFor(F &&f) {
+    staticForImpl<0, N>(f);
+}
 #ifndef DL_GEMV_KE
 #define DL_GEMV_KE 2
 #endif
@@ -398,21 +413,21 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
     // Full rounds: every slot is consumed and refilled, so the slots stay in fixed registers and
     // consuming slot s waits until only the other kRing-1 slots are in flight.
     int t0 = 0;
-    for (; t0 + D < T; t0 += D) {
-#pragma unroll
-        for (int s = 0; s < D; s++) {
-            asm volatile("s_waitcnt vmcnt(%3)" : "+v"(w[s][0]), "+v"(w[s][1]), "+v"(dh[s]) : "i"(3 * (D - 1)));
-            consume(w[s], dh[s], true);
-            if (a.trace && s == 0 && t0 == 0) tFirst = wall_clock64();
-            issue(w[s], dh[s]);
-            advance();
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
+    auto fullSlot = [&](auto sTag) {
+        constexpr int s = decltype(sTag)::value;
+        asm volatile("s_waitcnt vmcnt(%3)" : "+v"(w[s][0]), "+v"(w[s][1]), "+v"(dh[s]) : "i"(3 * (D - 1)));
+        consume(w[s], dh[s], true);
+        if (a.trace && s == 0 && t0 == 0) tFirst = wall_clock64();
+        issue(w[s], dh[s]);
+        advance();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    for (; t0 + D < T; t0 += D) staticFor<D>(fullSlot);
     // Last round: no refills; slot s waits for the loads issued after it (slots s+1..kRing-1), so
-    // every load has landed when the workgroup ends.
-#pragma unroll
-    for (int s = 0; s < D; s++) {
+    // every load has landed when the workgroup ends. (Slots expanded at compile time: the wait
+    // count must be an immediate even where the compiler declines to unroll a large body.)
+    auto lastSlot = [&](auto sTag) {
+        constexpr int s = decltype(sTag)::value;
         asm volatile("s_waitcnt vmcnt(%3)" : "+v"(w[s][0]), "+v"(w[s][1]), "+v"(dh[s]) : "i"(3 * (D - 1 - s)));
         if (t0 + s < T) {
             consume(w[s], dh[s], true);
@@ -420,7 +435,8 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
             advance();
         }
         __builtin_amdgcn_sched_barrier(0);
-    }
+    };
+    staticFor<D>(lastSlot);
     };
 
     const int unitsPerThread = PRO != PRO_GLOBAL ? (n + 8 * kThreads - 1) / (8 * kThreads)

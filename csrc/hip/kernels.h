@@ -124,6 +124,10 @@ struct TpXchg {
     long long timeoutTicks = 0;         // s_memrealtime ticks (100 MHz)
     int rank = 0, world = 1;
     int q80 = 0;                        // exchange Q80 blocks (the reference's ZQ wire format)
+    // measured sync (ForwardStats::syncMs): when set, every workgroup that exchanges raises this
+    // word to its exchange span (push -> every peer's words collected) in s_memrealtime ticks (10
+    // ns), so the word holds the slowest workgroup's span of this exchange
+    unsigned *ticks = nullptr;
 };
 
 struct GemvArgs {
@@ -320,8 +324,11 @@ int attnSplitGrid(int seqLen);
 int attnChunkMax(int seqLen, int splitGrid);
 
 // epoch (optional): one thread increments it - the per-forward epoch of the fused attention block.
+// zero / nZero (optional): words cleared at the start of the forward (the measured-sync slots).
 void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s,
-                     unsigned *epoch = nullptr);
+                     unsigned *epoch = nullptr, unsigned *zero = nullptr, int nZero = 0);
+// One s_memrealtime stamp (100 MHz) into *p: brackets a separate collective for the measured sync.
+void launchStamp(unsigned long long *p, hipStream_t s);
 // Parallel argmax over [B][vocab]; partials need B*256 floats + ints, counters B ints (zeroed).
 // When `tokens` is non-null the result is also fed back (tokens[b] = id; hist[b][pos] = id; pos += 1).
 struct ArgmaxArgs {

@@ -218,9 +218,12 @@ void launchAttentionValu(const AttnArgs &a, int B, hipStream_t s) {
 // ------------------------------------------------------------------------------------------------
 // Small kernels
 // ------------------------------------------------------------------------------------------------
-__global__ void embeddingKernel(const float *table, const int *tokens, float *x, int dim, unsigned *epoch) {
+__global__ void embeddingKernel(const float *table, const int *tokens, float *x, int dim, unsigned *epoch,
+                                unsigned *zero, int nZero) {
     const int b = blockIdx.x;
     if (epoch && b == 0 && threadIdx.x == 0) *epoch += 1;  // read by later kernels of this forward
+    if (b == 0)
+        for (int i = threadIdx.x; i < nZero; i += blockDim.x) zero[i] = 0u;
     const float *src = table + (size_t)tokens[b] * dim;
     float *dst = x + (size_t)b * dim;
     // all of a thread's row loads in flight before the first store (one HBM round trip, not four)
@@ -240,9 +243,16 @@ __global__ void embeddingKernel(const float *table, const int *tokens, float *x,
     }
 }
 
-void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s, unsigned *epoch) {
-    hipLaunchKernelGGL(embeddingKernel, dim3(B), dim3(256), 0, s, table, tokens, x, dim, epoch);
+void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s, unsigned *epoch,
+                     unsigned *zero, int nZero) {
+    hipLaunchKernelGGL(embeddingKernel, dim3(B), dim3(256), 0, s, table, tokens, x, dim, epoch, zero, nZero);
 }
+
+__global__ void stampKernel(unsigned long long *p) {
+    if (threadIdx.x == 0) *p = wall_clock64();
+}
+
+void launchStamp(unsigned long long *p, hipStream_t s) { hipLaunchKernelGGL(stampKernel, dim3(1), dim3(64), 0, s, p); }
 
 // In-place Q80 round trip of f32 values (32-element blocks, rintf like every Q80 producer here).
 __global__ void q80RoundtripKernel(float *x, size_t n) {

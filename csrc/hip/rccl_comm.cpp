@@ -52,6 +52,19 @@ class RcclComm : public DeviceComm {
     void allGather(const float *send, float *recv, size_t nPerRank, hipStream_t s) override {
         DL_NCCL(ncclAllGather(send, recv, nPerRank, ncclFloat32, comm_, s));
     }
+    // Root-only gather (the reference's SYNC_NODE_SLICES_EXCEPT_ROOT, llm.cpp:432): point-to-point
+    // sends to rank 0 move 1/N of an all-gather's bytes; rank 0 places its own slice locally.
+    void gatherToRoot(const float *send, float *recv, size_t nPerRank, hipStream_t s) override {
+        if (rank_ == 0) DL_HIP(hipMemcpyAsync(recv, send, nPerRank * sizeof(float), hipMemcpyDeviceToDevice, s));
+        if (size_ == 1) return;
+        DL_NCCL(ncclGroupStart());
+        if (rank_ == 0) {
+            for (int p = 1; p < size_; p++) DL_NCCL(ncclRecv(recv + (size_t)p * nPerRank, nPerRank, ncclFloat32, p, comm_, s));
+        } else {
+            DL_NCCL(ncclSend(send, nPerRank, ncclFloat32, 0, comm_, s));
+        }
+        DL_NCCL(ncclGroupEnd());
+    }
     void broadcastInts(int *buf, size_t n, int root, hipStream_t s) override {
         DL_NCCL(ncclBroadcast(buf, buf, n, ncclInt32, root, comm_, s));
     }

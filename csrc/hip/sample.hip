@@ -95,6 +95,7 @@ __global__ __launch_bounds__(256) void argmaxKernel(ArgmaxArgs a) {
         // pick the same one in rank order (ties -> lowest index, like a full-vocabulary argmax)
         const TpXchg &x = a.tp;
         const bool failed = tpFailed(x);
+        const long long t0 = tpSpanBegin(x);
         const unsigned ev = x.epochs[2 * b] + 1, ei = x.epochs[2 * b + 1] + 1;  // one epoch per word
         unsigned vv[kTpMaxRanks], vi[kTpMaxRanks];
         tpPushCollect(x, 2LL * b, ev, __float_as_uint(bv), vv, failed);
@@ -104,6 +105,7 @@ __global__ __launch_bounds__(256) void argmaxKernel(ArgmaxArgs a) {
         for (int p = 0; p < x.world; p++) argBetter(bv, bi, __uint_as_float(vv[p]), (int)vi[p]);
         x.epochs[2 * b] = ev;
         x.epochs[2 * b + 1] = ei;
+        tpSpanEnd(x, t0);
     }
     if (threadIdx.x == 0) argmaxStore(a, b, bi);
 }

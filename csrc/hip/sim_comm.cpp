@@ -1,7 +1,9 @@
 // Test-only DeviceComm: N tensor-parallel ranks simulated as N threads/engines on ONE GPU,
 // exchanging partial sums through host memory. Used to validate the multi-rank engine logic
 // (shard plan, per-layer all-reduce placement, logits all-gather + unshard) on hardware where
-// only one GPU is available; the production data plane is RCCL (rccl_comm.cpp).
+// only one GPU is available. The production data planes are the one-shot xGMI collectives and the
+// exchange fused into the wo / w2 kernels (xgmi_comm.cpp, decode_common.h), with RCCL
+// (rccl_comm.cpp) as the fallback when their self-test fails.
 #include <hip/hip_runtime.h>
 
 #include <condition_variable>

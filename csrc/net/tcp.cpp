@@ -240,7 +240,7 @@ std::string encodeWorkerConfig(const WorkerConfig &c) {
     const ModelHeader &h = e.syntheticHeader;
     o << "magic=" << kProtoMagic << "\nversion=" << kProtoVersion << "\nrank=" << c.rank << "\nworld=" << c.world
       << "\ngpu=" << (c.gpu ? 1 : 0) << "\nmodel=" << e.modelPath << "\nmax_seq_len=" << e.maxSeqLen
-      << "\nmax_batch=" << e.maxBatch << "\nn_slots=" << e.nSlots << "\nbuffer=" << (int)e.bufferType
+      << "\nmax_batch=" << e.maxBatch << "\nmax_decode=" << e.maxDecode << "\nn_slots=" << e.nSlots << "\nbuffer=" << (int)e.bufferType
       << "\nsync=" << (int)e.syncType
       << "\ngraphs=" << (e.useGraphs ? 1 : 0) << "\nkv_bf16=" << (e.kvBf16 ? 1 : 0) << "\nkv_pages=" << e.kvPages
       << "\nkv_page_size=" << e.kvPageSize
@@ -274,6 +274,7 @@ WorkerConfig decodeWorkerConfig(const std::string &s) {
         else if (k == "model") e.modelPath = v;
         else if (k == "max_seq_len") e.maxSeqLen = std::stoul(v);
         else if (k == "max_batch") e.maxBatch = std::stoul(v);
+        else if (k == "max_decode") e.maxDecode = std::stoul(v);
         else if (k == "n_slots") e.nSlots = std::stoul(v);
         else if (k == "buffer") e.bufferType = (FloatType)std::stoi(v);
         else if (k == "sync") e.syncType = (FloatType)std::stoi(v);

@@ -139,6 +139,7 @@ std::vector<int> runSample(Backend &b, const std::vector<int> &tokens, const std
 struct PyComm {
     std::shared_ptr<DeviceComm> comm;
 };
+struct PyRcclComm : PyComm {};
 
 // Keeps the device comm alive as long as the engine.
 struct PyHipEngine {
@@ -590,7 +591,9 @@ PYBIND11_MODULE(_C, m) {
           py::arg("rows"), py::arg("n"), py::arg("pro"), py::arg("epi"), py::arg("batch") = 1, py::arg("lanes") = 0,
           py::arg("passes") = 0, py::arg("copies") = 8, py::arg("iters") = 20,
           "bench_gemv_q40 with per-workgroup s_memrealtime stamps: (us, u64[iters*grid*4])");
-    m.def("bench_gemm_q40", &benchGemmQ40, py::arg("rows"), py::arg("n"), py::arg("tokens"), py::arg("epi") = 0,
+    m.def("bench_gemm_q40", [](int rows, int n, int M, int epi, int copies, int iters) {
+              return benchGemmQ40(rows, n, M, epi, copies, iters);
+          }, py::arg("rows"), py::arg("n"), py::arg("tokens"), py::arg("epi") = 0,
           py::arg("copies") = 8, py::arg("iters") = 100, py::call_guard<py::gil_scoped_release>());
     m.def("bench_attention",
           [](int nh, int kvm, int hs, int seq, int pos, int B, int copies, int iters) {
@@ -598,6 +601,19 @@ PYBIND11_MODULE(_C, m) {
           },
           py::arg("n_heads0"), py::arg("kv_mul"), py::arg("head_size"), py::arg("seq_len"), py::arg("pos"),
           py::arg("batch") = 1, py::arg("copies") = 32, py::arg("iters") = 200, py::call_guard<py::gil_scoped_release>());
+    m.def("trace_gemm_q40",
+          [](int rows, int n, int M, int epi, int copies, int iters) {
+              std::vector<unsigned long long> t;
+              double us;
+              {
+                  py::gil_scoped_release rel;
+                  us = benchGemmQ40(rows, n, M, epi, copies, iters, &t);
+              }
+              return py::make_tuple(us, t, (int)(t.size() / 8 / ((rows + 63) / 64)));
+          },
+          py::arg("rows"), py::arg("n"), py::arg("tokens"), py::arg("epi") = 0, py::arg("copies") = 8,
+          py::arg("iters") = 50,
+          "bench_gemm_q40, then one launch with per-workgroup stamps (gemm_dev.h gemmTrace): (us, u64[], splits)");
     m.def("trace_attention",
           [](int nh, int kvm, int hs, int seq, int pos, int B, int copies, int iters) {
               std::vector<unsigned long long> t;
@@ -739,7 +755,59 @@ PYBIND11_MODULE(_C, m) {
             }
             std::memcpy(out.mutable_data(), r.data(), n * w * 4);
             return out;
-        });
+        })
+        // rank 0 gets every rank's x in rank order (other ranks: zeros)
+        .def("gather_to_root", [](PyComm &c, py::array_t<float, py::array::c_style | py::array::forcecast> x) {
+            const size_t n = (size_t)x.size();
+            const int w = c.comm->size();
+            py::array_t<float> out((py::ssize_t)(n * w));
+            std::vector<float> h(x.data(), x.data() + n), r(n * w);
+            {
+                py::gil_scoped_release rel;
+                float *d, *o;
+                DL_HIP(hipMalloc(&d, n * 4));
+                DL_HIP(hipMalloc(&o, n * w * 4));
+                DL_HIP(hipMemset(o, 0, n * w * 4));
+                DL_HIP(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+                c.comm->gatherToRoot(d, o, n, nullptr);
+                DL_HIP(hipMemcpy(r.data(), o, n * w * 4, hipMemcpyDeviceToHost));
+                DL_HIP(hipFree(d));
+                DL_HIP(hipFree(o));
+            }
+            std::memcpy(out.mutable_data(), r.data(), n * w * 4);
+            return out;
+        })
+        .def("broadcast_ints", [](PyComm &c, std::vector<int> v, int root) {
+            py::gil_scoped_release rel;
+            int *d;
+            DL_HIP(hipMalloc(&d, v.size() * 4));
+            DL_HIP(hipMemcpy(d, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+            c.comm->broadcastInts(d, v.size(), root, nullptr);
+            DL_HIP(hipMemcpy(v.data(), d, v.size() * 4, hipMemcpyDeviceToHost));
+            DL_HIP(hipFree(d));
+            return v;
+        }, py::arg("values"), py::arg("root") = 0)
+        // the engine's separate-collective schedule, eager or captured + replayed (engine.h)
+        .def("schedule_check",
+             [](PyComm &c, int layers, int rows, int dim, int vocab0, int runs, bool graph) {
+                 py::gil_scoped_release rel;
+                 return commScheduleCheck(*c.comm, layers, rows, dim, vocab0, runs, graph);
+             },
+             py::arg("layers") = 4, py::arg("rows") = 4, py::arg("dim") = 4096, py::arg("vocab0") = 1000,
+             py::arg("runs") = 3, py::arg("graph") = true);
+
+    // RCCL data plane (the fallback of the xGMI one): same helpers, created from an RCCL unique id
+    py::class_<PyRcclComm, PyComm>(m, "RcclComm")
+        .def(py::init([](py::bytes uid, int rank, int world, int gpuIndex) {
+                 const std::string s = uid;
+                 auto *c = new PyRcclComm();
+                 py::gil_scoped_release rel;
+                 DL_HIP(hipSetDevice(gpuIndex));
+                 c->comm = std::shared_ptr<DeviceComm>(
+                     makeRcclComm(std::vector<unsigned char>(s.begin(), s.end()), rank, world).release());
+                 return c;
+             }),
+             py::arg("uid"), py::arg("rank") = 0, py::arg("world") = 1, py::arg("gpu_index") = 0);
 
     py::class_<PyHipEngine>(m, "HipEngine")
         .def(py::init([](const std::string &model, const std::string &bufferType, u32 maxSeqLen, u32 maxBatch,

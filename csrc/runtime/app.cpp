@@ -121,6 +121,7 @@ static EngineConfig engineConfigFrom(const AppArgs &a, int nSlots) {
     c.modelPath = a.modelPath;
     c.maxSeqLen = a.maxSeqLen;
     c.maxBatch = (u32)std::max(a.nBatches, prefillChunkOf(a));  // rows the engine's buffers hold
+    c.maxDecode = (u32)a.nBatches;  // decode-only state (chain history, argmax exchange) for decode rows
     c.nSlots = (u32)nSlots;
     c.bufferType = a.bufferType;
     c.syncType = a.syncType;
@@ -220,6 +221,15 @@ InferenceSession::InferenceSession(const AppArgs &args, int nSlots) : args_(args
             hostComm_.reset(new TcpHostComm(0, world, peers));
         }
         if (logLevel() >= 1) std::printf("⭕ Network is initialized (%d nodes)\n", world);
+        // ranks sharing one GPU (same-GPU rehearsals): a rank spinning in its exchange on a
+        // 256+-row forward can keep its peer's kernels off the CUs until the collective times out,
+        // so the default prompt chunk drops to 32 rows there (an explicit --prefill-chunk stays)
+        if (devComm_ && devComm_->ranksOnDevice() > 1 && args.prefillChunk <= 0 && prefillChunk_ > 32) {
+            prefillChunk_ = std::max(32, args.nBatches);
+            if (logLevel() >= 1)
+                std::printf("ℹ️  %d ranks share this GPU: prompt chunks of %d rows\n", devComm_->ranksOnDevice(),
+                            prefillChunk_);
+        }
     }
     backend_ = makeBackend(ec, gpu_, hostComm_.get(), devComm_.get());
     for (auto &s : workers_) {

@@ -20,6 +20,9 @@ struct EngineConfig {
     std::string modelPath;          // .m file (ignored when synthetic)
     u32 maxSeqLen = 0;              // clamp of header seqLen (0 = model's)
     u32 maxBatch = 32;              // max rows per forward (reference nBatches, app.cpp:37)
+    u32 maxDecode = 0;              // rows of decode-only state (greedy-chain history, fused argmax
+                                    // exchange); 0 = maxBatch. The CLI / API set --max-batch here and
+                                    // size maxBatch by the (larger) prefill chunk.
     u32 nSlots = 1;                 // independent KV-cache slots (concurrent sequences)
     FloatType bufferType = FloatType::F32;  // activation quantization: Q80 or F32
     FloatType syncType = FloatType::F32;    // CPU tensor-parallel wire format of partial sums:

@@ -75,7 +75,8 @@ def _preds(out):
 def test_cli_output_lines(assets):
     rc, out = _inference(assets, steps=12)
     assert rc == 0, out
-    assert re.search(r"🔷️ Eval\s+\d+ ms Sync\s+\d+ ms \| Sent\s+\d+ kB Recv\s+\d+ kB \| \(\d+ tokens\)", out)
+    # the reference's line (integer ms there; two decimals here: a GPU token takes ~1 ms)
+    assert re.search(r"🔷️ Eval\s+[\d.]+ ms Sync\s+[\d.]+ ms \| Sent\s+\d+ kB Recv\s+\d+ kB \| \(\d+ tokens\)", out)
     n_eval = int(re.search(r"Evaluation\n\s+nBatches: \d+\n\s+nTokens: (\d+)", out).group(1))
     assert len(_preds(out)) == 12 - n_eval
     assert re.search(r"Evaluation\n\s+nBatches: 32\n\s+nTokens: \d+\n\s+tokens/s: [\d.]+ \([\d.]+ ms/tok\)", out)
