@@ -11,21 +11,24 @@ namespace hipk {
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 static constexpr int kGemmRows = 64;  // weight rows per narrow-GEMM workgroup (4 waves x 16)
 
-// 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d via the 0x6400 | q magic (1024 + q)
+// 8 nibbles (lo or hi of 8 bytes) -> 8 f16 values (q - 8) * d. Low nibbles: f16 bits 0x64 | q =
+// 1024 + q; high nibbles stay in place (byte & 0xF0 = 16 q) under exponent byte 0x54, whose ulp
+// is 1/16: 64 + q. Subtracting 1032 / 72 gives q - 8 exactly; one rounding in the multiply by d.
+// The mask, magic and offset depend on nibHi only (per lane, loop-invariant): no per-lane shift.
 __device__ __forceinline__ half8 dequantQ40x8(u32x2 wv, int nibHi, uint32_t d16) {
-    // one variable shift per word instead of a shift + select (nibHi is per lane, not uniform)
-    const uint32_t sh = (uint32_t)nibHi << 2;
-    const uint32_t lo = (wv.x >> sh) & 0x0F0F0F0Fu;
-    const uint32_t hi = (wv.y >> sh) & 0x0F0F0F0Fu;
-    const uint32_t p0 = __builtin_amdgcn_perm(0x64646464u, lo, 0x07010700u);
-    const uint32_t p1 = __builtin_amdgcn_perm(0x64646464u, lo, 0x07030702u);
-    const uint32_t p2 = __builtin_amdgcn_perm(0x64646464u, hi, 0x07010700u);
-    const uint32_t p3 = __builtin_amdgcn_perm(0x64646464u, hi, 0x07030702u);
+    const uint32_t mask = nibHi ? 0xF0F0F0F0u : 0x0F0F0F0Fu;
+    const uint32_t magic = nibHi ? 0x54545454u : 0x64646464u;
+    const uint32_t lo = wv.x & mask;
+    const uint32_t hi = wv.y & mask;
+    const uint32_t p0 = __builtin_amdgcn_perm(magic, lo, 0x07010700u);
+    const uint32_t p1 = __builtin_amdgcn_perm(magic, lo, 0x07030702u);
+    const uint32_t p2 = __builtin_amdgcn_perm(magic, hi, 0x07010700u);
+    const uint32_t p3 = __builtin_amdgcn_perm(magic, hi, 0x07030702u);
     typedef _Float16 h2 __attribute__((ext_vector_type(2)));
     const _Float16 d = __builtin_bit_cast(_Float16, (uint16_t)d16);
-    // (1024 + q) - 1032 = q - 8 is exact in f16; one rounding in the multiply by d
     const h2 dd = {d, d};
-    const h2 off = {(_Float16)-1032.0f, (_Float16)-1032.0f};
+    const _Float16 o = nibHi ? (_Float16)-72.0f : (_Float16)-1032.0f;
+    const h2 off = {o, o};
     const h2 r0 = (__builtin_bit_cast(h2, p0) + off) * dd;
     const h2 r1 = (__builtin_bit_cast(h2, p1) + off) * dd;
     const h2 r2 = (__builtin_bit_cast(h2, p2) + off) * dd;
