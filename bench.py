@@ -158,6 +158,9 @@ def main() -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-f32kv", action="store_true", help="skip the f32 KV-cache decode point")
     ap.add_argument("--no-prefill4k", action="store_true", help="skip the 4096-token prompt-eval point")
+    ap.add_argument("--tp-rank-compute", default="2,4,8",
+                    help="1 GPU: TP degrees whose rank-0 shard is timed with the exchange removed "
+                         "(compute-only comm; '' = off)")
     ap.add_argument("--prefill-chunk", type=int, default=1024,
                     help="rows per forward of the second 4096-token prompt point (the first uses the reference's 32)")
     args = ap.parse_args()
@@ -397,9 +400,36 @@ def main() -> int:
             else BASELINE_MS_70B.get(world) if args.shape == "llama3_3_70b" and not args.model else None)
     if same_gpu:
         base = None  # a rehearsal on one device is not a point of the scaling curve
+    # a TP-N rank's own work on one GPU: rank 0's shard shapes and kernels (fused exchange in
+    # loopback, separate collectives no-ops), i.e. the per-token floor of a TP-N rank without sync
+    tp_rank = {}
+    if world == 1 and args.tp_rank_compute and not args.model:
+        del eng
+        for n in [int(v) for v in args.tp_rank_compute.split(",") if v]:
+            e = C.HipEngine("", "q80", max_seq_len=seq_len, max_batch=max_batch, n_slots=B, kv_bf16=True,
+                            gpu_index=local, use_graphs=not args.no_graphs, synthetic=dict(shape, seq_len=seq_len),
+                            seed=1234, rank=0, world=n, comm=C.ComputeOnlyComm(0, n, local),
+                            sync_type=args.sync_type)
+            for _ in range(2):
+                e.forward_argmax(prompt[:32], list(range(32)), [0] * 32)
+            torch.cuda.synchronize()
+            tq = time.perf_counter()
+            for s0 in range(0, len(prompt) - 31, 32):
+                e.forward_argmax(prompt[s0:s0 + 32], list(range(s0, s0 + 32)), [0] * 32)
+            torch.cuda.synchronize()
+            ev = (time.perf_counter() - tq) * 1000.0 / max(32, len(prompt) // 32 * 32)
+            e.decode_greedy(8, tokens, [pos0] * B, list(range(B)))
+            torch.cuda.synchronize()
+            tq = time.perf_counter()
+            e.decode_greedy(64, tokens, [pos0 + 8] * B, list(range(B)))
+            torch.cuda.synchronize()
+            tp_rank[f"tp{n}_rank_compute_ms_per_token"] = round((time.perf_counter() - tq) * 1000.0 / 64 / B, 4)
+            tp_rank[f"tp{n}_rank_compute_eval_ms_per_token"] = round(ev / B, 4)
+            del e
+        eng = None
     cli = {}
     if world == 1 and not args.no_cli and args.shape == "llama3_1_8b" and not args.model:
-        del eng
+        eng = None
         cli = _cli_point(local, min(args.prompt, 64), min(args.steps, 64), seq_len)
     result = {
         "metric": METRIC,
@@ -442,6 +472,7 @@ def main() -> int:
             "tp_sync": args.sync_type if world > 1 else None,
             "tp_fused_exchange": tp_fused,
             "tp_f32_pred_ms_per_token": round(tpf32_ms / B, 4) if tpf32_ms is not None else None,
+            **tp_rank,
             **cli,
         },
     }

@@ -368,6 +368,11 @@ __device__ __forceinline__ bool tpFailed(const TpXchg &x) {
 __device__ __forceinline__ void tpPushCollect(const TpXchg &x, long long w, unsigned e, unsigned payload,
                                               unsigned (&vals)[kTpMaxRanks], bool failed) {
     const int me = x.rank, W = x.world;
+    if (x.loopback) {
+#pragma unroll
+        for (int p = 0; p < kTpMaxRanks; p++) vals[p] = p == me ? payload : 0u;
+        return;
+    }
     const long long par = e & 1;
     const uint64_t word = (uint64_t)payload | ((uint64_t)e << 32);
 #pragma unroll

@@ -51,8 +51,15 @@ class DeviceComm {
         (void)region;
         (void)x;
         return false;
-    }
+    }    // No data plane at all (makeComputeOnlyComm): the engine skips the fused-exchange self-test.
+    virtual bool computeOnly() const { return false; }
 };
+
+// Rank `rank` of a `world`-rank tensor-parallel group with no peers (sim_comm.cpp): collectives
+// are no-ops and the fused exchange runs in loopback (TpXchg::loopback), so one GPU times a TP-N
+// rank's shard kernels with the exchange removed (bench.py --tp-rank-compute). Not a data plane:
+// the model's outputs are those of one shard.
+std::unique_ptr<DeviceComm> makeComputeOnlyComm(int rank, int world);
 
 // 128-byte RCCL unique id (generated on rank 0, distributed over the control plane).
 std::vector<unsigned char> rcclGetUniqueId();

@@ -322,7 +322,7 @@ void HipEngineImpl::launchStampAt(unsigned long long *p) { hipk::launchStamp(p, 
 // self-tested at start-up, or RCCL). DL_TP_FUSED=fail makes rank 1 report a failure (tests).
 void HipEngineImpl::tpFusedSelfTest() {
     tpTested_ = true;
-    if (!tpFused_) return;
+    if (!tpFused_ || comm_->computeOnly()) return;
     const int W = plan_.nRanks, me = rank();
     const char *e = std::getenv("DL_TP_FUSED");
     bool ok = !(e && std::strcmp(e, "fail") == 0 && me == 1);

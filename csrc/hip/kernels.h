@@ -128,6 +128,9 @@ struct TpXchg {
     // word to its exchange span (push -> every peer's words collected) in s_memrealtime ticks (10
     // ns), so the word holds the slowest workgroup's span of this exchange
     unsigned *ticks = nullptr;
+    // compute-only rank (makeComputeOnlyComm): nothing crosses a link, every peer contributes
+    // zeros - a TP-N rank's kernels timed on one GPU without the exchange
+    int loopback = 0;
 };
 
 struct GemvArgs {

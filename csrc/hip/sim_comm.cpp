@@ -15,6 +15,7 @@
 #include "../core/common.h"
 #include "device_comm.h"
 #include "engine.h"
+#include "kernels.h"
 
 namespace dl {
 
@@ -85,7 +86,60 @@ class SimComm : public DeviceComm {
     int rank_;
 };
 
+// Compute-only rank (device_comm.h makeComputeOnlyComm): the shard shapes and kernels of rank
+// `rank` of `world`, nothing exchanged. The fused exchange keeps its local work (Q80 quantize,
+// rank-order sum, epochs) with every peer's words read as zeros; the separate collectives are
+// no-ops except that an all-gather places this rank's own slice.
+class ComputeOnlyComm : public DeviceComm {
+  public:
+    ComputeOnlyComm(int rank, int world) : rank_(rank), world_(world) {
+        if (world < 2 || world > hipk::kTpMaxRanks || rank < 0 || rank >= world)
+            throw Error("compute-only comm: bad rank / world");
+        DL_HIP(hipMalloc(&epochs_, (kVec + kArg) * sizeof(unsigned)));
+        DL_HIP(hipMemset(epochs_, 0, (kVec + kArg) * sizeof(unsigned)));
+        DL_HIP(hipMalloc(&error_, sizeof(int)));
+        DL_HIP(hipMemset(error_, 0, sizeof(int)));
+    }
+    ~ComputeOnlyComm() override {
+        (void)hipFree(epochs_);
+        (void)hipFree(error_);
+    }
+    int rank() const override { return rank_; }
+    int size() const override { return world_; }
+    std::string name() const override { return "compute-only"; }
+    bool computeOnly() const override { return true; }
+    const int *deviceErrorFlag() const override { return error_; }
+    void resetError() override { DL_HIP(hipMemset(error_, 0, sizeof(int))); }
+    void allReduceSum(float *, size_t, hipStream_t) override {}
+    void allGather(const float *send, float *recv, size_t nPerRank, hipStream_t s) override {
+        DL_HIP(hipMemcpyAsync(recv + (size_t)rank_ * nPerRank, send, nPerRank * sizeof(float),
+                              hipMemcpyDeviceToDevice, s));
+    }
+    void broadcastInts(int *, size_t, int, hipStream_t) override {}
+    bool fusedXchg(int region, hipk::TpXchg *x) const override {
+        *x = hipk::TpXchg{};
+        x->epochs = region == 0 ? epochs_ : epochs_ + kVec;
+        x->error = error_;
+        x->stride = region == 0 ? kVec : kArg;
+        x->timeoutTicks = 1;
+        x->rank = rank_;
+        x->world = world_;
+        x->loopback = 1;
+        return true;
+    }
+
+  private:
+    static constexpr long long kVec = 1 << 18, kArg = 2048;  // the xGMI comm's fused regions
+    int rank_, world_;
+    unsigned *epochs_ = nullptr;
+    int *error_ = nullptr;
+};
+
 }  // namespace
+
+std::unique_ptr<DeviceComm> makeComputeOnlyComm(int rank, int world) {
+    return std::unique_ptr<DeviceComm>(new ComputeOnlyComm(rank, world));
+}
 
 // Runs `steps` single-token forwards (token i at position i) on `world` simulated ranks and
 // returns rank 0's logits, [steps][vocab].

@@ -140,6 +140,7 @@ struct PyComm {
     std::shared_ptr<DeviceComm> comm;
 };
 struct PyRcclComm : PyComm {};
+struct PyComputeOnlyComm : PyComm {};
 
 // Keeps the device comm alive as long as the engine.
 struct PyHipEngine {
@@ -808,6 +809,16 @@ PYBIND11_MODULE(_C, m) {
                  return c;
              }),
              py::arg("uid"), py::arg("rank") = 0, py::arg("world") = 1, py::arg("gpu_index") = 0);
+
+    // compute-only TP rank (no peers, nothing exchanged): times a TP-N rank's shard on one GPU
+    py::class_<PyComputeOnlyComm, PyComm>(m, "ComputeOnlyComm")
+        .def(py::init([](int rank, int world, int gpuIndex) {
+                 auto *c = new PyComputeOnlyComm();
+                 DL_HIP(hipSetDevice(gpuIndex));
+                 c->comm = std::shared_ptr<DeviceComm>(makeComputeOnlyComm(rank, world).release());
+                 return c;
+             }),
+             py::arg("rank") = 0, py::arg("world") = 2, py::arg("gpu_index") = 0);
 
     py::class_<PyHipEngine>(m, "HipEngine")
         .def(py::init([](const std::string &model, const std::string &bufferType, u32 maxSeqLen, u32 maxBatch,

@@ -502,3 +502,27 @@ def test_paged_kv_pool_exhaustion_raises(C, medium):
     pg.forward(list(range(1, 41)), list(range(40)), [0] * 40)  # 2 pages
     with pytest.raises(RuntimeError, match="KV page pool exhausted"):
         pg.forward([5], [0], [1])
+
+
+@pytest.mark.parametrize("sync", ["f32", "q80"])
+def test_compute_only_rank_fused_matches_separate(C, medium, sync, monkeypatch):
+    """bench.py --tp-rank-compute: a TP-2 rank with no peers (ComputeOnlyComm). The fused exchange
+    in loopback (peers read as zeros) and the separate collectives (no-ops) must give the same
+    shard logits: the timed kernels are the rank's real shard kernels, only the exchange removed."""
+    tokens = [3, 17, 101, 7]
+    out = {}
+    for fused in (True, False):
+        monkeypatch.setenv("DL_TP_FUSED", "1" if fused else "0")
+        e = C.HipEngine(medium, "q80", max_batch=8, rank=0, world=2, comm=C.ComputeOnlyComm(0, 2, 0),
+                        sync_type=sync)
+        assert bool(e.tp_fused) == fused
+        vocab0 = e.header["vocab_size"] // 2
+        out[fused] = np.stack([e.forward([t], [p], [0])[0][:vocab0] for p, t in enumerate(tokens)])
+        ids = e.forward_argmax(tokens, list(range(4)), [0] * 4)
+        assert all(0 <= i < vocab0 for i in ids)
+        del e
+    assert np.isfinite(out[True]).all()
+    if sync == "f32":
+        assert np.array_equal(out[True], out[False])
+    else:  # a Q80 rounding may flip by one step between the fused tail and the roundtrip kernel
+        assert _rel(out[True], out[False]) < 2e-3
