@@ -7,6 +7,8 @@
 // worker:    serve a root (app.cpp:405-463).
 // Deliberate fix: the first decoded position is fed the LAST prompt token (the reference feeds
 // inputTokens[pos + 1], one past the prompt end, dllama.cpp:53 and :179).
+// Greedy decoding on a GPU is pipelined (Backend::chainLaunch): step k + 1 runs while token k is
+// decoded and printed; the reference waits for each token (dllama.cpp:74-96).
 #include <cstdio>
 #include <cstring>
 #include <iostream>
@@ -96,6 +98,24 @@ static void inference(InferenceSession &sess, const AppArgs &args) {
     const int maxPos = (int)std::min<u32>(seqLen, (u32)args.steps);
     std::vector<float> logits;
     std::string piece;
+    if (sess.sampler().temperature() == 0.0f && sess.chainSupported() && pos < maxPos) {
+        // greedy on a GPU: chained steps (the token fed back on the device), one step kept in
+        // flight while the host decodes and prints the previous one; a token's time is the
+        // interval between consecutive results
+        Timer t;
+        sess.chainLaunch(token, pos, 0);
+        int launched = pos + 1;
+        for (; pos < maxPos; pos++) {
+            if (launched < maxPos) sess.chainLaunch(-1, launched++, 0);
+            token = sess.chainCollect();
+            const double ms = t.elapsedMs();
+            t.reset();
+            const bool has = tok.decode(token, piece);
+            printStatsLine("🔶 Pred", ms, sess.lastStats(), has ? piece : std::string("~"));
+            std::fflush(stdout);
+            predMs += ms;
+        }
+    }
     for (; pos < maxPos; pos++) {
         double ms;
         token = sampleOne(sess, token, pos, logits, ms);

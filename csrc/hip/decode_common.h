@@ -366,7 +366,7 @@ __device__ __forceinline__ bool tpFailed(const TpXchg &x) {
 // Push `payload` as exchange word `w` (epoch e) to every peer, then collect word `w` of every rank
 // into vals[p] (this rank's own payload included). Peer loads are all issued before any wait.
 __device__ __forceinline__ void tpPushCollect(const TpXchg &x, long long w, unsigned e, unsigned payload,
-                                              unsigned (&vals)[kTpMaxRanks], bool failed) {
+                                              unsigned (&vals)[kTpMaxRanks]) {
     const int me = x.rank, W = x.world;
     if (x.loopback) {
 #pragma unroll
@@ -388,7 +388,8 @@ __device__ __forceinline__ void tpPushCollect(const TpXchg &x, long long w, unsi
     for (int p = 0; p < kTpMaxRanks; p++) {
         if (p < W) {
             uint64_t v = got[p];
-            if ((unsigned)(v >> 32) != e && !failed) {
+            // the error word is read only when a wait is due (an earlier timeout: do not wait)
+            if ((unsigned)(v >> 32) != e && !tpFailed(x)) {
                 const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
                 while ((unsigned)(v >> 32) != e) {
                     __builtin_amdgcn_s_sleep(1);
@@ -417,24 +418,103 @@ __device__ __forceinline__ void tpSpanEnd(const TpXchg &x, long long t0) {
     }
 }
 
+// Argmax reductions (value, index): larger value wins, ties -> lower index (a full-vocabulary
+// argmax's pick). blockArgmax leaves the workgroup's winner in thread 0 (sv / si: NW scratch words).
+__device__ __forceinline__ void argBetter(float &bv, int &bi, float ov, int oi) {
+    if (ov > bv || (ov == bv && oi < bi)) {
+        bv = ov;
+        bi = oi;
+    }
+}
+
+__device__ __forceinline__ void blockArgmax(float &bv, int &bi, float *sv, int *si) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) argBetter(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
+    const int w = threadIdx.x / 64;
+    __syncthreads();
+    if (threadIdx.x % 64 == 0) {
+        sv[w] = bv;
+        si[w] = bi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int i = 1; i < (int)(blockDim.x / 64); i++) argBetter(bv, bi, sv[i], si[i]);
+}
+
+// Tensor-parallel argmax: every rank offers its slice's winner (value, global index) in the
+// argmax-winners exchange region (words 2b, 2b + 1); all ranks pick the same one in rank order.
+// Thread 0 only.
+__device__ __forceinline__ void tpArgmaxPick(const TpXchg &x, int b, float &bv, int &bi) {
+    const long long t0 = tpSpanBegin(x);
+    const unsigned ev = x.epochs[2 * b] + 1, ei = x.epochs[2 * b + 1] + 1;  // one epoch per word
+    unsigned vv[kTpMaxRanks], vi[kTpMaxRanks];
+    tpPushCollect(x, 2LL * b, ev, __float_as_uint(bv), vv);
+    tpPushCollect(x, 2LL * b + 1, ei, (unsigned)bi, vi);
+    bv = -INFINITY;
+    bi = 0x7fffffff;
+    for (int p = 0; p < x.world; p++) argBetter(bv, bi, __uint_as_float(vv[p]), (int)vi[p]);
+    x.epochs[2 * b] = ev;
+    x.epochs[2 * b + 1] = ei;
+    tpSpanEnd(x, t0);
+}
+
 // LDS bytes of the Q80 exchange staging for nEl elements over W ranks.
 __host__ __device__ static inline size_t tpQ80Lds(int nEl, int W) {
     return alignUp((size_t)nEl, 16) + alignUp((size_t)nEl / 32 * 4, 16) + (size_t)W * (nEl / 32) * 9 * 4;
 }
 
 // f32 exchange of a workgroup's partial rows res[B][R] (rows rowBase..) -> a.out summed over ranks.
+// Exchange words of a workgroup's partial rows, k-th of this thread (k = 0, 1, ...): f32 words are
+// the elements b * ldOut + row, Q80 words 9 per 32-row block. Returns -1 for a dead word.
+__device__ __forceinline__ long long tpWordOf(const GemvArgs &a, int R, int rowBase, int j, bool q80) {
+    const int i = q80 ? (j / 9) * 32 : j;
+    const int b = i / R, row = rowBase + i % R;
+    if (row >= a.rows) return -1;
+    const long long el = (long long)b * a.ldOut + row;
+    return q80 ? (el >> 5) * 9 + j % 9 : el;
+}
+
+// The epochs of this thread's first kTpPre exchange words, loaded when the workgroup starts (inline
+// asm: outside the compiler's wait accounting, so the GEMV ring keeps its own counted waits) and
+// consumed by the exchange after the main loop, instead of one dependent round trip there.
+static constexpr int kTpPre = 2;
+struct TpEpochs {
+    unsigned v[kTpPre];
+};
 template <int B>
-__device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *res, int R, int rowBase) {
+__device__ __forceinline__ TpEpochs tpPrefetchEpochs(const GemvArgs &a, int R, int rowBase) {
+    TpEpochs pe;
+    const bool q80 = a.tp.q80 != 0;
+    const int nw = q80 ? (B * R / 32) * 9 : B * R;
+#pragma unroll
+    for (int k = 0; k < kTpPre; k++) {
+        const int j = threadIdx.x + k * kThreads;
+        const long long w = j < nw ? tpWordOf(a, R, rowBase, j, q80) : -1;
+        const unsigned *p = a.tp.epochs + (w < 0 ? 0 : w);
+        asm volatile("global_load_dword %0, %1, off" : "=v"(pe.v[k]) : "v"(p));
+    }
+    return pe;
+}
+__device__ __forceinline__ unsigned tpEpochOf(const TpXchg &x, const TpEpochs &pe, int k, long long w) {
+    return k == 0 ? pe.v[0] : k == 1 ? pe.v[1] : x.epochs[w];
+}
+__device__ __forceinline__ void tpEpochsWait(TpEpochs &pe) {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(pe.v[0]), "+v"(pe.v[1]));
+}
+
+template <int B>
+__device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *res, int R, int rowBase, TpEpochs pe) {
     const TpXchg &x = a.tp;
-    const bool failed = tpFailed(x);
     const long long t0 = tpSpanBegin(x);
-    for (int i = threadIdx.x; i < B * R; i += kThreads) {
+    tpEpochsWait(pe);
+    int k = 0;
+    for (int i = threadIdx.x; i < B * R; i += kThreads, k++) {
         const int b = i / R, row = rowBase + i % R;
         if (row >= a.rows) continue;
         const long long el = (long long)b * a.ldOut + row;
-        const unsigned e = x.epochs[el] + 1;
+        const unsigned e = tpEpochOf(x, pe, k, el) + 1;
         unsigned v[kTpMaxRanks];
-        tpPushCollect(x, el, e, __float_as_uint(res[i]), v, failed);
+        tpPushCollect(x, el, e, __float_as_uint(res[i]), v);
         float s = 0.f;
 #pragma unroll
         for (int p = 0; p < kTpMaxRanks; p++)
@@ -452,14 +532,15 @@ __device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *re
 // rows, all ranks' blocks dequantized and summed in rank order, own included). R and rowBase are
 // multiples of 32. A block travels as 9 words: 8 x 4 int8 + the f16 scale. `lds` = free staging.
 template <int B>
-__device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *res, int R, int rowBase, char *lds) {
+__device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *res, int R, int rowBase, char *lds,
+                                              TpEpochs pe) {
     const TpXchg &x = a.tp;
     const int nEl = B * R, nBlk = nEl >> 5, W = x.world;
     int8_t *q8 = reinterpret_cast<int8_t *>(lds);
     uint32_t *dq = reinterpret_cast<uint32_t *>(lds + alignUp((size_t)nEl, 16));
     uint32_t *rv = reinterpret_cast<uint32_t *>(lds + alignUp((size_t)nEl, 16) + alignUp((size_t)nBlk * 4, 16));
-    const bool failed = tpFailed(x);
     const long long t0 = tpSpanBegin(x);
+    tpEpochsWait(pe);
     // 1. quantize this rank's partial (whole 32-lane groups per block: the loop is uniform)
     for (int base = 0; base < nEl; base += kThreads) {
         const int i = base + threadIdx.x;
@@ -481,16 +562,17 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
         return ((long long)b * a.ldOut + row) >> 5;
     };
     // 2. push / collect the 9 words of every block
-    for (int j = threadIdx.x; j < nBlk * 9; j += kThreads) {
+    int k = 0;
+    for (int j = threadIdx.x; j < nBlk * 9; j += kThreads, k++) {
         const int blk = j / 9, w = j % 9;
         bool live;
         const long long gb = blockId(blk, live);
         if (!live) continue;
         const long long wd = gb * 9 + w;
-        const unsigned e = x.epochs[wd] + 1;
+        const unsigned e = tpEpochOf(x, pe, k, wd) + 1;
         const unsigned payload = w < 8 ? reinterpret_cast<const uint32_t *>(q8)[blk * 8 + w] : dq[blk];
         unsigned v[kTpMaxRanks];
-        tpPushCollect(x, wd, e, payload, v, failed);
+        tpPushCollect(x, wd, e, payload, v);
 #pragma unroll
         for (int p = 0; p < kTpMaxRanks; p++)
             if (p < W) rv[(p * nBlk + blk) * 9 + w] = v[p];
@@ -513,10 +595,23 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
     }
 }
 
-// Sequence split of a decode-attention row of length `len`: nSplit chunks of ch positions
-// (~256 per chunk, at most splitGrid chunks).
-__device__ __forceinline__ void attnSplit(int len, int splitGrid, int &nSplit, int &ch) {
-    int ns = (len + 255) / 256;
+// Sequence chunks of an attention row of length `len` over `heads` query heads (the launch's head
+// groups fill the grid): ~256 positions per chunk with >= 32 heads (TP1 tuning); fewer heads
+// (tensor-parallel shards: 4 per rank at TP8) take chunks down to 8 * heads (>= 32) positions until
+// heads x chunks reaches 64 workgroups, so a short context does not run on 4 workgroups.
+__host__ __device__ inline int attnSplitsFor(int len, int heads) {
+    const int big = (len + 255) / 256;
+    if (heads >= 32) return big;
+    const int minCh = 8 * heads > 32 ? 8 * heads : 32, cap = heads > 0 ? 64 / heads : 1;
+    int small = (len + minCh - 1) / minCh;
+    if (small > cap) small = cap;
+    return big > small ? big : small;
+}
+
+// Sequence split of a decode-attention row of length `len`: nSplit chunks of ch positions (16-
+// aligned, at most splitGrid chunks; attnSplitsFor).
+__device__ __forceinline__ void attnSplit(int len, int splitGrid, int &nSplit, int &ch, int heads = 32) {
+    int ns = attnSplitsFor(len, heads);
     if (ns > splitGrid) ns = splitGrid;
     if (ns < 1) ns = 1;
     ch = (((len + ns - 1) / ns) + 15) & ~15;

@@ -78,6 +78,8 @@ HipEngineImpl::~HipEngineImpl() {
     for (void *p : allocs_) (void)hipFree(p);
     for (void *p : hostAllocs_) (void)hipHostFree(p);
     if (hLogits_) (void)hipHostFree(hLogits_);
+    for (auto &e : chainEv_)
+        if (e) (void)hipEventDestroy(e);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -172,6 +174,48 @@ void HipEngineImpl::collectIds(int *out) {
     stats_.syncMs = readSyncMs();
 }
 
+// Chained decode for the CLI: the CHAIN graph (forward -> argmax -> tokens := ids, pos += 1 on
+// the device) per step, each followed by the D2H copy of its id into a ring slot and an event. The
+// host keeps a step in flight while it decodes and prints the previous one (the reference's loop
+// waits for every token before starting the next: dllama.cpp:74-96). Graph / bucket choice
+// follow the step's position as in setInputs; error words are checked at every collect.
+void HipEngineImpl::chainLaunch(int token, int pos, int slot) {
+    DL_CHECK(pendingN_ == 0, "chainLaunch: a launchIds forward was not collected");
+    DL_CHECK(chainHead_ - chainTail_ < kChainDepth, "chainLaunch: too many steps in flight");
+    DL_CHECK(pos >= 0 && (u32)pos < h_.seqLen, "position out of range");
+    if (!hChain_) {
+        hChain_ = halloc<int>(kChainDepth);
+        for (auto &e : chainEv_) DL_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    if (token >= 0) {
+        DL_CHECK(chainHead_ == chainTail_, "chainLaunch: a chain restarted with steps in flight");
+        setInputs(1, &token, &pos, &slot, nullptr, 0);
+        chainSlot_ = slot;
+    } else {  // dTok_ / dPos_ hold the previous step's id and position + 1 (written on the device)
+        DL_CHECK(chainHead_ > 0, "chainLaunch: no chain started");
+        mapPages(1, &pos, &chainSlot_, 0);
+        attnLong_ = pos >= kAttnMfmaMinPos;
+        bucket_ = (int)(&bucketFor(pos) - buckets_.data());
+    }
+    runGraph(1, GraphKind::CHAIN);
+    const int k = (int)(chainHead_ % kChainDepth);
+    DL_HIP(hipMemcpyAsync(hChain_ + k, dIds_, sizeof(int), hipMemcpyDeviceToHost, stream_));
+    enqueueErrorCopies();
+    DL_HIP(hipEventRecord(chainEv_[k], stream_));
+    chainHead_++;
+}
+
+int HipEngineImpl::chainCollect() {
+    DL_CHECK(chainHead_ > chainTail_, "chainCollect: no step in flight");
+    const int k = (int)(chainTail_ % kChainDepth);
+    DL_HIP(hipEventSynchronize(chainEv_[k]));
+    chainTail_++;
+    if (chainTail_ == chainHead_) inputsInFlight_ = false;
+    checkErrorWords();
+    stats_.syncMs = readSyncMs();
+    return hChain_[k];
+}
+
 double HipEngineImpl::decodeGreedyBatch(int steps, int nSeq, const int *tokens, const int *pos, const int *slots,
                                         int *outTokens) {
     DL_CHECK(nSeq >= 1 && nSeq <= decodeRows_, "nSeq exceeds the engine's decode rows (max_decode)");
@@ -242,11 +286,22 @@ void HipEngineImpl::profileForward(int n, const int *tokens, const int *position
 // peer's stale data: the xGMI collectives flag a peer that did not arrive within 2 s, RCCL
 // reports asynchronous errors (the communicator is then released without waiting).
 void HipEngineImpl::syncAndCheckComm() {
+    enqueueErrorCopies();
+    DL_HIP(hipStreamSynchronize(stream_));
+    checkErrorWords();
+}
+
+// The device error words (transport timeout, in-launch hand-off timeout) to pinned host words, in
+// stream order behind the work they judge.
+void HipEngineImpl::enqueueErrorCopies() {
     const int *flag = comm_ ? comm_->deviceErrorFlag() : nullptr;
     if (flag) DL_HIP(hipMemcpyAsync(hErr_, flag, sizeof(int), hipMemcpyDeviceToHost, stream_));
+    if (blockOn_) DL_HIP(hipMemcpyAsync(hErr_ + 1, dBlockErr_, sizeof(int), hipMemcpyDeviceToHost, stream_));
+}
+
+void HipEngineImpl::checkErrorWords() {
+    const int *flag = comm_ ? comm_->deviceErrorFlag() : nullptr;
     const bool inLaunch = blockOn_;  // kernels with in-launch hand-offs
-    if (inLaunch) DL_HIP(hipMemcpyAsync(hErr_ + 1, dBlockErr_, sizeof(int), hipMemcpyDeviceToHost, stream_));
-    DL_HIP(hipStreamSynchronize(stream_));
     if (inLaunch && hErr_[1] != 0) {
         const int code = hErr_[1];
         hErr_[1] = 0;

@@ -243,7 +243,7 @@ double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B
     a.hs = hs;
     a.kv0 = kv0;
     a.seqLen = seqLen;
-    a.splitGrid = hipk::attnSplitGrid(seqLen);
+    a.splitGrid = hipk::attnSplitGrid(seqLen, nHeads0);
     a.chunkMax = hipk::attnChunkMax(seqLen, a.splitGrid);
     a.partO = (float *)alloc((size_t)B * nHeads0 * a.splitGrid * hs * 4);
     a.partML = (float *)alloc((size_t)B * nHeads0 * a.splitGrid * 2 * 4);

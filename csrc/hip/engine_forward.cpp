@@ -26,7 +26,7 @@ void HipEngineImpl::setupBuckets() {
     buckets_.push_back(last);
     DL_CHECK(buckets_.size() <= 16, "too many context buckets");
     for (CtxBucket &b : buckets_) {
-        b.splitGrid = hipk::attnSplitGrid(b.maxLen);
+        b.splitGrid = hipk::attnSplitGrid(b.maxLen, (int)plan_.nHeads0);
         b.chunkMax = hipk::attnChunkMax(b.maxLen, b.splitGrid);
     }
     bucket_ = (int)buckets_.size() - 1;
@@ -41,6 +41,7 @@ const CtxBucket &HipEngineImpl::bucketFor(int maxPos) const {
 void HipEngineImpl::setInputs(int n, const int *tokens, const int *positions, const int *slots, const SampleSpec *specs,
                               int ahead) {
     DL_CHECK(n >= 1 && (u32)n <= cfg_.maxBatch, "batch size out of range");
+    DL_CHECK(chainHead_ == chainTail_, "a chained decode step is still in flight");
     for (int b = 0; b < n; b++) {
         DL_CHECK(tokens[b] >= 0 && (u32)tokens[b] < h_.vocabSize, "token out of range");
         DL_CHECK(positions[b] >= 0 && (u32)positions[b] < h_.seqLen, "position out of range");
@@ -486,6 +487,11 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
         if (!fusedTp(bat) && !fz) allReduce(dY_, (size_t)n * dim);
     }
     xSlot_ = 2 * (int)h_.nLayers;  // logits gather / argmax winners
+    // one greedy decode row: the logits GEMV ends in the row's argmax (EPI_ARGMAX: no logits
+    // written, no argmax launch; under TP the winners trade over the fused exchange's region)
+    const bool argTail = argTailOn_ && q40_ && !bat && !fz && n == 1 &&
+                         (kind == GraphKind::ARGMAX || kind == GraphKind::CHAIN) &&
+                         (p.nRanks == 1 || (tpFused_ && tpArg_.stride >= 2));
     {
         ProfScope ps(this, "gemv_logits");
         if (fz)
@@ -494,9 +500,31 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
         else if (bat)
             gemmBatched(wcls_, n, hipk::EPI_STORE, dX_[cur], dim, dY_, nullptr, rmsFinal_, nullptr, dLogits_, p.vocab0,
                         nullptr, nullptr);
-        else
+        else if (argTail) {
+            hipk::GemvArgs a = gemvArgs(wcls_, 0, 1, hipk::EPI_ARGMAX, dX_[cur], dim, dY_, nullptr, rmsFinal_, nullptr,
+                                        p.vocab0, nullptr, nullptr, nullptr, nullptr, nullptr, false);
+            a.am.ids = dIds_;
+            a.am.partV = dArgV_;
+            a.am.partI = dArgI_;
+            a.am.counter = dArgCnt_;
+            a.am.vocabStart = p.vocabStart();
+            if (kind == GraphKind::CHAIN) {
+                a.am.tokens = dTok_;
+                a.am.pos = dPos_;
+                a.am.hist = dHist_;
+            }
+            if (p.nRanks > 1) {
+                a.tp = tpArg_;
+                a.tp.ticks = syncTicks(xSlot_);
+            }
+            hipk::launchGemv(a, 1, hipk::PRO_RESNORM, hipk::EPI_ARGMAX, true, stream_);
+        } else
             gemv(wcls_, n, hipk::PRO_RESNORM, hipk::EPI_STORE, dX_[cur], dim, dY_, nullptr, rmsFinal_, dLogits_,
                  p.vocab0, nullptr);
+    }
+    if (argTail) {
+        DL_HIP(hipGetLastError());
+        return;
     }
     const float *full = dLogits_;
     // greedy rows under tensor parallelism: each rank reduces its own vocab slice and only the

@@ -16,6 +16,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <string>
@@ -71,6 +72,10 @@ class HipEngineImpl : public HipEngine {
                        int *out) override;
     void launchIds(int n, const int *tokens, const int *positions, const int *slots, const SampleSpec *specs) override;
     void collectIds(int *out) override;
+    bool chainSupported() const override { return true; }
+    void chainLaunch(int token, int pos, int slot) override;
+    int chainCollect() override;
+    int chainInFlight() const override { return (int)(chainHead_ - chainTail_); }
     int kvPagesFree() const override { return paged() ? (int)freePages_.size() : -1; }
     int kvPageSize() const override { return paged() ? (int)cfg_.kvPageSize : 0; }
     void releaseSlot(int slot) override;
@@ -95,6 +100,8 @@ class HipEngineImpl : public HipEngine {
 
     // engine.cpp
     void syncAndCheckComm();
+    void enqueueErrorCopies();
+    void checkErrorWords();
     int rank() const { return comm_ ? comm_->rank() : 0; }
     void runGraph(int n, GraphKind kind);
     void accountForward(int n, GraphKind kind, int times);
@@ -253,6 +260,18 @@ class HipEngineImpl : public HipEngine {
     size_t hLogitsCap_ = 0;
     bool inputsInFlight_ = false;  // an H2D copy from hIn_ may still be pending
     int pendingN_ = 0;             // rows of a launchIds forward not collected yet
+    // chained decode (chainLaunch / chainCollect): a ring of pinned id words and their events
+    // the logits GEMV of a greedy decode row ends in its argmax (EPI_ARGMAX; DL_ARGMAX_TAIL=0: the
+    // separate argmax kernel, comparison runs)
+    const bool argTailOn_ = [] {
+        const char *e = std::getenv("DL_ARGMAX_TAIL");
+        return !(e && *e == '0');
+    }();
+    static constexpr int kChainDepth = 4;
+    int *hChain_ = nullptr;
+    hipEvent_t chainEv_[kChainDepth] = {};
+    long long chainHead_ = 0, chainTail_ = 0;  // steps launched / collected
+    int chainSlot_ = 0;
 
     // activations
     float *dX_[2] = {nullptr, nullptr};

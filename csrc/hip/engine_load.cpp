@@ -166,8 +166,11 @@ void HipEngineImpl::allocBuffers() {
     }
     dAttCnt_ = dalloc<int>((size_t)MB * p.nHeads0);
     DL_HIP(hipMemsetAsync(dAttCnt_, 0, sizeof(int) * (size_t)MB * p.nHeads0, stream_));
-    dArgV_ = dalloc<float>((size_t)MB * 64);
-    dArgI_ = dalloc<int>((size_t)MB * 64);
+    // argmax partials: 64 workgroups per row (argmaxKernel), or one per workgroup of the logits
+    // GEMV (EPI_ARGMAX: >= 8 rows per workgroup)
+    const size_t argParts = std::max<size_t>((size_t)MB * 64, p.vocab0 / 8 + 1);
+    dArgV_ = dalloc<float>(argParts);
+    dArgI_ = dalloc<int>(argParts);
     {
         void *ss = dalloc<uint8_t>(hipk::SampleScratch::bytes((int)MB));
         DL_HIP(hipMemsetAsync(ss, 0, hipk::SampleScratch::bytes((int)MB), stream_));

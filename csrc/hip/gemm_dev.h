@@ -128,7 +128,6 @@ __host__ __device__ inline size_t tpTileQ80Lds(int M, int W) {
 __device__ __forceinline__ void tpExchangeTile(const GemmArgs &ga, float *tile, int R0, char *lds) {
     const TpXchg &x = ga.e.tp;
     const int M = ga.M, nEl = M * 64, W = x.world;
-    const bool failed = tpFailed(x);
     __syncthreads();
     const long long t0 = tpSpanBegin(x);
     if (!x.q80) {
@@ -138,7 +137,7 @@ __device__ __forceinline__ void tpExchangeTile(const GemmArgs &ga, float *tile, 
             const long long el = (long long)t * ga.e.ldOut + row;
             const unsigned e = x.epochs[el] + 1;
             unsigned v[kTpMaxRanks];
-            tpPushCollect(x, el, e, __float_as_uint(tile[i]), v, failed);
+            tpPushCollect(x, el, e, __float_as_uint(tile[i]), v);
             float s = 0.f;
 #pragma unroll
             for (int p = 0; p < kTpMaxRanks; p++)
@@ -182,7 +181,7 @@ __device__ __forceinline__ void tpExchangeTile(const GemmArgs &ga, float *tile, 
         const unsigned e = x.epochs[wd] + 1;
         const unsigned payload = w < 8 ? reinterpret_cast<const uint32_t *>(q8)[blk * 8 + w] : dq[blk];
         unsigned v[kTpMaxRanks];
-        tpPushCollect(x, wd, e, payload, v, failed);
+        tpPushCollect(x, wd, e, payload, v);
 #pragma unroll
         for (int p = 0; p < kTpMaxRanks; p++)
             if (p < W) rv[(p * nBlk + blk) * 9 + w] = v[p];

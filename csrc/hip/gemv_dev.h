@@ -139,6 +139,8 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
     // timestamps stay in SGPRs until the end: a store here would join the ring's vmcnt accounting
     const unsigned long long tEntry = a.trace ? wall_clock64() : 0ull;
     unsigned long long tReady = 0ull, tLoaded = 0ull, tFirst = 0ull, tWaited = 0ull;
+    TpEpochs pe{};  // exchange epochs, in flight while the ring streams (tpPrefetchEpochs)
+    if constexpr (tpx) pe = tpPrefetchEpochs<B>(a, R, rowBase);
 
     // slot = 2 rows x 16 B of nibbles + the pair's two f16 scales in one 32-bit word
     u32x4 w[D][RG];
@@ -386,7 +388,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
 #pragma unroll
             for (int b = 0; b < B; b++) {
                 const float v0 = acc[0][b], v1 = acc[1][b];
-                if constexpr (EPI == EPI_STORE_TP) {
+                if constexpr (EPI == EPI_STORE_TP || EPI == EPI_ARGMAX) {
                     res[b * R + (r0 - rowBase)] = v0;
                     res[b * R + (r0 - rowBase) + 1] = v1;
                 } else if constexpr (EPI == EPI_STORE) {
@@ -482,8 +484,49 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
     }
     if constexpr (tpx) {  // all-reduce the partial rows over the TP ranks, then store (sq is free now)
         __syncthreads();
-        if (a.tp.q80) tpExchangeQ80<B>(a, res, R, rowBase, reinterpret_cast<char *>(sq));
-        else tpExchangeF32<B>(a, res, R, rowBase);
+        if (a.tp.q80) tpExchangeQ80<B>(a, res, R, rowBase, reinterpret_cast<char *>(sq), pe);
+        else tpExchangeF32<B>(a, res, R, rowBase, pe);
+    }
+    if constexpr (EPI == EPI_ARGMAX) {  // the row's argmax instead of its logits (ArgmaxTail)
+        static_assert(B == 1, "EPI_ARGMAX: one row");
+        __syncthreads();
+        float *sv = scratch;
+        int *si = reinterpret_cast<int *>(scratch + 8);
+        int *last = reinterpret_cast<int *>(scratch + 16);
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int i = tid; i < R; i += kThreads)
+            if (rowBase + i < a.rows) argBetter(bv, bi, res[i], rowBase + i);
+        blockArgmax(bv, bi, sv, si);
+        // fence-free hand-off (as argmaxKernel): agent-scope stores of the partial, drained, then counted
+        if (tid == 0) {
+            __hip_atomic_store(a.am.partV + blk, bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.am.partI + blk, bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int old = __hip_atomic_fetch_add(a.am.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *last = old == (int)gridDim.x - 1;
+        }
+        __syncthreads();
+        if (*last) {
+            if (tid == 0) __hip_atomic_store(a.am.counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bv = -INFINITY;
+            bi = 0x7fffffff;
+            for (int i = tid; i < (int)gridDim.x; i += kThreads)
+                argBetter(bv, bi, __hip_atomic_load(a.am.partV + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                          __hip_atomic_load(a.am.partI + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            blockArgmax(bv, bi, sv, si);
+            if (tid == 0) {
+                bi += a.am.vocabStart;
+                if (a.tp.world > 1) tpArgmaxPick(a.tp, 0, bv, bi);
+                a.am.ids[0] = bi;
+                if (a.am.tokens) {  // chained decode: feed the token back
+                    const int p = a.am.pos[0];
+                    a.am.hist[p] = bi;
+                    a.am.tokens[0] = bi;
+                    a.am.pos[0] = p + 1;
+                }
+            }
+        }
     }
     if (a.trace) {
         __syncthreads();

@@ -125,6 +125,7 @@ static const void *gemvFnPE(int pro, int epi) {
         DL_GEMV_CASE(PRO_RESNORM, EPI_ACT_Q80)
         DL_GEMV_CASE(PRO_GLOBAL, EPI_STORE_TP)
         DL_GEMV_CASE(PRO_RESNORM, EPI_STORE_TP)
+        if constexpr (B == 1) DL_GEMV_CASE(PRO_RESNORM, EPI_ARGMAX)
     }
 #undef DL_GEMV_CASE
     return nullptr;

@@ -32,7 +32,9 @@ enum Prologue : int { PRO_GLOBAL = 0, PRO_RESNORM = 1 };
 // EPI_STORE_TP: EPI_STORE whose rows are first all-reduced over the tensor-parallel ranks (GemvArgs::tp).
 // EPI_RES (batched GEMMs): residual update fused with the next RMS norm's elementwise half - see
 // GemmArgs::resIn.
-enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2, EPI_ACT_Q80 = 3, EPI_ACT_F16 = 4, EPI_STORE_TP = 5, EPI_RES = 6 };
+// EPI_ARGMAX (Q40 GEMV, one row, greedy logits): no logits are stored; the row's argmax (GemvArgs::am).
+enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2, EPI_ACT_Q80 = 3, EPI_ACT_F16 = 4, EPI_STORE_TP = 5, EPI_RES = 6,
+                      EPI_ARGMAX = 7 };
 
 // Q40 weights live on the device TILED in the ring GEMV's consumption order, for a lanes-per-row
 // count L fixed per matrix (NG = 256/L row pairs per workgroup pass, K = ceil(nb/L) steps):
@@ -133,6 +135,17 @@ struct TpXchg {
     int loopback = 0;
 };
 
+// EPI_ARGMAX: each workgroup's (value, row) winner goes to partV / partI[workgroup]; the last to
+// arrive (counter, reset by it) reduces them in workgroup order, trades the slice winner with the
+// other ranks over GemvArgs::tp (world > 1: the argmax winners region, rows start at vocabStart)
+// and writes ids[0] (CHAIN: also tokens[0], hist[pos[0]] and pos[0] += 1, as ArgmaxArgs).
+struct ArgmaxTail {
+    int *ids = nullptr, *tokens = nullptr, *pos = nullptr, *hist = nullptr;
+    float *partV = nullptr;
+    int *partI = nullptr, *counter = nullptr;
+    int vocabStart = 0;
+};
+
 struct GemvArgs {
     // weights: Q40 tiled (see Q40Tiling; `lanes` must be the tiling's L) or F32 [rows][n]
     const uint8_t *qs = nullptr;
@@ -170,6 +183,7 @@ struct GemvArgs {
     // EPI_STORE_TP (Q40 GEMV): the partial rows are all-reduced over the tensor-parallel ranks in
     // the kernel tail before `out` is written (exchange element = b * ldOut + row)
     TpXchg tp;
+    ArgmaxTail am;  // EPI_ARGMAX
     // diagnostics (gemvQ40Kernel): when set, workgroup g writes 8 u64 at trace[8g..]: s_memrealtime
     // at entry, prologue done, exit, (HW_ID << 32 | XCC_ID), prologue loads landed (early path),
     // first ring slot consumed (thread 0's view)
@@ -323,7 +337,7 @@ void launchTpSelfTest(const TpXchg &x, float *out, int n, float val, hipStream_t
 void launchAttentionPrefill(const AttnArgs &a, int nRows, hipStream_t s);
 int attnPrefillRowsPerBlock(int kvMul);
 bool attnPrefillSupported(int hs, int kvMul, bool kvBf16);
-int attnSplitGrid(int seqLen);
+int attnSplitGrid(int seqLen, int heads = 32);  // attnSplitsFor (decode_common.h)
 int attnChunkMax(int seqLen, int splitGrid);
 
 // epoch (optional): one thread increments it - the per-forward epoch of the fused attention block.

@@ -6,27 +6,6 @@
 namespace dl {
 namespace hipk {
 
-__device__ __forceinline__ void argBetter(float &bv, int &bi, float ov, int oi) {
-    if (ov > bv || (ov == bv && oi < bi)) {
-        bv = ov;
-        bi = oi;
-    }
-}
-
-__device__ __forceinline__ void blockArgmax(float &bv, int &bi, float *sv, int *si) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) argBetter(bv, bi, __shfl_xor(bv, off), __shfl_xor(bi, off));
-    const int w = threadIdx.x / 64;
-    __syncthreads();
-    if (threadIdx.x % 64 == 0) {
-        sv[w] = bv;
-        si[w] = bi;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0)
-        for (int i = 1; i < (int)(blockDim.x / 64); i++) argBetter(bv, bi, sv[i], si[i]);
-}
-
 constexpr int kArgmaxBlocks = 64;
 
 // The row's winner: ids, and for a chained decode the next step's token / position / history.
@@ -91,21 +70,9 @@ __global__ __launch_bounds__(256) void argmaxKernel(ArgmaxArgs a) {
         return;
     }
     if (threadIdx.x == 0 && a.tp.world > 1) {
-        // tensor parallel: every rank offers its slice's winner (value, global index); all ranks
-        // pick the same one in rank order (ties -> lowest index, like a full-vocabulary argmax)
-        const TpXchg &x = a.tp;
-        const bool failed = tpFailed(x);
-        const long long t0 = tpSpanBegin(x);
-        const unsigned ev = x.epochs[2 * b] + 1, ei = x.epochs[2 * b + 1] + 1;  // one epoch per word
-        unsigned vv[kTpMaxRanks], vi[kTpMaxRanks];
-        tpPushCollect(x, 2LL * b, ev, __float_as_uint(bv), vv, failed);
-        tpPushCollect(x, 2LL * b + 1, ei, (unsigned)(bi + a.vocabStart), vi, failed);
-        bv = -INFINITY;
-        bi = 0x7fffffff;
-        for (int p = 0; p < x.world; p++) argBetter(bv, bi, __uint_as_float(vv[p]), (int)vi[p]);
-        x.epochs[2 * b] = ev;
-        x.epochs[2 * b + 1] = ei;
-        tpSpanEnd(x, t0);
+        // tensor parallel: every rank offers its slice's winner (value, global index)
+        bi += a.vocabStart;
+        tpArgmaxPick(a.tp, b, bv, bi);
     }
     if (threadIdx.x == 0) argmaxStore(a, b, bi);
 }

@@ -11,12 +11,11 @@ namespace dl {
 namespace hipk {
 
 __global__ __launch_bounds__(kThreads) void tpSelfTestKernel(TpXchg x, float *out, int n, float val) {
-    const bool failed = tpFailed(x);
     for (int el = blockIdx.x * kThreads + threadIdx.x; el < n; el += gridDim.x * kThreads) {
         const unsigned e = x.epochs[el] + 1;
         // element-dependent payload: a stale or misrouted word cannot pass as a correct one
         unsigned v[kTpMaxRanks];
-        tpPushCollect(x, el, e, __float_as_uint(val + (float)(el & 1023)), v, failed);
+        tpPushCollect(x, el, e, __float_as_uint(val + (float)(el & 1023)), v);
         float s = 0.f;
 #pragma unroll
         for (int p = 0; p < kTpMaxRanks; p++)

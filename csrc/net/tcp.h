@@ -99,7 +99,10 @@ constexpr u32 kAck = 23571114;           // same ACK value as the reference (nn-
 
 // RELEASE: the first n ints of the payload are KV slots whose sequences ended (paged KV cache:
 // their pages return to the pool on every rank).
-enum class Cmd : u32 { FORWARD = 1, FORWARD_ARGMAX = 2, STOP = 3, PING = 4, FORWARD_SAMPLE = 5, RELEASE = 6 };
+// CHAIN: one step of a chained greedy decode (Backend::chainLaunch), n = 1: token (< 0: continue
+// the chain on the device), position, slot. Workers keep at most 2 steps in flight and drain them
+// before any other command.
+enum class Cmd : u32 { FORWARD = 1, FORWARD_ARGMAX = 2, STOP = 3, PING = 4, FORWARD_SAMPLE = 5, RELEASE = 6, CHAIN = 7 };
 
 struct ControlHeader {
     u32 cmd;

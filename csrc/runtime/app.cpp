@@ -318,6 +318,19 @@ void InferenceSession::launchIds(int n, const int *tokens, const int *positions,
     launchedSample_ = specs != nullptr;
 }
 
+void InferenceSession::chainLaunch(int token, int pos, int slot) {
+    if (token >= 0) launchTimer_.reset();
+    sendControl(Cmd::CHAIN, 1, &token, &pos, &slot);
+    backend_->chainLaunch(token, pos, slot);
+}
+
+int InferenceSession::chainCollect() {
+    const int id = backend_->chainCollect();
+    recordMetrics("forward_argmax", 1, launchTimer_.elapsedMs());
+    launchTimer_.reset();
+    return id;
+}
+
 void InferenceSession::collectIds(int n, int *out) {
     backend_->collectIds(out);
     recordMetrics(launchedSample_ ? "forward_sample" : "forward_argmax", n, launchTimer_.elapsedMs());
@@ -471,6 +484,8 @@ void runWorker(const AppArgs &args) {
                 root.recvAll(hdr, sizeof(hdr));
                 const Cmd cmd = (Cmd)hdr[0];
                 const int n = hdr[1];
+                if (cmd != Cmd::CHAIN)  // chained steps finish before anything else runs
+                    while (backend->chainInFlight() > 0) backend->chainCollect();
                 if (cmd == Cmd::STOP) {
                     if (logLevel() >= 1) std::printf("🛑 Stop signal\n");
                     break;
@@ -482,6 +497,9 @@ void runWorker(const AppArgs &args) {
                 } else if (cmd == Cmd::FORWARD_ARGMAX) {
                     ids.resize(n);
                     backend->forwardArgmax(n, &buf[0], &buf[n], &buf[2 * n], ids.data());
+                } else if (cmd == Cmd::CHAIN) {
+                    backend->chainLaunch(buf[0], buf[n], buf[2 * n]);
+                    while (backend->chainInFlight() > 2) backend->chainCollect();
                 } else if (cmd == Cmd::RELEASE) {
                     for (int i = 0; i < n; i++) backend->releaseSlot(buf[i]);
                 } else if (cmd == Cmd::FORWARD_SAMPLE) {

@@ -86,6 +86,10 @@ class InferenceSession {
     // Pipelined serving (Backend::launchIds / collectIds; workers run the forward in lockstep).
     void launchIds(int n, const int *tokens, const int *positions, const int *slots, const SampleSpec *specs);
     void collectIds(int n, int *out);
+    // Chained greedy decode of one sequence (Backend::chainLaunch; workers follow each step).
+    bool chainSupported() const { return backend_->chainSupported(); }
+    void chainLaunch(int token, int pos, int slot);
+    int chainCollect();
     ForwardStats lastStats();
     void finish();  // stop workers (they return to listening)
     // GPU only: one eager forward of these rows with a per-kernel-class device-time table.

@@ -42,4 +42,7 @@ void Backend::collectIds(int *out) {
     pendingIds_.clear();
 }
 
+void Backend::chainLaunch(int, int, int) { throw Error(name() + " backend: no chained decode"); }
+int Backend::chainCollect() { throw Error(name() + " backend: no chained decode"); }
+
 }  // namespace dl

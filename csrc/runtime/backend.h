@@ -79,6 +79,15 @@ class Backend {
     // runs the forward synchronously inside launchIds (host backends: no overlap).
     virtual void launchIds(int n, const int *tokens, const int *positions, const int *slots, const SampleSpec *specs);
     virtual void collectIds(int *out);
+    // Chained greedy decode of one sequence (GPU engines; dllama inference): each step's input
+    // token is the previous step's argmax, fed back on the device, so step k + 1 is enqueued
+    // before the host has read step k (the host decodes and prints while the device runs).
+    // chainLaunch: token >= 0 starts a chain at (token, pos, slot); token < 0 enqueues the next
+    // step, at position pos. chainCollect waits for the oldest step in flight and returns its id.
+    virtual bool chainSupported() const { return false; }
+    virtual void chainLaunch(int token, int pos, int slot);
+    virtual int chainCollect();
+    virtual int chainInFlight() const { return 0; }
     virtual ForwardStats lastStats() const { return stats_; }
     // Weight residency: time to load (file read + repack + upload, or on-device init), bytes read
     // from the model file by this rank, bytes resident on its device (0 for host backends).

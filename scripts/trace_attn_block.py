@@ -1,6 +1,7 @@
 """Timeline of one fused attention-block launch (8B decode shapes, TP1): per role, the median and
 spread of workgroup entry / wait-done / exit times (us from the earliest entry), so the hand-offs
-(qkv -> attention -> wo) can be priced. usage: python scripts/trace_attn_block.py [pos]"""
+(qkv -> attention -> wo) can be priced. usage: python scripts/trace_attn_block.py [pos] [tp]
+(tp > 1: rank 0 of a TP-tp group with the exchange in loopback, ComputeOnlyComm)"""
 import os
 import sys
 
@@ -11,9 +12,11 @@ import distributed_llama_multiusers_amd as dl
 
 C = dl.native()
 pos = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+tp = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 h = dict(dim=4096, hidden_dim=14336, n_layers=4, n_heads=32, n_kv_heads=8, vocab_size=128256, seq_len=pos + 64,
          rope_theta=500000, weight_type=2)
-eng = C.HipEngine("", "q80", synthetic=h, max_seq_len=pos + 64)
+eng = C.HipEngine("", "q80", synthetic=h, max_seq_len=pos + 64, sync_type="q80",
+                  **({} if tp == 1 else dict(rank=0, world=tp, comm=C.ComputeOnlyComm(0, tp, 0))))
 assert eng.attn_block
 for p in range(0, pos, 32):  # fill the KV cache
     n = min(32, pos - p)

@@ -319,15 +319,17 @@ def test_fused_exchange_residency_guard(C, tmp_path):
     assert a[0][3][:4] == b[0][3][:4] and a[1][3] == a[0][3] and b[1][3] == b[0][3]
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_xgmi_q80_tp_matches_cpu_q80_tp(C, tmp_path, world):
     """GPU TP with the Q80 exchange (fused GEMV-tail exchange of Q80-quantized partials) vs the CPU
     reference data plane with --sync-type q80 semantics at the same world size (in-process
-    ThreadGroupComm: every partial quantized once, dequantized sums in rank order)."""
+    ThreadGroupComm: every partial quantized once, dequantized sums in rank order). World 8 takes
+    8 KV heads (one per rank, the 70B / 405B split)."""
     from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
     from distributed_llama_multiusers_amd.utils.mfile import FloatType
-    m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=9, dim=512, n_heads=8,
-                               n_kv_heads=4, hidden_dim=1024, vocab_size=1024)
+    shape = dict(dim=1024, n_heads=16, n_kv_heads=8) if world == 8 else dict(dim=512, n_heads=8, n_kv_heads=4)
+    m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=9, hidden_dim=1024,
+                               vocab_size=1024, **shape)
     tokens = [5, 99, 300, 7, 1000, 2]
     steps = 12
     cpu_lg, cpu_toks = C.cpu_simulate_tp(m, "q80", world, tokens + [tokens[-1]], "q80", steps, 2)
@@ -342,18 +344,21 @@ def test_xgmi_q80_tp_matches_cpu_q80_tp(C, tmp_path, world):
     assert agree >= steps - 2 and res[0][1][:4] == list(cpu_toks[:4]), (res[0][1], cpu_toks)
 
 
-@pytest.mark.parametrize("n_workers", [1, 3])
+@pytest.mark.parametrize("n_workers", [1, 3, 7])
 def test_cli_root_workers_over_xgmi(tmp_path, n_workers):
     """`dllama inference` root + `dllama worker` processes (all on GPU 0 here): the TCP control plane
-    carries the IPC handles, collectives run over xGMI; greedy tokens == single process."""
+    carries the IPC handles, collectives run over xGMI; greedy tokens == single process. Seven
+    workers (the reference's 70B / 405B launch, examples/n-workers.sh) run a 70B-shaped layer:
+    64 query heads over 8 KV heads (kvMul 8), one KV head per rank."""
     import subprocess
     import time
     from conftest import REPO
     from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
     from distributed_llama_multiusers_amd.utils.mfile import FloatType
     dllama = os.path.join(REPO, "build", "dllama")
-    m, t, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=7, dim=512, n_heads=8,
-                               n_kv_heads=4, hidden_dim=1024)
+    shape = (dict(dim=4096, n_heads=64, n_kv_heads=8, hidden_dim=2048, n_layers=2) if n_workers == 7
+             else dict(dim=512, n_heads=8, n_kv_heads=4, hidden_dim=1024))
+    m, t, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=7, **shape)
     base = [dllama, "inference", "--model", m, "--tokenizer", t, "--buffer-float-type", "q80", "--prompt",
             "hello world the", "--steps", "24", "--temperature", "0", "--gpu-index", "0", "--sync-type", "f32"]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", DL_TP_COMM="xgmi", **_same_gpu_env(n_workers + 1))
