@@ -365,27 +365,31 @@ __device__ __forceinline__ bool tpFailed(const TpXchg &x) {
 
 // Push `payload` as exchange word `w` (epoch e) to every peer, then collect word `w` of every rank
 // into vals[p] (this rank's own payload included). Peer loads are all issued before any wait.
+// WM: compile-time bound on the ranks (x.world <= WM; tpDispatch picks it once per exchange): the
+// rank loops are unrolled WM times, so a TP2 exchange is not compiled as 16 predicated ranks (the
+// 16-way form measured ~1.1-2.3 us of scalar selects and spilled SGPRs per workgroup tail).
+template <int WM>
 __device__ __forceinline__ void tpPushCollect(const TpXchg &x, long long w, unsigned e, unsigned payload,
-                                              unsigned (&vals)[kTpMaxRanks]) {
+                                              unsigned (&vals)[WM]) {
     const int me = x.rank, W = x.world;
     if (x.loopback) {
 #pragma unroll
-        for (int p = 0; p < kTpMaxRanks; p++) vals[p] = p == me ? payload : 0u;
+        for (int p = 0; p < WM; p++) vals[p] = p == me ? payload : 0u;
         return;
     }
     const long long par = e & 1;
     const uint64_t word = (uint64_t)payload | ((uint64_t)e << 32);
 #pragma unroll
-    for (int p = 0; p < kTpMaxRanks; p++)
+    for (int p = 0; p < WM; p++)
         if (p < W && p != me)
             __hip_atomic_store(x.recv[p] + (par * W + me) * x.stride + w, word, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
     const uint64_t *mine = x.recv[me] + par * W * x.stride + w;
-    uint64_t got[kTpMaxRanks];
+    uint64_t got[WM];
 #pragma unroll
-    for (int p = 0; p < kTpMaxRanks; p++) got[p] = (p < W && p != me) ? tpLoad(mine + p * x.stride) : word;
+    for (int p = 0; p < WM; p++) got[p] = (p < W && p != me) ? tpLoad(mine + p * x.stride) : word;
 #pragma unroll
-    for (int p = 0; p < kTpMaxRanks; p++) {
+    for (int p = 0; p < WM; p++) {
         if (p < W) {
             uint64_t v = got[p];
             // the error word is read only when a wait is due (an earlier timeout: do not wait)
@@ -403,6 +407,15 @@ __device__ __forceinline__ void tpPushCollect(const TpXchg &x, long long w, unsi
             vals[p] = (unsigned)v;
         }
     }
+}
+
+// Calls f(std::integral_constant<int, WM>) with the smallest rank bound WM in {2, 4, 8, 16} >= world.
+template <typename F>
+__device__ __forceinline__ void tpDispatch(int world, F &&f) {
+    if (world <= 2) f(std::integral_constant<int, 2>{});
+    else if (world <= 4) f(std::integral_constant<int, 4>{});
+    else if (world <= 8) f(std::integral_constant<int, 8>{});
+    else f(std::integral_constant<int, 16>{});
 }
 
 // Measured sync: a workgroup's exchange span (ticks of s_memrealtime, 10 ns) raised into x.ticks
@@ -444,15 +457,18 @@ __device__ __forceinline__ void blockArgmax(float &bv, int &bi, float *sv, int *
 // Tensor-parallel argmax: every rank offers its slice's winner (value, global index) in the
 // argmax-winners exchange region (words 2b, 2b + 1); all ranks pick the same one in rank order.
 // Thread 0 only.
+template <int WM>
 __device__ __forceinline__ void tpArgmaxPick(const TpXchg &x, int b, float &bv, int &bi) {
     const long long t0 = tpSpanBegin(x);
     const unsigned ev = x.epochs[2 * b] + 1, ei = x.epochs[2 * b + 1] + 1;  // one epoch per word
-    unsigned vv[kTpMaxRanks], vi[kTpMaxRanks];
+    unsigned vv[WM], vi[WM];
     tpPushCollect(x, 2LL * b, ev, __float_as_uint(bv), vv);
     tpPushCollect(x, 2LL * b + 1, ei, (unsigned)bi, vi);
     bv = -INFINITY;
     bi = 0x7fffffff;
-    for (int p = 0; p < x.world; p++) argBetter(bv, bi, __uint_as_float(vv[p]), (int)vi[p]);
+#pragma unroll
+    for (int p = 0; p < WM; p++)
+        if (p < x.world) argBetter(bv, bi, __uint_as_float(vv[p]), (int)vi[p]);
     x.epochs[2 * b] = ev;
     x.epochs[2 * b + 1] = ei;
     tpSpanEnd(x, t0);
@@ -489,7 +505,13 @@ __device__ __forceinline__ TpEpochs tpPrefetchEpochs(const GemvArgs &a, int R, i
 #pragma unroll
     for (int k = 0; k < kTpPre; k++) {
         const int j = threadIdx.x + k * kThreads;
-        const long long w = j < nw ? tpWordOf(a, R, rowBase, j, q80) : -1;
+        long long w = -1;
+        if (B == 1) {  // one row: the words are contiguous (no division by R ahead of the ring)
+            const int row = rowBase + (q80 ? (j / 9) * 32 : j);
+            if (j < nw && row < a.rows) w = q80 ? (long long)(rowBase >> 5) * 9 + j : row;
+        } else if (j < nw) {
+            w = tpWordOf(a, R, rowBase, j, q80);
+        }
         const unsigned *p = a.tp.epochs + (w < 0 ? 0 : w);
         asm volatile("global_load_dword %0, %1, off" : "=v"(pe.v[k]) : "v"(p));
     }
@@ -502,22 +524,22 @@ __device__ __forceinline__ void tpEpochsWait(TpEpochs &pe) {
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(pe.v[0]), "+v"(pe.v[1]));
 }
 
-template <int B>
+template <int B, int WM>
 __device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *res, int R, int rowBase, TpEpochs pe) {
     const TpXchg &x = a.tp;
     const long long t0 = tpSpanBegin(x);
     tpEpochsWait(pe);
     int k = 0;
     for (int i = threadIdx.x; i < B * R; i += kThreads, k++) {
-        const int b = i / R, row = rowBase + i % R;
+        const int b = B == 1 ? 0 : i / R, row = rowBase + (B == 1 ? i : i % R);
         if (row >= a.rows) continue;
         const long long el = (long long)b * a.ldOut + row;
         const unsigned e = tpEpochOf(x, pe, k, el) + 1;
-        unsigned v[kTpMaxRanks];
+        unsigned v[WM];
         tpPushCollect(x, el, e, __float_as_uint(res[i]), v);
         float s = 0.f;
 #pragma unroll
-        for (int p = 0; p < kTpMaxRanks; p++)
+        for (int p = 0; p < WM; p++)
             if (p < x.world) s += __uint_as_float(v[p]);
         a.out[el] = s;
         x.epochs[el] = e;
@@ -531,7 +553,7 @@ __device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *re
 // Q80 exchange (the reference's ZQ pipe: every rank's partial quantized once to Q80 blocks of 32
 // rows, all ranks' blocks dequantized and summed in rank order, own included). R and rowBase are
 // multiples of 32. A block travels as 9 words: 8 x 4 int8 + the f16 scale. `lds` = free staging.
-template <int B>
+template <int B, int WM>
 __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *res, int R, int rowBase, char *lds,
                                               TpEpochs pe) {
     const TpXchg &x = a.tp;
@@ -557,7 +579,7 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
     }
     __syncthreads();
     auto blockId = [&](int blk, bool &live) -> long long {  // global block id in the exchange space
-        const int b = (blk * 32) / R, row = rowBase + (blk * 32) % R;
+        const int b = B == 1 ? 0 : (blk * 32) / R, row = rowBase + (B == 1 ? blk * 32 : (blk * 32) % R);
         live = row < a.rows;
         return ((long long)b * a.ldOut + row) >> 5;
     };
@@ -571,10 +593,10 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
         const long long wd = gb * 9 + w;
         const unsigned e = tpEpochOf(x, pe, k, wd) + 1;
         const unsigned payload = w < 8 ? reinterpret_cast<const uint32_t *>(q8)[blk * 8 + w] : dq[blk];
-        unsigned v[kTpMaxRanks];
+        unsigned v[WM];
         tpPushCollect(x, wd, e, payload, v);
 #pragma unroll
-        for (int p = 0; p < kTpMaxRanks; p++)
+        for (int p = 0; p < WM; p++)
             if (p < W) rv[(p * nBlk + blk) * 9 + w] = v[p];
         x.epochs[wd] = e;
     }
@@ -582,7 +604,7 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
     tpSpanEnd(x, t0);
     // 3. dequantize and sum in rank order
     for (int i = threadIdx.x; i < nEl; i += kThreads) {
-        const int b = i / R, row = rowBase + i % R, blk = i >> 5;
+        const int b = B == 1 ? 0 : i / R, row = rowBase + (B == 1 ? i : i % R), blk = i >> 5;
         if (row >= a.rows) continue;
         float s = 0.f;
         for (int p = 0; p < W; p++) {
@@ -595,23 +617,11 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
     }
 }
 
-// Sequence chunks of an attention row of length `len` over `heads` query heads (the launch's head
-// groups fill the grid): ~256 positions per chunk with >= 32 heads (TP1 tuning); fewer heads
-// (tensor-parallel shards: 4 per rank at TP8) take chunks down to 8 * heads (>= 32) positions until
-// heads x chunks reaches 64 workgroups, so a short context does not run on 4 workgroups.
-__host__ __device__ inline int attnSplitsFor(int len, int heads) {
-    const int big = (len + 255) / 256;
-    if (heads >= 32) return big;
-    const int minCh = 8 * heads > 32 ? 8 * heads : 32, cap = heads > 0 ? 64 / heads : 1;
-    int small = (len + minCh - 1) / minCh;
-    if (small > cap) small = cap;
-    return big > small ? big : small;
-}
-
-// Sequence split of a decode-attention row of length `len`: nSplit chunks of ch positions (16-
-// aligned, at most splitGrid chunks; attnSplitsFor).
-__device__ __forceinline__ void attnSplit(int len, int splitGrid, int &nSplit, int &ch, int heads = 32) {
-    int ns = attnSplitsFor(len, heads);
+// Sequence split of a decode-attention row of length `len`: nSplit chunks of ch positions
+// (~256 per chunk, at most splitGrid chunks). Shorter chunks for the few heads of a TP8 shard
+// (4 per rank) measured slower: 5.4 -> 7.6 us at 100 positions (profiles/r5_tp_rank.md).
+__device__ __forceinline__ void attnSplit(int len, int splitGrid, int &nSplit, int &ch) {
+    int ns = (len + 255) / 256;
     if (ns > splitGrid) ns = splitGrid;
     if (ns < 1) ns = 1;
     ch = (((len + ns - 1) / ns) + 15) & ~15;

@@ -1,6 +1,7 @@
 // Kernel microbenchmarks (scripts/bench_gemv.py, bench_gemm.py, bench_attn.py): each cycles
 // `copies` operand sets through a graph of `iters` launches so the 256 MB Infinity Cache cannot
 // serve them, and returns microseconds per launch.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -81,6 +82,20 @@ double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int pas
         a.slot = zeros;
         a.kcache = alloc((size_t)a.kv0 * 2);
         a.vcache = alloc((size_t)a.kv0 * 2);
+    }
+    if (epi == hipk::EPI_STORE_TP) {  // the TP tail in loopback (ComputeOnlyComm's exchange):
+        // DL_BENCH_TP_WORLD ranks (default 8), DL_BENCH_TP_Q80=0 for the f32 wire format
+        const char *w = std::getenv("DL_BENCH_TP_WORLD"), *q = std::getenv("DL_BENCH_TP_Q80");
+        a.tp.world = w ? std::atoi(w) : 8;
+        a.tp.q80 = q && *q == '0' ? 0 : 1;
+        a.tp.loopback = 1;
+        a.tp.stride = (long long)B * rows * 9;
+        a.tp.epochs = (unsigned *)alloc((size_t)a.tp.stride * 4);
+        a.tp.error = (int *)alloc(4);
+        DL_HIP(hipMemsetAsync(a.tp.epochs, 0, (size_t)a.tp.stride * 4, s));
+        DL_HIP(hipMemsetAsync(a.tp.error, 0, 4, s));
+        if (a.tp.q80 && passes <= 0)  // whole Q80 blocks of 32 rows per workgroup (engine tpPasses)
+            while ((256 / L * 2 * a.passes) % 32) a.passes++;
     }
     const int grid = (rows + (256 / L) * 2 * a.passes - 1) / ((256 / L) * 2 * a.passes);
     unsigned long long *tbuf = trace ? (unsigned long long *)alloc((size_t)iters * grid * 8 * 8) : nullptr;
@@ -243,7 +258,7 @@ double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B
     a.hs = hs;
     a.kv0 = kv0;
     a.seqLen = seqLen;
-    a.splitGrid = hipk::attnSplitGrid(seqLen, nHeads0);
+    a.splitGrid = hipk::attnSplitGrid(seqLen);
     a.chunkMax = hipk::attnChunkMax(seqLen, a.splitGrid);
     a.partO = (float *)alloc((size_t)B * nHeads0 * a.splitGrid * hs * 4);
     a.partML = (float *)alloc((size_t)B * nHeads0 * a.splitGrid * 2 * 4);

@@ -26,7 +26,7 @@ void HipEngineImpl::setupBuckets() {
     buckets_.push_back(last);
     DL_CHECK(buckets_.size() <= 16, "too many context buckets");
     for (CtxBucket &b : buckets_) {
-        b.splitGrid = hipk::attnSplitGrid(b.maxLen, (int)plan_.nHeads0);
+        b.splitGrid = hipk::attnSplitGrid(b.maxLen);
         b.chunkMax = hipk::attnChunkMax(b.maxLen, b.splitGrid);
     }
     bucket_ = (int)buckets_.size() - 1;
@@ -218,6 +218,10 @@ hipk::AttnBlockArgs HipEngineImpl::attnBlockArgs(const DevLayer &L, u32 l, int c
 void HipEngineImpl::setupAttnBlock() {
     const char *e = std::getenv("DL_ATTN_BLOCK");
     if ((e && *e == '0') || !q40_ || plan_.nKvHeads0 > kMaxKvGroups) return;
+    // one KV group per rank (8 KV heads at TP8): the attention role is a handful of workgroups
+    // the whole wo role waits on - measured 2x the three launches (8B TP8 rank: 38 vs ~18 us per
+    // layer, profiles/r5_tp_rank.md); DL_ATTN_BLOCK=1 forces it
+    if (plan_.nKvHeads0 < 2 && !(e && *e == '1')) return;
     const int share = comm_ ? std::max(1, comm_->ranksOnDevice()) : 1;
     const int keep = bucket_;
     // qkv / wo passes per workgroup: the GEMVs' own grids, except in same-GPU rehearsals (ranks

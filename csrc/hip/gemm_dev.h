@@ -125,7 +125,8 @@ __host__ __device__ inline size_t tpTileQ80Lds(int M, int W) {
     const int nEl = M * 64, nBlk = nEl / 32;
     return alignUp((size_t)nEl, 16) + alignUp((size_t)nBlk * 4, 16) + (size_t)W * nBlk * 9 * 4;
 }
-__device__ __forceinline__ void tpExchangeTile(const GemmArgs &ga, float *tile, int R0, char *lds) {
+template <int WM>
+__device__ __forceinline__ void tpExchangeTileW(const GemmArgs &ga, float *tile, int R0, char *lds) {
     const TpXchg &x = ga.e.tp;
     const int M = ga.M, nEl = M * 64, W = x.world;
     __syncthreads();
@@ -136,11 +137,11 @@ __device__ __forceinline__ void tpExchangeTile(const GemmArgs &ga, float *tile, 
             if (row >= ga.e.rows) continue;
             const long long el = (long long)t * ga.e.ldOut + row;
             const unsigned e = x.epochs[el] + 1;
-            unsigned v[kTpMaxRanks];
+            unsigned v[WM];
             tpPushCollect(x, el, e, __float_as_uint(tile[i]), v);
             float s = 0.f;
 #pragma unroll
-            for (int p = 0; p < kTpMaxRanks; p++)
+            for (int p = 0; p < WM; p++)
                 if (p < W) s += __uint_as_float(v[p]);
             tile[i] = s;
             x.epochs[el] = e;
@@ -180,10 +181,10 @@ __device__ __forceinline__ void tpExchangeTile(const GemmArgs &ga, float *tile, 
         const long long wd = gb * 9 + w;
         const unsigned e = x.epochs[wd] + 1;
         const unsigned payload = w < 8 ? reinterpret_cast<const uint32_t *>(q8)[blk * 8 + w] : dq[blk];
-        unsigned v[kTpMaxRanks];
+        unsigned v[WM];
         tpPushCollect(x, wd, e, payload, v);
 #pragma unroll
-        for (int p = 0; p < kTpMaxRanks; p++)
+        for (int p = 0; p < WM; p++)
             if (p < W) rv[(p * nBlk + blk) * 9 + w] = v[p];
         x.epochs[wd] = e;
     }
@@ -201,6 +202,9 @@ __device__ __forceinline__ void tpExchangeTile(const GemmArgs &ga, float *tile, 
         tile[i] = s;
     }
     __syncthreads();
+}
+__device__ __forceinline__ void tpExchangeTile(const GemmArgs &ga, float *tile, int R0, char *lds) {
+    tpDispatch(ga.e.tp.world, [&](auto wm) { tpExchangeTileW<decltype(wm)::value>(ga, tile, R0, lds); });
 }
 
 // Consumer of a fused residual + norm (ga.ssIn): per-token RMS scale of tokens [t0, t0 + nt) of the

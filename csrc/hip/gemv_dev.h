@@ -460,6 +460,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
         latePath();
         mainLoop();
     }
+    const unsigned long long tLoop = a.trace ? wall_clock64() : 0ull;  // main loop done (this wave)
     if constexpr (EPI == EPI_ACT_Q80) {
         __syncthreads();
         storeHiddenQ80<B, MODE == GEMV_PRODUCER>(a, hbuf, R >> 1, rowBase >> 1);
@@ -484,8 +485,11 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
     }
     if constexpr (tpx) {  // all-reduce the partial rows over the TP ranks, then store (sq is free now)
         __syncthreads();
-        if (a.tp.q80) tpExchangeQ80<B>(a, res, R, rowBase, reinterpret_cast<char *>(sq), pe);
-        else tpExchangeF32<B>(a, res, R, rowBase, pe);
+        tpDispatch(a.tp.world, [&](auto wm) {
+            constexpr int WM = decltype(wm)::value;
+            if (a.tp.q80) tpExchangeQ80<B, WM>(a, res, R, rowBase, reinterpret_cast<char *>(sq), pe);
+            else tpExchangeF32<B, WM>(a, res, R, rowBase, pe);
+        });
     }
     if constexpr (EPI == EPI_ARGMAX) {  // the row's argmax instead of its logits (ArgmaxTail)
         static_assert(B == 1, "EPI_ARGMAX: one row");
@@ -517,7 +521,8 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
             blockArgmax(bv, bi, sv, si);
             if (tid == 0) {
                 bi += a.am.vocabStart;
-                if (a.tp.world > 1) tpArgmaxPick(a.tp, 0, bv, bi);
+                if (a.tp.world > 1)
+                    tpDispatch(a.tp.world, [&](auto wm) { tpArgmaxPick<decltype(wm)::value>(a.tp, 0, bv, bi); });
                 a.am.ids[0] = bi;
                 if (a.am.tokens) {  // chained decode: feed the token back
                     const int p = a.am.pos[0];
@@ -542,6 +547,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
             t[4] = tLoaded;
             t[5] = tFirst;
             t[6] = tWaited;
+            t[7] = tLoop;
         }
     }
 }

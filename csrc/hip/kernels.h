@@ -337,7 +337,7 @@ void launchTpSelfTest(const TpXchg &x, float *out, int n, float val, hipStream_t
 void launchAttentionPrefill(const AttnArgs &a, int nRows, hipStream_t s);
 int attnPrefillRowsPerBlock(int kvMul);
 bool attnPrefillSupported(int hs, int kvMul, bool kvBf16);
-int attnSplitGrid(int seqLen, int heads = 32);  // attnSplitsFor (decode_common.h)
+int attnSplitGrid(int seqLen);
 int attnChunkMax(int seqLen, int splitGrid);
 
 // epoch (optional): one thread increments it - the per-forward epoch of the fused attention block.

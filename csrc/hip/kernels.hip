@@ -159,8 +159,8 @@ size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg, int pro) {
 // (head group, chunk, row). A single chunk writes the final output directly; with several chunks
 // each workgroup publishes its online-softmax partial and the last arriver combines them.
 // ------------------------------------------------------------------------------------------------
-int attnSplitGrid(int seqLen, int heads) {
-    int g = attnSplitsFor(seqLen, heads);
+int attnSplitGrid(int seqLen) {
+    int g = (seqLen + 255) / 256;
     return g < 1 ? 1 : (g > 128 ? 128 : g);
 }
 

@@ -379,7 +379,7 @@ std::vector<float> attention(const std::vector<float> &q, const std::vector<floa
     a.hs = hs;
     a.kv0 = kv0;
     a.seqLen = seqLen;
-    a.splitGrid = hipk::attnSplitGrid(seqLen, nHeads0);
+    a.splitGrid = hipk::attnSplitGrid(seqLen);
     a.chunkMax = hipk::attnChunkMax(seqLen, a.splitGrid);
     a.partO = sc.alloc<float>((size_t)B * nHeads0 * a.splitGrid * hs);
     a.partML = sc.alloc<float>((size_t)B * nHeads0 * a.splitGrid * 2);

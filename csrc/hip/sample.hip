@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void argmaxKernel(ArgmaxArgs a) {
     if (threadIdx.x == 0 && a.tp.world > 1) {
         // tensor parallel: every rank offers its slice's winner (value, global index)
         bi += a.vocabStart;
-        tpArgmaxPick(a.tp, b, bv, bi);
+        tpDispatch(a.tp.world, [&](auto wm) { tpArgmaxPick<decltype(wm)::value>(a.tp, b, bv, bi); });
     }
     if (threadIdx.x == 0) argmaxStore(a, b, bi);
 }

@@ -28,7 +28,8 @@ def main():
     shape = dict(LLAMA31_8B, **LLAMA_SHAPES[args.shape])
     e = C.HipEngine("", "q80", max_seq_len=4096, max_batch=32, n_slots=1, kv_bf16=True, gpu_index=0,
                     use_graphs=not args.no_graphs, synthetic=dict(shape, seq_len=4096), seed=1234, rank=args.rank,
-                    world=args.tp, comm=C.ComputeOnlyComm(args.rank, args.tp, 0), sync_type=args.sync_type)
+                    **(dict(world=args.tp, comm=C.ComputeOnlyComm(args.rank, args.tp, 0)) if args.tp > 1 else {}),
+                    sync_type=args.sync_type)
     prompt = [(i * 7919 + 13) % 128000 for i in range(64)]
     for _ in range(2):
         e.forward_argmax(prompt[:32], list(range(32)), [0] * 32)
@@ -45,7 +46,8 @@ def main():
     torch.cuda.synchronize()
     pred = (time.perf_counter() - t0) * 1000.0 / args.steps
     print(f"tp{args.tp} rank {args.rank} ({args.shape}, {args.sync_type}): pred {pred:.4f} ms/token, "
-          f"eval {ev:.4f} ms/token, fused {bool(e.tp_fused)}, attn block {bool(e.attn_block)}", flush=True)
+          f"eval {ev:.4f} ms/token, fused {bool(e.tp_fused)}, attn block {bool(e.attn_block)} "
+          f"[{' '.join(k + '=' + v for k, v in os.environ.items() if k.startswith('DL_'))}]", flush=True)
 
 
 if __name__ == "__main__":

@@ -10,7 +10,7 @@ Per shape this prints, averaged over the launches after the first few:
   ready  entry -> prologue done (median / p90; late path: first ring round landed too)
   first  entry -> first ring slot consumed (median)
   exit   spread of exit times relative to the launch's first entry (median / p90 / max)
-  python scripts/trace_gemv.py [shape ...]
+  [COPIES=n] python scripts/trace_gemv.py [shape ...]
 """
 import os
 import sys
@@ -29,6 +29,14 @@ SHAPES = {
     "w13": (28672, 4096, PRO_RESNORM, EPI_ACT_Q80),
     "w2": (4096, 14336, PRO_GLOBAL, EPI_STORE),
     "wcls": (128256, 4096, PRO_RESNORM, EPI_STORE),
+    # rank shards of Llama-3.1-8B at TP8 (w2 takes the norm prologue there: hidden0 / 32 < 192)
+    "qkv8": (768, 4096, PRO_RESNORM, EPI_QKV),
+    "wo8": (4096, 512, PRO_GLOBAL, EPI_STORE),
+    "w13_8": (3584, 4096, PRO_RESNORM, EPI_ACT),
+    "w2_8": (4096, 1792, PRO_RESNORM, EPI_STORE),
+    # their TP tails (EPI_STORE_TP in loopback: DL_BENCH_TP_WORLD / DL_BENCH_TP_Q80)
+    "wo8tp": (4096, 512, PRO_GLOBAL, 5),
+    "w2_8tp": (4096, 1792, PRO_RESNORM, 5),
 }
 TICK_US = 0.01  # s_memrealtime runs at 100 MHz
 
@@ -38,9 +46,10 @@ def analyse(name, us, t, iters):
     grid = t.shape[1]
     rows = []
     for i in range(4, iters):
-        e, r, x, ld, f = t[i, :, 0], t[i, :, 1], t[i, :, 2], t[i, :, 4], t[i, :, 5]
+        e, r, x, ld, f, lp = t[i, :, 0], t[i, :, 1], t[i, :, 2], t[i, :, 4], t[i, :, 5], t[i, :, 7]
         t0 = e.min()
-        rows.append(dict(loaded=np.median(ld - e) if ld.min() > 0 else np.nan, first=np.median(f - e),span=x.max() - t0, entry=e.max() - t0, ready_med=np.median(r - e), ready_p90=np.percentile(r - e, 90),
+        rows.append(dict(loaded=np.median(ld - e) if ld.min() > 0 else np.nan, first=np.median(f - e),
+                         loop=np.median(lp - e), tail=np.median(x - lp),span=x.max() - t0, entry=e.max() - t0, ready_med=np.median(r - e), ready_p90=np.percentile(r - e, 90),
                          exit_med=np.median(x - t0), exit_p90=np.percentile(x - t0, 90), exit_min=x.min() - t0,
                          gap=(t[i + 1, :, 0].min() - x.max()) if i + 1 < iters else np.nan))
     avg = {k: np.nanmean([r[k] for r in rows]) * TICK_US for k in rows[0]}
@@ -66,6 +75,7 @@ def analyse(name, us, t, iters):
           flush=True)
     print(f"{name:5s} grid {grid:4d} | {us:6.2f} us/launch | span {avg['span']:5.2f} gap {avg['gap']:4.2f} | "
           f"entry spread {avg['entry']:4.2f} | loaded {avg['loaded']:4.2f} | first {avg['first']:4.2f} | ready med {avg['ready_med']:4.2f} p90 {avg['ready_p90']:4.2f} | "
+          f"loop end {avg['loop']:4.2f} tail {avg['tail']:4.2f} | "
           f"exit min {avg['exit_min']:5.2f} med {avg['exit_med']:5.2f} p90 {avg['exit_p90']:5.2f} | WGs/XCC {per_xcc.tolist()}",
           flush=True)
 
@@ -75,7 +85,8 @@ def main():
     iters = int(os.environ.get("ITERS", "24"))
     for name in names:
         rows, n, pro, epi = SHAPES[name]
-        us, t = C.trace_gemv_q40(rows, n, pro, epi, 1, 0, 0, 8, iters)
+        # COPIES weight copies cycled per launch: 8 x a TP8 shard fits the 256 MB MALL, 48 do not
+        us, t = C.trace_gemv_q40(rows, n, pro, epi, 1, 0, 0, int(os.environ.get("COPIES", "8")), iters)
         analyse(name, us, t, iters)
 
 

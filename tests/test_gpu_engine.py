@@ -288,22 +288,24 @@ def kv8_gpu(tmp_path_factory):
     return m
 
 
-def test_simulated_tp8_matches_single(C, kv8_gpu):
+def test_simulated_tp8_matches_single(C, kv8_gpu, monkeypatch):
     """TP8 (one KV head per rank, q0 = 256, kv0 = 64) simulated on one GPU: same logits as TP1, and
-    every rank's single decode rows run the fused attention block."""
+    every rank's single decode rows run the fused attention block (forced: with one KV group per
+    rank the engine's default is the three launches)."""
     tokens = [5, 99, 300, 7, 1000, 2]
     single = C.HipEngine(kv8_gpu, "q80", kv_bf16=False)
     ref = np.stack([single.forward([t], [p], [0])[0] for p, t in enumerate(tokens)])
+    monkeypatch.setenv("DL_ATTN_BLOCK", "1")
     got, blocks = C.simulate_tp(kv8_gpu, "q80", 8, tokens, attn_block_flags=True)
     assert _rel(got, ref) < 3e-2
     assert (got.argmax(-1) == ref.argmax(-1)).all()
     assert all(blocks), blocks
 
 
-def test_simulated_tp8_70b_attention_shapes(C, tmp_path):
+def test_simulated_tp8_70b_attention_shapes(C, tmp_path, monkeypatch):
     """Llama-3.3-70B attention shapes at TP8 (dim 8192, 64 query / 8 KV heads of 128: per rank
     q0 = 1024, kv0 = 128, kvMul 8), one layer with a narrow FFN: simulated TP8 vs TP1 logits, the
-    fused attention block on every rank."""
+    fused attention block (forced) on every rank."""
     from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
     from distributed_llama_multiusers_amd.utils.mfile import FloatType
     m, _, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=64, seed=21, dim=8192, n_heads=64,
@@ -312,6 +314,7 @@ def test_simulated_tp8_70b_attention_shapes(C, tmp_path):
     single = C.HipEngine(m, "q80", kv_bf16=False)
     ref = np.stack([single.forward([t], [p], [0])[0] for p, t in enumerate(tokens)])
     del single
+    monkeypatch.setenv("DL_ATTN_BLOCK", "1")
     got, blocks = C.simulate_tp(m, "q80", 8, tokens, attn_block_flags=True)
     assert _rel(got, ref) < 3e-2
     assert all(blocks), blocks
