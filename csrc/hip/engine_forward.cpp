@@ -50,10 +50,12 @@ void HipEngineImpl::setInputs(int n, const int *tokens, const int *positions, co
     mapPages(n, positions, slots, ahead);
     // decode attention kernel for this forward (part of the graph key): the MFMA kernel once a
     // row's context reaches kAttnMfmaMinPos keys (measured faster from ~1.5K keys, slower on
-    // short contexts: profiles/r3_prefill_attention.md), else the VALU kernel
+    // short contexts: profiles/r3_prefill_attention.md) or the forward has kAttnMfmaMinRows rows
+    // (batch 16 / 64 at 150 keys: 8.2 / 17.2 us vs 9.5 / 22.8 on the VALU kernel, which stays
+    // ahead up to batch 8: profiles/r5_batched_attention.md), else the VALU kernel
     int maxPos = 0;
     for (int b = 0; b < n; b++) maxPos = std::max(maxPos, positions[b] + ahead);
-    attnLong_ = maxPos >= kAttnMfmaMinPos;
+    attnLong_ = maxPos >= kAttnMfmaMinPos || n >= kAttnMfmaMinRows;
     bucket_ = (int)(&bucketFor(maxPos) - buckets_.data());
     const u32 MB = cfg_.maxBatch;
     // keep the pinned staging buffer stable while a previous copy may still read it (every

@@ -228,6 +228,7 @@ class HipEngineImpl : public HipEngine {
     // 8 flags | spare line (every word on its own 256-B line; attn_block_inst.h carves them)
     static constexpr int kBlockCntWords = kMaxKvGroups * 64 + 64 + 8 * 64 + 64 + 8 * 64 + 64;
     static constexpr int kAttnMfmaMinPos = 1024;
+    static constexpr int kAttnMfmaMinRows = 16;
 
     EngineConfig cfg_;
     DeviceComm *comm_;

@@ -204,8 +204,12 @@ void launchAttentionValu(const AttnArgs &a, int B, hipStream_t s) {
     // (scripts/bench_attn.py, profiles/r1_attention.md): short contexts 7.9 -> 5.9 us (TP1) and
     // 7.7 -> 4.4 us (TP8) with one head per workgroup; long contexts keep 2-4 heads per workgroup.
     const int hgMax = (a.kvMul & (a.kvMul - 1)) == 0 ? (a.kvMul < 8 ? a.kvMul : 8) : 1;
+    static const long gridMax = [] {
+        const char *e = std::getenv("DL_ATTN_GRID_MAX");
+        return e ? std::atol(e) : 256L;
+    }();
     int HG = 1;
-    while (HG < hgMax && (long)(a.nHeads0 / HG) * a.splitGrid * B > 256) HG *= 2;
+    while (HG < hgMax && (long)(a.nHeads0 / HG) * a.splitGrid * B > gridMax) HG *= 2;
     if (a.hs == 128) {
         if (a.kvBf16) attnDispatchHG<128, true>(a, B, HG, s);
         else attnDispatchHG<128, false>(a, B, HG, s);
