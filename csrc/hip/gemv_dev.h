@@ -291,6 +291,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
                 ss = blockSum<kThreads>(ss, scratch);
                 inv = 1.0f / sqrtf(ss / (float)n + a.eps);
             }
+            if (MODE == GEMV_PLAIN && a.trace) tWaited = wall_clock64();  // norm reduced (plain GEMVs)
 #pragma unroll
             for (int k = 0; k < PK; k++) {
                 const int c = tid + k * kThreads;

@@ -49,7 +49,8 @@ def analyse(name, us, t, iters):
         e, r, x, ld, f, lp = t[i, :, 0], t[i, :, 1], t[i, :, 2], t[i, :, 4], t[i, :, 5], t[i, :, 7]
         t0 = e.min()
         rows.append(dict(loaded=np.median(ld - e) if ld.min() > 0 else np.nan, first=np.median(f - e),
-                         loop=np.median(lp - e), tail=np.median(x - lp),span=x.max() - t0, entry=e.max() - t0, ready_med=np.median(r - e), ready_p90=np.percentile(r - e, 90),
+                         loop=np.median(lp - e), tail=np.median(x - lp),
+                         summed=np.median(t[i, :, 6] - e) if t[i, :, 6].min() > 0 else np.nan,span=x.max() - t0, entry=e.max() - t0, ready_med=np.median(r - e), ready_p90=np.percentile(r - e, 90),
                          exit_med=np.median(x - t0), exit_p90=np.percentile(x - t0, 90), exit_min=x.min() - t0,
                          gap=(t[i + 1, :, 0].min() - x.max()) if i + 1 < iters else np.nan))
     avg = {k: np.nanmean([r[k] for r in rows]) * TICK_US for k in rows[0]}
@@ -74,7 +75,7 @@ def analyse(name, us, t, iters):
           f"| last-5% share {share[last].mean():.2f} vs all {share.mean():.2f} | blockIdx of last-5% mean {np.nonzero(last)[1].mean():.0f} of {grid}",
           flush=True)
     print(f"{name:5s} grid {grid:4d} | {us:6.2f} us/launch | span {avg['span']:5.2f} gap {avg['gap']:4.2f} | "
-          f"entry spread {avg['entry']:4.2f} | loaded {avg['loaded']:4.2f} | first {avg['first']:4.2f} | ready med {avg['ready_med']:4.2f} p90 {avg['ready_p90']:4.2f} | "
+          f"entry spread {avg['entry']:4.2f} | loaded {avg['loaded']:4.2f} | norm summed {avg['summed']:4.2f} | first {avg['first']:4.2f} | ready med {avg['ready_med']:4.2f} p90 {avg['ready_p90']:4.2f} | "
           f"loop end {avg['loop']:4.2f} tail {avg['tail']:4.2f} | "
           f"exit min {avg['exit_min']:5.2f} med {avg['exit_med']:5.2f} p90 {avg['exit_p90']:5.2f} | WGs/XCC {per_xcc.tolist()}",
           flush=True)

@@ -380,6 +380,44 @@ def test_cli_root_workers_over_xgmi(tmp_path, n_workers):
             p.wait()
 
 
+def test_cli_same_gpu_tp2_long_prompt(tmp_path):
+    """Root + one worker sharing GPU 0 with a prompt of 300+ tokens: the default prompt chunk is
+    capped to 32 rows when ranks share a device (a rank spinning on a 256+ row forward can keep
+    its peer's kernels from being dispatched), so the whole prompt evaluates without a collective
+    timeout and the greedy tokens equal the single-process run's."""
+    import subprocess
+    import time
+    from conftest import REPO
+    from distributed_llama_multiusers_amd.models.synthetic import make_test_assets
+    from distributed_llama_multiusers_amd.utils.mfile import FloatType
+    dllama = os.path.join(REPO, "build", "dllama")
+    m, t, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=512, seed=11, dim=512, n_heads=8,
+                               n_kv_heads=4, hidden_dim=1024)
+    prompt = " ".join(["hello world the"] * 50)  # ~300 tokens
+    base = [dllama, "inference", "--model", m, "--tokenizer", t, "--buffer-float-type", "q80", "--prompt", prompt,
+            "--steps", "340", "--temperature", "0", "--gpu-index", "0"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", DL_TP_COMM="xgmi")
+    ref = subprocess.run(base, capture_output=True, timeout=120, env=env)
+    assert ref.returncode == 0, ref.stdout.decode(errors="replace")
+    out = ref.stdout.decode(errors="replace")
+    evals = [l for l in out.splitlines() if l.startswith("🔷️ Eval")]
+    assert sum(int(l.split("(")[-1].split()[0]) for l in evals) > 256, evals[-3:]
+    preds = lambda o: [l.split("|")[-1] for l in o.decode(errors="replace").splitlines() if l.startswith("🔶 Pred")]
+    port = _port()
+    w = subprocess.Popen([dllama, "worker", "--port", str(port), "--gpu-index", "0"], stdout=subprocess.PIPE,
+                         stderr=subprocess.STDOUT, env=env)
+    try:
+        time.sleep(0.5)
+        r = subprocess.run(base + ["--workers", f"127.0.0.1:{port}"], capture_output=True, timeout=240, env=env)
+        text = r.stdout.decode(errors="replace")
+        assert r.returncode == 0, text
+        assert "ranks share this GPU" in text, text[:2000]
+        assert preds(r.stdout) == preds(ref.stdout) and len(preds(ref.stdout)) > 0
+    finally:
+        w.kill()
+        w.wait()
+
+
 def _data_plane_bytes(dim, n_layers, world, q80, rows=1):
     """Reference accounting of one forward's tensor-parallel payload per rank: two
     residual partials per layer to every peer (Q80: 34 B per 32 values), plus the greedy winner
