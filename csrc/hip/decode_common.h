@@ -506,9 +506,13 @@ __device__ __forceinline__ TpEpochs tpPrefetchEpochs(const GemvArgs &a, int R, i
     for (int k = 0; k < kTpPre; k++) {
         const int j = threadIdx.x + k * kThreads;
         long long w = -1;
-        if (B == 1) {  // one row: the words are contiguous (no division by R ahead of the ring)
-            const int row = rowBase + (q80 ? (j / 9) * 32 : j);
-            if (j < nw && row < a.rows) w = q80 ? (long long)(rowBase >> 5) * 9 + j : row;
+        if (B == 1) {  // one row: no division by R ahead of the ring
+            if (q80) {  // tpExchangeQ80Row: lane w < 9 of the 32-lane group of block j / 32
+                const int blk = j >> 5, wd = j & 31, row = rowBase + blk * 32;
+                if (wd < 9 && blk < nw / 9 && row < a.rows) w = (long long)((rowBase >> 5) + blk) * 9 + wd;
+            } else if (j < nw && rowBase + j < a.rows) {
+                w = rowBase + j;
+            }
         } else if (j < nw) {
             w = tpWordOf(a, R, rowBase, j, q80);
         }
@@ -553,6 +557,61 @@ __device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *re
 // Q80 exchange (the reference's ZQ pipe: every rank's partial quantized once to Q80 blocks of 32
 // rows, all ranks' blocks dequantized and summed in rank order, own included). R and rowBase are
 // multiples of 32. A block travels as 9 words: 8 x 4 int8 + the f16 scale. `lds` = free staging.
+// Q80 exchange of one row's partials (B = 1), wave-local: 32-row block g is quantized by the
+// 32-lane group of threads 32g..32g+31 (lane l = row rowBase + 32g + l), lanes 0-8 push / collect
+// the block's 9 words (8 x 4 int8 + the f16 scale), and every lane sums its row over the ranks
+// from those words by shuffles: no LDS staging and no barrier (the LDS form spent ~1.6 us per
+// workgroup tail, profiles/r5_tp_rank.md). Same rounding and rank order as tpExchangeQ80.
+template <int WM>
+__device__ __forceinline__ void tpExchangeQ80Row(const GemvArgs &a, const float *res, int R, int rowBase,
+                                                 TpEpochs pe) {
+    const TpXchg &x = a.tp;
+    const int nBlk = R >> 5, W = x.world;
+    const long long t0 = tpSpanBegin(x);
+    tpEpochsWait(pe);
+    const int l = threadIdx.x & 31;
+    int k = 0;
+    for (int base = 0; base < nBlk * 32; base += kThreads, k++) {  // uniform per 32-lane group
+        const int i = base + threadIdx.x, blk = i >> 5, row = rowBase + i;
+        const bool blkLive = blk < nBlk && rowBase + blk * 32 < a.rows;
+        const float v = blk < nBlk ? res[i] : 0.f;
+        const float amax = groupMax<32>(fabsf(v));
+        const float d = amax / 127.0f;
+        const float id = d != 0.f ? 1.0f / d : 0.f;
+        int q = (int)rintf(v * id);
+        q = q > 127 ? 127 : (q < -127 ? -127 : q);
+        const unsigned d16 = __half_as_ushort(__float2half(d));
+        // lane w < 8 packs the bytes of rows 4w .. 4w + 3; lane 8 carries the scale
+        const unsigned b0 = (unsigned)__shfl(q, 4 * (l & 7), 32) & 0xFFu, b1 = (unsigned)__shfl(q, 4 * (l & 7) + 1, 32) & 0xFFu;
+        const unsigned b2 = (unsigned)__shfl(q, 4 * (l & 7) + 2, 32) & 0xFFu, b3 = (unsigned)__shfl(q, 4 * (l & 7) + 3, 32) & 0xFFu;
+        const unsigned payload = l < 8 ? (b0 | (b1 << 8) | (b2 << 16) | (b3 << 24)) : d16;
+        unsigned vals[WM];
+#pragma unroll
+        for (int p = 0; p < WM; p++) vals[p] = 0u;
+        if (blkLive && l < 9) {
+            const long long wd = (long long)((rowBase >> 5) + blk) * 9 + l;
+            const unsigned e = (k < kTpPre ? pe.v[k] : x.epochs[wd]) + 1;
+            tpPushCollect<WM>(x, wd, e, payload, vals);
+            x.epochs[wd] = e;
+        }
+        float sum = 0.f;
+#pragma unroll
+        for (int p = 0; p < WM; p++) {
+            if (p < W) {
+                const unsigned wq = (unsigned)__shfl((int)vals[p], l >> 2, 32);
+                const unsigned ds = (unsigned)__shfl((int)vals[p], 8, 32);
+                const int qq = (int)(int8_t)(wq >> (8 * (l & 3)));
+                sum += (float)qq * __half2float(__ushort_as_half((uint16_t)(ds & 0xFFFFu)));
+            }
+        }
+        if (blkLive && row < a.rows) a.out[row] = sum;
+    }
+    if (x.ticks) {
+        __syncthreads();
+        tpSpanEnd(x, t0);
+    }
+}
+
 template <int B, int WM>
 __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *res, int R, int rowBase, char *lds,
                                               TpEpochs pe) {

@@ -488,7 +488,8 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
         __syncthreads();
         tpDispatch(a.tp.world, [&](auto wm) {
             constexpr int WM = decltype(wm)::value;
-            if (a.tp.q80) tpExchangeQ80<B, WM>(a, res, R, rowBase, reinterpret_cast<char *>(sq), pe);
+            if (a.tp.q80 && B == 1) tpExchangeQ80Row<WM>(a, res, R, rowBase, pe);
+            else if (a.tp.q80) tpExchangeQ80<B, WM>(a, res, R, rowBase, reinterpret_cast<char *>(sq), pe);
             else tpExchangeF32<B, WM>(a, res, R, rowBase, pe);
         });
     }

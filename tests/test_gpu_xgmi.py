@@ -29,8 +29,11 @@ def _port():
 def _same_gpu_env(world):
     """All ranks share one GPU here: a GEMV whose tail waits for its peers must leave room on the
     CUs for the peers' GEMVs, so each rank's grid is capped to its share of the resident slots
-    (on a real node every rank has its own GPU and the whole grid is resident)."""
-    return {"DL_GEMV_RESIDENT": str(max(32, 512 // world))} if world > 2 else {}
+    (on a real node every rank has its own GPU and the whole grid is resident). Each process also
+    keeps to one hardware queue: 8 processes x HIP's default 4 queues can exceed the queues the
+    device maps at once, and a rank spinning on a peer whose queue is not mapped waits until its
+    20 s timeout (seen once as a stalled 8-process CLI run)."""
+    return {"DL_GEMV_RESIDENT": str(max(32, 512 // world)), "GPU_MAX_HW_QUEUES": "1"} if world > 2 else {}
 
 
 def _setup(rank, world, port, max_floats):
