@@ -225,7 +225,9 @@ void launchAttentionValu(const AttnArgs &a, int B, hipStream_t s) {
 __global__ void embeddingKernel(const float *table, const int *tokens, float *x, int dim, unsigned *epoch,
                                 unsigned *zero, int nZero) {
     const int b = blockIdx.x;
-    if (epoch && b == 0 && threadIdx.x == 0) *epoch += 1;  // read by later kernels of this forward
+    // the forward's epoch, read by later kernels: a no-return atomic (the wave does not wait on a
+    // read-modify-write round trip before its row loads)
+    if (epoch && b == 0 && threadIdx.x == 0) __hip_atomic_fetch_add(epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (b == 0)
         for (int i = threadIdx.x; i < nZero; i += blockDim.x) zero[i] = 0u;
     const float *src = table + (size_t)tokens[b] * dim;
