@@ -206,7 +206,7 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
     const int pos = a.pos[b], sl = a.slot[b];
     const int len = pos + 1;
     int nSplit, ch;
-    attnSplit(len, a.splitGrid, nSplit, ch);
+    attnSplit(len, a.splitGrid, nSplit, ch, a.chunkMin);
     if (c >= nSplit) return false;
     const int t0 = c * ch;
     const int t1 = min(t0 + ch, len);

@@ -679,8 +679,8 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
 // Sequence split of a decode-attention row of length `len`: nSplit chunks of ch positions
 // (~256 per chunk, at most splitGrid chunks). Shorter chunks for the few heads of a TP8 shard
 // (4 per rank) measured slower: 5.4 -> 7.6 us at 100 positions (profiles/r5_tp_rank.md).
-__device__ __forceinline__ void attnSplit(int len, int splitGrid, int &nSplit, int &ch) {
-    int ns = (len + 255) / 256;
+__device__ __forceinline__ void attnSplit(int len, int splitGrid, int &nSplit, int &ch, int chunkMin = 256) {
+    int ns = (len + chunkMin - 1) / chunkMin;
     if (ns > splitGrid) ns = splitGrid;
     if (ns < 1) ns = 1;
     ch = (((len + ns - 1) / ns) + 15) & ~15;

@@ -260,6 +260,7 @@ double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B
     a.seqLen = seqLen;
     a.splitGrid = hipk::attnSplitGrid(seqLen);
     a.chunkMax = hipk::attnChunkMax(seqLen, a.splitGrid);
+    a.chunkMin = hipk::attnChunkMin();
     a.partO = (float *)alloc((size_t)B * nHeads0 * a.splitGrid * hs * 4);
     a.partML = (float *)alloc((size_t)B * nHeads0 * a.splitGrid * 2 * 4);
     a.outQ = (int8_t *)alloc((size_t)B * q0);

@@ -173,6 +173,7 @@ hipk::AttnArgs HipEngineImpl::attnArgs(const DevLayer &L, bool bat) const {
     a.seqLen = h_.seqLen;
     a.splitGrid = buckets_[bucket_].splitGrid;
     a.chunkMax = buckets_[bucket_].chunkMax;
+    a.chunkMin = hipk::attnChunkMin();
     a.partO = dPartO_;
     a.partML = dPartML_;
     a.out = dAtt_;

@@ -89,6 +89,7 @@ struct AttnArgs {
     int nHeads0 = 0, kvMul = 1, hs = 0, kv0 = 0, seqLen = 0;
     int splitGrid = 1;          // max sequence splits (grid.y)
     int chunkMax = 256;         // LDS capacity in positions per split
+    int chunkMin = 256;         // fewest positions per split (attnChunkMin)
     float *partO = nullptr;     // [B][nHeads0][splitGrid][hs]
     float *partML = nullptr;    // [B][nHeads0][splitGrid][2]
     float *out = nullptr;       // [B][ldOut] f32 output (when outQ and outH are null)
@@ -338,6 +339,8 @@ void launchAttentionPrefill(const AttnArgs &a, int nRows, hipStream_t s);
 int attnPrefillRowsPerBlock(int kvMul);
 bool attnPrefillSupported(int hs, int kvMul, bool kvBf16);
 int attnSplitGrid(int seqLen);
+// Fewest keys per attention split (DL_ATTN_CHUNK, default 256): sets the split grid of a context.
+int attnChunkMin();
 int attnChunkMax(int seqLen, int splitGrid);
 
 // epoch (optional): one thread increments it - the per-forward epoch of the fused attention block.

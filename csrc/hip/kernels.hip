@@ -159,8 +159,18 @@ size_t gemvLdsBytes(int n, int B, bool q40, int rowsPerWg, int pro) {
 // (head group, chunk, row). A single chunk writes the final output directly; with several chunks
 // each workgroup publishes its online-softmax partial and the last arriver combines them.
 // ------------------------------------------------------------------------------------------------
+int attnChunkMin() {
+    static const int v = [] {
+        const char *e = std::getenv("DL_ATTN_CHUNK");
+        const int c = e ? std::atoi(e) : 256;
+        return c >= 32 && c <= 1024 && (c & 15) == 0 ? c : 256;
+    }();
+    return v;
+}
+
 int attnSplitGrid(int seqLen) {
-    int g = (seqLen + 255) / 256;
+    const int cm = attnChunkMin();
+    int g = (seqLen + cm - 1) / cm;
     return g < 1 ? 1 : (g > 128 ? 128 : g);
 }
 

@@ -381,6 +381,7 @@ std::vector<float> attention(const std::vector<float> &q, const std::vector<floa
     a.seqLen = seqLen;
     a.splitGrid = hipk::attnSplitGrid(seqLen);
     a.chunkMax = hipk::attnChunkMax(seqLen, a.splitGrid);
+    a.chunkMin = hipk::attnChunkMin();
     a.partO = sc.alloc<float>((size_t)B * nHeads0 * a.splitGrid * hs);
     a.partML = sc.alloc<float>((size_t)B * nHeads0 * a.splitGrid * 2);
     a.out = sc.alloc<float>((size_t)B * q0);
