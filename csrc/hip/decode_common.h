@@ -370,7 +370,7 @@ __device__ __forceinline__ bool tpFailed(const TpXchg &x) {
 // 16-way form measured ~1.1-2.3 us of scalar selects and spilled SGPRs per workgroup tail).
 template <int WM>
 __device__ __forceinline__ void tpPushCollect(const TpXchg &x, long long w, unsigned e, unsigned payload,
-                                              unsigned (&vals)[WM]) {
+                                              unsigned (&vals)[WM], unsigned &waited) {
     const int me = x.rank, W = x.world;
     if (x.loopback) {
 #pragma unroll
@@ -403,10 +403,18 @@ __device__ __forceinline__ void tpPushCollect(const TpXchg &x, long long w, unsi
                         break;
                     }
                 }
+                waited += (unsigned)((long long)__builtin_amdgcn_s_memrealtime() - t0);
             }
             vals[p] = (unsigned)v;
         }
     }
+}
+
+template <int WM>
+__device__ __forceinline__ void tpPushCollect(const TpXchg &x, long long w, unsigned e, unsigned payload,
+                                              unsigned (&vals)[WM]) {
+    unsigned waited = 0;
+    tpPushCollect<WM>(x, w, e, payload, vals, waited);
 }
 
 // Calls f(std::integral_constant<int, WM>) with the smallest rank bound WM in {2, 4, 8, 16} >= world.
@@ -418,17 +426,23 @@ __device__ __forceinline__ void tpDispatch(int world, F &&f) {
     else f(std::integral_constant<int, 16>{});
 }
 
-// Measured sync: a workgroup's exchange span (ticks of s_memrealtime, 10 ns) raised into x.ticks
-// by thread 0 once every thread of the workgroup is past its collect (the caller's barrier).
-__device__ __forceinline__ long long tpSpanBegin(const TpXchg &x) {
-    return x.ticks ? (long long)__builtin_amdgcn_s_memrealtime() : 0ll;
-}
-__device__ __forceinline__ void tpSpanEnd(const TpXchg &x, long long t0) {
-    if (x.ticks && threadIdx.x == 0) {
-        const long long dt = (long long)__builtin_amdgcn_s_memrealtime() - t0;
-        __hip_atomic_fetch_max(x.ticks, (unsigned)(dt > 0xFFFFFFFFll ? 0xFFFFFFFFll : dt), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+// Measured sync (ForwardStats::syncMs): the time a wave spends waiting for peers' words, read from
+// s_memrealtime (10 ns ticks) only inside the wait loop - an exchange that finds every word
+// already there costs nothing (a stamp at every exchange's start stalled the tail's next LDS
+// access on the RTC read: ~4 % of a TP8 rank's decode). Per exchange the longest wave's wait is
+// raised into x.ticks (one no-return atomic per wave that waited). Wave-uniform control flow.
+__device__ __forceinline__ void tpWaitReport(const TpXchg &x, unsigned waited) {
+    if (!x.ticks || __ballot(waited != 0u) == 0ull) return;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned o = (unsigned)__shfl_xor((int)waited, off);
+        waited = o > waited ? o : waited;
     }
+    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_max(x.ticks, waited, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The same from a single thread (argmax winners).
+__device__ __forceinline__ void tpWaitReportThread(const TpXchg &x, unsigned waited) {
+    if (x.ticks && waited) __hip_atomic_fetch_max(x.ticks, waited, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Argmax reductions (value, index): larger value wins, ties -> lower index (a full-vocabulary
@@ -459,11 +473,11 @@ __device__ __forceinline__ void blockArgmax(float &bv, int &bi, float *sv, int *
 // Thread 0 only.
 template <int WM>
 __device__ __forceinline__ void tpArgmaxPick(const TpXchg &x, int b, float &bv, int &bi) {
-    const long long t0 = tpSpanBegin(x);
+    unsigned waited = 0;
     const unsigned ev = x.epochs[2 * b] + 1, ei = x.epochs[2 * b + 1] + 1;  // one epoch per word
     unsigned vv[WM], vi[WM];
-    tpPushCollect(x, 2LL * b, ev, __float_as_uint(bv), vv);
-    tpPushCollect(x, 2LL * b + 1, ei, (unsigned)bi, vi);
+    tpPushCollect(x, 2LL * b, ev, __float_as_uint(bv), vv, waited);
+    tpPushCollect(x, 2LL * b + 1, ei, (unsigned)bi, vi, waited);
     bv = -INFINITY;
     bi = 0x7fffffff;
 #pragma unroll
@@ -471,7 +485,7 @@ __device__ __forceinline__ void tpArgmaxPick(const TpXchg &x, int b, float &bv, 
         if (p < x.world) argBetter(bv, bi, __uint_as_float(vv[p]), (int)vi[p]);
     x.epochs[2 * b] = ev;
     x.epochs[2 * b + 1] = ei;
-    tpSpanEnd(x, t0);
+    tpWaitReportThread(x, waited);
 }
 
 // LDS bytes of the Q80 exchange staging for nEl elements over W ranks.
@@ -531,7 +545,7 @@ __device__ __forceinline__ void tpEpochsWait(TpEpochs &pe) {
 template <int B, int WM>
 __device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *res, int R, int rowBase, TpEpochs pe) {
     const TpXchg &x = a.tp;
-    const long long t0 = tpSpanBegin(x);
+    unsigned waited = 0;
     tpEpochsWait(pe);
     int k = 0;
     for (int i = threadIdx.x; i < B * R; i += kThreads, k++) {
@@ -540,7 +554,7 @@ __device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *re
         const long long el = (long long)b * a.ldOut + row;
         const unsigned e = tpEpochOf(x, pe, k, el) + 1;
         unsigned v[WM];
-        tpPushCollect(x, el, e, __float_as_uint(res[i]), v);
+        tpPushCollect(x, el, e, __float_as_uint(res[i]), v, waited);
         float s = 0.f;
 #pragma unroll
         for (int p = 0; p < WM; p++)
@@ -548,10 +562,7 @@ __device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *re
         a.out[el] = s;
         x.epochs[el] = e;
     }
-    if (x.ticks) {
-        __syncthreads();
-        tpSpanEnd(x, t0);
-    }
+    tpWaitReport(x, waited);
 }
 
 // Q80 exchange (the reference's ZQ pipe: every rank's partial quantized once to Q80 blocks of 32
@@ -567,7 +578,7 @@ __device__ __forceinline__ void tpExchangeQ80Row(const GemvArgs &a, const float 
                                                  TpEpochs pe) {
     const TpXchg &x = a.tp;
     const int nBlk = R >> 5, W = x.world;
-    const long long t0 = tpSpanBegin(x);
+    unsigned waited = 0;
     tpEpochsWait(pe);
     const int l = threadIdx.x & 31;
     int k = 0;
@@ -591,7 +602,7 @@ __device__ __forceinline__ void tpExchangeQ80Row(const GemvArgs &a, const float 
         if (blkLive && l < 9) {
             const long long wd = (long long)((rowBase >> 5) + blk) * 9 + l;
             const unsigned e = (k < kTpPre ? pe.v[k] : x.epochs[wd]) + 1;
-            tpPushCollect<WM>(x, wd, e, payload, vals);
+            tpPushCollect<WM>(x, wd, e, payload, vals, waited);
             x.epochs[wd] = e;
         }
         float sum = 0.f;
@@ -606,10 +617,7 @@ __device__ __forceinline__ void tpExchangeQ80Row(const GemvArgs &a, const float 
         }
         if (blkLive && row < a.rows) a.out[row] = sum;
     }
-    if (x.ticks) {
-        __syncthreads();
-        tpSpanEnd(x, t0);
-    }
+    tpWaitReport(x, waited);
 }
 
 template <int B, int WM>
@@ -620,7 +628,7 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
     int8_t *q8 = reinterpret_cast<int8_t *>(lds);
     uint32_t *dq = reinterpret_cast<uint32_t *>(lds + alignUp((size_t)nEl, 16));
     uint32_t *rv = reinterpret_cast<uint32_t *>(lds + alignUp((size_t)nEl, 16) + alignUp((size_t)nBlk * 4, 16));
-    const long long t0 = tpSpanBegin(x);
+    unsigned waited = 0;
     tpEpochsWait(pe);
     // 1. quantize this rank's partial (whole 32-lane groups per block: the loop is uniform)
     for (int base = 0; base < nEl; base += kThreads) {
@@ -653,14 +661,14 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
         const unsigned e = tpEpochOf(x, pe, k, wd) + 1;
         const unsigned payload = w < 8 ? reinterpret_cast<const uint32_t *>(q8)[blk * 8 + w] : dq[blk];
         unsigned v[WM];
-        tpPushCollect(x, wd, e, payload, v);
+        tpPushCollect(x, wd, e, payload, v, waited);
 #pragma unroll
         for (int p = 0; p < WM; p++)
             if (p < W) rv[(p * nBlk + blk) * 9 + w] = v[p];
         x.epochs[wd] = e;
     }
+    tpWaitReport(x, waited);
     __syncthreads();
-    tpSpanEnd(x, t0);
     // 3. dequantize and sum in rank order
     for (int i = threadIdx.x; i < nEl; i += kThreads) {
         const int b = B == 1 ? 0 : i / R, row = rowBase + (B == 1 ? i : i % R), blk = i >> 5;

@@ -351,8 +351,9 @@ void HipEngineImpl::accountForward(int n, GraphKind kind, int times) {
 }
 
 // Measured sync of the last forward (the host copy of its slots, enqueued by runGraph): per
-// exchange the slowest workgroup's fused-exchange span, or the stamped span of a separate
-// collective (launch gaps included), summed over the forward's exchanges. The reference times its
+// exchange the longest time a wave of the fused exchange waited for peers' words (tpWaitReport),
+// or the stamped span of a separate collective (launch gaps included), summed over the forward's
+// exchanges. The reference times its
 // sync steps the same way, per forward (nn-executor.cpp:150-155, printed per token dllama.cpp:57-64).
 double HipEngineImpl::readSyncMs() const {
     if (plan_.nRanks <= 1 || !hSync_) return 0;

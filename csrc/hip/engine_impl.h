@@ -110,7 +110,7 @@ class HipEngineImpl : public HipEngine {
     // workgroups) and a pair of u64 stamps around a separate collective; cleared by the forward's
     // embedding kernel, copied to the host after each forward
     int syncSlots() const { return 2 * (int)h_.nLayers + 2; }
-    // DL_SYNC_MEASURE=0: the fused exchanges keep no span words (comparison runs)
+    // DL_SYNC_MEASURE=0: the fused exchanges report no waiting time (comparison runs)
     const bool syncMeasure_ = [] {
         const char *e = std::getenv("DL_SYNC_MEASURE");
         return !(e && *e == '0');

@@ -130,7 +130,7 @@ __device__ __forceinline__ void tpExchangeTileW(const GemmArgs &ga, float *tile,
     const TpXchg &x = ga.e.tp;
     const int M = ga.M, nEl = M * 64, W = x.world;
     __syncthreads();
-    const long long t0 = tpSpanBegin(x);
+    unsigned waited = 0;
     if (!x.q80) {
         for (int i = threadIdx.x; i < nEl; i += kThreads) {
             const int t = i >> 6, row = R0 + (i & 63);
@@ -138,7 +138,7 @@ __device__ __forceinline__ void tpExchangeTileW(const GemmArgs &ga, float *tile,
             const long long el = (long long)t * ga.e.ldOut + row;
             const unsigned e = x.epochs[el] + 1;
             unsigned v[WM];
-            tpPushCollect(x, el, e, __float_as_uint(tile[i]), v);
+            tpPushCollect(x, el, e, __float_as_uint(tile[i]), v, waited);
             float s = 0.f;
 #pragma unroll
             for (int p = 0; p < WM; p++)
@@ -146,8 +146,8 @@ __device__ __forceinline__ void tpExchangeTileW(const GemmArgs &ga, float *tile,
             tile[i] = s;
             x.epochs[el] = e;
         }
+        tpWaitReport(x, waited);
         __syncthreads();
-        tpSpanEnd(x, t0);
         return;
     }
     const int nBlk = nEl >> 5;
@@ -182,14 +182,14 @@ __device__ __forceinline__ void tpExchangeTileW(const GemmArgs &ga, float *tile,
         const unsigned e = x.epochs[wd] + 1;
         const unsigned payload = w < 8 ? reinterpret_cast<const uint32_t *>(q8)[blk * 8 + w] : dq[blk];
         unsigned v[WM];
-        tpPushCollect(x, wd, e, payload, v);
+        tpPushCollect(x, wd, e, payload, v, waited);
 #pragma unroll
         for (int p = 0; p < WM; p++)
             if (p < W) rv[(p * nBlk + blk) * 9 + w] = v[p];
         x.epochs[wd] = e;
     }
+    tpWaitReport(x, waited);
     __syncthreads();
-    tpSpanEnd(x, t0);
     for (int i = threadIdx.x; i < nEl; i += kThreads) {
         const int blk = i >> 5;
         float s = 0.f;

@@ -127,9 +127,9 @@ struct TpXchg {
     long long timeoutTicks = 0;         // s_memrealtime ticks (100 MHz)
     int rank = 0, world = 1;
     int q80 = 0;                        // exchange Q80 blocks (the reference's ZQ wire format)
-    // measured sync (ForwardStats::syncMs): when set, every workgroup that exchanges raises this
-    // word to its exchange span (push -> every peer's words collected) in s_memrealtime ticks (10
-    // ns), so the word holds the slowest workgroup's span of this exchange
+    // measured sync (ForwardStats::syncMs): when set, every wave that had to wait for a peer's
+    // words raises this word to its waiting time in s_memrealtime ticks (10 ns), so the word holds
+    // the longest wait of this exchange (tpWaitReport)
     unsigned *ticks = nullptr;
     // compute-only rank (makeComputeOnlyComm): nothing crosses a link, every peer contributes
     // zeros - a TP-N rank's kernels timed on one GPU without the exchange

@@ -434,8 +434,8 @@ def test_data_plane_bytes_reported(tmp_path):
     of every decode forward in --metrics is the device data plane (formula above: 2 x layers x
     dim/32 x 34 B + the argmax winner) plus a few bytes of TCP control packets; the formula gives
     SURVEY §2.6's 272 KiB per token for Llama-3.1-8B at TP2. Sync ms is measured on the device: per
-    exchange the slowest workgroup's span (push -> every peer's words in), summed over the forward's
-    exchanges (engine.cpp readSyncMs)."""
+    exchange the longest time a wave waited for the peer's words, summed over the forward's
+    exchanges (engine.cpp readSyncMs): never more than the forward, and not zero over the run."""
     import json
     import subprocess
     import time
@@ -469,14 +469,16 @@ def test_data_plane_bytes_reported(tmp_path):
     for x in dec:
         assert expect <= x["sent_bytes"] <= expect + 256, (x, expect)
         assert expect <= x["recv_bytes"] <= expect + 256, (x, expect)
-        assert 0 < x["sync_ms"] < x["ms"], x  # measured exchange spans of the forward
+        assert 0 <= x["sync_ms"] < x["ms"], x  # measured waits of the forward's exchanges
+    assert sum(x["sync_ms"] for x in dec) > 0, dec
     # the Pred lines print the same (kB)
     kb = [int(l.split("Sent")[1].split("kB")[0]) for l in out.splitlines() if l.startswith("🔶 Pred")]
     assert kb and all(k == expect // 1024 for k in kb), (kb, expect)
-    # ... and the measured Sync column: > 0 and below the token's time
+    # ... and the measured Sync column (2 decimals: a short wait prints 0.00; the unrounded sum is
+    # checked above) next to the token's compute time
     sync = [float(l.split("Sync")[1].split("ms")[0]) for l in out.splitlines() if l.startswith("🔶 Pred")]
     tot = [float(l.split("Pred")[1].split("ms")[0]) for l in out.splitlines() if l.startswith("🔶 Pred")]
-    assert all(0 < s for s in sync) and all(t >= 0 for t in tot), out
+    assert sync and all(0 <= s for s in sync) and all(t >= 0 for t in tot), out
 
 
 def test_stalled_worker_gives_clean_root_error(tmp_path):
