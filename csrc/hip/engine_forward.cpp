@@ -227,13 +227,15 @@ void HipEngineImpl::setupAttnBlock() {
     if (plan_.nKvHeads0 < 2 && !(e && *e == '1')) return;
     const int share = comm_ ? std::max(1, comm_->ranksOnDevice()) : 1;
     const int keep = bucket_;
-    // qkv / wo passes per workgroup: the GEMVs' own grids, except in same-GPU rehearsals (ranks
-    // sharing one GPU's resident slots), which may double them so the block stays co-resident.
-    // On a GPU of its own a grid beyond one round of co-resident workgroups (70B / 405B at TP1)
-    // keeps the three launches: longer qkv / wo workgroups measured slower there (70B 8.10 ->
-    // 8.26, 405B 40.4 -> 43.3 ms/token).
+    // qkv / wo passes per workgroup: the GEMVs' own grids. A grid beyond one round of co-resident
+    // workgroups keeps the three launches: longer qkv / wo workgroups measured slower on a GPU of
+    // its own (70B 8.10 -> 8.26, 405B 40.4 -> 43.3 ms/token) and in same-GPU rehearsals (ranks
+    // sharing one GPU's resident slots: 8B TP2 2.91 vs 1.63 ms/token with the three launches), so
+    // a rehearsal makes the production choice. Only a forced block (DL_ATTN_BLOCK=1, tests of the
+    // block's exchange on one GPU) doubles the passes until the shared slots hold it.
+    const bool forced = e && *e == '1';
     bucket_ = 0;
-    for (blockPassMul_ = 1; share > 1 && blockPassMul_ < 8; blockPassMul_ *= 2) {
+    for (blockPassMul_ = 1; forced && share > 1 && blockPassMul_ < 8; blockPassMul_ *= 2) {
         const hipk::AttnBlockArgs b = attnBlockArgs(layers_[0], 0, 0);
         if (!hipk::attnBlockPlan(b, fusedTp(false)).fn) break;
         const hipk::GemvResidency r = hipk::attnBlockResidency(b, fusedTp(false));
