@@ -36,7 +36,9 @@ __device__ __forceinline__ void staticFor(F &&f) {
     staticForImpl<0, N>(f);
 }
 #ifndef DL_GEMV_KE
-#define DL_GEMV_KE 2
+// 4: same-box A/B of whole builds (profiles/r5_decode_profile.md): TP1 decode 1.386 vs 1.397
+// ms/token at 2, TP8 rank 0.965 vs 0.984; 1, 6 and 8 slower (6 and 8 at long context too)
+#define DL_GEMV_KE 4
 #endif
 static constexpr int kEarlySlots = DL_GEMV_KE;  // ring slots issued before the early prologue's wait
 
