@@ -19,7 +19,10 @@ namespace hipk {
 //   scripts/microbench_stream.hip). Activations always come from LDS (norm prologue or a copy
 //   of upstream Q80), row-pair epilogues (SwiGLU, RoPE + KV append) run in registers.
 // ------------------------------------------------------------------------------------------------
-static constexpr int kRing = 8;
+#ifndef DL_GEMV_RING
+#define DL_GEMV_RING 8
+#endif
+static constexpr int kRing = DL_GEMV_RING;
 
 // f(integral_constant<int, 0>), ..., f(integral_constant<int, N - 1>): ring slots addressed by
 // compile-time indices (fixed registers) however large the body (the compiler may decline to
