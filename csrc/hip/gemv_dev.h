@@ -20,7 +20,10 @@ namespace hipk {
 //   of upstream Q80), row-pair epilogues (SwiGLU, RoPE + KV append) run in registers.
 // ------------------------------------------------------------------------------------------------
 #ifndef DL_GEMV_RING
-#define DL_GEMV_RING 8
+// 4 slots: same-box A/B of whole builds (profiles/r5_decode_profile.md): TP1 decode 1.308-1.314 vs
+// 1.371-1.382 ms/token at 8 (fewer ring VGPRs, more waves per SIMD), long context 1.534-1.553 vs
+// 1.60-1.62; 2 / 3 / 5 / 6 / 12 slower at TP1 (2 is ahead only on a TP8 rank's small shards)
+#define DL_GEMV_RING 4
 #endif
 static constexpr int kRing = DL_GEMV_RING;
 
