@@ -24,7 +24,7 @@ ifeq ($(TSAN),1)
 endif
 
 HOSTFLAGS  := -std=c++17 $(OPT) -fPIC -march=x86-64-v3 -Wall -Wno-unused-function -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include $(SAN)
-HIPFLAGS   := -std=c++17 $(OPT) -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Wno-unused-result -munsafe-fp-atomics
+HIPFLAGS   := -std=c++17 $(OPT) -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Wno-unused-result -munsafe-fp-atomics $(EXTRA_HIPFLAGS)
 # Sanitizer builds instrument the g++-compiled host code (runtime, scheduler, API, TCP, CPU
 # backend, tokenizer); the hipcc translation units stay uninstrumented so that one sanitizer
 # runtime (gcc's) is linked. Device code is never sanitized on this pool.

@@ -11,6 +11,9 @@ random-init on device with the real Llama-3.1-8B shapes (no network for checkpoi
   logits -> argmax, the token fed back on device), K steps between barrier + device syncs;
 * value = B * 1000 / ((eval_ms_per_token + pred_ms_per_token) / 2), the named metric; the decode-only
   rate is reported as config.pred_tokens_per_s.
+The KV cache is f32, the reference's precision (src/llm.cpp:197-198, nn/nn-core.cpp:198-205), for
+the headline and every extra point (`--kv f32`, default); the same eval + pred with a bf16 cache is
+reported next to it (config.bf16_kv_*), never as `value`.
 The engine is sized to --max-seq-len positions (default 4096, the reference run script's
 `--max-seq-len 4096`); attention launches follow the context actually reached (context buckets),
 not the capacity. Extra points in `config`: decode at position >= 4096 (long_ctx_pred_ms_per_token),
@@ -52,7 +55,7 @@ LLAMA31_8B = dict(dim=4096, hidden_dim=14336, n_layers=32, n_heads=32, n_kv_head
                   weight_type=2, hidden_act=1)
 
 
-def _cli_point(local: int, prompt_tokens: int, steps: int, max_seq: int) -> dict:
+def _cli_point(local: int, prompt_tokens: int, steps: int, max_seq: int, kv: str) -> dict:
     """Product path on one GPU: `dllama inference --synthetic llama3_1_8b` with greedy sampling
     (per forward: H2D inputs, graph replay, D2H token, host sync), parsed from the reference's
     Evaluation / Prediction summary lines (src/dllama.cpp:98-113)."""
@@ -70,7 +73,7 @@ def _cli_point(local: int, prompt_tokens: int, steps: int, max_seq: int) -> dict
         prompt = ("The quick brown fox jumps over the lazy dog " * 8)[:prompt_tokens]
         cmd = [exe, "inference", "--synthetic", "llama3_1_8b", "--tokenizer", tok, "--prompt", prompt, "--steps",
                str(prompt_tokens + steps), "--temperature", "0", "--gpu-index", str(local), "--max-seq-len",
-               str(max_seq), "--buffer-float-type", "q80", "--log-level", "0"]
+               str(max_seq), "--buffer-float-type", "q80", "--kv-dtype", kv, "--log-level", "0"]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
         except subprocess.TimeoutExpired:
@@ -156,7 +159,10 @@ def main() -> int:
     ap.add_argument("--long-ctx", type=int, default=4096, help="position of the long-context decode point (0: off)")
     ap.add_argument("--no-cli", action="store_true", help="skip the dllama CLI product-path point (1 GPU)")
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--no-f32kv", action="store_true", help="skip the f32 KV-cache decode point")
+    ap.add_argument("--kv", default="f32", choices=["f32", "bf16"],
+                    help="KV-cache dtype of the headline and the extra points (f32: the reference's)")
+    ap.add_argument("--no-altkv", action="store_true",
+                    help="skip the eval + pred point with the other KV-cache dtype (bf16 next to an f32 headline)")
     ap.add_argument("--no-prefill4k", action="store_true", help="skip the 4096-token prompt-eval point")
     ap.add_argument("--tp-rank-compute", default="2,4,8",
                     help="1 GPU: TP degrees whose rank-0 shard is timed with the exchange removed "
@@ -213,7 +219,11 @@ def main() -> int:
         from distributed_llama_multiusers_amd.models.synthetic import LLAMA_SHAPES
         shape = dict(LLAMA31_8B, **LLAMA_SHAPES[args.shape])
 
-    def make_engine(max_seq=seq_len, kv_bf16=True, sync=None):
+    kv_bf16_main = args.kv == "bf16"
+
+    def make_engine(max_seq=seq_len, kv_bf16=None, sync=None):
+        if kv_bf16 is None:
+            kv_bf16 = kv_bf16_main
         synthetic = None if args.model else dict(shape, seq_len=max_seq)
         e = C.HipEngine(args.model, "q80", max_seq_len=max_seq, max_batch=max_batch, n_slots=args.batch,
                         kv_bf16=kv_bf16,
@@ -261,37 +271,41 @@ def main() -> int:
             uid = obj[0]
             eng = make_engine()
 
-    # eval: prefill the prompt (chunks of 32 rows per forward, like the reference nBatches=32);
-    # two untimed chunks first (the engine runs a row count eagerly on first use and captures its
-    # graph on the second) so the timed chunks replay the batch-32 graph
-    if len(prompt) >= 32:
-        for _ in range(2):
-            for b in range(B):
-                eng.forward_argmax(prompt[:32], list(range(32)), [b] * 32)
-    torch.cuda.synchronize()
-    barrier()
-    te = time.perf_counter()
-    for s in range(0, len(prompt), 32):
-        chunk = prompt[s:s + 32]
-        for b in range(B):
-            eng.forward_argmax(chunk, list(range(s, s + len(chunk))), [b] * len(chunk))
-    torch.cuda.synchronize()
-    eval_s = time.perf_counter() - te
-    barrier()
-
     pos0 = len(prompt)
     tokens = [prompt[-1]] * B
-    if args.warmup > 0:
-        eng.decode_greedy(args.warmup, tokens, [pos0] * B, list(range(B)))
-    pos1 = pos0 + args.warmup
 
-    barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    dev_ms, out = eng.decode_greedy(args.steps, tokens, [pos1] * B, list(range(B)))
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t_start
-    barrier()
+    def eval_pred(e, steps, warmup):
+        """eval: prefill the prompt (chunks of 32 rows per forward, like the reference nBatches=32);
+        two untimed chunks first (the engine runs a row count eagerly on first use and captures its
+        graph on the second) so the timed chunks replay the batch-32 graph. pred: `warmup` untimed
+        decode steps, then `steps` timed ones between barrier + device syncs."""
+        if len(prompt) >= 32:
+            for _ in range(2):
+                for b in range(B):
+                    e.forward_argmax(prompt[:32], list(range(32)), [b] * 32)
+        torch.cuda.synchronize()
+        barrier()
+        te = time.perf_counter()
+        for s in range(0, len(prompt), 32):
+            chunk = prompt[s:s + 32]
+            for b in range(B):
+                e.forward_argmax(chunk, list(range(s, s + len(chunk))), [b] * len(chunk))
+        torch.cuda.synchronize()
+        ev_s = time.perf_counter() - te
+        barrier()
+        if warmup > 0:
+            e.decode_greedy(warmup, tokens, [pos0] * B, list(range(B)))
+        p1 = pos0 + warmup
+        barrier()
+        torch.cuda.synchronize()
+        t_start = time.perf_counter()
+        dms, _ = e.decode_greedy(steps, tokens, [p1] * B, list(range(B)))
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t_start
+        barrier()
+        return ev_s, el, dms
+
+    eval_s, elapsed, dev_ms = eval_pred(eng, args.steps, args.warmup)
     tp_fused = bool(eng.tp_fused) if world > 1 else None  # after the first forward's self-test
 
     long_ms = None
@@ -320,18 +334,13 @@ def main() -> int:
         cap_ms = (time.perf_counter() - tc) * 1000.0 / 32
         barrier()
 
-    f32kv_ms = None
-    if not args.no_f32kv:  # the reference keeps its KV cache in f32: same decode with an f32 cache
+    alt_eval_s = alt_pred_s = None
+    alt_kv = "bf16" if args.kv == "f32" else "f32"
+    alt_steps = max(16, min(args.steps, 64))
+    if not args.no_altkv:  # the same eval + pred with the other KV-cache dtype (never the `value`)
         del eng
-        eng = make_engine(kv_bf16=False)
-        eng.decode_greedy(4, tokens, [pos0] * B, list(range(B)))
-        barrier()
-        torch.cuda.synchronize()
-        tf = time.perf_counter()
-        eng.decode_greedy(16, tokens, [pos0 + 4] * B, list(range(B)))
-        torch.cuda.synchronize()
-        f32kv_ms = (time.perf_counter() - tf) * 1000.0 / 16
-        barrier()
+        eng = make_engine(kv_bf16=not kv_bf16_main)
+        alt_eval_s, alt_pred_s, _ = eval_pred(eng, alt_steps, 4)
 
     tpf32_ms = None
     if world > 1 and args.sync_type != "f32":  # the exact f32 exchange next to the Q80 wire format
@@ -372,19 +381,20 @@ def main() -> int:
             del eng
             sl = max(seq_len, 4096 + 8)
             eng = C.HipEngine(args.model, "q80", max_seq_len=sl, max_batch=args.prefill_chunk, n_slots=1,
-                              kv_bf16=True, gpu_index=local, use_graphs=not args.no_graphs,
+                              kv_bf16=kv_bf16_main, gpu_index=local, use_graphs=not args.no_graphs,
                               synthetic=None if args.model else dict(shape, seq_len=sl), seed=1234, rank=rank,
                               world=world, uid=uid, comm=comm, sync_type=args.sync_type)
             barrier()
             p4k_big_ms = prefill(eng, args.prefill_chunk)
 
     if dist is not None:
-        t = torch.tensor([elapsed, eval_s, long_ms or 0.0, f32kv_ms or 0.0, p4k_ms or 0.0, tpf32_ms or 0.0,
-                          p4k_big_ms or 0.0, cap_ms or 0.0], dtype=torch.float64)
+        t = torch.tensor([elapsed, eval_s, long_ms or 0.0, alt_pred_s or 0.0, p4k_ms or 0.0, tpf32_ms or 0.0,
+                          p4k_big_ms or 0.0, cap_ms or 0.0, alt_eval_s or 0.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, eval_s = float(t[0]), float(t[1])
         long_ms = float(t[2]) if long_ms is not None else None
-        f32kv_ms = float(t[3]) if f32kv_ms is not None else None
+        alt_pred_s = float(t[3]) if alt_pred_s is not None else None
+        alt_eval_s = float(t[8]) if alt_eval_s is not None else None
         p4k_ms = float(t[4]) if p4k_ms is not None else None
         tpf32_ms = float(t[5]) if tpf32_ms is not None else None
         p4k_big_ms = float(t[6]) if p4k_big_ms is not None else None
@@ -395,6 +405,13 @@ def main() -> int:
     eval_ms_tok = eval_s * 1000.0 / max(1, len(prompt)) / B
     avg_ms_tok = (eval_ms_tok + pred_ms_tok) / 2 if prompt else pred_ms_tok
     tok_s = 1000.0 / avg_ms_tok
+    alt = {}
+    if alt_pred_s is not None:
+        a_eval = alt_eval_s * 1000.0 / max(1, len(prompt)) / B
+        a_pred = alt_pred_s * 1000.0 / alt_steps / B
+        a_avg = (a_eval + a_pred) / 2 if prompt else a_pred
+        alt = {f"{alt_kv}_kv_value": round(1000.0 / a_avg, 3), f"{alt_kv}_kv_eval_ms_per_token": round(a_eval, 4),
+               f"{alt_kv}_kv_pred_ms_per_token": round(a_pred, 4)}
     # the published baselines are per model family: 7B/8B at 1/2/4/8 devices, 70B at 8 devices
     base = (BASELINE_MS.get(world) if args.shape == "llama3_1_8b" and not args.model
             else BASELINE_MS_70B.get(world) if args.shape == "llama3_3_70b" and not args.model else None)
@@ -406,7 +423,7 @@ def main() -> int:
     if world == 1 and args.tp_rank_compute and not args.model:
         del eng
         for n in [int(v) for v in args.tp_rank_compute.split(",") if v]:
-            e = C.HipEngine("", "q80", max_seq_len=seq_len, max_batch=max_batch, n_slots=B, kv_bf16=True,
+            e = C.HipEngine("", "q80", max_seq_len=seq_len, max_batch=max_batch, n_slots=B, kv_bf16=kv_bf16_main,
                             gpu_index=local, use_graphs=not args.no_graphs, synthetic=dict(shape, seq_len=seq_len),
                             seed=1234, rank=0, world=n, comm=C.ComputeOnlyComm(0, n, local),
                             sync_type=args.sync_type)
@@ -430,7 +447,7 @@ def main() -> int:
     cli = {}
     if world == 1 and not args.no_cli and args.shape == "llama3_1_8b" and not args.model:
         eng = None
-        cli = _cli_point(local, min(args.prompt, 64), min(args.steps, 64), seq_len)
+        cli = _cli_point(local, min(args.prompt, 64), min(args.steps, 64), seq_len, args.kv)
     result = {
         "metric": METRIC,
         "value": round(tok_s, 3),
@@ -442,7 +459,7 @@ def main() -> int:
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": round(tok_s / (1000.0 / base), 2) if base else None,
-        "dtype": "q40-weights/q80-activations (f32 accumulate)",
+        "dtype": f"q40-weights/q80-activations/{args.kv}-kv-cache (f32 accumulate)",
         "data": (f"synthetic: random-init {args.shape} weights on device, synthetic prompt" if not args.model
                  else "model file weights, synthetic prompt"),
         "config": {
@@ -452,7 +469,7 @@ def main() -> int:
             "seq_len": seq_len,
             "prompt_tokens": args.prompt,
             "parallelism": f"tp{world}",
-            "kv_cache": "bf16",
+            "kv_cache": args.kv,
             "value_formula": "B*1000/((eval_ms_per_token+pred_ms_per_token)/2)",
             "eval_ms_per_token": round(eval_ms_tok, 4),
             "pred_ms_per_token": round(pred_ms_tok, 4),
@@ -461,7 +478,7 @@ def main() -> int:
             "long_ctx_pos": long_pos or None,
             "long_ctx_pred_ms_per_token": round(long_ms / B, 4) if long_ms is not None else None,
             "cap131072_pred_ms_per_token": round(cap_ms / B, 4) if cap_ms is not None else None,
-            "f32_kv_pred_ms_per_token": round(f32kv_ms / B, 4) if f32kv_ms is not None else None,
+            **alt,
             "prompt_4k_eval_ms_per_token": round(p4k_ms, 4) if p4k_ms is not None else None,
             "prompt_4k_chunk": args.prefill_chunk if p4k_big_ms is not None else None,
             "prompt_4k_eval_big_chunk_ms_per_token": round(p4k_big_ms, 4) if p4k_big_ms is not None else None,

@@ -8,6 +8,13 @@
 namespace dl {
 namespace hipk {
 
+#ifndef DL_ATTN_TU_F32_BLOCK
+#define DL_ATTN_TU_F32_BLOCK 7
+#endif
+#ifndef DL_ATTN_TU_BF16_BLOCK
+#define DL_ATTN_TU_BF16_BLOCK 8
+#endif
+
 template <int DPL, bool BF16>
 __device__ __forceinline__ void loadKv(const void *base, size_t off, float (&v)[DPL]) {
     if constexpr (BF16) {
@@ -201,7 +208,12 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
                                          const BlockSync *bs = nullptr, unsigned long long *trace = nullptr) {
     constexpr int NW = AT / 64, NG = AT / 16;
     constexpr int DPL = HS / 16;           // dims per lane: 16 lanes cover one position's head vector
-    constexpr int TU = BF16 ? 8 : 4;       // keys per group loaded before any is consumed
+    // keys per group loaded before any is consumed. The fused block (SYNC) issues its first round
+    // before waiting for the qkv workgroups: 7 keys per group there for f32 caches (112 keys per
+    // round instead of 64: f32-KV decode 1.322 -> 1.291 ms/token, same box; 8 keys took the block
+    // kernel to 178 VGPRs, 2 waves per SIMD, and off co-residency), bf16 stays at 8 (12 measured
+    // 1.357 vs 1.289 ms/token): profiles/r6_decode.md
+    constexpr int TU = BF16 ? (SYNC ? DL_ATTN_TU_BF16_BLOCK : 8) : (SYNC ? DL_ATTN_TU_F32_BLOCK : 4);
     constexpr int RW = BF16 ? DPL / 2 : DPL;  // 32-bit words per lane per key (packed bf16 pairs)
     const int pos = a.pos[b], sl = a.slot[b];
     const int len = pos + 1;
@@ -309,7 +321,7 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
         for (int i = 0; i < DPL; i++) o[h][i] = 0.f;
     }
     // each 16-lane group walks keys g16, g16+NG, ... with a running softmax; TU keys per group are
-    // in flight at once (NG*TU = 256 keys per memory round trip for bf16 caches)
+    // in flight at once (NG*TU keys per memory round trip)
     for (; tb < t1; tb += TU * NG) {
         loadRound(tb, prefetched ? 2 : 0);
         prefetched = false;

@@ -55,6 +55,11 @@ HipEngineImpl::HipEngineImpl(const EngineConfig &cfg, DeviceComm *comm) : cfg_(c
     {  // path knobs, read once: a captured graph replays the path it was captured with
         const char *e = std::getenv("DL_GEMM_MIN");
         gemmMin_ = e && *e ? std::atoi(e) : (plan_.nRanks > 1 ? 5 : 3);
+        // batch-invariant serving: every row of every forward takes the narrow MFMA GEMMs (fixed
+        // splits, no 16-lane / wide variants) and the VALU decode attention, so a row's math does
+        // not depend on how many rows share its forward (EngineConfig::batchInvariant)
+        invariant_ = cfg.batchInvariant;
+        if (invariant_) gemmMin_ = 1;
         const char *f = std::getenv("DL_GEMM_FUSE_NORM");
         fuseNormEnv_ = !(f && *f == '0');
     }
@@ -194,7 +199,7 @@ void HipEngineImpl::chainLaunch(int token, int pos, int slot) {
     } else {  // dTok_ / dPos_ hold the previous step's id and position + 1 (written on the device)
         DL_CHECK(chainHead_ > 0, "chainLaunch: no chain started");
         mapPages(1, &pos, &chainSlot_, 0);
-        attnLong_ = pos >= kAttnMfmaMinPos;
+        attnLong_ = !invariant_ && pos >= kAttnMfmaMinPos;
         bucket_ = (int)(&bucketFor(pos) - buckets_.data());
     }
     runGraph(1, GraphKind::CHAIN);

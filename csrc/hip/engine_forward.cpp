@@ -55,7 +55,7 @@ void HipEngineImpl::setInputs(int n, const int *tokens, const int *positions, co
     // ahead up to batch 8: profiles/r5_batched_attention.md), else the VALU kernel
     int maxPos = 0;
     for (int b = 0; b < n; b++) maxPos = std::max(maxPos, positions[b] + ahead);
-    attnLong_ = maxPos >= kAttnMfmaMinPos || n >= kAttnMfmaMinRows;
+    attnLong_ = !invariant_ && (maxPos >= kAttnMfmaMinPos || n >= kAttnMfmaMinRows);
     bucket_ = (int)(&bucketFor(maxPos) - buckets_.data());
     const u32 MB = cfg_.maxBatch;
     // keep the pinned staging buffer stable while a previous copy may still read it (every
@@ -66,7 +66,7 @@ void HipEngineImpl::setInputs(int n, const int *tokens, const int *positions, co
     std::memcpy(hIn_ + 2 * MB, slots, n * sizeof(int));
     size_t words = 2 * (size_t)MB + n;
     // prefill attention on MFMA: every block of rows it assigns to one workgroup is one slot
-    prefillOk_ = kvBf16_ && hipk::attnPrefillSupported(plan_.headSize, plan_.kvMul, true);
+    prefillOk_ = !invariant_ && kvBf16_ && hipk::attnPrefillSupported(plan_.headSize, plan_.kvMul, true);
     const int rpb = prefillOk_ ? hipk::attnPrefillRowsPerBlock(plan_.kvMul) : 1;
     for (int b = 0; prefillOk_ && b < n; b++) prefillOk_ = slots[b] == slots[b - b % rpb];
     if (specs) {
@@ -290,7 +290,7 @@ bool HipEngineImpl::tpBatchedOk(int n) const {
         const char *e = std::getenv("DL_TP_BATCHED");
         return !(e && *e == '0');
     }();
-    return on && tpFused_ && q40_ && !hipk::gemmUsesWide(n) &&
+    return on && !invariant_ && tpFused_ && q40_ && !hipk::gemmUsesWide(n) &&
            (size_t)n * h_.dim <= (size_t)tpVec_.stride && hipk::gemmTpxFits(n, plan_.nRanks, tpVec_.q80 != 0);
 }
 
@@ -299,7 +299,8 @@ void HipEngineImpl::gemmBatched(const DevMat &m, int n, int epi, const float *in
                  const DevLayer *L, const ResFuse *rf, bool ssIn) {
     // tokens per launch: the wide Q40 kernel takes the whole forward in one launch (one weight
     // pass per token tile, all tiles of a row tile on one XCD), the narrow one <= 128
-    const int chunk = q40_ ? (hipk::gemmUsesWide(n) ? n : kGemmMaxTokens) : hipk::kGemmF32MaxTokens;
+    // (batch-invariant engines: narrow launches only, the split count of a 16-token launch for all)
+    const int chunk = q40_ ? (hipk::gemmUsesWide(n) && !invariant_ ? n : kGemmMaxTokens) : hipk::kGemmF32MaxTokens;
     for (int c0 = 0; c0 < n; c0 += chunk) {
         const int bc = std::min(chunk, n - c0);
         hipk::GemmArgs g;
@@ -361,7 +362,8 @@ void HipEngineImpl::gemmBatched(const DevMat &m, int n, int epi, const float *in
             g.ldSS = (int)cfg_.maxBatch;
         }
         g.M = bc;
-        g.splits = hipk::gemmSplits(m.rows, m.n, bc, q40_ ? m.lanes : 0);
+        g.splits = invariant_ ? hipk::gemmSplits(m.rows, m.n, 16, 0) : hipk::gemmSplits(m.rows, m.n, bc, q40_ ? m.lanes : 0);
+        g.fixed = invariant_ ? 1 : 0;
         g.part = dPart_;
         g.counters = dGemmCnt_;
         if (q40_)

@@ -245,6 +245,7 @@ class HipEngineImpl : public HipEngine {
     int decodeRows_ = 1;       // EngineConfig::maxDecode (<= maxBatch): greedy-chain rows, fused argmax rows
     int attRows_ = 1;          // rows per attention launch (the split partials hold this many rows)
     bool fuseNormEnv_ = true;  // DL_GEMM_FUSE_NORM
+    bool invariant_ = false;   // EngineConfig::batchInvariant
     std::vector<void *> allocs_, hostAllocs_;
     size_t deviceBytes_ = 0;
     LoadStats load_;

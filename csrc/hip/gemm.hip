@@ -426,7 +426,7 @@ bool gemmTpxFits(int M, int world, bool q80) {
 }
 
 void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
-    if (gemmUsesWide(ga.M)) {
+    if (gemmUsesWide(ga.M) && !ga.fixed) {
         launchGemmWide(ga, epi, s);
         return;
     }
@@ -436,7 +436,7 @@ void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
     const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
     const int MT = gemmTokenPad(ga.M) / 16;
     const dim3 grid(tiles, ga.splits);
-    if (gemmL16Eligible(ga.e.n, ga.M, ga.e.lanes) && (ga.e.n / 32 / kG16Ch) % ga.splits == 0) {
+    if (!ga.fixed && gemmL16Eligible(ga.e.n, ga.M, ga.e.lanes) && (ga.e.n / 32 / kG16Ch) % ga.splits == 0) {
         const size_t lds = 2 * (size_t)gemm16StageBytes(MT) + 16 + kGemmScaleFloats * 4;
 #define DL_G16_CASE(M_, E)                                                                         \
     if (MT == M_ && epi == E) {                                                                    \
@@ -452,7 +452,7 @@ void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
 #undef DL_G16_CASE
     }
     const int stg = MT == 8 ? 1 : MT == 4 ? gemmStages4() : MT == 2 ? gemmStages2() : gemmStages1();
-    const int RT = MT == 8 ? 1 : gemmRowTiles(ga.M);
+    const int RT = MT == 8 || ga.fixed ? 1 : gemmRowTiles(ga.M);
     const size_t lds = gemmLds(MT, stg, RT);
     const dim3 gridRt((ga.e.rows + kGemmRows * RT - 1) / (kGemmRows * RT), ga.splits);
 #define DL_GEMM_CASE(M_, E, G, R)                                                                     \

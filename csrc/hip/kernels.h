@@ -218,6 +218,9 @@ struct GemmArgs {
     // tensor parallel (narrow kernel, wo / w2): the final tile [M][64 rows] is all-reduced over the
     // ranks in the epilogue (e.tp: f32 or Q80 blocks, summed in rank order) before EPI_RES / STORE
     int tpx = 0;
+    // batch-invariant launch: the narrow gemmQ40Kernel whatever M (no wide or 16-lane variant), so
+    // a token row's reduction order does not depend on the launch's token count (splits: the caller's)
+    int fixed = 0;
 };
 void launchGemmQ40(const GemmArgs &a, int epi, hipStream_t s);
 // Same contract for F32 weights (`e.wf` [rows][n] row-major; EPI_ACT_Q80 not supported).

@@ -243,7 +243,7 @@ std::string encodeWorkerConfig(const WorkerConfig &c) {
       << "\nmax_batch=" << e.maxBatch << "\nmax_decode=" << e.maxDecode << "\nn_slots=" << e.nSlots << "\nbuffer=" << (int)e.bufferType
       << "\nsync=" << (int)e.syncType
       << "\ngraphs=" << (e.useGraphs ? 1 : 0) << "\nkv_bf16=" << (e.kvBf16 ? 1 : 0) << "\nkv_pages=" << e.kvPages
-      << "\nkv_page_size=" << e.kvPageSize
+      << "\nkv_page_size=" << e.kvPageSize << "\nbatch_invariant=" << (e.batchInvariant ? 1 : 0)
       << "\nsynthetic=" << (e.synthetic ? 1 : 0) << "\nseed=" << e.seed << "\nh_dim=" << h.dim
       << "\nh_hidden=" << h.hiddenDim << "\nh_layers=" << h.nLayers << "\nh_heads=" << h.nHeads
       << "\nh_kv=" << h.nKvHeads << "\nh_vocab=" << h.vocabSize << "\nh_seq=" << h.seqLen
@@ -282,6 +282,7 @@ WorkerConfig decodeWorkerConfig(const std::string &s) {
         else if (k == "kv_bf16") e.kvBf16 = v == "1";
         else if (k == "kv_pages") e.kvPages = std::stoul(v);
         else if (k == "kv_page_size") e.kvPageSize = std::stoul(v);
+        else if (k == "batch_invariant") e.batchInvariant = v == "1";
         else if (k == "synthetic") e.synthetic = v == "1";
         else if (k == "seed") e.seed = std::stoull(v);
         else if (k == "h_dim") h.dim = std::stoul(v);

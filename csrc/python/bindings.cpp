@@ -824,12 +824,13 @@ PYBIND11_MODULE(_C, m) {
         .def(py::init([](const std::string &model, const std::string &bufferType, u32 maxSeqLen, u32 maxBatch,
                          u32 nSlots, int gpuIndex, bool useGraphs, bool kvBf16, py::object synthetic, u64 seed,
                          int rank, int world, py::object uid, py::object comm, const std::string &syncType,
-                         u32 kvPages, u32 kvPageSize) {
+                         u32 kvPages, u32 kvPageSize, bool batchInvariant) {
                  EngineConfig c = makeConfig(model, bufferType, 1, maxSeqLen, maxBatch, nSlots, gpuIndex, useGraphs,
                                              kvBf16, synthetic, seed);
                  c.syncType = parseFloatType(syncType);
                  c.kvPages = kvPages;
                  c.kvPageSize = kvPageSize;
+                 c.batchInvariant = batchInvariant;
                  auto *e = new PyHipEngine();
                  if (!comm.is_none()) e->comm = comm.cast<PyComm &>().comm;
                  py::gil_scoped_release rel;
@@ -850,7 +851,8 @@ PYBIND11_MODULE(_C, m) {
              py::arg("max_batch") = 32, py::arg("n_slots") = 1, py::arg("gpu_index") = 0, py::arg("use_graphs") = true,
              py::arg("kv_bf16") = true, py::arg("synthetic") = py::none(), py::arg("seed") = 1234, py::arg("rank") = 0,
              py::arg("world") = 1, py::arg("uid") = py::none(), py::arg("comm") = py::none(),
-             py::arg("sync_type") = "f32", py::arg("kv_pages") = 0, py::arg("kv_page_size") = 256)
+             py::arg("sync_type") = "f32", py::arg("kv_pages") = 0, py::arg("kv_page_size") = 256,
+             py::arg("batch_invariant") = false)
         .def_property_readonly("header", [](const PyHipEngine &e) { return headerToDict(e.engine->header()); })
         .def_property_readonly("device_bytes", [](const PyHipEngine &e) { return e.engine->deviceBytes(); })
         .def_property_readonly("tp_fused", [](const PyHipEngine &e) { return e.engine->tpFused(); })

@@ -70,6 +70,7 @@ AppArgs AppArgs::parse(int argc, char **argv, bool requireMode) {
             else throw Error("Invalid --kv-dtype (bf16|f32): " + v);
         } else if (name == "--kv-pages") a.kvPages = std::atoi(value);
         else if (name == "--kv-page-size") a.kvPageSize = std::atoi(value);
+        else if (name == "--batch-invariant") a.batchInvariant = std::atoi(value) != 0;
         else if (name == "--graph") a.graphs = std::atoi(value) != 0;
         else if (name == "--log-level") a.logLevel = std::atoi(value);
         else if (name == "--synthetic") a.synthetic = value;
@@ -131,6 +132,7 @@ static EngineConfig engineConfigFrom(const AppArgs &a, int nSlots) {
     c.kvBf16 = a.kvBf16;
     c.kvPages = (u32)std::max(0, a.kvPages);
     c.kvPageSize = (u32)std::max(32, a.kvPageSize);
+    c.batchInvariant = a.batchInvariant;
     if (!a.synthetic.empty()) {
         c.synthetic = true;
         c.syntheticHeader = syntheticHeader(a.synthetic, a.maxSeqLen);

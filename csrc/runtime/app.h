@@ -41,8 +41,9 @@ struct AppArgs {
     int gpuIndex = -1;
     int gpuSegmentFrom = -1, gpuSegmentTo = -1;  // accepted for CLI compatibility (no effect)
     int slots = 0;                               // KV slots (0 = 1 for CLI modes, 8 for the API)
-    bool kvBf16 = true;
+    bool kvBf16 = false;  // --kv-dtype: f32 by default (the reference's KV precision, llm.cpp:197-198)
     int kvPages = 0;       // --kv-pages: paged KV pool pages per layer (0 = contiguous per slot)
+    bool batchInvariant = false;  // --batch-invariant 1: rows take the same kernels whatever the batch
     int kvPageSize = 256;  // --kv-page-size: positions per page
     bool graphs = true;
     int logLevel = 1;

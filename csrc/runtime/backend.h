@@ -38,6 +38,9 @@ struct EngineConfig {
     bool synthetic = false;         // random-init weights of the header's shape (no file)
     ModelHeader syntheticHeader;    // used when synthetic
     u64 seed = 1234;                // synthetic weight seed
+    bool batchInvariant = false;    // GPU: every row takes the same kernels and reduction order
+                                    // whatever else shares its forward (reproducible serving: a
+                                    // request's tokens do not depend on who else is being served)
 };
 
 struct ForwardStats {

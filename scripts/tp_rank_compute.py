@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--sync-type", default="q80")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--kv", default="bf16", choices=["bf16", "f32"], help="KV-cache dtype")
     args = ap.parse_args()
     import torch
     import distributed_llama_multiusers_amd as dl
@@ -26,7 +27,7 @@ def main():
     C = dl.native()
     torch.cuda.set_device(0)
     shape = dict(LLAMA31_8B, **LLAMA_SHAPES[args.shape])
-    e = C.HipEngine("", "q80", max_seq_len=4096, max_batch=32, n_slots=1, kv_bf16=True, gpu_index=0,
+    e = C.HipEngine("", "q80", max_seq_len=4096, max_batch=32, n_slots=1, kv_bf16=args.kv == "bf16", gpu_index=0,
                     use_graphs=not args.no_graphs, synthetic=dict(shape, seq_len=4096), seed=1234, rank=args.rank,
                     **(dict(world=args.tp, comm=C.ComputeOnlyComm(args.rank, args.tp, 0)) if args.tp > 1 else {}),
                     sync_type=args.sync_type)
@@ -45,7 +46,7 @@ def main():
     e.decode_greedy(args.steps, [prompt[-1]], [72], [0])
     torch.cuda.synchronize()
     pred = (time.perf_counter() - t0) * 1000.0 / args.steps
-    print(f"tp{args.tp} rank {args.rank} ({args.shape}, {args.sync_type}): pred {pred:.4f} ms/token, "
+    print(f"tp{args.tp} rank {args.rank} ({args.shape}, {args.sync_type}, kv {args.kv}): pred {pred:.4f} ms/token, "
           f"eval {ev:.4f} ms/token, fused {bool(e.tp_fused)}, attn block {bool(e.attn_block)} "
           f"[{' '.join(k + '=' + v for k, v in os.environ.items() if k.startswith('DL_'))}]", flush=True)
 
