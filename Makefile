@@ -89,7 +89,11 @@ $(BUILD)/unit_tests: tests/cpp/unit_tests.cpp $(LIB) $(HDRS)
 test-cpp: $(BUILD)/unit_tests
 	$(BUILD)/unit_tests
 
+# ring GEMV / attention block instances compile without scratch (inline-asm ring registers are never spilled)
+check-isa:
+	python3 scripts/check_isa.py
+
 clean:
 	rm -rf $(BUILD) $(LIB) $(EXT)
 
-.PHONY: all lib clean test-cpp
+.PHONY: all lib clean test-cpp check-isa

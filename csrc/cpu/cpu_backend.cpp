@@ -8,10 +8,13 @@
 // Semantics follow the reference's CPU ops (src/nn/nn-cpu-ops.cpp): invRms/rmsNorm (105-166),
 // Q80xQ40 and F32 matmul (182-440), SiLU/GELU (445-491), RoPE over adjacent pairs (1090-1120),
 // KV append at `pos` (1253-1275) and multi-head attention with GQA (749-784). It is the test
-// oracle for the HIP engine and the `--nthreads` CPU path (BASELINE config #1). Differences
-// from the reference, all deliberate: partial sums are exchanged in f32 by default, which keeps
-// TP=N bit-compatible with TP=1 (`--sync-type q80` selects the reference's Q80 exchange,
-// llm.cpp:150); every row carries its own KV slot; GELU is honoured (Q6).
+// oracle for the HIP engine and the `--nthreads` CPU path (BASELINE config #1). Partial sums are
+// exchanged in the reference's wire format by default: with `--buffer-float-type q80` the
+// `--sync-type` is Q80 (every rank's partial quantized once to 32-value blocks, all ranks' blocks
+// dequantized and summed in rank order, llm.cpp:150); `--sync-type f32` exchanges exact f32
+// partials. Neither is bitwise TP=1: a rank-order sum of partials rounds differently from one
+// accumulation (the tests bound the difference). Deliberate differences from the reference:
+// every row carries its own KV slot; GELU is honoured (Q6).
 #include <immintrin.h>
 
 #include <algorithm>
@@ -385,6 +388,7 @@ class CpuBackend : public Backend {
         }
         syncMs += st.elapsedMs();
         stats_.syncMs = syncMs;
+        stats_.xchgMs = syncMs;  // the whole exchange step is timed (reference nn-executor.cpp:150-155)
         stats_.computeMs = timer.elapsedMs() - syncMs;
         comm_->stats(stats_.sentBytes, stats_.recvBytes);
     }

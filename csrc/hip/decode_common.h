@@ -384,7 +384,14 @@ __device__ __forceinline__ void tpPushCollect(const TpXchg &x, long long w, unsi
         if (p < W && p != me)
             __hip_atomic_store(x.recv[p] + (par * W + me) * x.stride + w, word, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint64_t *mine = x.recv[me] + par * W * x.stride + w;
+    // this rank's region picked with compile-time indices: a runtime index into the kernel
+    // argument's pointer array made the fused attention block copy its whole 1.2 KB argument
+    // struct to scratch at entry (the memcpy of a by-value kernel argument that SROA cannot undo)
+    const uint64_t *mine = nullptr;
+#pragma unroll
+    for (int p = 0; p < WM; p++)
+        if (p == me) mine = x.recv[p];
+    mine += par * W * x.stride + w;
     uint64_t got[WM];
 #pragma unroll
     for (int p = 0; p < WM; p++) got[p] = (p < W && p != me) ? tpLoad(mine + p * x.stride) : word;
@@ -473,6 +480,10 @@ __device__ __forceinline__ void blockArgmax(float &bv, int &bi, float *sv, int *
 // Thread 0 only.
 template <int WM>
 __device__ __forceinline__ void tpArgmaxPick(const TpXchg &x, int b, float &bv, int &bi) {
+    // compute-only rank (loopback): no peer offers anything, this shard's winner stands (peers read
+    // as zeros would otherwise offer value 0 at index 0 and win over a negative local maximum)
+    if (x.loopback) return;
+    const unsigned long long xs = x.span ? wall_clock64() : 0ull;
     unsigned waited = 0;
     const unsigned ev = x.epochs[2 * b] + 1, ei = x.epochs[2 * b + 1] + 1;  // one epoch per word
     unsigned vv[WM], vi[WM];
@@ -486,6 +497,8 @@ __device__ __forceinline__ void tpArgmaxPick(const TpXchg &x, int b, float &bv, 
     x.epochs[2 * b] = ev;
     x.epochs[2 * b + 1] = ei;
     tpWaitReportThread(x, waited);
+    if (x.span)
+        __hip_atomic_fetch_max(x.span, (unsigned)(wall_clock64() - xs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // LDS bytes of the Q80 exchange staging for nEl elements over W ranks.
@@ -504,55 +517,19 @@ __device__ __forceinline__ long long tpWordOf(const GemvArgs &a, int R, int rowB
     return q80 ? (el >> 5) * 9 + j % 9 : el;
 }
 
-// The epochs of this thread's first kTpPre exchange words, loaded when the workgroup starts (inline
-// asm: outside the compiler's wait accounting, so the GEMV ring keeps its own counted waits) and
-// consumed by the exchange after the main loop, instead of one dependent round trip there.
-static constexpr int kTpPre = 2;
-struct TpEpochs {
-    unsigned v[kTpPre];
-};
-template <int B>
-__device__ __forceinline__ TpEpochs tpPrefetchEpochs(const GemvArgs &a, int R, int rowBase) {
-    TpEpochs pe;
-    const bool q80 = a.tp.q80 != 0;
-    const int nw = q80 ? (B * R / 32) * 9 : B * R;
-#pragma unroll
-    for (int k = 0; k < kTpPre; k++) {
-        const int j = threadIdx.x + k * kThreads;
-        long long w = -1;
-        if (B == 1) {  // one row: no division by R ahead of the ring
-            if (q80) {  // tpExchangeQ80Row: lane w < 9 of the 32-lane group of block j / 32
-                const int blk = j >> 5, wd = j & 31, row = rowBase + blk * 32;
-                if (wd < 9 && blk < nw / 9 && row < a.rows) w = (long long)((rowBase >> 5) + blk) * 9 + wd;
-            } else if (j < nw && rowBase + j < a.rows) {
-                w = rowBase + j;
-            }
-        } else if (j < nw) {
-            w = tpWordOf(a, R, rowBase, j, q80);
-        }
-        const unsigned *p = a.tp.epochs + (w < 0 ? 0 : w);
-        asm volatile("global_load_dword %0, %1, off" : "=v"(pe.v[k]) : "v"(p));
-    }
-    return pe;
-}
-__device__ __forceinline__ unsigned tpEpochOf(const TpXchg &x, const TpEpochs &pe, int k, long long w) {
-    return k == 0 ? pe.v[0] : k == 1 ? pe.v[1] : x.epochs[w];
-}
-__device__ __forceinline__ void tpEpochsWait(TpEpochs &pe) {
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(pe.v[0]), "+v"(pe.v[1]));
-}
-
+// Exchange epochs are read with plain (compiler-visible) loads in the tail. An inline-asm prefetch
+// at kernel entry (round 5) saved nothing measurable and let the compiler copy the pending
+// registers before their s_waitcnt (an asm operand moved to other VGPRs: v_mov of a register whose
+// load was still in flight, ISA of gemvQ40Kernel<.., EPI_STORE_TP>), i.e. a stale-epoch hazard.
 template <int B, int WM>
-__device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *res, int R, int rowBase, TpEpochs pe) {
+__device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *res, int R, int rowBase) {
     const TpXchg &x = a.tp;
     unsigned waited = 0;
-    tpEpochsWait(pe);
-    int k = 0;
-    for (int i = threadIdx.x; i < B * R; i += kThreads, k++) {
+    for (int i = threadIdx.x; i < B * R; i += kThreads) {
         const int b = B == 1 ? 0 : i / R, row = rowBase + (B == 1 ? i : i % R);
         if (row >= a.rows) continue;
         const long long el = (long long)b * a.ldOut + row;
-        const unsigned e = tpEpochOf(x, pe, k, el) + 1;
+        const unsigned e = x.epochs[el] + 1;
         unsigned v[WM];
         tpPushCollect(x, el, e, __float_as_uint(res[i]), v, waited);
         float s = 0.f;
@@ -574,15 +551,12 @@ __device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *re
 // from those words by shuffles: no LDS staging and no barrier (the LDS form spent ~1.6 us per
 // workgroup tail, profiles/r5_tp_rank.md). Same rounding and rank order as tpExchangeQ80.
 template <int WM>
-__device__ __forceinline__ void tpExchangeQ80Row(const GemvArgs &a, const float *res, int R, int rowBase,
-                                                 TpEpochs pe) {
+__device__ __forceinline__ void tpExchangeQ80Row(const GemvArgs &a, const float *res, int R, int rowBase) {
     const TpXchg &x = a.tp;
     const int nBlk = R >> 5, W = x.world;
     unsigned waited = 0;
-    tpEpochsWait(pe);
     const int l = threadIdx.x & 31;
-    int k = 0;
-    for (int base = 0; base < nBlk * 32; base += kThreads, k++) {  // uniform per 32-lane group
+    for (int base = 0; base < nBlk * 32; base += kThreads) {  // uniform per 32-lane group
         const int i = base + threadIdx.x, blk = i >> 5, row = rowBase + i;
         const bool blkLive = blk < nBlk && rowBase + blk * 32 < a.rows;
         const float v = blk < nBlk ? res[i] : 0.f;
@@ -601,7 +575,7 @@ __device__ __forceinline__ void tpExchangeQ80Row(const GemvArgs &a, const float 
         for (int p = 0; p < WM; p++) vals[p] = 0u;
         if (blkLive && l < 9) {
             const long long wd = (long long)((rowBase >> 5) + blk) * 9 + l;
-            const unsigned e = (k < kTpPre ? pe.v[k] : x.epochs[wd]) + 1;
+            const unsigned e = x.epochs[wd] + 1;
             tpPushCollect<WM>(x, wd, e, payload, vals, waited);
             x.epochs[wd] = e;
         }
@@ -621,15 +595,13 @@ __device__ __forceinline__ void tpExchangeQ80Row(const GemvArgs &a, const float 
 }
 
 template <int B, int WM>
-__device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *res, int R, int rowBase, char *lds,
-                                              TpEpochs pe) {
+__device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *res, int R, int rowBase, char *lds) {
     const TpXchg &x = a.tp;
     const int nEl = B * R, nBlk = nEl >> 5, W = x.world;
     int8_t *q8 = reinterpret_cast<int8_t *>(lds);
     uint32_t *dq = reinterpret_cast<uint32_t *>(lds + alignUp((size_t)nEl, 16));
     uint32_t *rv = reinterpret_cast<uint32_t *>(lds + alignUp((size_t)nEl, 16) + alignUp((size_t)nBlk * 4, 16));
     unsigned waited = 0;
-    tpEpochsWait(pe);
     // 1. quantize this rank's partial (whole 32-lane groups per block: the loop is uniform)
     for (int base = 0; base < nEl; base += kThreads) {
         const int i = base + threadIdx.x;
@@ -651,14 +623,13 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
         return ((long long)b * a.ldOut + row) >> 5;
     };
     // 2. push / collect the 9 words of every block
-    int k = 0;
-    for (int j = threadIdx.x; j < nBlk * 9; j += kThreads, k++) {
+    for (int j = threadIdx.x; j < nBlk * 9; j += kThreads) {
         const int blk = j / 9, w = j % 9;
         bool live;
         const long long gb = blockId(blk, live);
         if (!live) continue;
         const long long wd = gb * 9 + w;
-        const unsigned e = tpEpochOf(x, pe, k, wd) + 1;
+        const unsigned e = x.epochs[wd] + 1;
         const unsigned payload = w < 8 ? reinterpret_cast<const uint32_t *>(q8)[blk * 8 + w] : dq[blk];
         unsigned v[WM];
         tpPushCollect(x, wd, e, payload, v, waited);

@@ -128,7 +128,7 @@ void HipEngineImpl::forward(int n, const int *tokens, const int *positions, cons
     inputsInFlight_ = false;
     if (root && logits) std::memcpy(logits, hLogits_, (size_t)n * h_.vocabSize * sizeof(float));
     stats_.computeMs = t.elapsedMs();
-    stats_.syncMs = std::min(readSyncMs(), stats_.computeMs);
+    setSyncStats(readSync(hSync_, false), stats_.computeMs);
 }
 
 void HipEngineImpl::forwardArgmax(int n, const int *tokens, const int *positions, const int *slots, int *out) {
@@ -140,7 +140,7 @@ void HipEngineImpl::forwardArgmax(int n, const int *tokens, const int *positions
     inputsInFlight_ = false;
     std::memcpy(out, hIds_, n * sizeof(int));
     stats_.computeMs = t.elapsedMs();
-    stats_.syncMs = std::min(readSyncMs(), stats_.computeMs);
+    setSyncStats(readSync(hSync_, false), stats_.computeMs);
 }
 
 void HipEngineImpl::forwardSample(int n, const int *tokens, const int *positions, const int *slots,
@@ -153,7 +153,7 @@ void HipEngineImpl::forwardSample(int n, const int *tokens, const int *positions
     inputsInFlight_ = false;
     std::memcpy(out, hIds_, n * sizeof(int));
     stats_.computeMs = t.elapsedMs();
-    stats_.syncMs = std::min(readSyncMs(), stats_.computeMs);
+    setSyncStats(readSync(hSync_, false), stats_.computeMs);
 }
 
 // Pipelined serving: the forward and the D2H copy of its ids are enqueued; the host returns at
@@ -176,7 +176,7 @@ void HipEngineImpl::collectIds(int *out) {
     syncAndCheckComm();
     inputsInFlight_ = false;
     std::memcpy(out, hIds_, n * sizeof(int));
-    stats_.syncMs = readSyncMs();
+    setSyncStats(readSync(hSync_, false), -1);
 }
 
 // Chained decode for the CLI: the CHAIN graph (forward -> argmax -> tokens := ids, pos += 1 on
@@ -202,8 +202,8 @@ void HipEngineImpl::chainLaunch(int token, int pos, int slot) {
         attnLong_ = !invariant_ && pos >= kAttnMfmaMinPos;
         bucket_ = (int)(&bucketFor(pos) - buckets_.data());
     }
-    runGraph(1, GraphKind::CHAIN);
     const int k = (int)(chainHead_ % kChainDepth);
+    runGraph(1, GraphKind::CHAIN, hSyncAt(1 + k));  // this step's own copy (steps in flight overlap)
     DL_HIP(hipMemcpyAsync(hChain_ + k, dIds_, sizeof(int), hipMemcpyDeviceToHost, stream_));
     enqueueErrorCopies();
     DL_HIP(hipEventRecord(chainEv_[k], stream_));
@@ -217,7 +217,7 @@ int HipEngineImpl::chainCollect() {
     chainTail_++;
     if (chainTail_ == chainHead_) inputsInFlight_ = false;
     checkErrorWords();
-    stats_.syncMs = readSyncMs();
+    setSyncStats(readSync(hSyncAt(1 + k), false), -1);
     return hChain_[k];
 }
 
@@ -239,9 +239,13 @@ double HipEngineImpl::decodeGreedyBatch(int steps, int nSeq, const int *tokens, 
     hipEvent_t e0, e1;
     DL_HIP(hipEventCreate(&e0));
     DL_HIP(hipEventCreate(&e1));
+    // measured sync of every step: the slots and running totals start at zero, each step's
+    // embedding folds the previous step's slots into the totals, one copy after the last step
+    if (plan_.nRanks > 1)
+        DL_HIP(hipMemsetAsync(dSync_, 0, hipk::syncFoldWords(syncSlots()) * sizeof(unsigned), stream_));
     // the chained graph: forward -> argmax -> (tokens := ids, pos += 1)
     DL_HIP(hipEventRecord(e0, stream_));
-    for (int s = 0; s < steps; s++) runGraph(nSeq, GraphKind::CHAIN);
+    for (int s = 0; s < steps; s++) runGraph(nSeq, GraphKind::CHAIN, s + 1 == steps ? hSync_ : nullptr);
     accountForward(nSeq, GraphKind::CHAIN, steps);
     DL_HIP(hipEventRecord(e1, stream_));
     DL_HIP(hipEventSynchronize(e1));
@@ -251,7 +255,7 @@ double HipEngineImpl::decodeGreedyBatch(int steps, int nSeq, const int *tokens, 
     (void)hipEventDestroy(e1);
     syncAndCheckComm();
     inputsInFlight_ = false;
-    stats_.syncMs = std::min(readSyncMs() * steps, (double)ms);  // the last step's exchanges x steps
+    setSyncStats(readSync(hSync_, true), ms);  // every step's exchanges, measured
     if (outTokens) {
         const int w = p1 - p0;
         std::vector<int> hist((size_t)nSeq * w);
@@ -355,21 +359,39 @@ void HipEngineImpl::accountForward(int n, GraphKind kind, int times) {
     stats_.recvBytes = recv * (u64)times;
 }
 
-// Measured sync of the last forward (the host copy of its slots, enqueued by runGraph): per
-// exchange the longest time a wave of the fused exchange waited for peers' words (tpWaitReport),
-// or the stamped span of a separate collective (launch gaps included), summed over the forward's
-// exchanges. The reference times its
-// sync steps the same way, per forward (nn-executor.cpp:150-155, printed per token dllama.cpp:57-64).
-double HipEngineImpl::readSyncMs() const {
-    if (plan_.nRanks <= 1 || !hSync_) return 0;
+// Measured sync of a forward (a host copy of its slots, enqueued by runGraph), summed over the
+// forward's exchanges and their launches: wait = per exchange launch the longest time a wave of the
+// fused exchange waited for peers' words (tpWaitReport); span = the longest exchange tail of a
+// workgroup (DL_SYNC_MEASURE=2); a separate collective counts its stamped span (launch gaps
+// included) in both. totals: plus the device running totals of every earlier folded forward (a
+// whole decode chain). The reference times its sync steps per forward (nn-executor.cpp:150-155,
+// printed per token dllama.cpp:57-64).
+HipEngineImpl::SyncRead HipEngineImpl::readSync(const unsigned *buf, bool totals) const {
+    SyncRead r;
+    if (plan_.nRanks <= 1 || !buf) return r;
     const int S = syncSlots();
-    const unsigned long long *st = reinterpret_cast<const unsigned long long *>(hSync_ + S);
-    double ticks = 0;
+    const unsigned long long *st = reinterpret_cast<const unsigned long long *>(buf + 2 * S);
+    const unsigned long long *acc = reinterpret_cast<const unsigned long long *>(buf + 6 * S);
+    double wait = 0, span = 0, stamp = 0;
     for (int i = 0; i < S; i++) {
-        ticks += hSync_[i];
-        if (st[2 * i] && st[2 * i + 1] > st[2 * i]) ticks += (double)(st[2 * i + 1] - st[2 * i]);
+        wait += buf[i];
+        span += buf[S + i];
+        if (st[2 * i] && st[2 * i + 1] > st[2 * i]) stamp += (double)(st[2 * i + 1] - st[2 * i]);
     }
-    return ticks * 1e-5;  // s_memrealtime: 100 MHz
+    if (totals) {
+        wait += (double)acc[0];
+        span += (double)acc[1];
+        stamp += (double)acc[2];
+    }
+    r.waitMs = (wait + stamp) * 1e-5;  // s_memrealtime: 100 MHz
+    if (syncLevel_ >= 2 || stamp > 0) r.spanMs = (span + stamp) * 1e-5;
+    return r;
+}
+
+// capMs >= 0: the forward's wall time bounds both (a wait cannot exceed the forward it is part of)
+void HipEngineImpl::setSyncStats(const SyncRead &r, double capMs) {
+    stats_.syncMs = capMs >= 0 ? std::min(r.waitMs, capMs) : r.waitMs;
+    stats_.xchgMs = r.spanMs < 0 ? -1 : (capMs >= 0 ? std::min(r.spanMs, capMs) : r.spanMs);
 }
 
 void HipEngineImpl::launchStampAt(unsigned long long *p) { hipk::launchStamp(p, stream_); }
@@ -452,12 +474,13 @@ void HipEngineImpl::tpFusedSelfTest() {
     setupAttnBlock();
 }
 
-void HipEngineImpl::runGraph(int n, GraphKind kind) {
+void HipEngineImpl::runGraph(int n, GraphKind kind, unsigned *syncDst) {
     if (!tpTested_) tpFusedSelfTest();
     accountForward(n, kind, 1);
     auto copySync = [&]() {  // the forward's measured-sync slots to the host (read after the sync)
-        if (plan_.nRanks > 1)
-            DL_HIP(hipMemcpyAsync(hSync_, dSync_, (size_t)syncSlots() * 5 * sizeof(unsigned), hipMemcpyDeviceToHost, stream_));
+        if (plan_.nRanks > 1 && syncDst)
+            DL_HIP(hipMemcpyAsync(syncDst, dSync_, hipk::syncFoldWords(syncSlots()) * sizeof(unsigned),
+                                  hipMemcpyDeviceToHost, stream_));
     };
     if (!cfg_.useGraphs || graphsBroken_) {
         enqueueForward(n, kind);

@@ -106,7 +106,8 @@ hipk::GemvArgs HipEngineImpl::gemvArgs(const DevMat &m, int c0, int bc, int epi,
     a.lanes = m.lanes;
     if (tp) {
         a.tp = tpVec_;
-        a.tp.ticks = syncTicks(xSlot_);
+        a.tp.ticks = syncTicks();
+        a.tp.span = syncSpan();
     }
     a.in = in ? in + (size_t)c0 * ldIn : nullptr;
     a.aq = aq ? aq + (size_t)c0 * m.n : nullptr;
@@ -145,7 +146,8 @@ void HipEngineImpl::gemv(const DevMat &m, int n, int pro, int epi, const float *
                          const float2 *as, int8_t *oq, float2 *os, bool tp) {
     if (tp) epi = hipk::EPI_STORE_TP;
     const int bcMax = batchChunk(m, pro, epi);
-    for (int c0 = 0; c0 < n;) {
+    xChunk_ = 0;  // each launch's exchange waits in a measured-sync slot of its own
+    for (int c0 = 0; c0 < n; xChunk_++) {
         int bc = n - c0;
         if (bc > bcMax) bc = bcMax;
         while (bc & (bc - 1)) bc &= bc - 1;  // 1, 2 or 4 rows per launch
@@ -153,6 +155,7 @@ void HipEngineImpl::gemv(const DevMat &m, int n, int pro, int epi, const float *
         hipk::launchGemv(a, bc, pro, epi, q40_, stream_);
         c0 += bc;
     }
+    xChunk_ = 0;
 }
 
 // Decode attention of this layer (rows 0..n of the forward).
@@ -303,6 +306,7 @@ void HipEngineImpl::gemmBatched(const DevMat &m, int n, int epi, const float *in
     const int chunk = q40_ ? (hipk::gemmUsesWide(n) && !invariant_ ? n : kGemmMaxTokens) : hipk::kGemmF32MaxTokens;
     for (int c0 = 0; c0 < n; c0 += chunk) {
         const int bc = std::min(chunk, n - c0);
+        xChunk_ = c0 / chunk;  // each launch's tile exchange waits in a measured-sync slot of its own
         hipk::GemmArgs g;
         hipk::GemvArgs &a = g.e;
         a.qs = m.qs;
@@ -351,7 +355,8 @@ void HipEngineImpl::gemmBatched(const DevMat &m, int n, int epi, const float *in
         if (rf && plan_.nRanks > 1) {  // the residual update needs the rank-summed tile
             g.tpx = 1;
             a.tp = tpVec_;
-            a.tp.ticks = syncTicks(xSlot_);
+            a.tp.ticks = syncTicks();
+            a.tp.span = syncSpan();
         }
         if (rf) {
             g.resIn = rf->resIn + (size_t)c0 * ldOut;
@@ -365,6 +370,7 @@ void HipEngineImpl::gemmBatched(const DevMat &m, int n, int epi, const float *in
         g.splits = invariant_ ? hipk::gemmSplits(m.rows, m.n, 16, 0) : hipk::gemmSplits(m.rows, m.n, bc, q40_ ? m.lanes : 0);
         g.fixed = invariant_ ? 1 : 0;
         g.part = dPart_;
+        g.partFloats = partFloats_;
         g.counters = dGemmCnt_;
         if (q40_)
             hipk::launchGemmQ40(g, epi, stream_);
@@ -401,7 +407,7 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
         ProfScope ps(this, "embedding");
         // the epoch counts the forwards that run the fused block (its counters' targets)
         hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_, blk ? dEpoch_ : nullptr,
-                              p.nRanks > 1 ? dSync_ : nullptr, p.nRanks > 1 ? syncSlots() * 5 : 0);
+                              p.nRanks > 1 ? dSync_ : nullptr, p.nRanks > 1 ? syncSlots() : 0);
     }
     // Q80 hand-off of h needs one workgroup per 32 hidden units; for skinny TP shards the w13
     // epilogue emits f32 and w2 quantizes in its prologue instead.
@@ -526,7 +532,8 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
             }
             if (p.nRanks > 1) {
                 a.tp = tpArg_;
-                a.tp.ticks = syncTicks(xSlot_);
+                a.tp.ticks = syncTicks();
+                a.tp.span = syncSpan();
             }
             hipk::launchGemv(a, 1, hipk::PRO_RESNORM, hipk::EPI_ARGMAX, true, stream_);
         } else
@@ -581,7 +588,8 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
             // fused winners exchange up to its region's rows (2 words per row), else one all-gather
             if (tpFused_ && (size_t)2 * n <= (size_t)tpArg_.stride) {
                 g.tp = tpArg_;
-                g.tp.ticks = syncTicks(xSlot_);
+                g.tp.ticks = syncTicks();
+                g.tp.span = syncSpan();
             } else {
                 g.pairs = dArgPairs_;
             }

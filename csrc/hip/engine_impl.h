@@ -103,28 +103,45 @@ class HipEngineImpl : public HipEngine {
     void enqueueErrorCopies();
     void checkErrorWords();
     int rank() const { return comm_ ? comm_->rank() : 0; }
-    void runGraph(int n, GraphKind kind);
+    // syncDst: host copy of the forward's measured-sync slots (null: none, e.g. inside a decode chain)
+    void runGraph(int n, GraphKind kind, unsigned *syncDst);
+    void runGraph(int n, GraphKind kind) { runGraph(n, kind, hSync_); }
     void accountForward(int n, GraphKind kind, int times);
-    // measured sync (ForwardStats::syncMs): one slot per exchange of a forward (layer l: wo 2l,
-    // w2 2l + 1; the logits / argmax exchange 2L): a u32 of fused-exchange ticks (max over the
-    // workgroups) and a pair of u64 stamps around a separate collective; cleared by the forward's
-    // embedding kernel, copied to the host after each forward
-    int syncSlots() const { return 2 * (int)h_.nLayers + 2; }
-    // DL_SYNC_MEASURE=0: the fused exchanges report no waiting time (comparison runs)
-    const bool syncMeasure_ = [] {
+    // measured sync (ForwardStats::syncMs / xchgMs): one slot per (exchange, launch) of a forward
+    // (exchange xSlot_: layer l's wo 2l, w2 2l + 1, the logits / argmax exchange 2L; launch xChunk_:
+    // the batch chunks of one GEMV / GEMM, each its own slot so their waits add up): a u32 of
+    // fused-exchange wait ticks (max over the waves), a u32 of exchange-tail ticks (max over the
+    // workgroups, DL_SYNC_MEASURE=2) and a pair of u64 stamps around a separate collective
+    // (hipk::syncFoldWords layout). Each forward's embedding kernel folds the previous forward's
+    // slots into device running totals and clears them; the host copies them after a forward
+    // (or one chain step) and reads the totals after a whole decode chain.
+    static constexpr int kSyncChunks = 4;
+    int syncSlots() const { return (2 * (int)h_.nLayers + 2) * kSyncChunks; }
+    // DL_SYNC_MEASURE: 0 off (comparison runs: no wait ticks, no stamp kernels), 1 (default) the
+    // longest peer wait per exchange, 2 also the longest exchange tail per exchange (the xchg span:
+    // a stamp pair and an atomic per workgroup tail, ~2.5 % of a TP8 rank's decode, r5_tp_rank.md)
+    const int syncLevel_ = [] {
         const char *e = std::getenv("DL_SYNC_MEASURE");
-        return !(e && *e == '0');
+        return e && *e ? std::max(0, std::min(2, std::atoi(e))) : 1;
     }();
-    unsigned *syncTicks(int slot) const { return syncMeasure_ ? dSync_ + slot : nullptr; }
-    unsigned long long *syncStamps(int slot) const {
-        return reinterpret_cast<unsigned long long *>(dSync_ + syncSlots()) + 2 * slot;
+    int xChunk_ = 0;  // launch index within the exchange being enqueued
+    int syncSlotNow() const { return xSlot_ * kSyncChunks + std::min(xChunk_, kSyncChunks - 1); }
+    unsigned *syncTicks() const { return syncLevel_ ? dSync_ + syncSlotNow() : nullptr; }
+    unsigned *syncSpan() const { return syncLevel_ >= 2 ? dSync_ + syncSlots() + syncSlotNow() : nullptr; }
+    unsigned long long *syncStamps() const {
+        return reinterpret_cast<unsigned long long *>(dSync_ + 2 * syncSlots()) + 2 * syncSlotNow();
     }
-    double readSyncMs() const;
+    struct SyncRead {
+        double waitMs = 0, spanMs = -1;  // spanMs < 0: not measured (DL_SYNC_MEASURE < 2, no collective)
+    };
+    // buf: a host copy of the slots; totals: add the running totals of the folded forwards
+    SyncRead readSync(const unsigned *buf, bool totals) const;
+    void setSyncStats(const SyncRead &r, double capMs);
     template <typename F>
-    void stamped(F &&collective) {  // a separate collective of slot xSlot_, bracketed by stamps
-        launchStampAt(syncStamps(xSlot_));
+    void stamped(F &&collective) {  // a separate collective, bracketed by stamps (when measured)
+        if (syncLevel_) launchStampAt(syncStamps());
         collective();
-        launchStampAt(syncStamps(xSlot_) + 1);
+        if (syncLevel_) launchStampAt(syncStamps() + 1);
     }
     void launchStampAt(unsigned long long *p);
     void tpFusedSelfTest();
@@ -288,6 +305,7 @@ class HipEngineImpl : public HipEngine {
     float2 *dAttS_ = nullptr, *dHS_ = nullptr;
     _Float16 *dXh_ = nullptr, *dAttH_ = nullptr, *dHh_ = nullptr;
     float *dPart_ = nullptr;
+    size_t partFloats_ = 0;
     int *dGemmCnt_ = nullptr;
     float *dSS_ = nullptr;
     float *dPartO_ = nullptr, *dPartML_ = nullptr;
@@ -295,7 +313,10 @@ class HipEngineImpl : public HipEngine {
     float *dArgV_ = nullptr;
     float *dArgPairs_ = nullptr, *dArgPairsAll_ = nullptr;  // separate-collective TP argmax
     hipk::SampleScratch sampleScratch_;
-    unsigned *dSync_ = nullptr, *hSync_ = nullptr;  // measured-sync slots (syncSlots) and their host copy
+    // measured-sync slots (syncSlots, hipk::syncFoldWords) and their host copies: [0] the last
+    // forward / chain, [1 + k] chain step k % kChainDepth (chainLaunch / chainCollect)
+    unsigned *dSync_ = nullptr, *hSync_ = nullptr;
+    unsigned *hSyncAt(int i) const { return hSync_ + (size_t)i * hipk::syncFoldWords(syncSlots()); }
     int xSlot_ = 0;                                  // slot of the exchange being enqueued
 
     // attention: context buckets (setupBuckets) and this forward's choices (setInputs, graph key)

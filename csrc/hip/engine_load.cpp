@@ -133,6 +133,7 @@ void HipEngineImpl::allocBuffers() {
         int cnt = 0;
         auto acc = [&](int rows, int n) {
             part = std::max(part, hipk::gemmPartFloats(rows, n, mt));
+            if (invariant_ && q40_) part = std::max(part, hipk::gemmPartFloatsFixed(rows, n));
             cnt = std::max(cnt, hipk::gemmCounterInts(rows, mt));
         };
         acc(p.q0 + 2 * p.kv0, h_.dim);
@@ -141,6 +142,7 @@ void HipEngineImpl::allocBuffers() {
         acc(h_.dim, p.hidden0);
         acc(p.vocab0, h_.dim);
         if (part) dPart_ = dalloc<float>(part);
+        partFloats_ = part;
         const int maxTiles = cnt;
         dGemmCnt_ = dalloc<int>(maxTiles);
         // fused residual + norm hand-off between batched GEMMs (TP1): per 64-row tile of dim,
@@ -150,12 +152,13 @@ void HipEngineImpl::allocBuffers() {
     }
     {  // fused attention block: epoch, monotonic counters, expected counts, timeout flag
         dEpoch_ = dalloc<unsigned>(4);
-        // measured-sync slots: syncSlots() u32 tick words + 2 u64 stamps per slot (cleared by the
-        // embedding kernel of every forward)
-        dSync_ = dalloc<unsigned>((size_t)syncSlots() * 5);
-        hSync_ = halloc<unsigned>((size_t)syncSlots() * 5);
-        DL_HIP(hipMemsetAsync(dSync_, 0, (size_t)syncSlots() * 5 * sizeof(unsigned), stream_));
-        std::memset(hSync_, 0, (size_t)syncSlots() * 5 * sizeof(unsigned));
+        // measured-sync slots (hipk::syncFoldWords: folded and cleared by the embedding kernel of
+        // every forward) and their host copies (the last forward + one per chain step in flight)
+        const size_t sw = hipk::syncFoldWords(syncSlots());
+        dSync_ = dalloc<unsigned>(sw);
+        hSync_ = halloc<unsigned>(sw * (1 + kChainDepth));
+        DL_HIP(hipMemsetAsync(dSync_, 0, sw * sizeof(unsigned), stream_));
+        std::memset(hSync_, 0, sw * (1 + kChainDepth) * sizeof(unsigned));
         dBlockCnt_ = dalloc<unsigned>(kBlockCntWords);
         dBlockExpect_ = dalloc<unsigned>(kMaxKvGroups);
         dBlockErr_ = dalloc<int>(4);

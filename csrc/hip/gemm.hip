@@ -112,6 +112,12 @@ size_t gemmPartFloats(int rows, int n, int maxTokens) {
     return best;
 }
 
+size_t gemmPartFloatsFixed(int rows, int n) {
+    // batch-invariant engines: narrow launches of up to 128 tokens with the 16-token split count
+    const int S = gemmSplits(rows, n, 16, 0), tiles = (rows + kGemmRows - 1) / kGemmRows;
+    return S > 1 ? (size_t)S * tiles * kGemmMaxTokens * kGemmRows : 0;
+}
+
 int gemmCounterInts(int rows, int maxTokens) {
     const int narrow = (rows + kGemmRows - 1) / kGemmRows;
     return std::max(narrow, gemmUsesWide(maxTokens) ? gemmWideCounters(rows, maxTokens) : 0);
@@ -431,6 +437,9 @@ void launchGemmQ40(const GemmArgs &ga, int epi, hipStream_t s) {
         return;
     }
     if (ga.M > kGemmMaxTokens) throw Error("launchGemmQ40: more than 128 tokens per narrow launch");
+    if (ga.splits > 1 && ga.partFloats &&
+        (size_t)ga.splits * ((ga.e.rows + kGemmRows - 1) / kGemmRows) * gemmTokenPad(ga.M) * kGemmRows > ga.partFloats)
+        throw Error("launchGemmQ40: split-K partials exceed the engine's buffer");
     if (ga.tpx && !gemmTpxFits(ga.M, ga.e.tp.world, ga.e.tp.q80 != 0))
         throw Error("launchGemmQ40: the tile exchange does not fit this launch's LDS");
     const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
@@ -531,6 +540,8 @@ __global__ __launch_bounds__(kThreads) void gemmF32Kernel(GemmArgs ga) {
 void launchGemmF32(const GemmArgs &ga, int epi, hipStream_t s) {
     const int tiles = (ga.e.rows + kGemmRows - 1) / kGemmRows;
     if (ga.M > kGemmF32MaxTokens) throw Error("launchGemmF32: more than 64 tokens per launch");
+    if (ga.splits > 1 && ga.partFloats && (size_t)ga.splits * tiles * gemmTokenPad(ga.M) * kGemmRows > ga.partFloats)
+        throw Error("launchGemmF32: split-K partials exceed the engine's buffer");
     const int MT = gemmTokenPad(ga.M) / 16;
     const dim3 grid(tiles, ga.splits);
     const size_t lds = (size_t)MT * 16 * kGemmRows * 4 + 16 + kGemmScaleFloats * 4;  // + flag, row scales

@@ -213,7 +213,9 @@ __device__ __forceinline__ void tpExchangeTile(const GemmArgs &ga, float *tile, 
 // slices in order (deterministic). slL: kThreads floats of scratch. Ends with a barrier.
 __device__ __forceinline__ void gemmRowScales(const GemmArgs &ga, int t0, int nt, float *rsL, float *slL) {
     const int tid = threadIdx.x;
-    const int TPT = nt <= 16 ? 16 : nt <= 32 ? 8 : nt <= 64 ? 4 : 2;
+    // threads per token summing its partials; a batch-invariant launch (ga.fixed) always uses 2, so
+    // the order of the sum does not depend on the launch's token count
+    const int TPT = ga.fixed ? 2 : nt <= 16 ? 16 : nt <= 32 ? 8 : nt <= 64 ? 4 : 2;
     const int t = tid / TPT, q = tid % TPT;
     float ssum = 0.f;
     if (t < nt && t0 + t < ga.M) {

@@ -147,8 +147,6 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
     // timestamps stay in SGPRs until the end: a store here would join the ring's vmcnt accounting
     const unsigned long long tEntry = a.trace ? wall_clock64() : 0ull;
     unsigned long long tReady = 0ull, tLoaded = 0ull, tFirst = 0ull, tWaited = 0ull;
-    TpEpochs pe{};  // exchange epochs, in flight while the ring streams (tpPrefetchEpochs)
-    if constexpr (tpx) pe = tpPrefetchEpochs<B>(a, R, rowBase);
 
     // slot = 2 rows x 16 B of nibbles + the pair's two f16 scales in one 32-bit word
     u32x4 w[D][RG];
@@ -494,12 +492,22 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
     }
     if constexpr (tpx) {  // all-reduce the partial rows over the TP ranks, then store (sq is free now)
         __syncthreads();
+        // exchange span (DL_SYNC_MEASURE=2, a.tp.span set): this workgroup's tail, first push to
+        // last summed store, raised into the exchange's slot (the longest tail of the launch)
+        const unsigned long long xs = a.tp.span ? wall_clock64() : 0ull;
         tpDispatch(a.tp.world, [&](auto wm) {
             constexpr int WM = decltype(wm)::value;
-            if (a.tp.q80 && B == 1) tpExchangeQ80Row<WM>(a, res, R, rowBase, pe);
-            else if (a.tp.q80) tpExchangeQ80<B, WM>(a, res, R, rowBase, reinterpret_cast<char *>(sq), pe);
-            else tpExchangeF32<B, WM>(a, res, R, rowBase, pe);
+            if (a.tp.q80 && B == 1) tpExchangeQ80Row<WM>(a, res, R, rowBase);
+            else if (a.tp.q80) tpExchangeQ80<B, WM>(a, res, R, rowBase, reinterpret_cast<char *>(sq));
+            else tpExchangeF32<B, WM>(a, res, R, rowBase);
         });
+        if (a.tp.span) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0)
+                __hip_atomic_fetch_max(a.tp.span, (unsigned)(wall_clock64() - xs), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     if constexpr (EPI == EPI_ARGMAX) {  // the row's argmax instead of its logits (ArgmaxTail)
         static_assert(B == 1, "EPI_ARGMAX: one row");

@@ -131,6 +131,9 @@ struct TpXchg {
     // words raises this word to its waiting time in s_memrealtime ticks (10 ns), so the word holds
     // the longest wait of this exchange (tpWaitReport)
     unsigned *ticks = nullptr;
+    // exchange span (DL_SYNC_MEASURE=2): the longest exchange tail of a workgroup of this exchange
+    // (its first push to its last summed store), s_memrealtime ticks, atomic max
+    unsigned *span = nullptr;
     // compute-only rank (makeComputeOnlyComm): nothing crosses a link, every peer contributes
     // zeros - a TP-N rank's kernels timed on one GPU without the exchange
     int loopback = 0;
@@ -202,6 +205,7 @@ struct GemmArgs {
     int M = 0;
     int splits = 1;
     float *part = nullptr;
+    size_t partFloats = 0;  // capacity of `part` (0: unchecked); launchers refuse a launch beyond it
     int *counters = nullptr;
     // EPI_RES (producer of the next norm's input, wo / w2 at TP1): x' = resIn + out -> resOut (f32,
     // [M][ldOut]), resX = x' * resW as f16 (the norm's per-column half) and per 64-row tile the
@@ -251,6 +255,8 @@ bool gemmSupported(int n);  // input width a multiple of 32 (whole Q40 blocks)
 int gemmSplits(int rows, int n, int M, int lanes = 0);
 // split-K partial floats for any launch of up to maxTokens tokens on this matrix
 size_t gemmPartFloats(int rows, int n, int maxTokens);
+// ... for the launches of a batch-invariant engine (GemmArgs::fixed: narrow, <= 128 tokens each)
+size_t gemmPartFloatsFixed(int rows, int n);
 // token rows one GEMM launch of M (1..128) tokens reads from its f16 activation operand (16/32/64/128)
 int gemmTokenPad(int M);
 // Residual add + RMS norm (normW may be null: no norm) of M rows -> f16:
@@ -347,9 +353,14 @@ int attnChunkMin();
 int attnChunkMax(int seqLen, int splitGrid);
 
 // epoch (optional): one thread increments it - the per-forward epoch of the fused attention block.
-// zero / nZero (optional): words cleared at the start of the forward (the measured-sync slots).
+// sync / nSync (optional): the measured-sync slots of the previous forward (syncFoldWords layout)
+// are folded into their running totals, then cleared for this forward.
 void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s,
-                     unsigned *epoch = nullptr, unsigned *zero = nullptr, int nZero = 0);
+                     unsigned *epoch = nullptr, unsigned *sync = nullptr, int nSync = 0);
+// Measured-sync slot layout (u32 words) for S slots: [0, S) the longest peer wait of each exchange,
+// [S, 2S) the longest exchange tail (span), [2S, 6S) a u64 stamp pair per slot (a separate
+// collective), then 4 u64 running totals over folded forwards: wait, span, stamped, forwards.
+inline size_t syncFoldWords(int S) { return 6 * (size_t)S + 8; }
 // One s_memrealtime stamp (100 MHz) into *p: brackets a separate collective for the measured sync.
 void launchStamp(unsigned long long *p, hipStream_t s);
 // Parallel argmax over [B][vocab]; partials need B*256 floats + ints, counters B ints (zeroed).

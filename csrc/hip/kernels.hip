@@ -233,13 +233,32 @@ void launchAttentionValu(const AttnArgs &a, int B, hipStream_t s) {
 // Small kernels
 // ------------------------------------------------------------------------------------------------
 __global__ void embeddingKernel(const float *table, const int *tokens, float *x, int dim, unsigned *epoch,
-                                unsigned *zero, int nZero) {
+                                unsigned *sync, int S) {
     const int b = blockIdx.x;
     // the forward's epoch, read by later kernels: a no-return atomic (the wave does not wait on a
     // read-modify-write round trip before its row loads)
     if (epoch && b == 0 && threadIdx.x == 0) __hip_atomic_fetch_add(epoch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (b == 0)
-        for (int i = threadIdx.x; i < nZero; i += blockDim.x) zero[i] = 0u;
+    if (b == 0 && S > 0) {
+        // fold the previous forward's measured-sync slots into the running totals, then clear them
+        // (each thread reads and clears only its own slots: no barrier)
+        unsigned long long *st = reinterpret_cast<unsigned long long *>(sync + 2 * S);
+        unsigned long long *acc = reinterpret_cast<unsigned long long *>(sync + 6 * S);
+        unsigned long long w = 0, sp = 0, sd = 0;
+        for (int i = threadIdx.x; i < S; i += blockDim.x) {
+            w += sync[i];
+            sp += sync[S + i];
+            const unsigned long long a = st[2 * i], e = st[2 * i + 1];
+            if (a && e > a) sd += e - a;
+            sync[i] = 0u;
+            sync[S + i] = 0u;
+            st[2 * i] = 0ull;
+            st[2 * i + 1] = 0ull;
+        }
+        if (w) __hip_atomic_fetch_add(acc, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (sp) __hip_atomic_fetch_add(acc + 1, sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (sd) __hip_atomic_fetch_add(acc + 2, sd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(acc + 3, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const float *src = table + (size_t)tokens[b] * dim;
     float *dst = x + (size_t)b * dim;
     // all of a thread's row loads in flight before the first store (one HBM round trip, not four)
@@ -260,8 +279,8 @@ __global__ void embeddingKernel(const float *table, const int *tokens, float *x,
 }
 
 void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s, unsigned *epoch,
-                     unsigned *zero, int nZero) {
-    hipLaunchKernelGGL(embeddingKernel, dim3(B), dim3(256), 0, s, table, tokens, x, dim, epoch, zero, nZero);
+                     unsigned *sync, int nSync) {
+    hipLaunchKernelGGL(embeddingKernel, dim3(B), dim3(256), 0, s, table, tokens, x, dim, epoch, sync, nSync);
 }
 
 __global__ void stampKernel(unsigned long long *p) {

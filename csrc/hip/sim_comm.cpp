@@ -89,7 +89,8 @@ class SimComm : public DeviceComm {
 // Compute-only rank (device_comm.h makeComputeOnlyComm): the shard shapes and kernels of rank
 // `rank` of `world`, nothing exchanged. The fused exchange keeps its local work (Q80 quantize,
 // rank-order sum, epochs) with every peer's words read as zeros; the separate collectives are
-// no-ops except that an all-gather places this rank's own slice.
+// no-ops except that an all-gather places this rank's own slice and fills the peers' with -inf
+// (gathered logits / argmax winners: a peer never wins over this shard's own maximum).
 class ComputeOnlyComm : public DeviceComm {
   public:
     ComputeOnlyComm(int rank, int world) : rank_(rank), world_(world) {
@@ -112,6 +113,8 @@ class ComputeOnlyComm : public DeviceComm {
     void resetError() override { DL_HIP(hipMemset(error_, 0, sizeof(int))); }
     void allReduceSum(float *, size_t, hipStream_t) override {}
     void allGather(const float *send, float *recv, size_t nPerRank, hipStream_t s) override {
+        for (int p = 0; p < world_; p++)
+            if (p != rank_) hipk::launchFillF32Const(recv + (size_t)p * nPerRank, nPerRank, -INFINITY, s);
         DL_HIP(hipMemcpyAsync(recv + (size_t)rank_ * nPerRank, send, nPerRank * sizeof(float),
                               hipMemcpyDeviceToDevice, s));
     }

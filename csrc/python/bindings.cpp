@@ -498,7 +498,7 @@ PYBIND11_MODULE(_C, m) {
              py::arg("tokens"), py::arg("positions"), py::arg("slots"))
         .def("last_stats", [](const Backend &b) {
             ForwardStats s = b.lastStats();
-            return py::make_tuple(s.computeMs, s.syncMs, s.sentBytes, s.recvBytes);
+            return py::make_tuple(s.computeMs, s.syncMs, s.sentBytes, s.recvBytes, s.xchgMs);
         });
 
     m.def("cpu_backend",
@@ -884,6 +884,11 @@ PYBIND11_MODULE(_C, m) {
              py::arg("coins"))
         .def("forward_argmax", [](PyHipEngine &e, std::vector<int> t, std::vector<int> p, std::vector<int> s) { return runArgmax(*e.engine, t, p, s); },
              py::arg("tokens"), py::arg("positions"), py::arg("slots"))
+        .def("last_stats",
+             [](const PyHipEngine &e) {  // (compute ms, sync ms, sent B, recv B, xchg ms) of the last call
+                 ForwardStats s = e.engine->lastStats();
+                 return py::make_tuple(s.computeMs, s.syncMs, s.sentBytes, s.recvBytes, s.xchgMs);
+             })
         .def("decode_greedy",
              [](PyHipEngine &e, int steps, std::vector<int> tokens, std::vector<int> pos, std::vector<int> slots) {
                  const int nSeq = (int)tokens.size();

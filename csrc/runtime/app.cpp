@@ -353,11 +353,14 @@ void InferenceSession::recordMetrics(const char *kind, int n, double ms) {
     const unsigned long long fr = recv - mRecv_ + (gpu_ ? st.recvBytes : 0);
     mSent_ = sent;
     mRecv_ = recv;
-    char buf[512];
+    char buf[512], xchg[32];
+    // xchg_ms: the exchange span (null when not measured: DL_SYNC_MEASURE < 2 on the fused exchange)
+    if (st.xchgMs >= 0) std::snprintf(xchg, sizeof(xchg), "%.4f", st.xchgMs);
+    else std::snprintf(xchg, sizeof(xchg), "null");
     std::snprintf(buf, sizeof(buf),
                   "{\"ts_ms\":%.3f,\"event\":\"%s\",\"rows\":%d,\"ms\":%.4f,\"compute_ms\":%.4f,\"sync_ms\":%.4f,"
-                  "\"sent_bytes\":%llu,\"recv_bytes\":%llu,\"nodes\":%d,\"backend\":\"%s\"}",
-                  epochMs(), kind, n, ms, st.computeMs, st.syncMs, fs, fr, nNodes(), gpu_ ? "hip" : "cpu");
+                  "\"xchg_ms\":%s,\"sent_bytes\":%llu,\"recv_bytes\":%llu,\"nodes\":%d,\"backend\":\"%s\"}",
+                  epochMs(), kind, n, ms, st.computeMs, st.syncMs, xchg, fs, fr, nNodes(), gpu_ ? "hip" : "cpu");
     m.write(buf);
 }
 

@@ -46,6 +46,7 @@ struct EngineConfig {
 struct ForwardStats {
     double computeMs = 0;
     double syncMs = 0;
+    double xchgMs = -1;  // exchange span (GPU: DL_SYNC_MEASURE=2 or separate collectives; CPU: = syncMs); < 0 unmeasured
     u64 sentBytes = 0;
     u64 recvBytes = 0;
 };

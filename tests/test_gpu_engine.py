@@ -524,6 +524,13 @@ def test_compute_only_rank_fused_matches_separate(C, medium, sync, monkeypatch):
         ids = e.forward_argmax(tokens, list(range(4)), [0] * 4)
         assert all(0 <= i < vocab0 for i in ids)
         del e
+        # single-row greedy forwards (the argmax fused into the logits GEMV, or the separate argmax
+        # + pick): the winner is this shard's own argmax (no phantom peer offering value 0 at index 0)
+        e = C.HipEngine(medium, "q80", max_batch=8, rank=0, world=2, comm=C.ComputeOnlyComm(0, 2, 0),
+                        sync_type=sync)
+        ids1 = [e.forward_argmax([t], [p], [0])[0] for p, t in enumerate(tokens)]
+        assert ids1 == [int(i) for i in out[fused].argmax(-1)], (ids1, out[fused].argmax(-1), out[fused].max(-1))
+        del e
     assert np.isfinite(out[True]).all()
     if sync == "f32":
         assert np.array_equal(out[True], out[False])

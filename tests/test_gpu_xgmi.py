@@ -87,7 +87,10 @@ def _engine_tp(rank, world, port, model, tokens, q, sync_type="f32", steps=4, bu
         _, toks = eng.decode_greedy(steps, [tokens[-1]], [len(tokens)], [0])
         for p, t in enumerate(tokens):
             eng.forward_argmax([t], [p], [1])
-        _, toks2 = eng.decode_greedy(steps, [toks[-1], tokens[-1]], [len(tokens) + steps, len(tokens)], [0, 1])
+        dms, toks2 = eng.decode_greedy(steps, [toks[-1], tokens[-1]], [len(tokens) + steps, len(tokens)], [0, 1])
+        st = eng.last_stats()  # every step's measured waits (device running totals), not last x steps
+        if not 0.0 <= st[1] <= dms + 1e-6:
+            raise AssertionError(f"decode sync {st[1]} ms outside [0, {dms}]")
         if comm.timed_out():
             raise AssertionError("a flag wait timed out")
         dist.barrier()
@@ -458,13 +461,17 @@ def _data_plane_bytes(dim, n_layers, world, q80, rows=1):
     return 2 * n_layers * (world - 1) * rows * row + (world - 1) * rows * 8
 
 
-def test_data_plane_bytes_reported(tmp_path):
+@pytest.mark.parametrize("measure", ["1", "2"])
+def test_data_plane_bytes_reported(tmp_path, measure):
     """`dllama inference` at TP2 over xGMI (same GPU) with the reference's Q80 sync: the Sent / Recv
     of every decode forward in --metrics is the device data plane (formula above: 2 x layers x
     dim/32 x 34 B + the argmax winner) plus a few bytes of TCP control packets; the formula gives
     SURVEY §2.6's 272 KiB per token for Llama-3.1-8B at TP2. Sync ms is measured on the device: per
-    exchange the longest time a wave waited for the peer's words, summed over the forward's
-    exchanges (engine.cpp readSyncMs): never more than the forward, and not zero over the run."""
+    exchange launch the longest time a wave waited for the peer's words, summed over the forward's
+    exchanges (engine.cpp readSync): never more than the forward, and not zero over the run. With
+    DL_SYNC_MEASURE=2 every forward also carries xchg_ms, the exchange span (per exchange the
+    longest workgroup tail, first push to last summed store): a wait happens inside a tail, so
+    sync_ms <= xchg_ms <= ms; at the default level the fused exchange reports no span (null)."""
     import json
     import subprocess
     import time
@@ -476,7 +483,8 @@ def test_data_plane_bytes_reported(tmp_path):
     m, t, _ = make_test_assets(str(tmp_path), "tiny", FloatType.Q40, seq_len=128, seed=7, dim=512, n_heads=8,
                                n_kv_heads=4, hidden_dim=1024)
     metrics = str(tmp_path / "m.jsonl")
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", DL_TP_COMM="xgmi", **_same_gpu_env(2))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", DL_TP_COMM="xgmi", DL_SYNC_MEASURE=measure,
+               **_same_gpu_env(2))
     port = _port()
     w = subprocess.Popen([dllama, "worker", "--port", str(port), "--gpu-index", "0"], stdout=subprocess.PIPE,
                          stderr=subprocess.STDOUT, env=env)
@@ -499,7 +507,13 @@ def test_data_plane_bytes_reported(tmp_path):
         assert expect <= x["sent_bytes"] <= expect + 256, (x, expect)
         assert expect <= x["recv_bytes"] <= expect + 256, (x, expect)
         assert 0 <= x["sync_ms"] < x["ms"], x  # measured waits of the forward's exchanges
+        if measure == "2":
+            assert x["xchg_ms"] is not None and x["sync_ms"] <= x["xchg_ms"] <= x["ms"], x
+        else:
+            assert x["xchg_ms"] is None, x
     assert sum(x["sync_ms"] for x in dec) > 0, dec
+    if measure == "2":
+        assert sum(x["xchg_ms"] for x in dec) > 0, dec
     # the Pred lines print the same (kB)
     kb = [int(l.split("Sent")[1].split("kB")[0]) for l in out.splitlines() if l.startswith("🔶 Pred")]
     assert kb and all(k == expect // 1024 for k in kb), (kb, expect)
