@@ -163,6 +163,7 @@ def main() -> int:
                     help="KV-cache dtype of the headline and the extra points (f32: the reference's)")
     ap.add_argument("--no-altkv", action="store_true",
                     help="skip the eval + pred point with the other KV-cache dtype (bf16 next to an f32 headline)")
+    ap.add_argument("--no-f32kv", dest="no_altkv", action="store_true", help=argparse.SUPPRESS)  # round-5 name
     ap.add_argument("--no-prefill4k", action="store_true", help="skip the 4096-token prompt-eval point")
     ap.add_argument("--tp-rank-compute", default="2,4,8",
                     help="1 GPU: TP degrees whose rank-0 shard is timed with the exchange removed "

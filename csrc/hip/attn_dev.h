@@ -203,9 +203,19 @@ __device__ __forceinline__ bool attnFinish(const AttnArgs &a, int b, int hgIdx, 
 // chunk to arrive combined all of them).
 // SYNC (fused attention block): q and the current position's K / V rows are produced by the qkv
 // workgroups of the same launch - wait for this KV group's producers, read those write-through.
-template <int HG, int HS, bool BF16, int AT, bool SYNC = false>
+// LOCAL (the wo GEMV's attention prologue, PRO_ATTN): the whole context in one chunk, nothing
+// written to global memory: the normalised output of the HG heads is left in LDS at attnLocalOut.
+template <int HG, int HS, int AT>
+__host__ __device__ constexpr int attnLocalOut() {  // float offset of the LOCAL output in the task's LDS
+    return 2 * (AT / 64) * HG + (AT / 64) * HG * HS;
+}
+template <int HG, int HS, int AT>
+__host__ __device__ constexpr int attnTaskLdsBytes() {
+    return (int)sizeof(float) * (attnLocalOut<HG, HS, AT>() + HG * HS + 2 * HG) + 16;
+}
+template <int HG, int HS, bool BF16, int AT, bool SYNC, bool LOCAL>
 __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, int c, char *smem,
-                                         const BlockSync *bs = nullptr, unsigned long long *trace = nullptr) {
+                                         const BlockSync *bs, unsigned long long *trace) {
     constexpr int NW = AT / 64, NG = AT / 16;
     constexpr int DPL = HS / 16;           // dims per lane: 16 lanes cover one position's head vector
     // keys per group loaded before any is consumed. The fused block (SYNC) issues its first round
@@ -218,7 +228,12 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
     const int pos = a.pos[b], sl = a.slot[b];
     const int len = pos + 1;
     int nSplit, ch;
-    attnSplit(len, a.splitGrid, nSplit, ch, a.chunkMin);
+    if constexpr (LOCAL) {
+        nSplit = 1;
+        ch = len;
+    } else {
+        attnSplit(len, a.splitGrid, nSplit, ch, a.chunkMin);
+    }
     if (c >= nSplit) return false;
     const int t0 = c * ch;
     const int t1 = min(t0 + ch, len);
@@ -405,6 +420,11 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
     if (trace && threadIdx.x == 0) {
         trace[1] = tWaited;
         trace[2] = wall_clock64();
+    }
+    if constexpr (LOCAL) {  // one chunk: normalise in place, the caller reads redL
+        for (int i = tid; i < HG * HS; i += AT) redL[i] = redL[i] / mlL[(i / HS) * 2 + 1];
+        __syncthreads();
+        return true;
     }
     return attnFinish<HG, HS, AT, SYNC>(a, b, hgIdx, c, nSplit, redL, mlL, flagL, oW);
 }

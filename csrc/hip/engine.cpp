@@ -72,6 +72,7 @@ HipEngineImpl::HipEngineImpl(const EngineConfig &cfg, DeviceComm *comm) : cfg_(c
     uploadRope();
     DL_HIP(hipStreamSynchronize(stream_));
     setupAttnBlock();
+    setupWoAttn();
     hipk::preloadModules();  // no code-object load inside the first forwards
     load_.ms = timer.elapsedMs();
     load_.deviceBytes = deviceBytes_;
@@ -472,6 +473,7 @@ void HipEngineImpl::tpFusedSelfTest() {
     blockOn_ = false;  // the attention block's wo role was chosen for the fused exchange: decide again
     for (CtxBucket &b : buckets_) b.block = false;
     setupAttnBlock();
+    setupWoAttn();
 }
 
 void HipEngineImpl::runGraph(int n, GraphKind kind, unsigned *syncDst) {

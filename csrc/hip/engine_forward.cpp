@@ -270,6 +270,42 @@ void HipEngineImpl::setupAttnBlock() {
                      off.maxResident / share);
 }
 
+// The wo GEMV with the layer's attention in its prologue (PRO_ATTN, gemv_dev.h): every wo workgroup
+// recomputes the rank's decode attention from the L2-resident cache instead of waiting for an
+// attention launch, which at a TP-N rank's few heads is a handful of workgroups and a whole kernel
+// boundary (TP8 rank of 8B: 4 heads, attention launch 5.8 us of a ~28 us layer, r5_decode_profile.md).
+// The redundant work grows with the heads and the context, so it is taken for <= DL_WO_ATTN_HEADS
+// (default 8) query heads per rank and context buckets of <= DL_WO_ATTN_LEN (256) positions; the
+// block (TP1) and batched rows keep their own attention. With the fused exchange the kernel spins
+// on peers, so its grid must be co-resident like the plain wo GEMV's.
+// Measured (8B TP8 rank, f32 KV, same box): 0.973 ms/token with it vs 0.894 without - one
+// workgroup computing all 4 heads of the rank serially (2 dependent key rounds, the per-key
+// softmax of 4 heads on 256 lanes, then the ring's HBM latency, which cannot be issued before the
+// attention: check_isa.py --hazards) costs more than the 4-workgroup attention launch it replaces.
+// Opt-in (DL_WO_ATTN=1) for that reason; profiles/r6_tp_rank.md.
+void HipEngineImpl::setupWoAttn() {
+    woAttnOn_ = false;
+    const char *e = std::getenv("DL_WO_ATTN");
+    if (!(e && *e == '1') || !q40_) return;
+    const char *hm = std::getenv("DL_WO_ATTN_HEADS");
+    const char *lm = std::getenv("DL_WO_ATTN_LEN");
+    const int maxHeads = hm && *hm ? std::atoi(hm) : 8;
+    woAttnMaxLen_ = lm && *lm ? std::atoi(lm) : 256;
+    if ((int)plan_.nHeads0 > maxHeads) return;
+    const bool tp = fusedTp(false);
+    const int epi = tp ? hipk::EPI_STORE_TP : hipk::EPI_STORE;
+    const hipk::GemvArgs a = gemvArgs(layers_[0].wo, 0, 1, epi, nullptr, plan_.q0, nullptr, nullptr, nullptr, dY_,
+                                      h_.dim, nullptr, dAttQ_, dAttS_, nullptr, nullptr, tp);
+    const hipk::AttnArgs at = attnArgs(layers_[0], false);
+    if (!hipk::gemvAttnSupported(a, at, epi)) return;
+    if (tp) {
+        const int share = comm_ ? std::max(1, comm_->ranksOnDevice()) : 1;
+        const hipk::GemvResidency r = hipk::gemvAttnResidency(a, at, epi);
+        if (r.maxResident <= 0 || r.grid > r.maxResident / share) return;
+    }
+    woAttnOn_ = true;
+}
+
 // A fused-block wait gave up (a workgroup of the launch never arrived): reset the monotonic
 // counters and the epoch so the engine stays usable, then raise.
 void HipEngineImpl::resetAttnBlockState() {
@@ -412,6 +448,7 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
     // Q80 hand-off of h needs one workgroup per 32 hidden units; for skinny TP shards the w13
     // epilogue emits f32 and w2 quantizes in its prologue instead.
     const bool hQ80 = q40_ && p.hidden0 / 32 >= 192;
+    const bool woAttn = woAttnNow(n, bat, blk);  // attention inside the wo GEMV's prologue
     for (u32 l = 0; l < h_.nLayers; l++) {
         DevLayer &L = layers_[l];
         const bool hasDelta = l > 0;
@@ -436,7 +473,7 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
                          hasDelta ? dX_[cur ^ 1] : nullptr, L.rmsAtt, dQ_, p.q0, &L);
             }
             if (hasDelta) cur ^= 1;
-            {
+            if (!woAttn) {
                 ProfScope ps(this, "attention");
                 const hipk::AttnArgs a = attnArgs(L, bat);
                 for (int r0 = 0; r0 < n; r0 += attRows_) {  // one launch unless the partials cap the rows
@@ -464,7 +501,14 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
                 } else if (bat)
                     gemmBatched(L.wo, n, hipk::EPI_STORE, nullptr, 0, nullptr, nullptr, nullptr, dAttH_, dY_, dim,
                                 nullptr, nullptr);
-                else
+                else if (woAttn) {
+                    const bool tp = fusedTp(bat);
+                    const int epi = tp ? hipk::EPI_STORE_TP : hipk::EPI_STORE;
+                    xChunk_ = 0;
+                    const hipk::GemvArgs a = gemvArgs(L.wo, 0, 1, epi, nullptr, p.q0, nullptr, nullptr, nullptr, dY_, dim,
+                                                      nullptr, dAttQ_, dAttS_, nullptr, nullptr, tp);
+                    hipk::launchGemvAttn(a, attnArgs(L, false), epi, stream_);
+                } else
                     gemv(L.wo, n, hipk::PRO_GLOBAL, hipk::EPI_STORE, q40_ ? nullptr : dAtt_, p.q0, nullptr, nullptr,
                          nullptr, dY_, dim, nullptr, dAttQ_, dAttS_, nullptr, nullptr, fusedTp(bat));
             }

@@ -217,6 +217,12 @@ class HipEngineImpl : public HipEngine {
     hipk::AttnBlockArgs attnBlockArgs(const DevLayer &L, u32 l, int cur) const;
     void setupAttnBlock();
     void resetAttnBlockState();
+    // the wo GEMV with the attention in its prologue (PRO_ATTN) for single decode rows of short
+    // contexts when a rank holds few heads: decided once (setupWoAttn), taken per forward (woAttnNow)
+    void setupWoAttn();
+    bool woAttnNow(int n, bool bat, bool blk) const {
+        return woAttnOn_ && n == 1 && !bat && !blk && buckets_[bucket_].maxLen <= woAttnMaxLen_;
+    }
     bool batchedPath(int n) const {
         return n >= gemmMin_ && hipk::gemmSupported(h_.dim) && hipk::gemmSupported(plan_.q0) &&
                hipk::gemmSupported(plan_.hidden0);
@@ -329,6 +335,8 @@ class HipEngineImpl : public HipEngine {
     unsigned *dEpoch_ = nullptr, *dBlockCnt_ = nullptr, *dBlockExpect_ = nullptr;
     int *dBlockErr_ = nullptr;
     bool blockOn_ = false;   // decode rows may run the fused attention block (per bucket: CtxBucket::block)
+    bool woAttnOn_ = false;  // setupWoAttn
+    int woAttnMaxLen_ = 256; // DL_WO_ATTN_LEN: context buckets up to this length
     int blockPassMul_ = 1;   // qkv / wo passes multiplier of the block's roles (same-GPU rehearsals)
     int traceLayer_ = -1;    // traceAttnBlock: the layer whose block launch is traced
     unsigned long long *traceBuf_ = nullptr;

@@ -130,8 +130,16 @@ __host__ __device__ inline unsigned long long qkvGroupMask(int r0, int r1, int q
     return m;
 }
 
-template <int L, int B, int PRO, int EPI, int MODE = GEMV_PLAIN>
-__device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, char *smem, const BlockSync *bs = nullptr) {
+// attn_dev.h (included after this header): the decode attention task, used by PRO_ATTN
+template <int HG, int HS, int AT>
+__host__ __device__ constexpr int attnLocalOut();
+template <int HG, int HS, bool BF16, int AT, bool SYNC = false, bool LOCAL = false>
+__device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, int c, char *smem,
+                                         const BlockSync *bs = nullptr, unsigned long long *trace = nullptr);
+
+template <int L, int B, int PRO, int EPI, int MODE = GEMV_PLAIN, int AHG = 1, bool ABF16 = false>
+__device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, char *smem, const BlockSync *bs = nullptr,
+                                            const AttnArgs *at = nullptr) {
     constexpr int RG = 2, NG = kThreads / L, RP = NG * RG, D = kRing;
     const int n = a.n, nb = n >> 5, K = (nb + L - 1) / L, P = a.passes, T = P * K;
     const int R = RP * P;
@@ -364,6 +372,43 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
         if (a.trace) tReady = wall_clock64();
     };
 
+    // PRO_ATTN: the rank's attention heads, one KV group at a time (AHG query heads sharing its
+    // keys), computed into this workgroup's LDS from the L2-resident cache and quantized to the Q80
+    // image the main loop reads (32-lane groups = one block, the attention kernel's own rounding);
+    // then the weight ring. The ring is NOT issued first: under the attention's register pressure
+    // the compiler moved pending ring registers to AGPRs before their s_waitcnt (stale copies,
+    // scripts/check_isa.py --hazards), so no inline-asm load is in flight during the attention.
+    auto attnPath = [&]() {
+      if constexpr (PRO == PRO_ATTN && B == 1) {
+        char *asmem = smem + alignUp(lay.total, 16);
+        const float *o = reinterpret_cast<const float *>(asmem) + attnLocalOut<AHG, 128, kThreads>();
+        const int groups = at->nHeads0 / AHG;
+        for (int g = 0; g < groups; g++) {
+            attnTask<AHG, 128, ABF16, kThreads, false, true>(*at, 0, g, 0, asmem);
+            for (int i = tid; i < AHG * 128; i += kThreads) {  // AHG * 128 is a multiple of 256
+                const float v = o[i];
+                const float amax = groupMax<32>(fabsf(v));
+                const float d = amax / 127.0f;
+                const float id = d != 0.f ? 1.0f / d : 0.f;
+                int q = (int)rintf(v * id);
+                q = q > 127 ? 127 : (q < -127 ? -127 : q);
+                const int col = g * AHG * 128 + i;
+                sq[col] = (int8_t)q;
+                const float qs = groupSum<32>((float)q);
+                if ((i & 31) == 0) ssc[col >> 5] = make_float2(roundF16(d), qs);
+            }
+            __syncthreads();  // the next group's task reuses the scratch
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < D; s++) {
+            issue(w[s], dh[s]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (a.trace) tReady = wall_clock64();
+      }
+    };
+
     // The ring's consume loop. Each prologue path below inlines its own copy, so no ring register
     // is live across a join of two paths (a join could copy a register whose load is in flight).
     auto mainLoop = [&]() __attribute__((always_inline)) {
@@ -451,7 +496,10 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
     const int unitsPerThread = PRO != PRO_GLOBAL ? (n + 8 * kThreads - 1) / (8 * kThreads)
                                                   : (n + 16 * kThreads - 1) / (16 * kThreads);
     static_assert(MODE != GEMV_CONSUMER || PRO == PRO_GLOBAL, "a consumer GEMV reads Q80 activations");
-    if constexpr (MODE == GEMV_CONSUMER) {
+    if constexpr (PRO == PRO_ATTN) {
+        attnPath();
+        mainLoop();
+    } else if constexpr (MODE == GEMV_CONSUMER) {
         latePath();
         mainLoop();
     } else if (B == 1 && unitsPerThread <= 1) {

@@ -12,6 +12,25 @@ __global__ __launch_bounds__(kThreads) void gemvQ40Kernel(GemvArgs a) {
     gemvQ40Body<L, B, PRO, EPI>(a, blockIdx.x, smem);
 }
 
+// The wo GEMV of one decode row with the layer's attention in its prologue (PRO_ATTN, kernels.h
+// launchGemvAttn): HG query heads per KV head, bf16 or f32 cache, head size 128.
+template <int L, int EPI, int HG, bool BF16>
+__global__ __launch_bounds__(kThreads) void gemvAttnKernel(GemvArgs a, AttnArgs at) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    gemvQ40Body<L, 1, PRO_ATTN, EPI, GEMV_PLAIN, HG, BF16>(a, blockIdx.x, smem, nullptr, &at);
+}
+
+template <int L>
+static const void *gemvAttnFnL(int epi, int hg, bool bf16) {
+#define DL_GA(E, G, F) \
+    if (epi == E && hg == G && bf16 == F) return (const void *)gemvAttnKernel<L, E, G, F>;
+#define DL_GA4(E, F) DL_GA(E, 1, F) DL_GA(E, 2, F) DL_GA(E, 4, F) DL_GA(E, 8, F)
+    DL_GA4(EPI_STORE_TP, true) DL_GA4(EPI_STORE_TP, false) DL_GA4(EPI_STORE, true) DL_GA4(EPI_STORE, false)
+#undef DL_GA4
+#undef DL_GA
+    return nullptr;
+}
+
 // ------------------------------------------------------------------------------------------------
 // F32-weight GEMV: out[b][row] = W[row,:] . act(in[b,:]), fused prologue/epilogue (Q40 weights use
 // gemvQ40Kernel / gemmQ40Kernel).

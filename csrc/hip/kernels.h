@@ -27,7 +27,11 @@ namespace hipk {
 //             Q40 weights, f32 for F32 weights) - no prologue, no LDS, no barrier.
 // PRO_RESNORM: (x + delta) -> RMS norm -> Q80 (or f32) staged once per workgroup in LDS
 //             (normW == null: no norm, plain quantization of `in`).
-enum Prologue : int { PRO_GLOBAL = 0, PRO_RESNORM = 1 };
+// PRO_ATTN (Q40 ring GEMV, one row: the wo GEMV of a short-context decode step): the layer's
+//             decode attention for every head of the rank is computed in the prologue of EVERY
+//             workgroup (redundantly, from L2) and quantized to Q80 into LDS - no attention
+//             launch and no hand-off (launchGemvAttn; the engine takes it for few heads per rank).
+enum Prologue : int { PRO_GLOBAL = 0, PRO_RESNORM = 1, PRO_ATTN = 2 };
 // EPI_ACT_Q80: act(w1 x) * (w3 x), quantized to Q80 blocks for the next GEMV (32 hidden units/block).
 // EPI_STORE_TP: EPI_STORE whose rows are first all-reduced over the tensor-parallel ranks (GemvArgs::tp).
 // EPI_RES (batched GEMMs): residual update fused with the next RMS norm's elementwise half - see
@@ -266,6 +270,13 @@ void launchNormF16(const GemvArgs &a, _Float16 *out, int M, hipStream_t s);
 
 // B = batch rows in this launch (1, 2 or 4); q40 = weight format.
 void launchGemv(const GemvArgs &a, int B, int pro, int epi, bool q40, hipStream_t s);
+// The wo GEMV of one decode row with the layer's attention in its prologue (PRO_ATTN): `at` is the
+// row's attention (every head of the rank, one chunk over the whole context); epi EPI_STORE or
+// EPI_STORE_TP. Supported: gemvAttnSupported (Q40, head size 128, query heads per KV head 1/2/4/8).
+bool gemvAttnSupported(const GemvArgs &a, const AttnArgs &at, int epi);
+void launchGemvAttn(const GemvArgs &a, const AttnArgs &at, int epi, hipStream_t s);
+struct GemvResidency;
+GemvResidency gemvAttnResidency(const GemvArgs &a, const AttnArgs &at, int epi);
 // Co-residency of one GEMV launch on the current device: its grid and the most workgroups of that
 // kernel (at its LDS size) the device holds at once (occupancy per CU x CUs). A kernel whose
 // workgroups spin on peers (EPI_STORE_TP) is deadlock-free only if grid <= maxResident.

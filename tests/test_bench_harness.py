@@ -30,7 +30,7 @@ def test_same_gpu_rehearsal_self_launch_is_labelled():
     env = dict(os.environ, DL_BENCH_SAME_GPU="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--shape", "llama3_2_1b", "--steps", "8", "--warmup", "2",
-                        "--prompt", "32", "--long-ctx", "0", "--no-f32kv", "--no-cli"],
+                        "--prompt", "32", "--long-ctx", "0", "--no-altkv", "--no-cli"],
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]

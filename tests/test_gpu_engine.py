@@ -403,6 +403,26 @@ def test_attn_block_matches_separate_kernels(C, assets, medium, monkeypatch, kv_
         assert list(ca) == list(cb)
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_wo_attention_prologue_matches_attention_launch(C, medium, monkeypatch, world):
+    """DL_WO_ATTN=1: a TP rank's wo GEMV computes the layer's decode attention in every workgroup's
+    prologue (PRO_ATTN, no attention launch): same shard logits as the attention launch + wo GEMV
+    (another reduction order: tolerance) and the same greedy chain, rank in loopback."""
+    out = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("DL_WO_ATTN", on)
+        e = C.HipEngine(medium, "q80", max_batch=8, rank=0, world=world, comm=C.ComputeOnlyComm(0, world, 0),
+                        sync_type="f32", kv_bf16=False)
+        v0 = e.header["vocab_size"] // world
+        toks = [3, 17, 101, 7, 250, 9]
+        lg = np.stack([e.forward([t], [p], [0])[0][:v0] for p, t in enumerate(toks)])
+        _, ch = e.decode_greedy(12, [int(lg[-1].argmax())], [len(toks)], [0])
+        out[on] = (lg, list(ch))
+        del e
+    assert _rel(out["1"][0], out["0"][0]) < 1e-3
+    assert out["1"][1] == out["0"][1]
+
+
 def test_engine_8b_shape_matches_cpu(C, tmp_path):
     """Llama-3.1-8B layer shapes (2 layers, 2048-token vocabulary, kvMul 4, head size 128): the
     fused attention block's decode logits against the CPU reference backend, token by token."""
