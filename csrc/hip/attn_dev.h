@@ -298,13 +298,14 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
     int tb = t0 + g16;
     bool prefetched = false;
     unsigned long long tWaited = 0ull;
-    if constexpr (SYNC) {
-        if (tb < t1) {
-            loadRound(tb, 1);
-            prefetched = true;
-        }
-        tWaited = blockWait(bs->qkvCnt + kvh * kCntStride, bs->step * bs->qkvExpect[kvh], *bs, 2);
+    // the first round of keys goes out before the query loads (the keys do not depend on q, so
+    // both round trips overlap instead of following each other)
+    if (tb < t1) {
+        loadRound(tb, 1);
+        prefetched = true;
     }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (SYNC) tWaited = blockWait(bs->qkvCnt + kvh * kCntStride, bs->step * bs->qkvExpect[kvh], *bs, 2);
     // this lane's slice of the HG query heads (pre-scaled), vector loads
     const float scale = 1.0f / sqrtf((float)HS);
     float qr[HG][DPL];

@@ -51,6 +51,10 @@ HipEngineImpl::HipEngineImpl(const EngineConfig &cfg, DeviceComm *comm) : cfg_(c
         tpVec_.q80 = syncQ80_ ? 1 : 0;
     }
     checkFits();
+    {
+        const char *hq = std::getenv("DL_H_Q80");
+        hQ80_ = hq && *hq ? *hq == '1' : plan_.hidden0 / 32 >= 192;
+    }
     if (tpFused_) checkFusedResidency();
     {  // path knobs, read once: a captured graph replays the path it was captured with
         const char *e = std::getenv("DL_GEMM_MIN");

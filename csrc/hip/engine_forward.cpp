@@ -447,7 +447,7 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
     }
     // Q80 hand-off of h needs one workgroup per 32 hidden units; for skinny TP shards the w13
     // epilogue emits f32 and w2 quantizes in its prologue instead.
-    const bool hQ80 = q40_ && p.hidden0 / 32 >= 192;
+    const bool hQ80 = q40_ && hQ80_;
     const bool woAttn = woAttnNow(n, bat, blk);  // attention inside the wo GEMV's prologue
     for (u32 l = 0; l < h_.nLayers; l++) {
         DevLayer &L = layers_[l];

@@ -269,6 +269,10 @@ class HipEngineImpl : public HipEngine {
     int attRows_ = 1;          // rows per attention launch (the split partials hold this many rows)
     bool fuseNormEnv_ = true;  // DL_GEMM_FUSE_NORM
     bool invariant_ = false;   // EngineConfig::batchInvariant
+    // single-row decode: w13 hands h to w2 as Q80 blocks (64-row w13 workgroups) when the shard has
+    // >= 192 blocks of 32 hidden units, else as f32 that w2 quantizes in its prologue (DL_H_Q80=0/1
+    // forces either)
+    bool hQ80_ = true;
     std::vector<void *> allocs_, hostAllocs_;
     size_t deviceBytes_ = 0;
     LoadStats load_;

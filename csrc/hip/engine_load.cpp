@@ -55,7 +55,7 @@ void HipEngineImpl::checkFusedResidency() {
     // overrides the limit (diagnostics / tests of the fallback)
     const int share = std::max(1, comm_->ranksOnDevice());
     const char *ov = std::getenv("DL_FUSED_RESIDENT");
-    const bool hQ80 = p.hidden0 / 32 >= 192;
+    const bool hQ80 = hQ80_;
     struct Shape {
         int rows, n, pro;
     } shapes[2] = {{(int)h_.dim, (int)p.q0, hipk::PRO_GLOBAL},

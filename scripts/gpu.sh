@@ -12,6 +12,7 @@
 #   batch [B list]               batched decode steps (bench.py --batch B)
 #   big                          70B-shaped decode on one GPU + dllama-api throughput (64 / 16 requests)
 #   tp-rehearse                  same-GPU multi-rank bench rehearsals (TP2 8B, TP4 1B; not scaling points)
+#                                + the CLI root/worker TP2 product path (scripts/cli_tp_probe.py)
 #   pmc <name> "<counters>" <cmd..>   one rocprofv3 PMC pass (counters only) over a command
 set -o pipefail
 task=$1; shift
@@ -80,7 +81,8 @@ case $task in
       bench.py --gpus 2 $F > $O/tp2.log 2>&1 || exit 1
     timeout -k 10 500 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29532 \
       bench.py --gpus 4 --shape llama3_2_1b $F > $O/tp4_1b.log 2>&1 || exit 1
-    tail -1 $O/tp2.log $O/tp4_1b.log ;;
+    timeout -k 10 600 python3 -u scripts/cli_tp_probe.py --tp 2 > $O/cli_tp2.json 2> $O/cli_tp2.err || exit 1
+    tail -1 $O/tp2.log $O/tp4_1b.log $O/cli_tp2.json ;;
   pmc)
     name=$1; counters=$2; shift 2
     timeout -s KILL 120 rocprofv3 --pmc $counters --output-format csv -d $O/$name -- "$@" > $O/$name.log 2>&1 || exit 1
