@@ -11,6 +11,9 @@ namespace hipk {
 #ifndef DL_ATTN_TU_F32_BLOCK
 #define DL_ATTN_TU_F32_BLOCK 7
 #endif
+#ifndef DL_ATTN_TU_F32
+#define DL_ATTN_TU_F32 4  // f32 caches outside the block: keys per 16-lane group per round
+#endif
 #ifndef DL_ATTN_TU_BF16_BLOCK
 #define DL_ATTN_TU_BF16_BLOCK 8
 #endif
@@ -223,7 +226,7 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
     // round instead of 64: f32-KV decode 1.322 -> 1.291 ms/token, same box; 8 keys took the block
     // kernel to 178 VGPRs, 2 waves per SIMD, and off co-residency), bf16 stays at 8 (12 measured
     // 1.357 vs 1.289 ms/token): profiles/r6_decode.md
-    constexpr int TU = BF16 ? (SYNC ? DL_ATTN_TU_BF16_BLOCK : 8) : (SYNC ? DL_ATTN_TU_F32_BLOCK : 4);
+    constexpr int TU = BF16 ? (SYNC ? DL_ATTN_TU_BF16_BLOCK : 8) : (SYNC ? DL_ATTN_TU_F32_BLOCK : DL_ATTN_TU_F32);
     constexpr int RW = BF16 ? DPL / 2 : DPL;  // 32-bit words per lane per key (packed bf16 pairs)
     const int pos = a.pos[b], sl = a.slot[b];
     const int len = pos + 1;

@@ -7,7 +7,7 @@
 #   ab "<bench flags>" N a b ..  same-box A/B of bench.py: this tree (".") vs side builds ab/<name>
 #                                (scripts/ab_build.sh), N alternating rounds -> gpurun_out/ab/runs.log
 #   env "<bench flags>" N "A=1 B=2" "A=0" ..   bench.py under each set of environment switches
-#   prof-decode [tp list] [kv]   rocprofv3 kernel trace of batch-1 decode (TP1 / a TP-N rank in
+#   prof-decode [tp list] [kv] [pos]  rocprofv3 kernel trace of batch-1 decode (TP1 / a TP-N rank in
 #                                loopback, scripts/tp_rank_compute.py) + per-kernel tables
 #   batch [B list]               batched decode steps (bench.py --batch B)
 #   big                          70B-shaped decode on one GPU + dllama-api throughput (64 / 16 requests)
@@ -35,7 +35,7 @@ case $task in
     timeout -k 10 1500 python3 -u -m pytest ${@:-tests -m gpu} -v --timeout 170 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
     tail -3 $O/tests.log
     timeout -k 10 180 python3 -u __graft_entry__.py > $O/smoke.log 2>&1 || exit 1
-    tail -2 $O/smoke.log ;;
+    tail -n 2 $O/smoke.log ;;
   bench)
     timeout -k 10 600 python3 -u bench.py "$@" > $O/bench.json 2> $O/bench.err || exit 1
     cat $O/bench.json ;;
@@ -57,11 +57,12 @@ case $task in
     done
     cat $O/runs.log ;;
   prof-decode)
-    kv=${2:-f32}
+    kv=${2:-f32}; pos=${3:-64}
     for tp in ${1:-1 8}; do
-      timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tp$tp -o p -- python3 scripts/tp_rank_compute.py --tp $tp --steps 64 --kv $kv > $O/tp$tp.log 2>&1 || exit 1
-      python3 scripts/prof_summary.py $O/tp$tp --skip-first 3000 > $O/tp$tp.md 2>&1
-      grep "pred" $O/tp$tp.log
+      n=tp${tp}_${kv}_p$pos
+      timeout -k 10 300 rocprofv3 --kernel-trace -d $O/$n -o p -- python3 scripts/tp_rank_compute.py --tp $tp --steps 64 --kv $kv --pos $pos > $O/$n.log 2>&1 || exit 1
+      python3 scripts/prof_summary.py $O/$n --skip-first 3000 > $O/$n.md 2>&1
+      grep "pred" $O/$n.log
     done ;;
   batch)
     for b in ${1:-8 16 64}; do
@@ -73,7 +74,7 @@ case $task in
     timeout -k 10 500 python3 -u bench.py --shape llama3_3_70b $QUICK --long-ctx 0 --tp-rank-compute= --no-altkv > $O/b70.json 2> $O/b70.err || exit 1
     timeout -k 10 400 python3 -u scripts/bench_api.py --n 64 > $O/api64.log 2>&1 || exit 1
     timeout -k 10 300 python3 -u scripts/bench_api.py --n 16 > $O/api16.log 2>&1 || exit 1
-    tail -1 $O/b70.json; tail -2 $O/api64.log $O/api16.log ;;
+    tail -n 1 $O/b70.json; tail -n 2 $O/api64.log $O/api16.log ;;
   tp-rehearse)
     export DL_BENCH_SAME_GPU=1
     F="--steps 32 --warmup 8 --no-prefill4k --no-cap128k --no-altkv --long-ctx 0"
@@ -82,7 +83,7 @@ case $task in
     timeout -k 10 500 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29532 \
       bench.py --gpus 4 --shape llama3_2_1b $F > $O/tp4_1b.log 2>&1 || exit 1
     timeout -k 10 600 python3 -u scripts/cli_tp_probe.py --tp 2 > $O/cli_tp2.json 2> $O/cli_tp2.err || exit 1
-    tail -1 $O/tp2.log $O/tp4_1b.log $O/cli_tp2.json ;;
+    tail -n 1 $O/tp2.log $O/tp4_1b.log $O/cli_tp2.json ;;
   pmc)
     name=$1; counters=$2; shift 2
     timeout -s KILL 120 rocprofv3 --pmc $counters --output-format csv -d $O/$name -- "$@" > $O/$name.log 2>&1 || exit 1

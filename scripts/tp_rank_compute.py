@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--sync-type", default="q80")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--kv", default="bf16", choices=["bf16", "f32"], help="KV-cache dtype")
+    ap.add_argument("--pos", type=int, default=64, help="decode position (context length) of the timed steps")
     args = ap.parse_args()
     import torch
     import distributed_llama_multiusers_amd as dl
@@ -27,8 +28,8 @@ def main():
     C = dl.native()
     torch.cuda.set_device(0)
     shape = dict(LLAMA31_8B, **LLAMA_SHAPES[args.shape])
-    e = C.HipEngine("", "q80", max_seq_len=4096, max_batch=32, n_slots=1, kv_bf16=args.kv == "bf16", gpu_index=0,
-                    use_graphs=not args.no_graphs, synthetic=dict(shape, seq_len=4096), seed=1234, rank=args.rank,
+    e = C.HipEngine("", "q80", max_seq_len=max(4096, args.pos + 128), max_batch=32, n_slots=1, kv_bf16=args.kv == "bf16", gpu_index=0,
+                    use_graphs=not args.no_graphs, synthetic=dict(shape, seq_len=max(4096, args.pos + 128)), seed=1234, rank=args.rank,
                     **(dict(world=args.tp, comm=C.ComputeOnlyComm(args.rank, args.tp, 0)) if args.tp > 1 else {}),
                     sync_type=args.sync_type)
     prompt = [(i * 7919 + 13) % 128000 for i in range(64)]
@@ -40,13 +41,14 @@ def main():
         e.forward_argmax(prompt[s:s + 32], list(range(s, s + 32)), [0] * 32)
     torch.cuda.synchronize()
     ev = (time.perf_counter() - t0) * 1000.0 / 64
-    e.decode_greedy(8, [prompt[-1]], [64], [0])
+    p0 = max(64, args.pos)
+    e.decode_greedy(8, [prompt[-1]], [p0], [0])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    e.decode_greedy(args.steps, [prompt[-1]], [72], [0])
+    e.decode_greedy(args.steps, [prompt[-1]], [p0 + 8], [0])
     torch.cuda.synchronize()
     pred = (time.perf_counter() - t0) * 1000.0 / args.steps
-    print(f"tp{args.tp} rank {args.rank} ({args.shape}, {args.sync_type}, kv {args.kv}): pred {pred:.4f} ms/token, "
+    print(f"tp{args.tp} rank {args.rank} ({args.shape}, {args.sync_type}, kv {args.kv}, pos {max(64, args.pos)}): pred {pred:.4f} ms/token, "
           f"eval {ev:.4f} ms/token, fused {bool(e.tp_fused)}, attn block {bool(e.attn_block)} "
           f"[{' '.join(k + '=' + v for k, v in os.environ.items() if k.startswith('DL_'))}]", flush=True)
 
