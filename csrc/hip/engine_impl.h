@@ -91,6 +91,7 @@ class HipEngineImpl : public HipEngine {
     void profileForward(int n, const int *tokens, const int *positions, const int *slots) override;
     bool tpFused() const override { return tpFused_; }
     bool attnBlock() const override { return blockOn_; }
+    bool woAttn() const override { return woAttnOn_; }
     std::vector<unsigned long long> traceAttnBlock(int token, int pos, int slot, int layer) override;
     int fusedGridMax() const override { return fusedGridMax_; }
     bool tpBatchedFused(int n) const override { return plan_.nRanks > 1 && batchedPath(n) && fuseNorm(n); }

@@ -857,6 +857,7 @@ PYBIND11_MODULE(_C, m) {
         .def_property_readonly("device_bytes", [](const PyHipEngine &e) { return e.engine->deviceBytes(); })
         .def_property_readonly("tp_fused", [](const PyHipEngine &e) { return e.engine->tpFused(); })
         .def_property_readonly("attn_block", [](const PyHipEngine &e) { return e.engine->attnBlock(); })
+        .def_property_readonly("wo_attn", [](const PyHipEngine &e) { return e.engine->woAttn(); })
         .def("trace_attn_block",
              [](PyHipEngine &e, int token, int pos, int slot, int layer) {
                  py::gil_scoped_release rel;

@@ -36,6 +36,15 @@ SHAPES = {
     "w2_8": (4096, 1792, PRO_RESNORM, EPI_STORE),
     # their TP tails (EPI_STORE_TP in loopback: DL_BENCH_TP_WORLD / DL_BENCH_TP_Q80)
     "wo8tp": (4096, 512, PRO_GLOBAL, 5),
+    # the same matrices with / without the norm prologue (plain store): its cost on the launch
+    "w13n": (28672, 4096, PRO_RESNORM, EPI_STORE),
+    "w13g": (28672, 4096, PRO_GLOBAL, EPI_STORE),
+    "qkvn": (6144, 4096, PRO_RESNORM, EPI_STORE),
+    "qkvg": (6144, 4096, PRO_GLOBAL, EPI_STORE),
+    "w13_8n": (3584, 4096, PRO_RESNORM, EPI_STORE),
+    "w13_8g": (3584, 4096, PRO_GLOBAL, EPI_STORE),
+    "qkv8n": (768, 4096, PRO_RESNORM, EPI_STORE),
+    "qkv8g": (768, 4096, PRO_GLOBAL, EPI_STORE),
     "w2_8tp": (4096, 1792, PRO_RESNORM, 5),
 }
 TICK_US = 0.01  # s_memrealtime runs at 100 MHz

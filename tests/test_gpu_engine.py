@@ -403,7 +403,7 @@ def test_attn_block_matches_separate_kernels(C, assets, medium, monkeypatch, kv_
         assert list(ca) == list(cb)
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2])
 def test_wo_attention_prologue_matches_attention_launch(C, medium, monkeypatch, world):
     """DL_WO_ATTN=1: a TP rank's wo GEMV computes the layer's decode attention in every workgroup's
     prologue (PRO_ATTN, no attention launch): same shard logits as the attention launch + wo GEMV
@@ -413,6 +413,7 @@ def test_wo_attention_prologue_matches_attention_launch(C, medium, monkeypatch, 
         monkeypatch.setenv("DL_WO_ATTN", on)
         e = C.HipEngine(medium, "q80", max_batch=8, rank=0, world=world, comm=C.ComputeOnlyComm(0, world, 0),
                         sync_type="f32", kv_bf16=False)
+        assert bool(e.wo_attn) == (on == "1")
         v0 = e.header["vocab_size"] // world
         toks = [3, 17, 101, 7, 250, 9]
         lg = np.stack([e.forward([t], [p], [0])[0][:v0] for p, t in enumerate(toks)])
