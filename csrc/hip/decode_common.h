@@ -521,8 +521,10 @@ __device__ __forceinline__ long long tpWordOf(const GemvArgs &a, int R, int rowB
 // at kernel entry (round 5) saved nothing measurable and let the compiler copy the pending
 // registers before their s_waitcnt (an asm operand moved to other VGPRs: v_mov of a register whose
 // load was still in flight, ISA of gemvQ40Kernel<.., EPI_STORE_TP>), i.e. a stale-epoch hazard.
-template <int B, int WM>
-__device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *res, int R, int rowBase) {
+// TO_LDS (EPI_RESQ_TP): the rank-summed rows replace the partials in res[] (the tail continues
+// from LDS) instead of going to a.out.
+template <int B, int WM, bool TO_LDS = false>
+__device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, float *res, int R, int rowBase) {
     const TpXchg &x = a.tp;
     unsigned waited = 0;
     for (int i = threadIdx.x; i < B * R; i += kThreads) {
@@ -536,7 +538,8 @@ __device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *re
 #pragma unroll
         for (int p = 0; p < WM; p++)
             if (p < x.world) s += __uint_as_float(v[p]);
-        a.out[el] = s;
+        if constexpr (TO_LDS) res[i] = s;
+        else a.out[el] = s;
         x.epochs[el] = e;
     }
     tpWaitReport(x, waited);
@@ -550,8 +553,8 @@ __device__ __forceinline__ void tpExchangeF32(const GemvArgs &a, const float *re
 // the block's 9 words (8 x 4 int8 + the f16 scale), and every lane sums its row over the ranks
 // from those words by shuffles: no LDS staging and no barrier (the LDS form spent ~1.6 us per
 // workgroup tail, profiles/r5_tp_rank.md). Same rounding and rank order as tpExchangeQ80.
-template <int WM>
-__device__ __forceinline__ void tpExchangeQ80Row(const GemvArgs &a, const float *res, int R, int rowBase) {
+template <int WM, bool TO_LDS = false>
+__device__ __forceinline__ void tpExchangeQ80Row(const GemvArgs &a, float *res, int R, int rowBase) {
     const TpXchg &x = a.tp;
     const int nBlk = R >> 5, W = x.world;
     unsigned waited = 0;
@@ -589,7 +592,11 @@ __device__ __forceinline__ void tpExchangeQ80Row(const GemvArgs &a, const float 
                 sum += (float)qq * __half2float(__ushort_as_half((uint16_t)(ds & 0xFFFFu)));
             }
         }
-        if (blkLive && row < a.rows) a.out[row] = sum;
+        if constexpr (TO_LDS) {
+            if (blk < nBlk) res[i] = sum;  // this lane read res[i] above: no other lane touches it
+        } else if (blkLive && row < a.rows) {
+            a.out[row] = sum;
+        }
     }
     tpWaitReport(x, waited);
 }
@@ -653,6 +660,37 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
         }
         a.out[(size_t)b * a.ldOut + row] = s;
     }
+}
+
+// EPI_RESQ_TP tail (one row; R a multiple of 32, rowBase too): res[i] holds the rank-summed delta
+// of row rowBase + i. x' = resIn + delta -> resOut; x' * resW quantized to Q80 blocks (d' =
+// amax / 127 unrounded: the consumer folds in 1 / rms and rounds) -> xq / xs; the workgroup's
+// sum of x'^2 -> ssp[blk]. Uniform loop over whole 32-lane groups (one block each).
+__device__ __forceinline__ void resqTail(const GemvArgs &a, const float *res, int R, int rowBase, int blk,
+                                         float *scratch) {
+    const PrenormOut &o = a.rq;
+    float ss = 0.f;
+    for (int base = 0; base < R; base += kThreads) {
+        const int i = base + threadIdx.x, row = rowBase + i;
+        const bool live = i < R && row < a.rows;  // a.rows % 32 == 0: whole blocks live or dead
+        float g = 0.f;
+        if (live) {
+            const float xn = o.resIn[row] + res[i];
+            o.resOut[row] = xn;
+            g = xn * o.resW[row];
+            ss += xn * xn;
+        }
+        const float amax = groupMax<32>(fabsf(g));
+        const float d = amax / 127.0f;
+        const float id = d != 0.f ? 1.0f / d : 0.f;
+        int q = (int)rintf(g * id);
+        q = q > 127 ? 127 : (q < -127 ? -127 : q);
+        const float qs = groupSum<32>((float)q);
+        if (live) o.xq[row] = (int8_t)q;
+        if (live && (i & 31) == 0) o.xs[row >> 5] = make_float2(d, qs);
+    }
+    ss = blockSum<kThreads>(ss, scratch);
+    if (threadIdx.x == 0) o.ssp[blk] = ss;
 }
 
 // Sequence split of a decode-attention row of length `len`: nSplit chunks of ch positions

@@ -77,6 +77,7 @@ HipEngineImpl::HipEngineImpl(const EngineConfig &cfg, DeviceComm *comm) : cfg_(c
     DL_HIP(hipStreamSynchronize(stream_));
     setupAttnBlock();
     setupWoAttn();
+    setupPrenorm();
     hipk::preloadModules();  // no code-object load inside the first forwards
     load_.ms = timer.elapsedMs();
     load_.deviceBytes = deviceBytes_;
@@ -478,6 +479,7 @@ void HipEngineImpl::tpFusedSelfTest() {
     for (CtxBucket &b : buckets_) b.block = false;
     setupAttnBlock();
     setupWoAttn();
+    setupPrenorm();
 }
 
 void HipEngineImpl::runGraph(int n, GraphKind kind, unsigned *syncDst) {

@@ -270,6 +270,129 @@ void HipEngineImpl::setupAttnBlock() {
                      off.maxResident / share);
 }
 
+// Pre-normalized hand-off between the single-row GEMVs of a tensor-parallel rank (kernels.h
+// PRO_PRENORM / EPI_RESQ_TP): the wo / w2 exchange tails, which already hold the rank-summed rows,
+// also apply the residual update and the next RMS norm's weights and quantize x * normW to Q80
+// blocks, plus one sum of squares per workgroup; the consumers (qkv, w13, logits) copy those blocks
+// and fold in 1 / rms instead of re-reading x and the delta and reducing 4096 values in every
+// workgroup. Measured per launch (scripts/trace_gemv.py, norm vs copy prologue): qkv 5.71 vs 4.69
+// us at TP1 shapes, and at a TP8 rank's shards qkv 4.35 vs 3.13, w13 5.18 vs 3.96.
+// Needs producers whose workgroups own whole 32-row blocks (the Q80 exchange's tpPasses) and at
+// most kMaxSsp of them, the fused exchange (separate collectives keep the norm prologue) and
+// no attention block in the forward (the block's roles keep theirs). DL_PRENORM=0 disables it.
+void HipEngineImpl::setupPrenorm() {
+    prenormOn_ = false;
+    const char *e = std::getenv("DL_PRENORM");
+    if ((e && *e == '0') || !q40_ || !fusedTp(false) || h_.dim % 32 || h_.dim > 16384) return;
+    const int share = comm_ ? std::max(1, comm_->ranksOnDevice()) : 1;
+    for (int w = 0; w < 2; w++) {
+        const DevMat &m = w == 0 ? layers_[0].wo : layers_[0].w2;
+        const int pro = w == 1 && !hQ80_ ? hipk::PRO_RESNORM : hipk::PRO_GLOBAL;
+        const hipk::GemvArgs a = gemvArgs(m, 0, 1, hipk::EPI_RESQ_TP, nullptr, m.n, nullptr, nullptr, nullptr, dY_,
+                                          h_.dim, nullptr, nullptr, nullptr, nullptr, nullptr, true);
+        const int R = (256 / a.lanes) * 2 * a.passes, grid = (a.rows + R - 1) / R;
+        if (R % 32 || grid > kMaxSsp) return;
+        const hipk::GemvResidency r = hipk::gemvResidency(a, 1, pro, hipk::EPI_RESQ_TP, true);
+        if (r.maxResident <= 0 || r.grid > r.maxResident / share) return;
+    }
+    prenormOn_ = true;
+}
+
+// The layers + logits of one decode row with the pre-normalized hand-offs (setupPrenorm). The
+// residual lives in dX_[cur]; its Q80 image for the next consumer in dXQ_ / dXS_ [cur] with sspN
+// partial sums in dSSP_[cur]; each producer writes the other parity and flips cur.
+void HipEngineImpl::enqueuePrenormLayers(GraphKind kind, bool argTail) {
+    const ShardPlan &p = plan_;
+    const int dim = h_.dim;
+    const bool hQ80 = hQ80_;
+    int cur = 0, sspN[2] = {1, 0};  // the embedding produced parity 0 with one partial
+    auto consumer = [&](hipk::GemvArgs &a) {
+        a.aq = dXQ_[cur];
+        a.as = dXS_[cur];
+        a.sspIn = dSSP_[cur];
+        a.nSsp = sspN[cur];
+    };
+    auto producer = [&](hipk::GemvArgs &a, const float *normW) {
+        a.rq.resIn = dX_[cur];
+        a.rq.resOut = dX_[cur ^ 1];
+        a.rq.resW = normW;
+        a.rq.xq = dXQ_[cur ^ 1];
+        a.rq.xs = dXS_[cur ^ 1];
+        a.rq.ssp = dSSP_[cur ^ 1];
+        const int R = (256 / a.lanes) * 2 * a.passes;
+        sspN[cur ^ 1] = (a.rows + R - 1) / R;
+    };
+    for (u32 l = 0; l < h_.nLayers; l++) {
+        DevLayer &L = layers_[l];
+        xSlot_ = 2 * (int)l;
+        xChunk_ = 0;
+        {
+            ProfScope ps(this, "gemv_qkv");
+            hipk::GemvArgs a = gemvArgs(L.qkv, 0, 1, hipk::EPI_QKV, nullptr, dim, nullptr, nullptr, nullptr, dQ_, p.q0, &L,
+                                        nullptr, nullptr, nullptr, nullptr, false);
+            consumer(a);
+            hipk::launchGemv(a, 1, hipk::PRO_PRENORM, hipk::EPI_QKV, true, stream_);
+        }
+        {
+            ProfScope ps(this, "attention");
+            hipk::launchAttention(attnArgs(L, false), 1, stream_);
+        }
+        {
+            ProfScope ps(this, "gemv_wo");
+            hipk::GemvArgs a = gemvArgs(L.wo, 0, 1, hipk::EPI_RESQ_TP, nullptr, p.q0, nullptr, nullptr, nullptr, dY_, dim,
+                                        nullptr, dAttQ_, dAttS_, nullptr, nullptr, true);
+            producer(a, L.rmsFfn);
+            hipk::launchGemv(a, 1, hipk::PRO_GLOBAL, hipk::EPI_RESQ_TP, true, stream_);
+            cur ^= 1;
+        }
+        xSlot_ = 2 * (int)l + 1;
+        {
+            ProfScope ps(this, "gemv_w13");
+            const int epi = hQ80 ? hipk::EPI_ACT_Q80 : hipk::EPI_ACT;
+            hipk::GemvArgs a = gemvArgs(L.w13, 0, 1, epi, nullptr, dim, nullptr, nullptr, nullptr, dH_, p.hidden0, nullptr,
+                                        nullptr, nullptr, dHQ_, dHS_, false);
+            consumer(a);
+            hipk::launchGemv(a, 1, hipk::PRO_PRENORM, epi, true, stream_);
+        }
+        {
+            ProfScope ps(this, "gemv_w2");
+            const float *wNext = l + 1 < h_.nLayers ? layers_[l + 1].rmsAtt : rmsFinal_;
+            hipk::GemvArgs a = gemvArgs(L.w2, 0, 1, hipk::EPI_RESQ_TP, hQ80 ? nullptr : dH_, p.hidden0, nullptr, nullptr,
+                                        nullptr, dY_, dim, nullptr, hQ80 ? dHQ_ : nullptr, hQ80 ? dHS_ : nullptr, nullptr,
+                                        nullptr, true);
+            producer(a, wNext);
+            hipk::launchGemv(a, 1, hQ80 ? hipk::PRO_GLOBAL : hipk::PRO_RESNORM, hipk::EPI_RESQ_TP, true, stream_);
+            cur ^= 1;
+        }
+    }
+    xSlot_ = 2 * (int)h_.nLayers;  // logits gather / argmax winners
+    ProfScope ps(this, "gemv_logits");
+    if (argTail) {
+        hipk::GemvArgs a = gemvArgs(wcls_, 0, 1, hipk::EPI_ARGMAX, nullptr, dim, nullptr, nullptr, nullptr, nullptr,
+                                    p.vocab0, nullptr, nullptr, nullptr, nullptr, nullptr, false);
+        consumer(a);
+        a.am.ids = dIds_;
+        a.am.partV = dArgV_;
+        a.am.partI = dArgI_;
+        a.am.counter = dArgCnt_;
+        a.am.vocabStart = p.vocabStart();
+        if (kind == GraphKind::CHAIN) {
+            a.am.tokens = dTok_;
+            a.am.pos = dPos_;
+            a.am.hist = dHist_;
+        }
+        a.tp = tpArg_;
+        a.tp.ticks = syncTicks();
+        a.tp.span = syncSpan();
+        hipk::launchGemv(a, 1, hipk::PRO_PRENORM, hipk::EPI_ARGMAX, true, stream_);
+    } else {
+        hipk::GemvArgs a = gemvArgs(wcls_, 0, 1, hipk::EPI_STORE, nullptr, dim, nullptr, nullptr, nullptr, dLogits_,
+                                    p.vocab0, nullptr, nullptr, nullptr, nullptr, nullptr, false);
+        consumer(a);
+        hipk::launchGemv(a, 1, hipk::PRO_PRENORM, hipk::EPI_STORE, true, stream_);
+    }
+}
+
 // The wo GEMV with the layer's attention in its prologue (PRO_ATTN, gemv_dev.h): every wo workgroup
 // recomputes the rank's decode attention from the L2-resident cache instead of waiting for an
 // attention launch, which at a TP-N rank's few heads is a handful of workgroups and a whole kernel
@@ -439,17 +562,35 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
     const bool bat = batchedPath(n);                                   // MFMA GEMMs on f16 activations
     const bool fz = bat && fuseNorm(n);                                // residual + norm in the GEMM epilogues
     const bool blk = blockOn_ && buckets_[bucket_].block && n == 1 && !bat;  // fused attention block
+    const bool pre = prenormNow(n, bat, blk);  // pre-normalized Q80 hand-offs between the GEMVs
     {
         ProfScope ps(this, "embedding");
         // the epoch counts the forwards that run the fused block (its counters' targets)
+        hipk::PrenormOut po;
+        po.resW = layers_[0].rmsAtt;
+        po.xq = dXQ_[0];
+        po.xs = dXS_[0];
+        po.ssp = dSSP_[0];
         hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_, blk ? dEpoch_ : nullptr,
-                              p.nRanks > 1 ? dSync_ : nullptr, p.nRanks > 1 ? syncSlots() : 0);
+                              p.nRanks > 1 ? dSync_ : nullptr, p.nRanks > 1 ? syncSlots() : 0, pre ? &po : nullptr);
+    }
+    // one greedy decode row: the logits GEMV ends in the row's argmax (EPI_ARGMAX: no logits
+    // written, no argmax launch; under TP the winners trade over the fused exchange's region)
+    const bool argTail = argTailOn_ && q40_ && !bat && !fz && n == 1 &&
+                         (kind == GraphKind::ARGMAX || kind == GraphKind::CHAIN) &&
+                         (p.nRanks == 1 || (tpFused_ && tpArg_.stride >= 2));
+    if (pre) {
+        enqueuePrenormLayers(kind, argTail);
+        if (argTail) {
+            DL_HIP(hipGetLastError());
+            return;
+        }
     }
     // Q80 hand-off of h needs one workgroup per 32 hidden units; for skinny TP shards the w13
     // epilogue emits f32 and w2 quantizes in its prologue instead.
     const bool hQ80 = q40_ && hQ80_;
     const bool woAttn = woAttnNow(n, bat, blk);  // attention inside the wo GEMV's prologue
-    for (u32 l = 0; l < h_.nLayers; l++) {
+    for (u32 l = 0; l < h_.nLayers && !pre; l++) {
         DevLayer &L = layers_[l];
         const bool hasDelta = l > 0;
         xSlot_ = 2 * (int)l;  // the wo exchange (fused in the wo kernel, or the all-reduce after it)
@@ -548,12 +689,7 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
         if (!fusedTp(bat) && !fz) allReduce(dY_, (size_t)n * dim);
     }
     xSlot_ = 2 * (int)h_.nLayers;  // logits gather / argmax winners
-    // one greedy decode row: the logits GEMV ends in the row's argmax (EPI_ARGMAX: no logits
-    // written, no argmax launch; under TP the winners trade over the fused exchange's region)
-    const bool argTail = argTailOn_ && q40_ && !bat && !fz && n == 1 &&
-                         (kind == GraphKind::ARGMAX || kind == GraphKind::CHAIN) &&
-                         (p.nRanks == 1 || (tpFused_ && tpArg_.stride >= 2));
-    {
+    if (!pre) {
         ProfScope ps(this, "gemv_logits");
         if (fz)
             gemmBatched(wcls_, n, hipk::EPI_STORE, nullptr, dim, nullptr, nullptr, nullptr, nullptr, dLogits_, p.vocab0,

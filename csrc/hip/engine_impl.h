@@ -92,6 +92,7 @@ class HipEngineImpl : public HipEngine {
     bool tpFused() const override { return tpFused_; }
     bool attnBlock() const override { return blockOn_; }
     bool woAttn() const override { return woAttnOn_; }
+    bool prenorm() const override { return prenormOn_; }
     std::vector<unsigned long long> traceAttnBlock(int token, int pos, int slot, int layer) override;
     int fusedGridMax() const override { return fusedGridMax_; }
     bool tpBatchedFused(int n) const override { return plan_.nRanks > 1 && batchedPath(n) && fuseNorm(n); }
@@ -221,6 +222,11 @@ class HipEngineImpl : public HipEngine {
     // the wo GEMV with the attention in its prologue (PRO_ATTN) for single decode rows of short
     // contexts when a rank holds few heads: decided once (setupWoAttn), taken per forward (woAttnNow)
     void setupWoAttn();
+    // pre-normalized hand-off for single decode rows (EPI_RESQ_TP producers -> PRO_PRENORM
+    // consumers): decided once (setupPrenorm), taken per forward (prenormNow)
+    void setupPrenorm();
+    bool prenormNow(int n, bool bat, bool blk) const { return prenormOn_ && n == 1 && !bat && !blk; }
+    void enqueuePrenormLayers(GraphKind kind, bool argTail);
     bool woAttnNow(int n, bool bat, bool blk) const {
         return woAttnOn_ && n == 1 && !bat && !blk && buckets_[bucket_].maxLen <= woAttnMaxLen_;
     }
@@ -313,6 +319,10 @@ class HipEngineImpl : public HipEngine {
     float *dY_ = nullptr, *dQ_ = nullptr, *dAtt_ = nullptr, *dH_ = nullptr, *dLogits_ = nullptr;
     float *dLogitsAll_ = nullptr, *dLogitsFull_ = nullptr;
     int8_t *dAttQ_ = nullptr, *dHQ_ = nullptr;
+    // pre-normalized hand-off (one row), by residual parity: Q80 of x * normW, scales, partial sums
+    int8_t *dXQ_[2] = {nullptr, nullptr};
+    float2 *dXS_[2] = {nullptr, nullptr};
+    float *dSSP_[2] = {nullptr, nullptr};
     float2 *dAttS_ = nullptr, *dHS_ = nullptr;
     _Float16 *dXh_ = nullptr, *dAttH_ = nullptr, *dHh_ = nullptr;
     float *dPart_ = nullptr;
@@ -341,6 +351,8 @@ class HipEngineImpl : public HipEngine {
     int *dBlockErr_ = nullptr;
     bool blockOn_ = false;   // decode rows may run the fused attention block (per bucket: CtxBucket::block)
     bool woAttnOn_ = false;  // setupWoAttn
+    bool prenormOn_ = false; // setupPrenorm
+    static constexpr int kMaxSsp = 256;  // producer workgroups of a pre-normalized hand-off
     int woAttnMaxLen_ = 256; // DL_WO_ATTN_LEN: context buckets up to this length
     int blockPassMul_ = 1;   // qkv / wo passes multiplier of the block's roles (same-GPU rehearsals)
     int traceLayer_ = -1;    // traceAttnBlock: the layer whose block launch is traced

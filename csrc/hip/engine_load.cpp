@@ -120,6 +120,11 @@ void HipEngineImpl::allocBuffers() {
     dAttS_ = dalloc<float2>((size_t)MB * p.q0 / 32);
     dHQ_ = dalloc<int8_t>((size_t)MB * p.hidden0);
     dHS_ = dalloc<float2>((size_t)MB * p.hidden0 / 32);
+    for (int i = 0; i < 2; i++) {
+        dXQ_[i] = dalloc<int8_t>(h_.dim);
+        dXS_[i] = dalloc<float2>((h_.dim + 31) / 32);
+        dSSP_[i] = dalloc<float>(kMaxSsp);
+    }
     {  // batched (MFMA) path, Q40 and F32 weights: f16 activations, split-K partials, counters
         const size_t rowsH = ((size_t)MB + 2 * kGemmMaxTokens - 1) / kGemmMaxTokens * kGemmMaxTokens;
         dXh_ = dalloc<_Float16>(rowsH * h_.dim);

@@ -25,7 +25,7 @@ static GemvLaunch gemvLaunchOf(const GemvArgs &a, int B, int pro, int epi, bool 
     const int R = (kThreads / L) * gemvRowGroup(B, q40) * a.passes;
     g.grid = (a.rows + R - 1) / R;
     g.lds = gemvLdsBytes(a.n, B, q40, R, pro);
-    if (q40 && epi == EPI_STORE_TP && a.tp.q80) {  // Q80 exchange staging reuses `act`
+    if (q40 && (epi == EPI_STORE_TP || epi == EPI_RESQ_TP) && a.tp.q80) {  // Q80 exchange staging reuses `act`
         const GemvLds lay = gemvLayout(a.n, B, true, R, PRO_RESNORM);
         g.lds = std::max(g.lds, lay.act + tpQ80Lds(B * R, a.tp.world));
     }

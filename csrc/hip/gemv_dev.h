@@ -149,7 +149,9 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
     int8_t *sq = reinterpret_cast<int8_t *>(smem + lay.act);
     float2 *ssc = reinterpret_cast<float2 *>(smem + lay.sc);
     float *res = reinterpret_cast<float *>(smem + lay.res);  // partial rows held for the TP exchange
-    constexpr bool tpx = EPI == EPI_STORE_TP;
+    constexpr bool tpx = EPI == EPI_STORE_TP || EPI == EPI_RESQ_TP;
+    constexpr bool pren = PRO == PRO_PRENORM;  // pre-normalized Q80 input (copy + 1 / rms)
+    static_assert(!pren || B == 1, "PRO_PRENORM: one row");
     const int tid = threadIdx.x, gi = tid / L, li = tid % L;
     const int rowBase = blk * R;
     // timestamps stay in SGPRs until the end: a store here would join the ring's vmcnt accounting
@@ -215,6 +217,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
         // waited for on its own inside it (the first slot's dot products start while the rest of
         // the first round is still in flight). Loads are unconditional and clamped.
         auto ld4a = [](f32x4 &r, const float *p) { asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p)); };
+        uint32_t spv = 0u;  // PRO_PRENORM: the producer's partial sum of squares
         u32x2 ropeV = {0u, 0u};
         if constexpr (EPI == EPI_QKV) {
             const float2 *rp = a.rope + (size_t)posB[0] * (a.hs >> 1) + min(tid, (a.hs >> 1) - 1);
@@ -243,6 +246,10 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
             for (int k = 0; k < PS; k++) {
                 const u32x2 *src = reinterpret_cast<const u32x2 *>(a.as) + min(tid + k * kThreads, nb - 1);
                 asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(es[k]) : "v"(src));
+            }
+            if constexpr (pren) {  // this thread's partial sum of squares (nSsp <= 256: one each)
+                const float *src = a.sspIn + min(tid, a.nSsp - 1);
+                asm volatile("global_load_dword %0, %1, off" : "=v"(spv) : "v"(src));
             }
         }
         // A CU returns vector loads in issue order across its waves: without this barrier a wave's
@@ -273,6 +280,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
             for (int k = 0; k < PK; k++) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(eq[k]) : "i"(3 * KE));
 #pragma unroll
             for (int k = 0; k < PS; k++) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(es[k]) : "i"(3 * KE));
+            if constexpr (pren) asm volatile("s_waitcnt vmcnt(%1)" : "+v"(spv) : "i"(3 * KE));
         }
         if (a.trace) tLoaded = wall_clock64();
         if constexpr (EPI == EPI_QKV)
@@ -320,12 +328,23 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
                 }
             }
         } else {
+            float inv = 1.0f;
+            if constexpr (pren) {  // 1 / rms from the producer's partials, summed in workgroup order
+                const float ss = blockSum<kThreads>(tid < a.nSsp ? __uint_as_float(spv) : 0.f, scratch);
+                inv = 1.0f / sqrtf(ss / (float)n + a.eps);
+            }
 #pragma unroll
             for (int k = 0; k < PK; k++)
                 if (tid + k * kThreads < n16) reinterpret_cast<u32x4 *>(sq)[tid + k * kThreads] = eq[k];
 #pragma unroll
             for (int k = 0; k < PS; k++)
-                if (tid + k * kThreads < nb) reinterpret_cast<u32x2 *>(ssc)[tid + k * kThreads] = es[k];
+                if (tid + k * kThreads < nb) {
+                    u32x2 e = es[k];
+                    // the block's scale of x * normW / rms: f16(d' / rms), as the norm prologue's
+                    // f16(amax(x * normW / rms) / 127) up to the last ulp (stageChunk)
+                    if constexpr (pren) e.x = __float_as_uint(roundF16(__uint_as_float(e.x) * inv));
+                    reinterpret_cast<u32x2 *>(ssc)[tid + k * kThreads] = e;
+                }
         }
         __syncthreads();
         if (a.trace) tReady = wall_clock64();
@@ -440,7 +459,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
 #pragma unroll
             for (int b = 0; b < B; b++) {
                 const float v0 = acc[0][b], v1 = acc[1][b];
-                if constexpr (EPI == EPI_STORE_TP || EPI == EPI_ARGMAX) {
+                if constexpr (EPI == EPI_STORE_TP || EPI == EPI_RESQ_TP || EPI == EPI_ARGMAX) {
                     res[b * R + (r0 - rowBase)] = v0;
                     res[b * R + (r0 - rowBase) + 1] = v1;
                 } else if constexpr (EPI == EPI_STORE) {
@@ -493,8 +512,8 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
     staticFor<D>(lastSlot);
     };
 
-    const int unitsPerThread = PRO != PRO_GLOBAL ? (n + 8 * kThreads - 1) / (8 * kThreads)
-                                                  : (n + 16 * kThreads - 1) / (16 * kThreads);
+    const int unitsPerThread = (PRO != PRO_GLOBAL && PRO != PRO_PRENORM) ? (n + 8 * kThreads - 1) / (8 * kThreads)
+                                                                         : (n + 16 * kThreads - 1) / (16 * kThreads);
     static_assert(MODE != GEMV_CONSUMER || PRO == PRO_GLOBAL, "a consumer GEMV reads Q80 activations");
     if constexpr (PRO == PRO_ATTN) {
         attnPath();
@@ -545,10 +564,22 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
         const unsigned long long xs = a.tp.span ? wall_clock64() : 0ull;
         tpDispatch(a.tp.world, [&](auto wm) {
             constexpr int WM = decltype(wm)::value;
-            if (a.tp.q80 && B == 1) tpExchangeQ80Row<WM>(a, res, R, rowBase);
-            else if (a.tp.q80) tpExchangeQ80<B, WM>(a, res, R, rowBase, reinterpret_cast<char *>(sq));
-            else tpExchangeF32<B, WM>(a, res, R, rowBase);
+            if constexpr (EPI == EPI_RESQ_TP) {  // sums back into res[], then the residual + norm tail
+                static_assert(B == 1, "EPI_RESQ_TP: one row");
+                if (a.tp.q80) tpExchangeQ80Row<WM, true>(a, res, R, rowBase);
+                else tpExchangeF32<1, WM, true>(a, res, R, rowBase);
+            } else if (a.tp.q80 && B == 1) {
+                tpExchangeQ80Row<WM>(a, res, R, rowBase);
+            } else if (a.tp.q80) {
+                tpExchangeQ80<B, WM>(a, res, R, rowBase, reinterpret_cast<char *>(sq));
+            } else {
+                tpExchangeF32<B, WM>(a, res, R, rowBase);
+            }
         });
+        if constexpr (EPI == EPI_RESQ_TP) {
+            __syncthreads();
+            resqTail(a, res, R, rowBase, blk, scratch);
+        }
         if (a.tp.span) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();

@@ -144,7 +144,17 @@ static const void *gemvFnPE(int pro, int epi) {
         DL_GEMV_CASE(PRO_RESNORM, EPI_ACT_Q80)
         DL_GEMV_CASE(PRO_GLOBAL, EPI_STORE_TP)
         DL_GEMV_CASE(PRO_RESNORM, EPI_STORE_TP)
-        if constexpr (B == 1) DL_GEMV_CASE(PRO_RESNORM, EPI_ARGMAX)
+        if constexpr (B == 1) {
+            DL_GEMV_CASE(PRO_RESNORM, EPI_ARGMAX)
+            // pre-normalized hand-off (tensor-parallel single rows): producers and consumers
+            DL_GEMV_CASE(PRO_GLOBAL, EPI_RESQ_TP)
+            DL_GEMV_CASE(PRO_RESNORM, EPI_RESQ_TP)
+            DL_GEMV_CASE(PRO_PRENORM, EPI_QKV)
+            DL_GEMV_CASE(PRO_PRENORM, EPI_ACT)
+            DL_GEMV_CASE(PRO_PRENORM, EPI_ACT_Q80)
+            DL_GEMV_CASE(PRO_PRENORM, EPI_STORE)
+            DL_GEMV_CASE(PRO_PRENORM, EPI_ARGMAX)
+        }
     }
 #undef DL_GEMV_CASE
     return nullptr;

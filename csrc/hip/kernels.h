@@ -31,14 +31,33 @@ namespace hipk {
 //             decode attention for every head of the rank is computed in the prologue of EVERY
 //             workgroup (redundantly, from L2) and quantized to Q80 into LDS - no attention
 //             launch and no hand-off (launchGemvAttn; the engine takes it for few heads per rank).
-enum Prologue : int { PRO_GLOBAL = 0, PRO_RESNORM = 1, PRO_ATTN = 2 };
+// PRO_PRENORM (Q40 ring GEMV, one row): the producer of this input (EPI_RESQ_TP, or the embedding)
+//             already applied the residual update and the RMS norm's weights and quantized
+//             x * normW to Q80 blocks (aq / as, unrounded block scale d' = amax / 127); the
+//             workgroup only sums the producer's per-workgroup sums of squares (sspIn, nSsp, in
+//             order) and folds 1 / rms into each block scale (d = f16(d' / rms)) while copying.
+enum Prologue : int { PRO_GLOBAL = 0, PRO_RESNORM = 1, PRO_ATTN = 2, PRO_PRENORM = 3 };
 // EPI_ACT_Q80: act(w1 x) * (w3 x), quantized to Q80 blocks for the next GEMV (32 hidden units/block).
 // EPI_STORE_TP: EPI_STORE whose rows are first all-reduced over the tensor-parallel ranks (GemvArgs::tp).
 // EPI_RES (batched GEMMs): residual update fused with the next RMS norm's elementwise half - see
 // GemmArgs::resIn.
 // EPI_ARGMAX (Q40 GEMV, one row, greedy logits): no logits are stored; the row's argmax (GemvArgs::am).
+// EPI_RESQ_TP (Q40 GEMV, one row, 32-row workgroups): EPI_STORE_TP's rank-order sum, then the
+// residual update and the NEXT RMS norm's elementwise half in the tail (GemvArgs::rq): x' = resIn +
+// sum -> resOut, x' * resW quantized to Q80 blocks -> xq / xs, and this workgroup's sum of x'^2 ->
+// ssp[workgroup] (the consumer, PRO_PRENORM, finishes the norm).
 enum Epilogue : int { EPI_STORE = 0, EPI_ACT = 1, EPI_QKV = 2, EPI_ACT_Q80 = 3, EPI_ACT_F16 = 4, EPI_STORE_TP = 5, EPI_RES = 6,
-                      EPI_ARGMAX = 7 };
+                      EPI_ARGMAX = 7, EPI_RESQ_TP = 8 };
+
+// Pre-normalized hand-off (EPI_RESQ_TP producer / embedding -> PRO_PRENORM consumer), one row.
+struct PrenormOut {
+    const float *resIn = nullptr;  // residual before this update (producer)
+    float *resOut = nullptr;       // x' = residual after it
+    const float *resW = nullptr;   // the next RMS norm's weights
+    int8_t *xq = nullptr;          // [n] Q80 values of x' * resW
+    float2 *xs = nullptr;          // [n / 32] (d' = amax / 127 unrounded, sum of q)
+    float *ssp = nullptr;          // [workgroups] sums of x'^2
+};
 
 // Q40 weights live on the device TILED in the ring GEMV's consumption order, for a lanes-per-row
 // count L fixed per matrix (NG = 256/L row pairs per workgroup pass, K = ceil(nb/L) steps):
@@ -192,6 +211,9 @@ struct GemvArgs {
     // the kernel tail before `out` is written (exchange element = b * ldOut + row)
     TpXchg tp;
     ArgmaxTail am;  // EPI_ARGMAX
+    PrenormOut rq;  // EPI_RESQ_TP
+    const float *sspIn = nullptr;  // PRO_PRENORM: the producer's per-workgroup sums of squares
+    int nSsp = 0;                  //   (<= 256) summed in order; aq / as hold its Q80 blocks
     // diagnostics (gemvQ40Kernel): when set, workgroup g writes 8 u64 at trace[8g..]: s_memrealtime
     // at entry, prologue done, exit, (HW_ID << 32 | XCC_ID), prologue loads landed (early path),
     // first ring slot consumed (thread 0's view)
@@ -367,7 +389,8 @@ int attnChunkMax(int seqLen, int splitGrid);
 // sync / nSync (optional): the measured-sync slots of the previous forward (syncFoldWords layout)
 // are folded into their running totals, then cleared for this forward.
 void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s,
-                     unsigned *epoch = nullptr, unsigned *sync = nullptr, int nSync = 0);
+                     unsigned *epoch = nullptr, unsigned *sync = nullptr, int nSync = 0,
+                     const PrenormOut *pre = nullptr);  // B == 1: also the first layer's PRO_PRENORM input
 // Measured-sync slot layout (u32 words) for S slots: [0, S) the longest peer wait of each exchange,
 // [S, 2S) the longest exchange tail (span), [2S, 6S) a u64 stamp pair per slot (a separate
 // collective), then 4 u64 running totals over folded forwards: wait, span, stamped, forwards.

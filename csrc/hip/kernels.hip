@@ -233,7 +233,7 @@ void launchAttentionValu(const AttnArgs &a, int B, hipStream_t s) {
 // Small kernels
 // ------------------------------------------------------------------------------------------------
 __global__ void embeddingKernel(const float *table, const int *tokens, float *x, int dim, unsigned *epoch,
-                                unsigned *sync, int S) {
+                                unsigned *sync, int S, PrenormOut pre) {
     const int b = blockIdx.x;
     // the forward's epoch, read by later kernels: a no-return atomic (the wave does not wait on a
     // read-modify-write round trip before its row loads)
@@ -261,6 +261,7 @@ __global__ void embeddingKernel(const float *table, const int *tokens, float *x,
     }
     const float *src = table + (size_t)tokens[b] * dim;
     float *dst = x + (size_t)b * dim;
+    extern __shared__ float xs[];  // the row (pre.xq set: dim floats of dynamic LDS)
     // all of a thread's row loads in flight before the first store (one HBM round trip, not four)
     constexpr int U = 4;
     for (int i0 = threadIdx.x * 4; i0 < dim; i0 += U * blockDim.x * 4) {
@@ -274,13 +275,50 @@ __global__ void embeddingKernel(const float *table, const int *tokens, float *x,
         for (int u = 0; u < U; u++) {
             const int i = i0 + u * blockDim.x * 4;
             if (i < dim) st4(dst + i, v[u]);
+            if (pre.xq && i < dim) st4(xs + i, v[u]);
         }
+    }
+    if (!pre.xq) return;
+    // one decode row (B == 1): the first layer's pre-normalized input (PrenormOut, PRO_PRENORM):
+    // x * rmsAtt as Q80 blocks with the unrounded d' = amax / 127, and sum(x^2) as one partial
+    __syncthreads();
+    float ss = 0.f;
+    for (int base = 0; base < dim; base += blockDim.x) {  // dim % 32 == 0: whole 32-lane groups
+        const int i = base + threadIdx.x;
+        const float xv = i < dim ? xs[i] : 0.f;
+        const float g = i < dim ? xv * pre.resW[i] : 0.f;
+        ss += xv * xv;
+        const float amax = groupMax<32>(fabsf(g));
+        const float d = amax / 127.0f;
+        const float id = d != 0.f ? 1.0f / d : 0.f;
+        int q = (int)rintf(g * id);
+        q = q > 127 ? 127 : (q < -127 ? -127 : q);
+        const float qs = groupSum<32>((float)q);
+        if (i < dim) pre.xq[i] = (int8_t)q;
+        if (i < dim && (i & 31) == 0) pre.xs[i >> 5] = make_float2(d, qs);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) ss += __shfl_xor(ss, off);
+    __shared__ float red[16];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float t = 0.f;
+        for (int w = 0; w < (int)(blockDim.x >> 6); w++) t += red[w];
+        pre.ssp[0] = t;
     }
 }
 
 void launchEmbedding(const float *table, const int *tokens, float *x, int dim, int B, hipStream_t s, unsigned *epoch,
-                     unsigned *sync, int nSync) {
-    hipLaunchKernelGGL(embeddingKernel, dim3(B), dim3(256), 0, s, table, tokens, x, dim, epoch, sync, nSync);
+                     unsigned *sync, int nSync, const PrenormOut *pre) {
+    PrenormOut p;
+    size_t lds = 0;
+    if (pre) {
+        if (B != 1 || dim % 32 || (size_t)dim * 4 > 65536) throw Error("launchEmbedding: prenorm output needs one row, dim % 32 == 0, dim <= 16384");
+        p = *pre;
+        lds = (size_t)dim * 4;
+    }
+    hipLaunchKernelGGL(embeddingKernel, dim3(B), dim3(256), lds, s, table, tokens, x, dim, epoch, sync, nSync, p);
 }
 
 __global__ void stampKernel(unsigned long long *p) {

@@ -403,6 +403,32 @@ def test_attn_block_matches_separate_kernels(C, assets, medium, monkeypatch, kv_
         assert list(ca) == list(cb)
 
 
+@pytest.mark.parametrize("sync", ["q80", "f32"])
+def test_prenorm_handoff_matches_norm_prologue(C, medium, monkeypatch, sync):
+    """A TP rank's single decode rows with the pre-normalized hand-off (wo / w2 exchange tails apply
+    the residual update and the next norm's weights and emit Q80 blocks + sums of squares; qkv,
+    w13 and the logits GEMV only copy them and fold in 1 / rms) vs the norm prologues: the same
+    shard logits up to Q80 rounding ties and the same greedy chain (rank in loopback). The f32
+    exchange keeps 16-row workgroups, so the hand-off stays off there (same results both ways)."""
+    out = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("DL_PRENORM", on)
+        e = C.HipEngine(medium, "q80", max_batch=8, rank=0, world=2, comm=C.ComputeOnlyComm(0, 2, 0),
+                        sync_type=sync, kv_bf16=False)
+        assert bool(e.prenorm) == (on == "1" and sync == "q80")
+        v0 = e.header["vocab_size"] // 2
+        toks = [3, 17, 101, 7, 250, 9]
+        lg = np.stack([e.forward([t], [p], [0])[0][:v0] for p, t in enumerate(toks)])
+        _, ch = e.decode_greedy(12, [int(lg[-1].argmax())], [len(toks)], [0])
+        ids = [e.forward_argmax([t], [p], [0])[0] for p, t in enumerate(toks)]  # the EPI_ARGMAX consumer
+        out[on] = (lg, list(ch), ids)
+        del e
+    assert np.isfinite(out["1"][0]).all()
+    assert _rel(out["1"][0], out["0"][0]) < 2e-3
+    assert sum(a == b for a, b in zip(out["1"][1], out["0"][1])) >= 10, (out["1"][1], out["0"][1])
+    assert out["1"][2] == [int(i) for i in out["1"][0].argmax(-1)]
+
+
 @pytest.mark.parametrize("world", [2])
 def test_wo_attention_prologue_matches_attention_launch(C, medium, monkeypatch, world):
     """DL_WO_ATTN=1: a TP rank's wo GEMV computes the layer's decode attention in every workgroup's
