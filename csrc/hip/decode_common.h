@@ -666,8 +666,22 @@ __device__ __forceinline__ void tpExchangeQ80(const GemvArgs &a, const float *re
 // of row rowBase + i. x' = resIn + delta -> resOut; x' * resW quantized to Q80 blocks (d' =
 // amax / 127 unrounded: the consumer folds in 1 / rms and rounds) -> xq / xs; the workgroup's
 // sum of x'^2 -> ssp[blk]. Uniform loop over whole 32-lane groups (one block each).
+// resqPrefetch: this thread's residual and norm weight (R <= 256: one row per thread), loaded
+// before the exchange so their round trip overlaps the peers' wait instead of following it.
+struct ResqPre {
+    float x = 0.f, w = 0.f;
+};
+__device__ __forceinline__ ResqPre resqPrefetch(const GemvArgs &a, int R, int rowBase) {
+    ResqPre p;
+    const int row = rowBase + (int)threadIdx.x;
+    if ((int)threadIdx.x < R && row < a.rows) {
+        p.x = a.rq.resIn[row];
+        p.w = a.rq.resW[row];
+    }
+    return p;
+}
 __device__ __forceinline__ void resqTail(const GemvArgs &a, const float *res, int R, int rowBase, int blk,
-                                         float *scratch) {
+                                         float *scratch, ResqPre pf) {
     const PrenormOut &o = a.rq;
     float ss = 0.f;
     for (int base = 0; base < R; base += kThreads) {
@@ -675,9 +689,10 @@ __device__ __forceinline__ void resqTail(const GemvArgs &a, const float *res, in
         const bool live = i < R && row < a.rows;  // a.rows % 32 == 0: whole blocks live or dead
         float g = 0.f;
         if (live) {
-            const float xn = o.resIn[row] + res[i];
+            const bool pre1 = R <= kThreads;  // prefetched (one row per thread)
+            const float xn = (pre1 ? pf.x : o.resIn[row]) + res[i];
             o.resOut[row] = xn;
-            g = xn * o.resW[row];
+            g = xn * (pre1 ? pf.w : o.resW[row]);
             ss += xn * xn;
         }
         const float amax = groupMax<32>(fabsf(g));
@@ -688,6 +703,14 @@ __device__ __forceinline__ void resqTail(const GemvArgs &a, const float *res, in
         const float qs = groupSum<32>((float)q);
         if (live) o.xq[row] = (int8_t)q;
         if (live && (i & 31) == 0) o.xs[row >> 5] = make_float2(d, qs);
+    }
+    if (R <= 64) {  // every row in wave 0: a wave reduction, no workgroup barrier
+        if (threadIdx.x < 64) {
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) ss += __shfl_xor(ss, off);
+            if (threadIdx.x == 0) o.ssp[blk] = ss;
+        }
+        return;
     }
     ss = blockSum<kThreads>(ss, scratch);
     if (threadIdx.x == 0) o.ssp[blk] = ss;

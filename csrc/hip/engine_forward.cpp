@@ -305,7 +305,9 @@ void HipEngineImpl::enqueuePrenormLayers(GraphKind kind, bool argTail) {
     const ShardPlan &p = plan_;
     const int dim = h_.dim;
     const bool hQ80 = hQ80_;
-    int cur = 0, sspN[2] = {1, 0};  // the embedding produced parity 0 with one partial
+    // layer 0's qkv normalizes the embedding's row itself (norm prologue): the one-workgroup
+    // embedding kernel measured 12.8 vs 4.9 us with the pre-normalized output (PrenormOut)
+    int cur = 0, sspN[2] = {0, 0};
     auto consumer = [&](hipk::GemvArgs &a) {
         a.aq = dXQ_[cur];
         a.as = dXS_[cur];
@@ -326,7 +328,10 @@ void HipEngineImpl::enqueuePrenormLayers(GraphKind kind, bool argTail) {
         DevLayer &L = layers_[l];
         xSlot_ = 2 * (int)l;
         xChunk_ = 0;
-        {
+        if (l == 0) {
+            ProfScope ps(this, "gemv_qkv");
+            gemv(L.qkv, 1, hipk::PRO_RESNORM, hipk::EPI_QKV, dX_[0], dim, nullptr, nullptr, L.rmsAtt, dQ_, p.q0, &L);
+        } else {
             ProfScope ps(this, "gemv_qkv");
             hipk::GemvArgs a = gemvArgs(L.qkv, 0, 1, hipk::EPI_QKV, nullptr, dim, nullptr, nullptr, nullptr, dQ_, p.q0, &L,
                                         nullptr, nullptr, nullptr, nullptr, false);
@@ -566,13 +571,8 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
     {
         ProfScope ps(this, "embedding");
         // the epoch counts the forwards that run the fused block (its counters' targets)
-        hipk::PrenormOut po;
-        po.resW = layers_[0].rmsAtt;
-        po.xq = dXQ_[0];
-        po.xs = dXS_[0];
-        po.ssp = dSSP_[0];
         hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_, blk ? dEpoch_ : nullptr,
-                              p.nRanks > 1 ? dSync_ : nullptr, p.nRanks > 1 ? syncSlots() : 0, pre ? &po : nullptr);
+                              p.nRanks > 1 ? dSync_ : nullptr, p.nRanks > 1 ? syncSlots() : 0);
     }
     // one greedy decode row: the logits GEMV ends in the row's argmax (EPI_ARGMAX: no logits
     // written, no argmax launch; under TP the winners trade over the fused exchange's region)

@@ -562,6 +562,8 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
         // exchange span (DL_SYNC_MEASURE=2, a.tp.span set): this workgroup's tail, first push to
         // last summed store, raised into the exchange's slot (the longest tail of the launch)
         const unsigned long long xs = a.tp.span ? wall_clock64() : 0ull;
+        ResqPre rpf;
+        if constexpr (EPI == EPI_RESQ_TP) rpf = resqPrefetch(a, R, rowBase);
         tpDispatch(a.tp.world, [&](auto wm) {
             constexpr int WM = decltype(wm)::value;
             if constexpr (EPI == EPI_RESQ_TP) {  // sums back into res[], then the residual + norm tail
@@ -578,7 +580,7 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
         });
         if constexpr (EPI == EPI_RESQ_TP) {
             __syncthreads();
-            resqTail(a, res, R, rowBase, blk, scratch);
+            resqTail(a, res, R, rowBase, blk, scratch, rpf);
         }
         if (a.tp.span) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -283,10 +283,23 @@ __global__ void embeddingKernel(const float *table, const int *tokens, float *x,
     // x * rmsAtt as Q80 blocks with the unrounded d' = amax / 127, and sum(x^2) as one partial
     __syncthreads();
     float ss = 0.f;
+    constexpr int WU = 16;  // norm weights of 16 passes loaded at once (one round trip, not 16)
+    float wv[WU];
     for (int base = 0; base < dim; base += blockDim.x) {  // dim % 32 == 0: whole 32-lane groups
+        const int u = (base / blockDim.x) % WU;
+        if (u == 0) {
+#pragma unroll
+            for (int k = 0; k < WU; k++) {
+                const int j = base + k * blockDim.x + threadIdx.x;
+                wv[k] = j < dim ? pre.resW[j] : 0.f;
+            }
+        }
         const int i = base + threadIdx.x;
         const float xv = i < dim ? xs[i] : 0.f;
-        const float g = i < dim ? xv * pre.resW[i] : 0.f;
+        float w = 0.f;
+#pragma unroll
+        for (int k = 0; k < WU; k++) w = k == u ? wv[k] : w;
+        const float g = i < dim ? xv * w : 0.f;
         ss += xv * xv;
         const float amax = groupMax<32>(fabsf(g));
         const float d = amax / 127.0f;
