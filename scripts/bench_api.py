@@ -71,6 +71,7 @@ def main():
     ap.add_argument("--kv-pages", type=int, default=0,
                     help="paged KV cache: pool pages per layer (0: contiguous slots x seq_len)")
     ap.add_argument("--kv-page-size", type=int, default=64)
+    ap.add_argument("--kv-dtype", default="f32", choices=["f32", "bf16"], help="KV cache (f32: the reference's, the default)")
     args = ap.parse_args()
     from distributed_llama_multiusers_amd.models.synthetic import make_tokenizer
     tmp = tempfile.mkdtemp()
@@ -79,7 +80,7 @@ def main():
     port = args.port or _port()
     cmd = [os.path.join(REPO, "build", "dllama-api"), "--synthetic", "llama3_1_8b", "--tokenizer", tok,
            "--gpu-index", "0", "--port", str(port), "--slots", str(args.n), "--max-batch", str(args.max_batch or 4 * args.n),
-           "--max-seq-len", str(64 + args.max_tokens + 32), "--buffer-float-type", "q80"]
+           "--max-seq-len", str(64 + args.max_tokens + 32), "--buffer-float-type", "q80", "--kv-dtype", args.kv_dtype]
     if args.kv_pages:
         cmd += ["--kv-pages", str(args.kv_pages), "--kv-page-size", str(args.kv_page_size)]
     log = open(os.path.join(tmp, "api.log"), "w")
@@ -117,6 +118,7 @@ def main():
             print(name, res[name], flush=True)
         res["sampled_vs_greedy"] = round(res["sampled"]["tok_s"] / res["greedy"]["tok_s"], 3)
         res["concurrent_requests"] = args.n
+        res["kv_cache"] = args.kv_dtype
         res["max_batch"] = args.max_batch or 4 * args.n
         res["max_tokens"] = args.max_tokens
         print(json.dumps(res), flush=True)
