@@ -20,6 +20,8 @@ namespace hipk {
 // K / V tiles of 32 keys are staged global -> registers -> LDS (double-buffered, the next tile's
 // loads in flight during the current tile's MFMAs). Long contexts split the keys into chunks of
 // 256 over grid.y; the last-arriving chunk combines the partials (as attnFinish).
+// An f32 cache (the reference's KV precision) runs the same schedule on v_mfma_f32_16x16x4_f32
+// (attnPrefillF32Kernel below): f32 Q, K, V and P, no rounding beyond f32 reassociation.
 // ------------------------------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -28,7 +30,8 @@ static constexpr int kPfVtStride = 40;  // bf16 per transposed-V row in LDS (32 
 
 int attnPrefillRowsPerBlock(int kvMul) { return kPfWaves * (16 / kvMul); }
 bool attnPrefillSupported(int hs, int kvMul, bool kvBf16) {
-    return kvBf16 && (hs == 64 || hs == 128) && kvMul >= 1 && kvMul <= 16 && (kvMul & (kvMul - 1)) == 0;
+    (void)kvBf16;  // bf16: attnPrefillKernel (or the LDS-DMA kernel), f32: attnPrefillF32Kernel
+    return (hs == 64 || hs == 128) && kvMul >= 1 && kvMul <= 16 && (kvMul & (kvMul - 1)) == 0;
 }
 
 __device__ __forceinline__ bf16x8 f32x8ToBf16(const float (&v)[8]) {
@@ -36,6 +39,99 @@ __device__ __forceinline__ bf16x8 f32x8ToBf16(const float (&v)[8]) {
 #pragma unroll
     for (int j = 0; j < 8; j++) r[j] = (__bf16)v[j];
     return r;
+}
+
+// Shared tail of both prefill kernels: normalize and store (one chunk), or publish the chunk's
+// partials and let the last-arriving chunk combine them. wts ([64 columns][nSplit]) and tot ([64])
+// reuse the workgroup's K / V tile LDS.
+template <int HS>
+__device__ __forceinline__ void pfFinish(const AttnArgs &a, int nRows, const f32x4 (&o)[HS / 16], float m, float lsum,
+                                         int nSplit, int rb, int g, int c, int b0, int row, int head, float *wts,
+                                         float *tot, int &flagL) {
+    constexpr int NT = HS / 16;
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 4;
+    const int kvMul = a.kvMul, rpb = kPfWaves * (16 / kvMul), nKv = a.nHeads0 / kvMul;
+    const bool rowOk = row < nRows;
+    lsum += __shfl_xor(lsum, 16);
+    lsum += __shfl_xor(lsum, 32);
+    // O^T accumulators: lane holds O[column][dim 16 n + 4 h + i]
+    auto writeOut = [&](int r, int hd, int d, const float (&v)[4]) {
+        const size_t at = (size_t)r * a.ldOut + (size_t)hd * HS + d;
+        if (a.outH) {
+            typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<h4 *>(a.outH + at) = h4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+        } else {
+            *reinterpret_cast<float4 *>(a.out + at) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+    };
+    if (nSplit == 1) {
+        if (rowOk) {
+            const float il = lsum > 0.f ? 1.0f / lsum : 0.f;
+#pragma unroll
+            for (int n = 0; n < NT; n++) {
+                const float v[4] = {o[n][0] * il, o[n][1] * il, o[n][2] * il, o[n][3] * il};
+                writeOut(row, head, 16 * n + 4 * h, v);
+            }
+        }
+        return;
+    }
+    // several chunks: publish (every column of the block, masked ones as (-inf, 0, 0)), count in,
+    // the last arriver combines
+    const int G = a.splitGrid;
+    // fence-free hand-off (see gemmFinish): agent-scope atomic stores here, atomic loads below
+    auto st = [](float *q, float v) { __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto ld = [](const float *q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    if (rowOk) {
+        const size_t pb = ((size_t)row * a.nHeads0 + head) * G + c;
+#pragma unroll
+        for (int n = 0; n < NT; n++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) st(a.partO + pb * HS + 16 * n + 4 * h + e, o[n][e]);
+        if (h == 0) {
+            st(a.partML + pb * 2, m);
+            st(a.partML + pb * 2 + 1, lsum);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int *cnt = a.counters + (size_t)rb * nKv + g;
+    if (tid == 0) flagL = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nSplit - 1;
+    __syncthreads();
+    if (!flagL) return;
+    if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // per column: chunk weights exp(m_c - M) and the total sum (LDS: the tiles are free now)
+    const int nCol = rpb * kvMul;  // 64 columns
+    if (tid < nCol) {
+        const int r = b0 + tid / kvMul, hd = g * kvMul + tid % kvMul;
+        float M = -INFINITY, L = 0.f;
+        if (r < nRows) {
+            const float *ml = a.partML + ((size_t)r * a.nHeads0 + hd) * G * 2;
+            for (int cc = 0; cc < nSplit; cc++) M = fmaxf(M, ld(ml + 2 * cc));
+            for (int cc = 0; cc < nSplit; cc++) {
+                const float mc = ld(ml + 2 * cc);
+                const float w = (M == -INFINITY || mc == -INFINITY) ? 0.f : __expf(mc - M);
+                wts[tid * nSplit + cc] = w;
+                L += w * ld(ml + 2 * cc + 1);
+            }
+        }
+        tot[tid] = L;
+    }
+    __syncthreads();
+    for (int i = tid; i < nCol * (HS / 4); i += kPfThreads) {
+        const int cl = i / (HS / 4), d = (i % (HS / 4)) * 4;
+        const int r = b0 + cl / kvMul, hd = g * kvMul + cl % kvMul;
+        if (r >= nRows) continue;
+        const float *po = a.partO + ((size_t)r * a.nHeads0 + hd) * G * HS + d;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int cc = 0; cc < nSplit; cc++) {
+            const float w = wts[cl * nSplit + cc];
+            const float *x = po + (size_t)cc * HS;
+            acc[0] += w * ld(x); acc[1] += w * ld(x + 1); acc[2] += w * ld(x + 2); acc[3] += w * ld(x + 3);
+        }
+        const float il = tot[cl] > 0.f ? 1.0f / tot[cl] : 0.f;
+        const float v[4] = {acc[0] * il, acc[1] * il, acc[2] * il, acc[3] * il};
+        writeOut(r, hd, d, v);
+    }
 }
 
 template <int HS>
@@ -163,88 +259,133 @@ __global__ __launch_bounds__(kPfThreads) void attnPrefillKernel(AttnArgs a, int 
         if (more) lstore(buf ^ 1);
         __syncthreads();
     }
-    lsum += __shfl_xor(lsum, 16);
-    lsum += __shfl_xor(lsum, 32);
-    // O^T accumulators: lane holds O[column][dim 16 n + 4 h + i]
-    auto writeOut = [&](int r, int hd, int d, const float (&v)[4]) {
-        const size_t at = (size_t)r * a.ldOut + (size_t)hd * HS + d;
-        if (a.outH) {
-            typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-            *reinterpret_cast<h4 *>(a.outH + at) = h4{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
-        } else {
-            *reinterpret_cast<float4 *>(a.out + at) = make_float4(v[0], v[1], v[2], v[3]);
+    pfFinish<HS>(a, nRows, o, m, lsum, nSplit, rb, g, c, b0, row, head, reinterpret_cast<float *>(&kT[0][0]),
+                 reinterpret_cast<float *>(&vT[0][0]), flagL);
+}
+
+// f32 cache: the same row-block schedule on v_mfma_f32_16x16x4_f32 (A: lane (col, h) holds
+// A[col][h], B: B[h][col], D: D[4 h + i][col]). S^T: MFMA e multiplies K[key 16 u + col][dim
+// QD h + e] by Q[column col][dim QD h + e] (lane group h owns a contiguous quarter of the head,
+// read as 16-byte LDS vectors); O^T: MFMA (u, i) multiplies V[key 16 u + 4 h + i][dim 16 n + col]
+// by P[key 16 u + 4 h + i][col], which is exactly the S^T accumulator lane (col, h) already holds,
+// so P never moves. K and V stay row-major in LDS (row stride HS + 4 floats: the 16 columns of a
+// K read and the two lane groups of a V read fall on distinct banks). One tile buffer (34 KB) so
+// four workgroups share a CU; the next tile's loads are in flight during the MFMAs.
+template <int HS>
+__global__ __launch_bounds__(kPfThreads) void attnPrefillF32Kernel(AttnArgs a, int nRows) {
+    constexpr int NT = HS / 16, QD = HS / 4, SR = HS + 4;
+    constexpr int U4 = HS / 4;                        // 16-byte units per key row
+    constexpr int PER = kPfTile * U4 / kPfThreads;    // 16-byte units per thread per operand and tile
+    static_assert(PER >= 1 && kPfTile * U4 % kPfThreads == 0, "tile / workgroup shape");
+    static_assert(kPfTile * SR >= 64 * (HS / 2), "combine weights must fit the K tile");
+    __shared__ __attribute__((aligned(16))) float kT[1][kPfTile * SR];
+    __shared__ __attribute__((aligned(16))) float vT[1][kPfTile * SR];
+    __shared__ int flagL;
+    const int kvMul = a.kvMul, rpw = 16 / kvMul, rpb = kPfWaves * rpw, nKv = a.nHeads0 / kvMul;
+    const int g = blockIdx.x % nKv, rb = blockIdx.x / nKv, c = blockIdx.y;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, col = lane & 15, h = lane >> 4;
+    const int b0 = rb * rpb;
+    int maxLen = 0;
+    for (int r = 0; r < rpb && b0 + r < nRows; r++) maxLen = max(maxLen, a.pos[b0 + r] + 1);
+    int nSplit = (maxLen + kPfChunk - 1) / kPfChunk;
+    nSplit = max(1, min(min(nSplit, a.splitGrid), HS / 2));
+    const int ch = ((maxLen + nSplit - 1) / nSplit + kPfTile - 1) / kPfTile * kPfTile;
+    if (c >= nSplit) return;
+    const int k0 = c * ch, k1 = min(k0 + ch, maxLen);
+    const int sl = a.slot[b0];
+    const int row = b0 + wave * rpw + col / kvMul, head = g * kvMul + col % kvMul;
+    const bool rowOk = row < nRows;
+    const int myLen = rowOk ? a.pos[row] + 1 : 0;
+    const float scale = 1.0f / sqrtf((float)HS);
+    float q[QD];
+#pragma unroll
+    for (int e = 0; e < QD; e += 4) {
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (rowOk) x = ld4(a.q + (size_t)row * a.ldq + (size_t)head * HS + QD * h + e);
+        q[e] = x.x * scale; q[e + 1] = x.y * scale; q[e + 2] = x.z * scale; q[e + 3] = x.w * scale;
+    }
+    const float *kc = reinterpret_cast<const float *>(a.kcache);
+    const float *vc = reinterpret_cast<const float *>(a.vcache);
+    f32x4 kr[PER], vr[PER];
+    auto gload = [&](int t0) {
+#pragma unroll
+        for (int u = 0; u < PER; u++) {
+            const int e = tid + u * kPfThreads;
+            const int key = min(t0 + e / U4, k1 - 1);  // past the range: masked in compute
+            const size_t off = kvOff(a.kvMap, a.seqLen, nKv, HS, sl, key, g) + (e % U4) * 4;
+            kr[u] = *reinterpret_cast<const f32x4 *>(kc + off);
+            vr[u] = *reinterpret_cast<const f32x4 *>(vc + off);
         }
     };
-    if (nSplit == 1) {
-        if (rowOk) {
-            const float il = lsum > 0.f ? 1.0f / lsum : 0.f;
+    auto lstore = [&]() {
 #pragma unroll
-            for (int n = 0; n < NT; n++) {
-                const float v[4] = {o[n][0] * il, o[n][1] * il, o[n][2] * il, o[n][3] * il};
-                writeOut(row, head, 16 * n + 4 * h, v);
+        for (int u = 0; u < PER; u++) {
+            const int e = tid + u * kPfThreads, at = (e / U4) * SR + (e % U4) * 4;
+            *reinterpret_cast<f32x4 *>(&kT[0][at]) = kr[u];
+            *reinterpret_cast<f32x4 *>(&vT[0][at]) = vr[u];
+        }
+    };
+    f32x4 o[NT];
+#pragma unroll
+    for (int n = 0; n < NT; n++) o[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, lsum = 0.f;
+    auto compute = [&](int t0) {
+        f32x4 st[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int e = 0; e < QD; e += 4) {
+#pragma unroll
+            for (int u = 0; u < 2; u++) {  // two independent accumulator chains
+                const f32x4 kf = *reinterpret_cast<const f32x4 *>(&kT[0][(16 * u + col) * SR + QD * h + e]);
+#pragma unroll
+                for (int j = 0; j < 4; j++) st[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[j], q[e + j], st[u], 0, 0, 0);
             }
         }
-        return;
-    }
-    // several chunks: publish (every column of the block, masked ones as (-inf, 0, 0)), count in,
-    // the last arriver combines
-    const int G = a.splitGrid;
-    // fence-free hand-off (see gemmFinish): agent-scope atomic stores here, atomic loads below
-    auto st = [](float *q, float v) { __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    auto ld = [](const float *q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    if (rowOk) {
-        const size_t pb = ((size_t)row * a.nHeads0 + head) * G + c;
+        float mx = -INFINITY;
 #pragma unroll
-        for (int n = 0; n < NT; n++)
+        for (int u = 0; u < 2; u++)
 #pragma unroll
-            for (int e = 0; e < 4; e++) st(a.partO + pb * HS + 16 * n + 4 * h + e, o[n][e]);
-        if (h == 0) {
-            st(a.partML + pb * 2, m);
-            st(a.partML + pb * 2 + 1, lsum);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int *cnt = a.counters + (size_t)rb * nKv + g;
-    if (tid == 0) flagL = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nSplit - 1;
-    __syncthreads();
-    if (!flagL) return;
-    if (tid == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // per column: chunk weights exp(m_c - M) and the total sum (LDS: the tiles are free now)
-    const int nCol = rpb * kvMul;  // 64 columns
-    float *wts = reinterpret_cast<float *>(&kT[0][0]);  // [nCol][nSplit]
-    float *tot = reinterpret_cast<float *>(&vT[0][0]);  // [nCol]
-    if (tid < nCol) {
-        const int r = b0 + tid / kvMul, hd = g * kvMul + tid % kvMul;
-        float M = -INFINITY, L = 0.f;
-        if (r < nRows) {
-            const float *ml = a.partML + ((size_t)r * a.nHeads0 + hd) * G * 2;
-            for (int cc = 0; cc < nSplit; cc++) M = fmaxf(M, ld(ml + 2 * cc));
-            for (int cc = 0; cc < nSplit; cc++) {
-                const float mc = ld(ml + 2 * cc);
-                const float w = (M == -INFINITY || mc == -INFINITY) ? 0.f : __expf(mc - M);
-                wts[tid * nSplit + cc] = w;
-                L += w * ld(ml + 2 * cc + 1);
+            for (int i = 0; i < 4; i++) {
+                const int t = t0 + 16 * u + 4 * h + i;
+                if (t >= k1 || t >= myLen) st[u][i] = -INFINITY;
+                mx = fmaxf(mx, st[u][i]);
             }
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float mn = fmaxf(m, mx);
+        const float corr = m == -INFINITY ? 0.f : __expf(m - mn);
+        float p[8], ps = 0.f;
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                p[4 * u + i] = st[u][i] == -INFINITY ? 0.f : __expf(st[u][i] - mn);
+                ps += p[4 * u + i];
+            }
+        lsum = lsum * corr + ps;
+        m = mn;
+#pragma unroll
+        for (int n = 0; n < NT; n++) o[n] *= corr;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const float *vrow = &vT[0][(16 * (j >> 2) + 4 * h + (j & 3)) * SR + col];
+#pragma unroll
+            for (int n = 0; n < NT; n++) o[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(vrow[16 * n], p[j], o[n], 0, 0, 0);
         }
-        tot[tid] = L;
-    }
+    };
+    gload(k0);
+    lstore();
     __syncthreads();
-    for (int i = tid; i < nCol * (HS / 4); i += kPfThreads) {
-        const int cl = i / (HS / 4), d = (i % (HS / 4)) * 4;
-        const int r = b0 + cl / kvMul, hd = g * kvMul + cl % kvMul;
-        if (r >= nRows) continue;
-        const float *po = a.partO + ((size_t)r * a.nHeads0 + hd) * G * HS + d;
-        float acc[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int cc = 0; cc < nSplit; cc++) {
-            const float w = wts[cl * nSplit + cc];
-            const float *x = po + (size_t)cc * HS;
-            acc[0] += w * ld(x); acc[1] += w * ld(x + 1); acc[2] += w * ld(x + 2); acc[3] += w * ld(x + 3);
+    for (int t0 = k0; t0 < k1; t0 += kPfTile) {
+        const bool more = t0 + kPfTile < k1;
+        if (more) gload(t0 + kPfTile);
+        compute(t0);
+        __syncthreads();
+        if (more) {
+            lstore();
+            __syncthreads();
         }
-        const float il = tot[cl] > 0.f ? 1.0f / tot[cl] : 0.f;
-        const float v[4] = {acc[0] * il, acc[1] * il, acc[2] * il, acc[3] * il};
-        writeOut(r, hd, d, v);
     }
+    pfFinish<HS>(a, nRows, o, m, lsum, nSplit, rb, g, c, b0, row, head, &kT[0][0], &vT[0][0], flagL);
 }
 
 void launchAttentionPrefill(const AttnArgs &a, int nRows, hipStream_t s) {
@@ -254,6 +395,13 @@ void launchAttentionPrefill(const AttnArgs &a, int nRows, hipStream_t s) {
     }
     const int nKv = a.nHeads0 / a.kvMul, rpb = attnPrefillRowsPerBlock(a.kvMul);
     const dim3 grid(nKv * ((nRows + rpb - 1) / rpb), a.splitGrid);
+    if (!attnPrefillSupported(a.hs, a.kvMul, a.kvBf16 != 0) || a.nHeads0 % a.kvMul)
+        throw Error("launchAttentionPrefill: head size 64 / 128 and a power-of-two GQA group <= 16");
+    if (!a.kvBf16) {
+        if (a.hs == 128) hipLaunchKernelGGL(attnPrefillF32Kernel<128>, grid, dim3(kPfThreads), 0, s, a, nRows);
+        else hipLaunchKernelGGL(attnPrefillF32Kernel<64>, grid, dim3(kPfThreads), 0, s, a, nRows);
+        return;
+    }
     if (a.hs == 128) hipLaunchKernelGGL(attnPrefillKernel<128>, grid, dim3(kPfThreads), 0, s, a, nRows);
     else hipLaunchKernelGGL(attnPrefillKernel<64>, grid, dim3(kPfThreads), 0, s, a, nRows);
 }

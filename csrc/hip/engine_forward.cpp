@@ -66,7 +66,7 @@ void HipEngineImpl::setInputs(int n, const int *tokens, const int *positions, co
     std::memcpy(hIn_ + 2 * MB, slots, n * sizeof(int));
     size_t words = 2 * (size_t)MB + n;
     // prefill attention on MFMA: every block of rows it assigns to one workgroup is one slot
-    prefillOk_ = !invariant_ && kvBf16_ && hipk::attnPrefillSupported(plan_.headSize, plan_.kvMul, true);
+    prefillOk_ = !invariant_ && hipk::attnPrefillSupported(plan_.headSize, plan_.kvMul, kvBf16_);
     const int rpb = prefillOk_ ? hipk::attnPrefillRowsPerBlock(plan_.kvMul) : 1;
     for (int b = 0; prefillOk_ && b < n; b++) prefillOk_ = slots[b] == slots[b - b % rpb];
     if (specs) {

@@ -338,7 +338,7 @@ std::vector<float> attention(const std::vector<float> &q, const std::vector<floa
     const int B = (int)pos.size();
     DL_CHECK(B >= 1 && slot.size() == pos.size(), "attention rows");
     if (impl == 1) {
-        DL_CHECK(hipk::attnPrefillSupported(hs, kvMul, kvBf16), "prefill attention needs a bf16 cache");
+        DL_CHECK(hipk::attnPrefillSupported(hs, kvMul, kvBf16), "prefill attention: head size 64 / 128, power-of-two GQA group");
         const int rpb = hipk::attnPrefillRowsPerBlock(kvMul);
         for (int b = 0; b < B; b++) DL_CHECK(slot[b] == slot[b - b % rpb], "prefill row blocks must share a slot");
     }

@@ -84,8 +84,8 @@ def qkv_rope(blocks, q0: int, kv0: int, head_size: int, n: int, x, norm_w, eps: 
 def attention(q, k_cache, v_cache, n_heads0: int, kv_mul: int, head_size: int, pos, slot,
               kv_bf16: bool = True, prefill: bool = False, impl: str = "auto") -> torch.Tensor:
     """Decode attention. k_cache / v_cache: [slots, seq_len, kv0]; q: [B, n_heads0 * head_size].
-    prefill=True (impl "prefill"): the MFMA prefill kernel (bf16 cache; row blocks of 64 / kv_mul rows
-    share a slot). impl "valu" / "mfma": force the VALU or the MFMA decode kernel ("auto": the
+    prefill=True (impl "prefill"): the MFMA prefill kernel (bf16 MFMAs for a bf16 cache, f32 MFMAs
+    for an f32 one; row blocks of 64 / kv_mul rows share a slot). impl "valu" / "mfma": force the VALU or the MFMA decode kernel ("auto": the
     engine's choice, MFMA for bf16 caches of >= 1024 positions)."""
     n_slots, seq_len, _ = k_cache.shape
     code = {"auto": 0, "prefill": 1, "valu": 2, "mfma": 3}["prefill" if prefill else impl]

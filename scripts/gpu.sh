@@ -32,7 +32,8 @@ print('$1', 'value', d['value'], 'pred', c['pred_ms_per_token'], 'eval', c['eval
 QUICK="--no-cli --no-cap128k --no-prefill4k --steps 64 --warmup 8"
 case $task in
   tests)
-    timeout -k 10 1500 python3 -u -m pytest ${@:-tests -m gpu} -v --timeout 170 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+    [ $# -eq 0 ] && set -- tests -m gpu
+    timeout -k 10 1500 python3 -u -m pytest "$@" -v --timeout 170 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
     tail -3 $O/tests.log
     timeout -k 10 180 python3 -u __graft_entry__.py > $O/smoke.log 2>&1 || exit 1
     tail -n 2 $O/smoke.log ;;

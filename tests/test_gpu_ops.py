@@ -194,6 +194,29 @@ def test_attention_prefill_mfma(ops, n_heads0, kv_mul, hs, seq, p0, rows):
     assert rel(ops.attention(q, k, v, n_heads0, kv_mul, hs, pos, slots, True, impl="valu"), want) < 1e-4
 
 
+@pytest.mark.parametrize("n_heads0,kv_mul,hs,seq,p0,rows", [
+    (32, 4, 128, 512, 0, 32),       # 8B shard, prompt start
+    (32, 4, 128, 4608, 4000, 32),   # deep chunk: key splits + combine
+    (8, 8, 128, 1024, 700, 20),     # GQA 8, partial row block
+    (16, 16, 128, 1024, 100, 7),    # GQA 16
+    (8, 2, 64, 2048, 1500, 40),     # head size 64, two row blocks
+    (8, 1, 64, 640, 300, 70),       # MHA
+])
+def test_attention_prefill_f32(ops, n_heads0, kv_mul, hs, seq, p0, rows):
+    """Prefill attention over an f32 cache (the reference's KV precision) on f32 MFMAs
+    (v_mfma_f32_16x16x4_f32: f32 Q, K, V and P) vs the fp32 reference: f32 reassociation only."""
+    kv0 = n_heads0 // kv_mul * hs
+    g = torch.Generator().manual_seed(23)
+    k = torch.randn(2, seq, kv0, generator=g)
+    v = torch.randn(2, seq, kv0, generator=g)
+    q = torch.randn(rows, n_heads0 * hs, generator=g) * 2
+    pos = list(range(p0, p0 + rows))
+    slots = [1] * rows
+    out = ops.attention(q, k, v, n_heads0, kv_mul, hs, pos, slots, False, prefill=True)
+    want = ops.ref_attention(q, k, v, n_heads0, kv_mul, hs, pos, slots)
+    assert rel(out, want) < 1e-5, rel(out, want)
+
+
 @pytest.mark.parametrize("n_heads0,kv_mul,hs,seq,pos", [
     (4, 4, 128, 8192, [8100, 3, 511, 512, 513]),  # long context, chunk edges, several rows
     (16, 16, 128, 1024, [1000]),                 # 405B-like GQA group of 16 heads
