@@ -36,7 +36,7 @@ LDROCM     := -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lrccl
 
 HOST_SRCS  := csrc/core/quant.cpp csrc/core/model_file.cpp csrc/core/plan.cpp csrc/text/tokenizer.cpp \
               csrc/cpu/thread_pool.cpp csrc/cpu/cpu_ops.cpp csrc/cpu/cpu_backend.cpp $(wildcard csrc/net/*.cpp) $(wildcard csrc/runtime/*.cpp)
-HIP_SRCS   := csrc/hip/kernels.hip csrc/hip/attn_prefill.hip csrc/hip/sample.hip csrc/hip/tp_check.hip csrc/hip/gemm.hip csrc/hip/gemm_wide.hip csrc/hip/attn_mfma.hip csrc/hip/gemv.hip csrc/hip/gemv_l16.hip csrc/hip/gemv_l32.hip csrc/hip/gemv_l64.hip csrc/hip/attn_block.hip csrc/hip/attn_block_16_16_128.hip csrc/hip/attn_block_16_32_128.hip csrc/hip/attn_block_32_32_128.hip csrc/hip/attn_block_64_32_128.hip csrc/hip/attn_block_64_16_128.hip csrc/hip/attn_block_64_64_128.hip csrc/hip/attn_block_32_64_128.hip csrc/hip/attn_block_64_64_64.hip csrc/hip/engine.cpp csrc/hip/engine_load.cpp csrc/hip/engine_kv.cpp csrc/hip/engine_forward.cpp csrc/hip/engine_bench.cpp csrc/hip/rccl_comm.cpp csrc/hip/sim_comm.cpp csrc/hip/xgmi_comm.cpp csrc/hip/ops.cpp
+HIP_SRCS   := csrc/hip/kernels.hip csrc/hip/attn_prefill.hip csrc/hip/sample.hip csrc/hip/tp_check.hip csrc/hip/gemm.hip csrc/hip/gemm_wide.hip csrc/hip/attn_mfma.hip csrc/hip/gemv.hip csrc/hip/gemv_l16.hip csrc/hip/gemv_l32.hip csrc/hip/gemv_l64.hip csrc/hip/attn_block.hip csrc/hip/ffn_block.hip csrc/hip/attn_block_16_16_128.hip csrc/hip/attn_block_16_32_128.hip csrc/hip/attn_block_32_32_128.hip csrc/hip/attn_block_64_32_128.hip csrc/hip/attn_block_64_16_128.hip csrc/hip/attn_block_64_64_128.hip csrc/hip/attn_block_32_64_128.hip csrc/hip/attn_block_64_64_64.hip csrc/hip/engine.cpp csrc/hip/engine_load.cpp csrc/hip/engine_kv.cpp csrc/hip/engine_forward.cpp csrc/hip/engine_bench.cpp csrc/hip/rccl_comm.cpp csrc/hip/sim_comm.cpp csrc/hip/xgmi_comm.cpp csrc/hip/ops.cpp
 HOST_OBJS  := $(patsubst csrc/%.cpp,$(BUILD)/obj/%.o,$(HOST_SRCS))
 HIP_OBJS   := $(patsubst csrc/%,$(BUILD)/obj/%.o,$(HIP_SRCS))
 HDRS       := $(wildcard csrc/*/*.h)

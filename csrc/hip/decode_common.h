@@ -346,6 +346,29 @@ __device__ __forceinline__ void stageQ80(const GemvArgs &a, int8_t *sq, float2 *
     __syncthreads();
 }
 
+// B rows of f32 activations produced in this launch (write-through loads) quantized into the LDS
+// Q80 image: the fused FFN block's w2 role when w13 hands the hidden rows off in f32. Same values
+// as resNormPrologue without a norm (n % 32 == 0: the quads of a block stay together).
+template <int B>
+__device__ __forceinline__ void stageF32WT(const GemvArgs &a, int8_t *sq, float2 *ssc) {
+    const int n = a.n, nChunks = n >> 3;
+#pragma unroll
+    for (int b = 0; b < B; b++) {
+        const float *xi = a.in + (size_t)b * a.ldIn;
+        for (int c = threadIdx.x; c < nChunks; c += kThreads) {
+            float v[8];
+#pragma unroll
+            for (int i = 0; i < 8; i += 2) {
+                const uint64_t u = ldWT64(xi + c * 8 + i);
+                v[i] = __uint_as_float((uint32_t)u);
+                v[i + 1] = __uint_as_float((uint32_t)(u >> 32));
+            }
+            stageChunk<true>(v, b, c, n, sq, ssc, nullptr);
+        }
+    }
+    __syncthreads();
+}
+
 // ------------------------------------------------------------------------------------------------
 // Fused tensor-parallel exchange (TpXchg, kernels.h). Peer words are 8-byte {payload, epoch}
 // granules in uncached memory: one relaxed system-scope store publishes data and flag together,

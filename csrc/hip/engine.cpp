@@ -78,6 +78,7 @@ HipEngineImpl::HipEngineImpl(const EngineConfig &cfg, DeviceComm *comm) : cfg_(c
     setupAttnBlock();
     setupWoAttn();
     setupPrenorm();
+    setupFfnBlock();
     hipk::preloadModules();  // no code-object load inside the first forwards
     load_.ms = timer.elapsedMs();
     load_.deviceBytes = deviceBytes_;
@@ -311,18 +312,18 @@ void HipEngineImpl::syncAndCheckComm() {
 void HipEngineImpl::enqueueErrorCopies() {
     const int *flag = comm_ ? comm_->deviceErrorFlag() : nullptr;
     if (flag) DL_HIP(hipMemcpyAsync(hErr_, flag, sizeof(int), hipMemcpyDeviceToHost, stream_));
-    if (blockOn_) DL_HIP(hipMemcpyAsync(hErr_ + 1, dBlockErr_, sizeof(int), hipMemcpyDeviceToHost, stream_));
+    if (blockOn_ || ffnOn_) DL_HIP(hipMemcpyAsync(hErr_ + 1, dBlockErr_, sizeof(int), hipMemcpyDeviceToHost, stream_));
 }
 
 void HipEngineImpl::checkErrorWords() {
     const int *flag = comm_ ? comm_->deviceErrorFlag() : nullptr;
-    const bool inLaunch = blockOn_;  // kernels with in-launch hand-offs
+    const bool inLaunch = blockOn_ || ffnOn_;  // kernels with in-launch hand-offs
     if (inLaunch && hErr_[1] != 0) {
         const int code = hErr_[1];
         hErr_[1] = 0;
         resetAttnBlockState();
         throw Error("in-launch hand-off wait timed out (code " + std::to_string(code) +
-                    ": attention block 2 qkv->attention, 3 attention->wo, 4 qkv phase; not all workgroups "
+                    ": attention block 2 qkv->attention, 3 attention->wo, 4 qkv phase; FFN block 7 w13->w2; not all workgroups "
                     "resident?)");
     }
     if (flag && *hErr_ != 0)
@@ -480,6 +481,7 @@ void HipEngineImpl::tpFusedSelfTest() {
     setupAttnBlock();
     setupWoAttn();
     setupPrenorm();
+    setupFfnBlock();
 }
 
 void HipEngineImpl::runGraph(int n, GraphKind kind, unsigned *syncDst) {

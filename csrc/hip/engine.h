@@ -31,6 +31,7 @@ class HipEngine : public Backend {
     // Single decode rows run the fused attention block (qkv + attention + wo in one launch).
     virtual bool attnBlock() const { return false; }
     virtual bool woAttn() const { return false; }  // DL_WO_ATTN: the wo GEMV with the attention prologue
+    virtual bool ffnBlock() const { return false; } // fused w13 + w2 launch in the pre-normalized layers
     virtual bool prenorm() const { return false; } // pre-normalized Q80 hand-offs of single decode rows
     // Diagnostics: one eager single-row forward with the fused attention block of `layer` traced
     // (kernels.h AttnBlockArgs::trace, 8 u64 per workgroup); returns {gq, ga, gw, trace...}.

@@ -298,6 +298,46 @@ void HipEngineImpl::setupPrenorm() {
     prenormOn_ = true;
 }
 
+hipk::FfnBlockArgs HipEngineImpl::ffnBlockArgs(const hipk::GemvArgs &w13, const hipk::GemvArgs &w2, u32 l) {
+    hipk::FfnBlockArgs f;
+    f.w13 = w13;
+    f.w2 = w2;
+    f.hQ80 = hQ80_ ? 1 : 0;
+    f.layer = (int)l;
+    f.nLayers = (int)h_.nLayers;
+    f.epoch = dEpoch_ + 1;
+    f.cnt = dBlockCnt_ + kFfnCntOff;
+    f.flag = dBlockCnt_ + kFfnCntOff + 64;
+    f.error = dBlockErr_;
+    return f;
+}
+
+// Fused FFN block (kernels.h FfnBlockArgs) for the pre-normalized single rows of a TP rank: a
+// compiled (w13 lanes, w2 lanes) instance and the whole w13 + w2 grid co-resident, shared with the
+// other ranks on this GPU. DL_FFN_BLOCK=0 keeps the two launches.
+void HipEngineImpl::setupFfnBlock() {
+    ffnOn_ = false;
+    const char *e = std::getenv("DL_FFN_BLOCK");
+    if (!prenormOn_ || !(e && *e == '1')) return;
+    const DevLayer &L = layers_[0];
+    const int epi = hQ80_ ? hipk::EPI_ACT_Q80 : hipk::EPI_ACT;
+    const hipk::GemvArgs a13 = gemvArgs(L.w13, 0, 1, epi, nullptr, h_.dim, nullptr, nullptr, nullptr, dH_,
+                                        plan_.hidden0, nullptr, nullptr, nullptr, dHQ_, dHS_, false);
+    const hipk::GemvArgs a2 = gemvArgs(L.w2, 0, 1, hipk::EPI_RESQ_TP, hQ80_ ? nullptr : dH_, plan_.hidden0, nullptr,
+                                       nullptr, nullptr, dY_, h_.dim, nullptr, hQ80_ ? dHQ_ : nullptr,
+                                       hQ80_ ? dHS_ : nullptr, nullptr, nullptr, true);
+    const hipk::FfnBlockArgs f = ffnBlockArgs(a13, a2, 0);
+    if (!hipk::ffnBlockPlan(f).fn) return;
+    const int share = comm_ ? std::max(1, comm_->ranksOnDevice()) : 1;
+    const hipk::GemvResidency r = hipk::ffnBlockResidency(f);
+    if (r.maxResident <= 0 || r.grid > r.maxResident / share) {
+        std::fprintf(stderr, "ℹ️  fused FFN block off: grid %d > %d co-resident workgroups per rank\n", r.grid,
+                     r.maxResident / share);
+        return;
+    }
+    ffnOn_ = true;
+}
+
 // The layers + logits of one decode row with the pre-normalized hand-offs (setupPrenorm). The
 // residual lives in dX_[cur]; its Q80 image for the next consumer in dXQ_ / dXS_ [cur] with sspN
 // partial sums in dSSP_[cur]; each producer writes the other parity and flips cur.
@@ -352,21 +392,26 @@ void HipEngineImpl::enqueuePrenormLayers(GraphKind kind, bool argTail) {
         }
         xSlot_ = 2 * (int)l + 1;
         {
-            ProfScope ps(this, "gemv_w13");
             const int epi = hQ80 ? hipk::EPI_ACT_Q80 : hipk::EPI_ACT;
-            hipk::GemvArgs a = gemvArgs(L.w13, 0, 1, epi, nullptr, dim, nullptr, nullptr, nullptr, dH_, p.hidden0, nullptr,
-                                        nullptr, nullptr, dHQ_, dHS_, false);
-            consumer(a);
-            hipk::launchGemv(a, 1, hipk::PRO_PRENORM, epi, true, stream_);
-        }
-        {
-            ProfScope ps(this, "gemv_w2");
+            hipk::GemvArgs a13 = gemvArgs(L.w13, 0, 1, epi, nullptr, dim, nullptr, nullptr, nullptr, dH_, p.hidden0,
+                                          nullptr, nullptr, nullptr, dHQ_, dHS_, false);
+            consumer(a13);
             const float *wNext = l + 1 < h_.nLayers ? layers_[l + 1].rmsAtt : rmsFinal_;
-            hipk::GemvArgs a = gemvArgs(L.w2, 0, 1, hipk::EPI_RESQ_TP, hQ80 ? nullptr : dH_, p.hidden0, nullptr, nullptr,
-                                        nullptr, dY_, dim, nullptr, hQ80 ? dHQ_ : nullptr, hQ80 ? dHS_ : nullptr, nullptr,
-                                        nullptr, true);
-            producer(a, wNext);
-            hipk::launchGemv(a, 1, hQ80 ? hipk::PRO_GLOBAL : hipk::PRO_RESNORM, hipk::EPI_RESQ_TP, true, stream_);
+            hipk::GemvArgs a2 = gemvArgs(L.w2, 0, 1, hipk::EPI_RESQ_TP, hQ80 ? nullptr : dH_, p.hidden0, nullptr, nullptr,
+                                         nullptr, dY_, dim, nullptr, hQ80 ? dHQ_ : nullptr, hQ80 ? dHS_ : nullptr, nullptr,
+                                         nullptr, true);
+            producer(a2, wNext);
+            if (ffnOn_) {  // one launch: w13 role + w2 role (weights prefetched before the hand-off wait)
+                ProfScope ps(this, "ffn_block");
+                hipk::launchFfnBlock(ffnBlockArgs(a13, a2, l), stream_);
+            } else {
+                {
+                    ProfScope ps(this, "gemv_w13");
+                    hipk::launchGemv(a13, 1, hipk::PRO_PRENORM, epi, true, stream_);
+                }
+                ProfScope ps(this, "gemv_w2");
+                hipk::launchGemv(a2, 1, hQ80 ? hipk::PRO_GLOBAL : hipk::PRO_RESNORM, hipk::EPI_RESQ_TP, true, stream_);
+            }
             cur ^= 1;
         }
     }
@@ -437,8 +482,8 @@ void HipEngineImpl::setupWoAttn() {
 // A fused-block wait gave up (a workgroup of the launch never arrived): reset the monotonic
 // counters and the epoch so the engine stays usable, then raise.
 void HipEngineImpl::resetAttnBlockState() {
-    DL_HIP(hipMemsetAsync(dBlockCnt_, 0, sizeof(unsigned) * kBlockCntWords, stream_));
-    DL_HIP(hipMemsetAsync(dEpoch_, 0, sizeof(unsigned), stream_));
+    DL_HIP(hipMemsetAsync(dBlockCnt_, 0, sizeof(unsigned) * kAllCntWords, stream_));
+    DL_HIP(hipMemsetAsync(dEpoch_, 0, 2 * sizeof(unsigned), stream_));
     DL_HIP(hipMemsetAsync(dBlockErr_, 0, sizeof(int), stream_));
     DL_HIP(hipStreamSynchronize(stream_));
 }
@@ -570,8 +615,10 @@ void HipEngineImpl::enqueueForward(int n, GraphKind kind) {
     const bool pre = prenormNow(n, bat, blk);  // pre-normalized Q80 hand-offs between the GEMVs
     {
         ProfScope ps(this, "embedding");
-        // the epoch counts the forwards that run the fused block (its counters' targets)
-        hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_, blk ? dEpoch_ : nullptr,
+        // the epochs count the forwards that run the fused attention block / the FFN block (their
+        // counters' targets); the two never run in the same forward (prenormNow excludes blk)
+        unsigned *ep = blk ? dEpoch_ : (pre && ffnOn_) ? dEpoch_ + 1 : nullptr;
+        hipk::launchEmbedding(emb_, dTok_, dX_[0], dim, n, stream_, ep,
                               p.nRanks > 1 ? dSync_ : nullptr, p.nRanks > 1 ? syncSlots() : 0);
     }
     // one greedy decode row: the logits GEMV ends in the row's argmax (EPI_ARGMAX: no logits

@@ -93,6 +93,7 @@ class HipEngineImpl : public HipEngine {
     bool attnBlock() const override { return blockOn_; }
     bool woAttn() const override { return woAttnOn_; }
     bool prenorm() const override { return prenormOn_; }
+    bool ffnBlock() const override { return ffnOn_; }
     std::vector<unsigned long long> traceAttnBlock(int token, int pos, int slot, int layer) override;
     int fusedGridMax() const override { return fusedGridMax_; }
     bool tpBatchedFused(int n) const override { return plan_.nRanks > 1 && batchedPath(n) && fuseNorm(n); }
@@ -226,6 +227,9 @@ class HipEngineImpl : public HipEngine {
     // consumers): decided once (setupPrenorm), taken per forward (prenormNow)
     void setupPrenorm();
     bool prenormNow(int n, bool bat, bool blk) const { return prenormOn_ && n == 1 && !bat && !blk; }
+    // fused FFN block (w13 + w2 roles in one launch) inside the pre-normalized layers: setupFfnBlock
+    void setupFfnBlock();
+    hipk::FfnBlockArgs ffnBlockArgs(const hipk::GemvArgs &w13, const hipk::GemvArgs &w2, u32 l);
     void enqueuePrenormLayers(GraphKind kind, bool argTail);
     bool woAttnNow(int n, bool bat, bool blk) const {
         return woAttnOn_ && n == 1 && !bat && !blk && buckets_[bucket_].maxLen <= woAttnMaxLen_;
@@ -257,6 +261,8 @@ class HipEngineImpl : public HipEngine {
     // attention block counters: qkv counters per KV group | attention counter | 8 flags | qkv counter |
     // 8 flags | spare line (every word on its own 256-B line; attn_block_inst.h carves them)
     static constexpr int kBlockCntWords = kMaxKvGroups * 64 + 64 + 8 * 64 + 64 + 8 * 64 + 64;
+    // the FFN block's words after the attention block's: [64] arrivals, [8 * 64] per-XCD flags
+    static constexpr int kFfnCntOff = kBlockCntWords, kAllCntWords = kBlockCntWords + 64 + 8 * 64;
     static constexpr int kAttnMfmaMinPos = 1024;
     static constexpr int kAttnMfmaMinRows = 16;
 
@@ -352,6 +358,7 @@ class HipEngineImpl : public HipEngine {
     bool blockOn_ = false;   // decode rows may run the fused attention block (per bucket: CtxBucket::block)
     bool woAttnOn_ = false;  // setupWoAttn
     bool prenormOn_ = false; // setupPrenorm
+    bool ffnOn_ = false;     // setupFfnBlock (prenorm forwards only)
     static constexpr int kMaxSsp = 256;  // producer workgroups of a pre-normalized hand-off
     int woAttnMaxLen_ = 256; // DL_WO_ATTN_LEN: context buckets up to this length
     int blockPassMul_ = 1;   // qkv / wo passes multiplier of the block's roles (same-GPU rehearsals)

@@ -164,11 +164,11 @@ void HipEngineImpl::allocBuffers() {
         hSync_ = halloc<unsigned>(sw * (1 + kChainDepth));
         DL_HIP(hipMemsetAsync(dSync_, 0, sw * sizeof(unsigned), stream_));
         std::memset(hSync_, 0, sw * (1 + kChainDepth) * sizeof(unsigned));
-        dBlockCnt_ = dalloc<unsigned>(kBlockCntWords);
+        dBlockCnt_ = dalloc<unsigned>(kAllCntWords);
         dBlockExpect_ = dalloc<unsigned>(kMaxKvGroups);
         dBlockErr_ = dalloc<int>(4);
         DL_HIP(hipMemsetAsync(dEpoch_, 0, 4 * sizeof(unsigned), stream_));
-        DL_HIP(hipMemsetAsync(dBlockCnt_, 0, kBlockCntWords * sizeof(unsigned), stream_));
+        DL_HIP(hipMemsetAsync(dBlockCnt_, 0, kAllCntWords * sizeof(unsigned), stream_));
         DL_HIP(hipMemsetAsync(dBlockExpect_, 0, kMaxKvGroups * sizeof(unsigned), stream_));
         DL_HIP(hipMemsetAsync(dBlockErr_, 0, 4 * sizeof(int), stream_));
     }

@@ -381,7 +381,8 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
             // the activations are produced in this launch: wait for every producer (the ring's
             // weight loads are already in flight), then read them write-through
             tWaited = blockWait(bs->attnFlag + xccId() * kCntStride, bs->step, *bs, bs->codeBase + 3);
-            stageQ80<B, true>(a, sq, ssc);
+            if constexpr (PRO == PRO_RESNORM) stageF32WT<B>(a, sq, ssc);  // f32 rows (FFN block, skinny w13)
+            else stageQ80<B, true>(a, sq, ssc);
         } else if constexpr (PRO == PRO_RESNORM)
             resNormPrologue<B, true>(a, scratch, sq, ssc, nullptr);
         else {
@@ -467,7 +468,11 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
                     o[0] = v0;
                     if (r0 + 1 < a.rows) o[1] = v1;
                 } else if constexpr (EPI == EPI_ACT) {
-                    a.out[(size_t)b * a.ldOut + (r0 >> 1)] = gateAct(a, v0) * v1;
+                    float *o = a.out + (size_t)b * a.ldOut + (r0 >> 1);
+                    if constexpr (MODE == GEMV_PRODUCER)  // read by the FFN block's w2 role in this launch
+                        __hip_atomic_store(o, gateAct(a, v0) * v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    else
+                        *o = gateAct(a, v0) * v1;
                 } else if constexpr (EPI == EPI_ACT_Q80) {
                     hbuf[b * (R >> 1) + ((r0 - rowBase) >> 1)] = gateAct(a, v0) * v1;
                 } else {
@@ -514,7 +519,8 @@ __device__ __forceinline__ void gemvQ40Body(const GemvArgs &a, const int blk, ch
 
     const int unitsPerThread = (PRO != PRO_GLOBAL && PRO != PRO_PRENORM) ? (n + 8 * kThreads - 1) / (8 * kThreads)
                                                                          : (n + 16 * kThreads - 1) / (16 * kThreads);
-    static_assert(MODE != GEMV_CONSUMER || PRO == PRO_GLOBAL, "a consumer GEMV reads Q80 activations");
+    static_assert(MODE != GEMV_CONSUMER || PRO == PRO_GLOBAL || PRO == PRO_RESNORM,
+                  "a consumer GEMV reads Q80 activations (or un-normalized f32 rows: PRO_RESNORM, no norm)");
     if constexpr (PRO == PRO_ATTN) {
         attnPath();
         mainLoop();

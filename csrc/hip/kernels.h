@@ -371,6 +371,34 @@ void attnBlockExpect(const GemvArgs &qkv, int nKv, unsigned *out);
 GemvResidency attnBlockResidency(const AttnBlockArgs &a, bool tp);
 void launchAttnBlock(const AttnBlockArgs &a, bool tp, hipStream_t s);
 
+// Fused FFN block of one decode row at a tensor-parallel rank with the pre-normalized hand-off
+// (ffn_block.hip): w13 (PRO_PRENORM, SwiGLU epilogue, hidden rows stored write-through as f32 or
+// Q80) and w2 (EPI_RESQ_TP exchange tail) in ONE launch as two workgroup roles
+//   [0, g13) w13 rows | [g13, g13 + g2) w2 rows.
+// The w2 workgroups issue their weight ring at entry - it streams while w13 runs - then wait for
+// every w13 workgroup (a monotonic counter, per-XCD "phase done" flags as the attention block's)
+// and read the hidden rows write-through. Removes a kernel boundary and w2's start-up latency per
+// layer. Requires the whole grid co-resident (ffnBlockResidency); waits are bounded (error word).
+struct FfnBlockArgs {
+    GemvArgs w13;                 // PRO_PRENORM + EPI_ACT (f32 hidden) or EPI_ACT_Q80 (hQ80)
+    GemvArgs w2;                  // EPI_RESQ_TP: PRO_RESNORM (f32 hidden, no norm) or PRO_GLOBAL (Q80)
+    int hQ80 = 0;
+    int layer = 0, nLayers = 1;
+    const unsigned *epoch = nullptr;  // per-forward epoch of the FFN block (incremented by launchEmbedding)
+    unsigned *cnt = nullptr;          // [1] monotonic w13 arrivals (zeroed once)
+    unsigned *flag = nullptr;         // [8 * 64] per-XCD "w13 phase done" step flags (zeroed once)
+    int *error = nullptr;             // wait timeout flag (codes 7 data, 8 ring start)
+    long long timeoutTicks = 200LL * 1000 * 1000;
+};
+struct FfnBlockPlan {
+    const void *fn = nullptr;
+    int g13 = 0, g2 = 0;
+    size_t lds = 0;
+};
+FfnBlockPlan ffnBlockPlan(const FfnBlockArgs &a);
+GemvResidency ffnBlockResidency(const FfnBlockArgs &a);
+void launchFfnBlock(const FfnBlockArgs &a, hipStream_t s);
+
 // Fused-exchange self-test (tp_check.hip): out[el] = sum over ranks of (val_rank + el % 1024) for
 // el < n (n <= x.stride), through the transport of the fused exchange; every rank must call it.
 void launchTpSelfTest(const TpXchg &x, float *out, int n, float val, hipStream_t s);

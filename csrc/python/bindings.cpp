@@ -859,6 +859,7 @@ PYBIND11_MODULE(_C, m) {
         .def_property_readonly("attn_block", [](const PyHipEngine &e) { return e.engine->attnBlock(); })
         .def_property_readonly("wo_attn", [](const PyHipEngine &e) { return e.engine->woAttn(); })
         .def_property_readonly("prenorm", [](const PyHipEngine &e) { return e.engine->prenorm(); })
+        .def_property_readonly("ffn_block", [](const PyHipEngine &e) { return e.engine->ffnBlock(); })
         .def("trace_attn_block",
              [](PyHipEngine &e, int token, int pos, int slot, int layer) {
                  py::gil_scoped_release rel;

@@ -12,7 +12,7 @@ import sys
 from concurrent.futures import ThreadPoolExecutor
 
 SRCS = ["csrc/hip/gemv_l16.hip", "csrc/hip/gemv_l32.hip", "csrc/hip/gemv_l64.hip", "csrc/hip/attn_block_16_32_128.hip",
-        "csrc/hip/attn_block_64_64_128.hip", "csrc/hip/attn_block_64_64_64.hip"]
+        "csrc/hip/attn_block_64_64_128.hip", "csrc/hip/attn_block_64_64_64.hip", "csrc/hip/ffn_block.hip"]
 FLAGS = ["-std=c++17", "-O3", "--offload-arch=gfx950", "-munsafe-fp-atomics", "--offload-device-only", "-c",
          "-o", "/dev/null", "-Rpass-analysis=kernel-resource-usage"]
 
@@ -28,7 +28,7 @@ def check(src):
             fn = m.group(1)
             continue
         m = re.search(r"ScratchSize \[bytes/lane\]: (\d+)", line)
-        if m and fn and ("gemvQ40Kernel" in fn or "attnBlockKernel" in fn or "gemvAttnKernel" in fn):
+        if m and fn and ("gemvQ40Kernel" in fn or "attnBlockKernel" in fn or "gemvAttnKernel" in fn or "ffnBlockKernel" in fn):
             n += 1
             if int(m.group(1)) != 0:
                 bad.append(f"{fn}: scratch {m.group(1)} B/lane")
@@ -128,14 +128,15 @@ def hazard_check():
     import tempfile
     ok = True
     with tempfile.TemporaryDirectory() as d:
-        for src in ["csrc/hip/gemv_l16.hip", "csrc/hip/gemv_l32.hip", "csrc/hip/gemv_l64.hip", "csrc/hip/attn_block_16_32_128.hip"]:
+        for src in ["csrc/hip/gemv_l16.hip", "csrc/hip/gemv_l32.hip", "csrc/hip/gemv_l64.hip", "csrc/hip/attn_block_16_32_128.hip",
+                    "csrc/hip/ffn_block.hip"]:
             r = subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS[:5], "--save-temps", "-c", "-o", os.path.join(d, "x.o"),
                                 os.path.abspath(src)], capture_output=True, text=True, cwd=d)
             s_files = glob.glob(os.path.join(d, "*gfx950.s"))
             if r.returncode != 0 or not s_files:
                 print(f"{src}: no assembly ({r.stderr[-300:]})")
                 return False
-            hz = scan_asm(s_files[0], ["gemvQ40Kernel", "attnBlockKernel", "gemvAttnKernel"])
+            hz = scan_asm(s_files[0], ["gemvQ40Kernel", "attnBlockKernel", "gemvAttnKernel", "ffnBlockKernel"])
             print(f"{src}: {len(hz)} reads of pending inline-asm load registers")
             for h in hz[:20]:
                 print("  " + h)

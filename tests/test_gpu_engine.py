@@ -429,6 +429,32 @@ def test_prenorm_handoff_matches_norm_prologue(C, medium, monkeypatch, sync):
     assert out["1"][2] == [int(i) for i in out["1"][0].argmax(-1)]
 
 
+@pytest.mark.parametrize("hq80", ["1", "0"])
+def test_ffn_block_matches_two_launches(C, medium, monkeypatch, hq80):
+    """DL_FFN_BLOCK=1: a TP rank's pre-normalized single rows run w13 and w2 as two workgroup roles of
+    one launch (w2 prefetches its weights, waits on the w13 arrival counter, reads the hidden rows
+    write-through: Q80 blocks or f32 rows) - bitwise the same logits and greedy chain as the two
+    launches (same arithmetic, only the hand-off changes), rank in loopback, over several forwards
+    (the monotonic step targets) and a decode chain."""
+    monkeypatch.setenv("DL_H_Q80", hq80)
+    out = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("DL_FFN_BLOCK", on)
+        e = C.HipEngine(medium, "q80", max_batch=8, rank=0, world=2, comm=C.ComputeOnlyComm(0, 2, 0),
+                        sync_type="q80", kv_bf16=False)
+        assert e.prenorm and bool(e.ffn_block) == (on == "1")
+        v0 = e.header["vocab_size"] // 2
+        toks = [3, 17, 101, 7, 250, 9]
+        lg = np.stack([e.forward([t], [p], [0])[0][:v0] for p, t in enumerate(toks)])
+        _, ch = e.decode_greedy(12, [int(lg[-1].argmax())], [len(toks)], [0])
+        ids = [e.forward_argmax([t], [p], [0])[0] for p, t in enumerate(toks)]
+        out[on] = (lg, list(ch), ids)
+        del e
+    assert np.isfinite(out["1"][0]).all()
+    assert np.array_equal(out["1"][0], out["0"][0])
+    assert out["1"][1] == out["0"][1] and out["1"][2] == out["0"][2]
+
+
 @pytest.mark.parametrize("world", [2])
 def test_wo_attention_prologue_matches_attention_launch(C, medium, monkeypatch, world):
     """DL_WO_ATTN=1: a TP rank's wo GEMV computes the layer's decode attention in every workgroup's
