@@ -69,6 +69,18 @@ void HipEngineImpl::setInputs(int n, const int *tokens, const int *positions, co
     prefillOk_ = !invariant_ && hipk::attnPrefillSupported(plan_.headSize, plan_.kvMul, kvBf16_);
     const int rpb = prefillOk_ ? hipk::attnPrefillRowsPerBlock(plan_.kvMul) : 1;
     for (int b = 0; prefillOk_ && b < n; b++) prefillOk_ = slots[b] == slots[b - b % rpb];
+    // f32 caches: the f32 MFMA prefill kernel from 128 keys on; below, the per-row decode attention
+    // is faster (a 32-row chunk at positions 0-63: eval 0.0957 vs 0.0993 ms/token; crossover ~135
+    // keys from the 4k-prompt slopes, profiles/r6_decode.md). DL_PREFILL_F32_MIN overrides.
+    if (prefillOk_ && !kvBf16_) {
+        static const int f32Min = [] {
+            const char *e = std::getenv("DL_PREFILL_F32_MIN");
+            return e ? std::atoi(e) : 128;
+        }();
+        int mx = 0;
+        for (int b = 0; b < n; b++) mx = std::max(mx, positions[b] + 1);
+        prefillOk_ = mx >= f32Min;
+    }
     if (specs) {
         static_assert(sizeof(SampleSpec) == 4 * sizeof(float), "spec layout");
         std::memcpy(hIn_ + 3 * MB, specs, n * sizeof(SampleSpec));

@@ -27,7 +27,8 @@ pj() {
 d=json.loads([l for l in sys.stdin.read().splitlines() if l.startswith('{')][-1]); c=d['config']
 print('$1', 'value', d['value'], 'pred', c['pred_ms_per_token'], 'eval', c['eval_ms_per_token'], 'bf16kv_pred',
       c.get('bf16_kv_pred_ms_per_token'), 'long', c.get('long_ctx_pred_ms_per_token'), 'tp2', c.get('tp2_rank_compute_ms_per_token'),
-      'tp4', c.get('tp4_rank_compute_ms_per_token'), 'tp8', c.get('tp8_rank_compute_ms_per_token'))"
+      'tp4', c.get('tp4_rank_compute_ms_per_token'), 'tp8', c.get('tp8_rank_compute_ms_per_token'),
+      'p4k', c.get('prompt_4k_eval_ms_per_token'), 'p4k_big', c.get('prompt_4k_eval_big_chunk_ms_per_token'))"
 }
 QUICK="--no-cli --no-cap128k --no-prefill4k --steps 64 --warmup 8"
 case $task in

@@ -11,6 +11,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--model", default="llama3_1_8b")
 ap.add_argument("--tokens", type=int, default=32)
 ap.add_argument("--reps", type=int, default=8)
+ap.add_argument("--kv", choices=["f32", "bf16"], default="f32")
 args = ap.parse_args()
 
 import distributed_llama_multiusers_amd as dl
@@ -18,7 +19,8 @@ from distributed_llama_multiusers_amd.models.synthetic import LLAMA_SHAPES
 
 C = dl.native()
 h = dict(LLAMA_SHAPES[args.model], seq_len=1024, rope_theta=500000, weight_type=2)
-eng = C.HipEngine("", "q80", synthetic=h, max_seq_len=1024, n_slots=1, max_batch=max(32, args.tokens))
+eng = C.HipEngine("", "q80", synthetic=h, max_seq_len=1024, n_slots=1, max_batch=max(32, args.tokens),
+                  kv_bf16=args.kv == "bf16")
 n = args.tokens
 toks = [(i * 31 + 7) % 1000 for i in range(n)]
 eng.forward_argmax(toks, list(range(n)), [0] * n)
