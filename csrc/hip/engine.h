@@ -63,10 +63,11 @@ double benchGemvQ40(int rows, int n, int pro, int epi, int B, int lanes, int pas
 // workgroup, grid x then splits) appended after the timed graph.
 double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters,
                     std::vector<unsigned long long> *trace = nullptr);
-// Micro-benchmark of the decode attention kernel (bf16 KV, Q80 output): `copies` KV caches cycled
-// through a graph of `iters` launches, every row at position `pos`. Returns microseconds per launch.
+// Micro-benchmark of the decode attention kernel (bf16 or f32 KV, Q80 output): `copies` KV caches
+// cycled through a graph of `iters` launches, every row at position `pos`. Returns microseconds per
+// launch.
 double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B, int copies, int iters,
-                      std::vector<unsigned long long> *trace = nullptr);
+                      std::vector<unsigned long long> *trace = nullptr, bool kvBf16 = true);
 // Check a transport on the engine's separate-collective schedule (per layer Q80-rounded
 // all-reduces, root gather of logits slices, all-gather of argmax pairs), eagerly or captured in a
 // hipGraph and replayed `runs` times: returns the largest error against exact host sums (engine_bench.cpp).

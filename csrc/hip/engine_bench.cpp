@@ -220,7 +220,7 @@ double benchGemmQ40(int rows, int n, int M, int epi, int copies, int iters, std:
 }
 
 double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B, int copies, int iters,
-                      std::vector<unsigned long long> *trace) {
+                      std::vector<unsigned long long> *trace, bool kvBf16) {
     hipStream_t s;
     DL_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     std::vector<void *> mem;
@@ -235,11 +235,12 @@ double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B
     const int kv0 = nHeads0 / kvMul * hs, q0 = nHeads0 * hs;
     const size_t kvElems = (size_t)B * seqLen * kv0;  // one slot per row
     std::vector<void *> kc(copies), vc(copies);
+    const size_t kvWords = kvBf16 ? kvElems / 2 : kvElems;  // bf16 pairs of small values, or f32
     for (int c = 0; c < copies; c++) {
-        kc[c] = alloc(kvElems * 2);
-        vc[c] = alloc(kvElems * 2);
-        hipk::launchFillF32Uniform((float *)kc[c], kvElems / 2, 1.f, 5 + c, s);  // bf16 pairs of small values
-        hipk::launchFillF32Uniform((float *)vc[c], kvElems / 2, 1.f, 9 + c, s);
+        kc[c] = alloc(kvWords * 4);
+        vc[c] = alloc(kvWords * 4);
+        hipk::launchFillF32Uniform((float *)kc[c], kvWords, 1.f, 5 + c, s);
+        hipk::launchFillF32Uniform((float *)vc[c], kvWords, 1.f, 9 + c, s);
     }
     float *q = (float *)alloc((size_t)B * q0 * 4);
     hipk::launchFillF32Uniform(q, (size_t)B * q0, 1.f, 3, s);
@@ -266,7 +267,7 @@ double benchAttention(int nHeads0, int kvMul, int hs, int seqLen, int pos, int B
     a.outQ = (int8_t *)alloc((size_t)B * q0);
     a.outS = (float2 *)alloc((size_t)B * q0 / 32 * 8);
     a.ldOut = q0;
-    a.kvBf16 = 1;
+    a.kvBf16 = kvBf16 ? 1 : 0;
     a.counters = (int *)alloc((size_t)B * nHeads0 * 4);
     DL_HIP(hipStreamSynchronize(s));
     auto launch = [&](int c) {

@@ -597,11 +597,12 @@ PYBIND11_MODULE(_C, m) {
           }, py::arg("rows"), py::arg("n"), py::arg("tokens"), py::arg("epi") = 0,
           py::arg("copies") = 8, py::arg("iters") = 100, py::call_guard<py::gil_scoped_release>());
     m.def("bench_attention",
-          [](int nh, int kvm, int hs, int seq, int pos, int B, int copies, int iters) {
-              return benchAttention(nh, kvm, hs, seq, pos, B, copies, iters);
+          [](int nh, int kvm, int hs, int seq, int pos, int B, int copies, int iters, bool kvBf16) {
+              return benchAttention(nh, kvm, hs, seq, pos, B, copies, iters, nullptr, kvBf16);
           },
           py::arg("n_heads0"), py::arg("kv_mul"), py::arg("head_size"), py::arg("seq_len"), py::arg("pos"),
-          py::arg("batch") = 1, py::arg("copies") = 32, py::arg("iters") = 200, py::call_guard<py::gil_scoped_release>());
+          py::arg("batch") = 1, py::arg("copies") = 32, py::arg("iters") = 200, py::arg("kv_bf16") = true,
+          py::call_guard<py::gil_scoped_release>());
     m.def("trace_gemm_q40",
           [](int rows, int n, int M, int epi, int copies, int iters) {
               std::vector<unsigned long long> t;
