@@ -301,8 +301,7 @@ __global__ __launch_bounds__(kAmThreads) void attnPrefillDmaKernel(AttnArgs a, i
     const int g = blockIdx.x % nKv, rb = blockIdx.x / nKv, c = blockIdx.y;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, col = lane & 15, h = lane >> 4;
     const int b0 = rb * RPB;
-    int maxLen = 0;
-    for (int r = 0; r < RPB && b0 + r < nRows; r++) maxLen = max(maxLen, a.pos[b0 + r] + 1);
+    const int maxLen = rowsMaxLen(a.pos, b0, RPB, nRows);
     int nSplit = (maxLen + 255) / 256;
     nSplit = max(1, min(min(nSplit, a.splitGrid), HS / 2));  // combine weights: 64 columns x nSplit in LDS
     const int ch = ((maxLen + nSplit - 1) / nSplit + kAmTile - 1) / kAmTile * kAmTile;

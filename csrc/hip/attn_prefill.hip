@@ -27,6 +27,10 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 static constexpr int kPfThreads = 256, kPfWaves = 4, kPfChunk = 256, kPfTile = 32;
 static constexpr int kPfVtStride = 40;  // bf16 per transposed-V row in LDS (32 keys + 8 pad)
+#ifndef DL_PF_F32_SMALL_CHUNK
+#define DL_PF_F32_SMALL_CHUNK 128
+#endif
+static constexpr int kPfChunkF32Small = DL_PF_F32_SMALL_CHUNK;  // keys per split, f32 kernel, small grids
 
 int attnPrefillRowsPerBlock(int kvMul) { return kPfWaves * (16 / kvMul); }
 bool attnPrefillSupported(int hs, int kvMul, bool kvBf16) {
@@ -147,8 +151,7 @@ __global__ __launch_bounds__(kPfThreads) void attnPrefillKernel(AttnArgs a, int 
     const int g = blockIdx.x % nKv, rb = blockIdx.x / nKv, c = blockIdx.y;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, col = lane & 15, h = lane >> 4;
     const int b0 = rb * rpb;
-    int maxLen = 0;
-    for (int r = 0; r < rpb && b0 + r < nRows; r++) maxLen = max(maxLen, a.pos[b0 + r] + 1);
+    const int maxLen = rowsMaxLen(a.pos, b0, rpb, nRows);
     int nSplit = (maxLen + kPfChunk - 1) / kPfChunk;
     nSplit = max(1, min(min(nSplit, a.splitGrid), HS / 2));  // combine weights: 64 columns x nSplit in the K tiles' LDS
     const int ch = ((maxLen + nSplit - 1) / nSplit + kPfTile - 1) / kPfTile * kPfTile;
@@ -285,9 +288,11 @@ __global__ __launch_bounds__(kPfThreads) void attnPrefillF32Kernel(AttnArgs a, i
     const int g = blockIdx.x % nKv, rb = blockIdx.x / nKv, c = blockIdx.y;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, col = lane & 15, h = lane >> 4;
     const int b0 = rb * rpb;
-    int maxLen = 0;
-    for (int r = 0; r < rpb && b0 + r < nRows; r++) maxLen = max(maxLen, a.pos[b0 + r] + 1);
-    int nSplit = (maxLen + kPfChunk - 1) / kPfChunk;
+    const int maxLen = rowsMaxLen(a.pos, b0, rpb, nRows);
+    // with few row blocks (a 32-row chunk: 16 workgroups per split) the keys are split finer so
+    // more CUs share them (4k prompt in 32-row chunks 0.1526 -> 0.1498 ms/token, raw/r6_prefill_f32_chunk_ab.txt)
+    const int chunkKeys = gridDim.x >= 256 ? kPfChunk : kPfChunkF32Small;
+    int nSplit = (maxLen + chunkKeys - 1) / chunkKeys;
     nSplit = max(1, min(min(nSplit, a.splitGrid), HS / 2));
     const int ch = ((maxLen + nSplit - 1) / nSplit + kPfTile - 1) / kPfTile * kPfTile;
     if (c >= nSplit) return;

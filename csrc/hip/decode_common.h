@@ -739,6 +739,17 @@ __device__ __forceinline__ void resqTail(const GemvArgs &a, const float *res, in
     if (threadIdx.x == 0) o.ssp[blk] = ss;
 }
 
+// Longest context (max position + 1) over rows [b0, b0 + n) below nRows, n <= 64: one load per
+// lane and a wave max, the same value in every wave. (A loop of dependent per-row loads put ~16
+// serial memory round trips at the start of every prefill-attention workgroup.)
+__device__ __forceinline__ int rowsMaxLen(const int *pos, int b0, int n, int nRows) {
+    const int lane = threadIdx.x & 63;
+    int v = (lane < n && b0 + lane < nRows) ? pos[b0 + lane] + 1 : 0;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v = max(v, __shfl_xor(v, off));
+    return v;
+}
+
 // Sequence split of a decode-attention row of length `len`: nSplit chunks of ch positions
 // (~256 per chunk, at most splitGrid chunks). Shorter chunks for the few heads of a TP8 shard
 // (4 per rank) measured slower: 5.4 -> 7.6 us at 100 positions (profiles/r5_tp_rank.md).
