@@ -259,12 +259,21 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
     // phase 0: every key (the current one write-through under SYNC); 1: all but the current one;
     // 2: only the current one
     auto loadRound = [&](int tb, int phase) {
+        // the round's cache blocks first (pool pages of a paged cache, else the slot): a page-table
+        // load inside the key loop put a full vmcnt(0) drain at its join before every key, so
+        // the round's TU keys went out one memory round trip after another
+        size_t blk[TU];
+#pragma unroll
+        for (int u = 0; u < TU; u++) {
+            const int t = min(tb + u * NG, t1 - 1);
+            blk[u] = a.kvMap.table ? kvPageOf(a.kvMap, sl, t) : (size_t)sl;
+        }
 #pragma unroll
         for (int u = 0; u < TU; u++) {
             const int t = min(tb + u * NG, t1 - 1);  // clamped: no divergent loads
             const bool cur = SYNC && t == pos;
             if ((phase == 1 && cur) || (phase == 2 && !cur)) continue;
-            const size_t off = kvOff(a.kvMap, a.seqLen, a.kv0 / HS, HS, sl, t, kvh) + l16 * DPL;
+            const size_t off = kvOffAt(a.kvMap, a.seqLen, a.kv0 / HS, HS, blk[u], t, kvh) + l16 * DPL;
             const uint32_t *kp = reinterpret_cast<const uint32_t *>(
                 BF16 ? (const void *)(reinterpret_cast<const uint16_t *>(a.kcache) + off)
                      : (const void *)(reinterpret_cast<const float *>(a.kcache) + off));

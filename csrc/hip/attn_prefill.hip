@@ -2,6 +2,7 @@
 #include "decode_dev.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace dl {
 namespace hipk {
@@ -31,6 +32,16 @@ static constexpr int kPfVtStride = 40;  // bf16 per transposed-V row in LDS (32 
 #define DL_PF_F32_SMALL_CHUNK 128
 #endif
 static constexpr int kPfChunkF32Small = DL_PF_F32_SMALL_CHUNK;  // keys per split, f32 kernel, small grids
+// Paged caches: the chunk's per-tile pool pages go to LDS once (a tile of 32 keys never crosses a
+// page). A page-table load inside the tile loads put a full vmcnt(0) drain at its join before every
+// 16-byte load - taken on the contiguous path too - and serialised the tile's memory round trips.
+static constexpr int kPfMaxTiles = 256;
+__device__ __forceinline__ void pfPages(const AttnArgs &a, int sl, int k0, int k1, int *pageL) {
+    if (a.kvMap.table)
+        for (int i = threadIdx.x; i < (k1 - k0 + kPfTile - 1) / kPfTile; i += kPfThreads)
+            pageL[i] = (int)kvPageOf(a.kvMap, sl, k0 + i * kPfTile);
+    __syncthreads();
+}
 
 int attnPrefillRowsPerBlock(int kvMul) { return kPfWaves * (16 / kvMul); }
 bool attnPrefillSupported(int hs, int kvMul, bool kvBf16) {
@@ -177,13 +188,16 @@ __global__ __launch_bounds__(kPfThreads) void attnPrefillKernel(AttnArgs a, int 
     }
     const uint16_t *kc = reinterpret_cast<const uint16_t *>(a.kcache);
     const uint16_t *vc = reinterpret_cast<const uint16_t *>(a.vcache);
+    __shared__ int pageL[kPfMaxTiles];
+    pfPages(a, sl, k0, k1, pageL);
     u32x4 kr[PER], vr[PER];
     auto gload = [&](int t0) {
+        const size_t blk = a.kvMap.table ? (size_t)pageL[(t0 - k0) / kPfTile] : (size_t)sl;
 #pragma unroll
         for (int u = 0; u < PER; u++) {
             const int e = tid + u * kPfThreads;
             const int key = min(t0 + e / U8, k1 - 1);  // past the range: masked in compute (and mapped)
-            const size_t off = kvOff(a.kvMap, a.seqLen, nKv, HS, sl, key, g) + (e % U8) * 8;
+            const size_t off = kvOffAt(a.kvMap, a.seqLen, nKv, HS, blk, key, g) + (e % U8) * 8;
             kr[u] = *reinterpret_cast<const u32x4 *>(kc + off);
             vr[u] = *reinterpret_cast<const u32x4 *>(vc + off);
         }
@@ -311,23 +325,30 @@ __global__ __launch_bounds__(kPfThreads) void attnPrefillF32Kernel(AttnArgs a, i
     }
     const float *kc = reinterpret_cast<const float *>(a.kcache);
     const float *vc = reinterpret_cast<const float *>(a.vcache);
-    f32x4 kr[PER], vr[PER];
-    auto gload = [&](int t0) {
+    // two register staging sets: tile t + 2's loads go out while tile t computes and tile t + 1's
+    // are still in flight (one set left each tile waiting on a full memory round trip)
+    f32x4 kr[2][PER], vr[2][PER];
+    __shared__ int pageL[kPfMaxTiles];
+    pfPages(a, sl, k0, k1, pageL);
+    auto gload = [&](auto sTag, int t0) {
+        constexpr int S = decltype(sTag)::value;
+        const size_t blk = a.kvMap.table ? (size_t)pageL[(t0 - k0) / kPfTile] : (size_t)sl;
 #pragma unroll
         for (int u = 0; u < PER; u++) {
             const int e = tid + u * kPfThreads;
             const int key = min(t0 + e / U4, k1 - 1);  // past the range: masked in compute
-            const size_t off = kvOff(a.kvMap, a.seqLen, nKv, HS, sl, key, g) + (e % U4) * 4;
-            kr[u] = *reinterpret_cast<const f32x4 *>(kc + off);
-            vr[u] = *reinterpret_cast<const f32x4 *>(vc + off);
+            const size_t off = kvOffAt(a.kvMap, a.seqLen, nKv, HS, blk, key, g) + (e % U4) * 4;
+            kr[S][u] = *reinterpret_cast<const f32x4 *>(kc + off);
+            vr[S][u] = *reinterpret_cast<const f32x4 *>(vc + off);
         }
     };
-    auto lstore = [&]() {
+    auto lstore = [&](auto sTag) {
+        constexpr int S = decltype(sTag)::value;
 #pragma unroll
         for (int u = 0; u < PER; u++) {
             const int e = tid + u * kPfThreads, at = (e / U4) * SR + (e % U4) * 4;
-            *reinterpret_cast<f32x4 *>(&kT[0][at]) = kr[u];
-            *reinterpret_cast<f32x4 *>(&vT[0][at]) = vr[u];
+            *reinterpret_cast<f32x4 *>(&kT[0][at]) = kr[S][u];
+            *reinterpret_cast<f32x4 *>(&vT[0][at]) = vr[S][u];
         }
     };
     f32x4 o[NT];
@@ -377,18 +398,26 @@ __global__ __launch_bounds__(kPfThreads) void attnPrefillF32Kernel(AttnArgs a, i
             for (int n = 0; n < NT; n++) o[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(vrow[16 * n], p[j], o[n], 0, 0, 0);
         }
     };
-    gload(k0);
-    lstore();
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    gload(S0{}, k0);
+    if (k0 + kPfTile < k1) gload(S1{}, k0 + kPfTile);
+    lstore(S0{});
     __syncthreads();
-    for (int t0 = k0; t0 < k1; t0 += kPfTile) {
-        const bool more = t0 + kPfTile < k1;
-        if (more) gload(t0 + kPfTile);
+    // tile t in LDS (from set t & 1), tile t + 1 in flight in the other set: issue t + 2 into the
+    // set just stored, compute t, then store t + 1 (the loop is unrolled by two: static sets)
+    auto step = [&](auto cur, auto nxt, int t0) {
+        if (t0 + 2 * kPfTile < k1) gload(cur, t0 + 2 * kPfTile);
         compute(t0);
         __syncthreads();
-        if (more) {
-            lstore();
+        if (t0 + kPfTile < k1) {
+            lstore(nxt);
             __syncthreads();
         }
+    };
+    for (int t0 = k0; t0 < k1; t0 += 2 * kPfTile) {
+        step(S0{}, S1{}, t0);
+        if (t0 + kPfTile < k1) step(S1{}, S0{}, t0 + kPfTile);
     }
     pfFinish<HS>(a, nRows, o, m, lsum, nSplit, rb, g, c, b0, row, head, &kT[0][0], &vT[0][0], flagL);
 }
@@ -402,6 +431,11 @@ void launchAttentionPrefill(const AttnArgs &a, int nRows, hipStream_t s) {
     const dim3 grid(nKv * ((nRows + rpb - 1) / rpb), a.splitGrid);
     if (!attnPrefillSupported(a.hs, a.kvMul, a.kvBf16 != 0) || a.nHeads0 % a.kvMul)
         throw Error("launchAttentionPrefill: head size 64 / 128 and a power-of-two GQA group <= 16");
+    {  // the longest split chunk's tiles fit the kernels' LDS page list (pfPages)
+        const int minSplits = std::max(1, std::min(a.splitGrid, a.hs / 2));
+        if (a.kvMap.table && ((a.seqLen + minSplits - 1) / minSplits + kPfTile - 1) / kPfTile + 1 > kPfMaxTiles)
+            throw Error("launchAttentionPrefill: paged context too long for the per-chunk page list");
+    }
     if (!a.kvBf16) {
         if (a.hs == 128) hipLaunchKernelGGL(attnPrefillF32Kernel<128>, grid, dim3(kPfThreads), 0, s, a, nRows);
         else hipLaunchKernelGGL(attnPrefillF32Kernel<64>, grid, dim3(kPfThreads), 0, s, a, nRows);
