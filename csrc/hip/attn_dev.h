@@ -14,6 +14,9 @@ namespace hipk {
 #ifndef DL_ATTN_TU_F32
 #define DL_ATTN_TU_F32 4  // f32 caches outside the block: keys per 16-lane group per round
 #endif
+#ifndef DL_ATTN_HOIST_SYNC
+#define DL_ATTN_HOIST_SYNC 0  // fused block: per-key lookups measured 0.3-0.5 % faster (raw/r6_kvload_ab.txt)
+#endif
 #ifndef DL_ATTN_TU_BF16_BLOCK
 #define DL_ATTN_TU_BF16_BLOCK 8
 #endif
@@ -266,14 +269,17 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
 #pragma unroll
         for (int u = 0; u < TU; u++) {
             const int t = min(tb + u * NG, t1 - 1);
-            blk[u] = a.kvMap.table ? kvPageOf(a.kvMap, sl, t) : (size_t)sl;
+            if constexpr (SYNC && !DL_ATTN_HOIST_SYNC) blk[u] = 0;  // per key below (A/B switch)
+            else blk[u] = a.kvMap.table ? kvPageOf(a.kvMap, sl, t) : (size_t)sl;
         }
 #pragma unroll
         for (int u = 0; u < TU; u++) {
             const int t = min(tb + u * NG, t1 - 1);  // clamped: no divergent loads
             const bool cur = SYNC && t == pos;
             if ((phase == 1 && cur) || (phase == 2 && !cur)) continue;
-            const size_t off = kvOffAt(a.kvMap, a.seqLen, a.kv0 / HS, HS, blk[u], t, kvh) + l16 * DPL;
+            const size_t off = (SYNC && !DL_ATTN_HOIST_SYNC)
+                                   ? kvOff(a.kvMap, a.seqLen, a.kv0 / HS, HS, sl, t, kvh) + l16 * DPL
+                                   : kvOffAt(a.kvMap, a.seqLen, a.kv0 / HS, HS, blk[u], t, kvh) + l16 * DPL;
             const uint32_t *kp = reinterpret_cast<const uint32_t *>(
                 BF16 ? (const void *)(reinterpret_cast<const uint16_t *>(a.kcache) + off)
                      : (const void *)(reinterpret_cast<const float *>(a.kcache) + off));
