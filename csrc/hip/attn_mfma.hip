@@ -78,7 +78,9 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
     // vmcnt(0) - every DMA already in flight - before each of the 16 wave-instructions of a tile.)
     const KvMap &km = a.kvMap;
     const int pg0 = km.table ? t0 >> km.pageShift : 0;
-    const bool pgLanes = km.table && ((t1 - 1) >> km.pageShift) - pg0 < 64;
+    // a chunk spans at most 64 pages (launchAttentionMfma checks): no per-key table load remains in
+    // the issue loop, whose join would put a vmcnt(0) drain before every DMA pair
+    const bool pgLanes = km.table != nullptr;
     int pgReg = 0;
     if (pgLanes) {
         // retired here, before any DMA: the waitcnt pass cannot track this load into the issue
@@ -88,8 +90,7 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
         pgReg = v;
     }
     auto offOf = [&](int key) -> size_t {  // element offset of head g's vector at this key
-        if (!km.table) return kvOffAt(km, a.seqLen, nKv, HS, (size_t)sl, key, g);
-        if (!pgLanes) return kvOff(km, a.seqLen, nKv, HS, sl, key, g);
+        if (!pgLanes) return kvOffAt(km, a.seqLen, nKv, HS, (size_t)sl, key, g);
         const int pg = __shfl(pgReg, (key >> km.pageShift) - pg0);
         return kvOffAt(km, a.seqLen, nKv, HS, (size_t)pg, key, g);
     };
@@ -293,6 +294,8 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
 static constexpr int kApRound = 4;  // tiles per round (one per wave)
 static constexpr size_t kApLds = 2 * kApRound * 2 * kAmTileBytes + 64;
 
+static constexpr int kApMaxTiles = 256;  // per-chunk page list of the prefill kernel (paged caches)
+
 template <int KM>
 __global__ __launch_bounds__(kAmThreads) void attnPrefillDmaKernel(AttnArgs a, int nRows) {
     constexpr int HS = kAmHS, DS = HS / 32, NT = HS / 16, RPW = 16 / KM, RPB = kAmWaves * RPW;
@@ -328,6 +331,12 @@ __global__ __launch_bounds__(kAmThreads) void attnPrefillDmaKernel(AttnArgs a, i
     const uint16_t *kc = reinterpret_cast<const uint16_t *>(a.kcache);
     const uint16_t *vc = reinterpret_cast<const uint16_t *>(a.vcache);
     const int nTiles = (k1 - k0 + kAmTile - 1) / kAmTile, nRounds = (nTiles + kApRound - 1) / kApRound;
+    // paged cache: the chunk's per-tile pages in LDS before any DMA (a tile never crosses a page; a
+    // table load per key row put a vmcnt(0) drain before every DMA pair, contiguous caches included)
+    __shared__ int pageL[kApMaxTiles];
+    if (a.kvMap.table)
+        for (int i = tid; i < nTiles; i += kAmThreads) pageL[i] = (int)kvPageOf(a.kvMap, sl, k0 + i * kAmTile);
+    __syncthreads();
     auto tileBuf = [&](int bf, int tt) { return smem + (size_t)(bf * kApRound + tt) * 2 * kAmTileBytes; };
     // wave w copies tile kApRound * r + w of round r into buffer bf (16 wave-instructions, or none)
     auto issue = [&](int r, int bf) {
@@ -338,7 +347,8 @@ __global__ __launch_bounds__(kAmThreads) void attnPrefillDmaKernel(AttnArgs a, i
         for (int j = 0; j < kAmTile / 4; j++) {
             const int rr = 4 * j + (lane >> 4), p = lane & 15;
             const int key = min(k0 + kAmTile * t + rr, k1 - 1);  // past the chunk: masked below
-            const size_t off = kvOff(a.kvMap, a.seqLen, nKv, HS, sl, key, g) + (size_t)(p ^ amSwz(rr)) * 8;
+            const size_t blk = a.kvMap.table ? (size_t)pageL[t] : (size_t)sl;
+            const size_t off = kvOffAt(a.kvMap, a.seqLen, nKv, HS, blk, key, g) + (size_t)(p ^ amSwz(rr)) * 8;
             __builtin_amdgcn_global_load_lds(const_cast<uint16_t *>(kc + off),
                                              reinterpret_cast<__attribute__((address_space(3))) void *>(
                                                  reinterpret_cast<uintptr_t>(kb + j * 1024)), 16, 0, 0);
@@ -514,6 +524,11 @@ bool attnPrefillDmaSupported(const AttnArgs &a) {
 
 void launchAttentionPrefillDma(const AttnArgs &a, int nRows, hipStream_t s) {
     const int nKv = a.nHeads0 / a.kvMul, rpb = kAmWaves * (16 / a.kvMul);
+    {  // the longest chunk's tiles fit the kernel's LDS page list
+        const int minSplits = std::max(1, std::min(a.splitGrid, kAmHS / 2));
+        if (a.kvMap.table && ((a.seqLen + minSplits - 1) / minSplits + kAmTile - 1) / kAmTile + 1 > kApMaxTiles)
+            throw Error("launchAttentionPrefillDma: paged context too long for the per-chunk page list");
+    }
     const dim3 grid(nKv * ((nRows + rpb - 1) / rpb), a.splitGrid);
 #define DL_AP_CASE(K)                                                                                 \
     if (a.kvMul == K) {                                                                               \
@@ -555,6 +570,8 @@ const void *attnMfmaModuleKernel() { return (const void *)attnDecodeMfmaKernel<4
 void launchAttentionMfma(const AttnArgs &a, int B, hipStream_t s) {
     const dim3 grid(a.nHeads0 / a.kvMul, a.splitGrid, B);
     if (2 * a.kvMul * a.splitGrid * 4 + 4096 > (int)kAmLds) throw Error("attention split grid too large");
+    if (a.kvMap.table && (a.chunkMax >> a.kvMap.pageShift) + 2 > 64)
+        throw Error("launchAttentionMfma: a chunk spans more than 64 pages (one page id per lane)");
 #define DL_AM_CASE(K)                                                                             \
     if (a.kvMul == K) {                                                                           \
         allowLds((const void *)attnDecodeMfmaKernel<K>, kAmLds);                                  \
