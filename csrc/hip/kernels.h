@@ -409,6 +409,8 @@ void launchAttentionPrefill(const AttnArgs &a, int nRows, hipStream_t s);
 int attnPrefillRowsPerBlock(int kvMul);
 bool attnPrefillSupported(int hs, int kvMul, bool kvBf16);
 int attnSplitGrid(int seqLen);
+// rows of at most kAttnShortLen keys split into chunks of kAttnShortChunk (attnSplit)
+constexpr int kAttnShortLen = 512, kAttnShortChunk = 128;
 // Fewest keys per attention split (DL_ATTN_CHUNK, default 256): sets the split grid of a context.
 int attnChunkMin();
 int attnChunkMax(int seqLen, int splitGrid);

@@ -171,6 +171,7 @@ int attnChunkMin() {
 int attnSplitGrid(int seqLen) {
     const int cm = attnChunkMin();
     int g = (seqLen + cm - 1) / cm;
+    if (cm >= 256) g = std::max(g, (std::min(seqLen, kAttnShortLen) + kAttnShortChunk - 1) / kAttnShortChunk);
     return g < 1 ? 1 : (g > 128 ? 128 : g);
 }
 
