@@ -238,7 +238,7 @@ __device__ __forceinline__ bool attnTask(const AttnArgs &a, int b, int hgIdx, in
         nSplit = 1;
         ch = len;
     } else {
-        attnSplit(len, a.splitGrid, nSplit, ch, a.chunkMin);
+        attnSplit(len, a.splitGrid, nSplit, ch, a.chunkMin, a.shortLen);
     }
     if (c >= nSplit) return false;
     const int t0 = c * ch;

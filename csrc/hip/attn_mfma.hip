@@ -50,7 +50,7 @@ __global__ __launch_bounds__(kAmThreads) void attnDecodeMfmaKernel(AttnArgs a) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, col = lane & 15, h = lane >> 4;
     const int pos = a.pos[b], sl = a.slot[b], len = pos + 1;
     int nSplit, ch;
-    attnSplit(len, a.splitGrid, nSplit, ch, a.chunkMin);
+    attnSplit(len, a.splitGrid, nSplit, ch, a.chunkMin, a.shortLen);
     if (c >= nSplit) return;
     const int t0 = c * ch, t1 = min(t0 + ch, len);
     const int nTiles = (t1 - t0 + kAmTile - 1) / kAmTile;

@@ -753,12 +753,13 @@ __device__ __forceinline__ int rowsMaxLen(const int *pos, int b0, int n, int nRo
 // Sequence split of a decode-attention row of length `len`: nSplit chunks of ch positions
 // (~256 per chunk, at most splitGrid chunks). Shorter chunks for the few heads of a TP8 shard
 // (4 per rank) measured slower: 5.4 -> 7.6 us at 100 positions (profiles/r5_tp_rank.md).
-__device__ __forceinline__ void attnSplit(int len, int splitGrid, int &nSplit, int &ch, int chunkMin = 256) {
-    // short rows (<= kAttnShortLen keys) split at 128 keys: one 256-thread task walks 112-128 keys
-    // per memory round trip, so 129..256 keys in one chunk cost a second dependent round trip per
-    // layer (decode from position 80: 1.39-1.44 vs 1.35-1.37 ms/token at 164-204, r6_decode.md).
-    // A function of the row's own length only: bucket- and batch-independent splits.
-    if (chunkMin >= 256 && len <= kAttnShortLen) chunkMin = kAttnShortChunk;
+__device__ __forceinline__ void attnSplit(int len, int splitGrid, int &nSplit, int &ch, int chunkMin = 256,
+                                          int shortLen = 0) {
+    // single decode rows (shortLen set) of <= shortLen keys split at 128 keys: one 256-thread task
+    // walks 112-128 keys per memory round trip, so 129..256 keys in one chunk cost a second
+    // dependent round trip per layer (decode at 164-204: 1.39-1.44 vs 1.35-1.37 ms/token,
+    // r6_decode.md). Batched launches keep 256 (their grid would double for it).
+    if (chunkMin >= 256 && len <= shortLen) chunkMin = kAttnShortChunk;
     int ns = (len + chunkMin - 1) / chunkMin;
     if (ns > splitGrid) ns = splitGrid;
     if (ns < 1) ns = 1;

@@ -26,8 +26,9 @@ void HipEngineImpl::setupBuckets() {
     buckets_.push_back(last);
     DL_CHECK(buckets_.size() <= 16, "too many context buckets");
     for (CtxBucket &b : buckets_) {
-        b.splitGrid = hipk::attnSplitGrid(b.maxLen);
-        b.chunkMax = hipk::attnChunkMax(b.maxLen, b.splitGrid);
+        b.splitGrid = hipk::attnSplitGrid(b.maxLen, true);
+        b.splitGridBat = hipk::attnSplitGrid(b.maxLen, false);
+        b.chunkMax = hipk::attnChunkMax(b.maxLen, b.splitGridBat);
     }
     bucket_ = (int)buckets_.size() - 1;
 }
@@ -186,7 +187,8 @@ hipk::AttnArgs HipEngineImpl::attnArgs(const DevLayer &L, bool bat) const {
     a.hs = p.headSize;
     a.kv0 = p.kv0;
     a.seqLen = h_.seqLen;
-    a.splitGrid = buckets_[bucket_].splitGrid;
+    a.splitGrid = bat ? buckets_[bucket_].splitGridBat : buckets_[bucket_].splitGrid;
+    a.shortLen = bat ? 0 : hipk::kAttnShortLen;
     a.chunkMax = buckets_[bucket_].chunkMax;
     a.chunkMin = hipk::attnChunkMin();
     a.partO = dPartO_;

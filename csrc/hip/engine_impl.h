@@ -51,7 +51,8 @@ struct DevLayer {
 // the fused attention block). Part of the graph key.
 struct CtxBucket {
     int maxLen = 0;     // positions covered (<= seqLen)
-    int splitGrid = 1;  // attention sequence splits at this length
+    int splitGrid = 1;  // attention sequence splits at this length (single decode rows: short chunks)
+    int splitGridBat = 1;  // the same for batched rows (256-key chunks throughout)
     int chunkMax = 256;
     bool block = false; // the fused attention block fits co-resident at this bucket's grid
 };

@@ -113,6 +113,7 @@ struct AttnArgs {
     int splitGrid = 1;          // max sequence splits (grid.y)
     int chunkMax = 256;         // LDS capacity in positions per split
     int chunkMin = 256;         // fewest positions per split (attnChunkMin)
+    int shortLen = 0;           // rows of <= shortLen keys split at kAttnShortChunk (single decode rows)
     float *partO = nullptr;     // [B][nHeads0][splitGrid][hs]
     float *partML = nullptr;    // [B][nHeads0][splitGrid][2]
     float *out = nullptr;       // [B][ldOut] f32 output (when outQ and outH are null)
@@ -408,8 +409,8 @@ void launchTpSelfTest(const TpXchg &x, float *out, int n, float val, hipStream_t
 void launchAttentionPrefill(const AttnArgs &a, int nRows, hipStream_t s);
 int attnPrefillRowsPerBlock(int kvMul);
 bool attnPrefillSupported(int hs, int kvMul, bool kvBf16);
-int attnSplitGrid(int seqLen);
-// rows of at most kAttnShortLen keys split into chunks of kAttnShortChunk (attnSplit)
+int attnSplitGrid(int seqLen, bool shortChunks = false);
+// single decode rows of at most kAttnShortLen keys split into chunks of kAttnShortChunk (attnSplit)
 constexpr int kAttnShortLen = 512, kAttnShortChunk = 128;
 // Fewest keys per attention split (DL_ATTN_CHUNK, default 256): sets the split grid of a context.
 int attnChunkMin();

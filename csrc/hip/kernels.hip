@@ -168,10 +168,11 @@ int attnChunkMin() {
     return v;
 }
 
-int attnSplitGrid(int seqLen) {
+int attnSplitGrid(int seqLen, bool shortChunks) {
     const int cm = attnChunkMin();
     int g = (seqLen + cm - 1) / cm;
-    if (cm >= 256) g = std::max(g, (std::min(seqLen, kAttnShortLen) + kAttnShortChunk - 1) / kAttnShortChunk);
+    if (shortChunks && cm >= 256)
+        g = std::max(g, (std::min(seqLen, kAttnShortLen) + kAttnShortChunk - 1) / kAttnShortChunk);
     return g < 1 ? 1 : (g > 128 ? 128 : g);
 }
 
